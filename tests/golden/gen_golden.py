@@ -1,0 +1,360 @@
+#!/usr/bin/env python
+"""Golden-vector generator for the approx_v9 hot path (TEST INFRASTRUCTURE ONLY).
+
+Runs ONLY in the build container, where the reference checkout is mounted read-only at
+/root/reference.  It imports the reference UNMODIFIED through a small import shim (SURVEY.md
+§8(c)): module-level ``device='cuda'`` tensors are redirected to the CPU, and the
+un-installed ``cupy`` / ``timm`` imports are satisfied by empty stub modules.  Nothing here is
+shipped; the GPU box only sees the ``.npz`` fixtures this script writes next to itself.
+
+Fixture groups:
+  g1_decompose.npz  DEC / Q_R known-answer table      (approx_matmul_whole_v9.py:189-362)
+  g2_matmul.npz     custom_matmul_vectorize, scalar biases, flag matrix, sums + per-term
+                    values                            (approx_matmul_whole_v9.py:10-169)
+  g3_debug.npz      the captured MobileNetV2 layer in debug_params/*.csv through the
+                    per-column loop of approx_multiply (approx_calculation.py:749-814)
+  g4_tensorbias.npz single-column (tensor-bias) calls, quirk F5 (approx_calculation.py:800-809)
+  g5_operator.npz   QCustomBNConv2dTorch / QCustomLinearTorch through estimate->fix->approx
+                    (quantized_folded_bn.py:30-83, hijacker.py:77-115)
+
+Usage:  python tests/golden/gen_golden.py      (about a minute on 8 cores)
+"""
+import io
+import contextlib
+import json
+import os
+import random
+import sys
+import types
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+# ----------------------------------------------------------------------------- import shim
+def _install_shim():
+    orig_tensor, orig_zeros = torch.tensor, torch.zeros
+
+    def _cpu(kw):
+        d = kw.get("device")
+        if d is not None and str(d).startswith("cuda"):
+            kw["device"] = "cpu"
+        return kw
+
+    torch.tensor = lambda *a, **kw: orig_tensor(*a, **_cpu(kw))
+    torch.zeros = lambda *a, **kw: orig_zeros(*a, **_cpu(kw))
+    sys.modules.setdefault("cupy", types.ModuleType("cupy"))
+    mods = ["timm", "timm.models", "timm.models.layers",
+            "timm.models.layers.activations", "timm.models.layers.activations_me"]
+    for m in mods:
+        sys.modules.setdefault(m, types.ModuleType(m))
+    for c in ("Swish", "HardSwish", "HardSigmoid"):
+        setattr(sys.modules["timm.models.layers.activations"], c, type(c, (nn.Module,), {}))
+    for c in ("SwishMe", "HardSwishMe", "HardSigmoidMe"):
+        setattr(sys.modules["timm.models.layers.activations_me"], c, type(c, (nn.Module,), {}))
+    sys.path.insert(0, REF)
+
+
+_install_shim()
+import approx.approx_matmul_whole_v9 as v9  # noqa: E402  (reference, unmodified)
+import approx.approx_calculation as ac  # noqa: E402
+from quantization.quantizers.fp8_quantizer import FPQuantizer  # noqa: E402
+from quantization.range_estimators import RangeEstimators  # noqa: E402
+
+FORMATS = [(4, 3), (3, 4), (2, 5), (5, 2)]
+
+
+def table(E, M, with_comp, dnsmp):
+    """Error table as the operator would pick it; E5M2 (unsupported by the reference,
+    SURVEY F3) gets an all-zero table so its arithmetic can still be pinned."""
+    if (E, M) == (5, 2):
+        return torch.zeros((4, 4), dtype=torch.int32)
+    return v9.get_error_table_NN(E, M, withComp=with_comp, dnsmp_factor=dnsmp)
+
+
+TABLE_VARIANTS = {
+    (4, 3): [("comp", True, 3), ("nocomp", False, 3)],
+    (3, 4): [("comp3", True, 3), ("comp4", True, 4), ("nocomp", False, 3)],
+    (2, 5): [("comp3", True, 3), ("comp4", True, 4), ("comp5", True, 5), ("nocomp", False, 3)],
+    (5, 2): [("zero", True, 3)],
+}
+
+
+# ----------------------------------------------------------------------------- G1
+def grid_values(E, M, b, extra_expo=3):
+    vals = []
+    for expo in range(0, 2 ** E + extra_expo):
+        for mant in range(2 ** M):
+            if expo == 0:
+                vals.append(2.0 ** (1 - b) * mant / 2 ** M)
+            else:
+                vals.append(2.0 ** (expo - b) * (1 + mant / 2 ** M))
+    v = np.array(vals, dtype=np.float64)
+    return np.concatenate([v, -v])
+
+
+def edge_values(E, M, b, rng):
+    min_norm = 2.0 ** (1 - b)
+    min_sub = min_norm * 2.0 ** -M
+    max_norm = 2.0 ** (2 ** E - 1 - b) * (2 - 2.0 ** -M)
+    f32 = np.float32
+    e = [0.0, min_sub / 2, min_sub * 0.5000001, min_sub * 0.4999999, min_sub * 1.5, min_sub * 2.5,
+         min_norm * (1 - 2.0 ** -(M + 2)), min_norm * (1 - 2.0 ** -(M + 1)),
+         float(np.nextafter(f32(min_norm), f32(0))), min_norm,
+         max_norm, max_norm * 1.01, max_norm * 4, 1e30, 1e-30, 1e-40, 3e-39]
+    for ex in range(-6, 6):
+        base = 2.0 ** ex
+        e += [base * (2 - 2.0 ** -M - 2.0 ** -(M + 2)), base * (2 - 2.0 ** -(M + 1)),
+              base * (2 - 2.0 ** -(M + 1)) * (1 + 1e-6), base * (1 + 2.0 ** -(M + 1)),
+              base * (1 + 3 * 2.0 ** -(M + 1))]
+    rnd = rng.standard_normal(300) * 2.0 ** rng.integers(-24, 10, 300)
+    v = np.concatenate([np.array(e), rnd])
+    return np.concatenate([v, -v])
+
+
+def gen_g1():
+    rng = np.random.default_rng(1234)
+    out, meta = {}, []
+    for (E, M) in FORMATS:
+        for b in sorted({2 ** (E - 1) - 1, 3, 5, 9, 14, 19}):
+            x = np.concatenate([grid_values(E, M, b), edge_values(E, M, b, rng)]).astype(np.float32)
+            x[len(x) // 2] = -0.0
+            xt = torch.from_numpy(x.copy())
+            key = f"E{E}M{M}_b{b}"
+            out[key + "_x"] = x
+            for tb in (False, True):
+                bias = torch.tensor([b], dtype=torch.int32) if tb else b
+                for clip in (False, True):
+                    pd = v9.param_prepare(E, M, custom_bias=bias)
+                    expo, mant = v9.float_to_fpany_absint_torch(pd, xt.clone(), clip_OF=clip)
+                    q = v9.quant_to_fp_any_vectorize_torch(xt.clone(), E, M, custom_bias=bias,
+                                                           clip_OF=clip)
+                    sfx = f"_tb{int(tb)}_c{int(clip)}"
+                    out[key + sfx + "_expo"] = expo.numpy().astype(np.int32)
+                    out[key + sfx + "_mant"] = mant.numpy().astype(np.int32)
+                    out[key + sfx + "_q"] = q.numpy().astype(np.float32)
+            meta.append(dict(key=key, E=E, M=M, b=b))
+    np.savez_compressed(os.path.join(HERE, "g1_decompose.npz"), **out)
+    return meta
+
+
+# ----------------------------------------------------------------------------- G2
+def random_grid_tensor(E, M, bias, rows, cols, seed):
+    """Same draw as the reference self-check harness (approx_matmul_whole_v9.py:794-804):
+    numpy picks a code of the value space, python's random picks the sign."""
+    np.random.seed(seed)
+    random.seed(seed)
+    space = v9.show_value_space(E, M, bias, show_style=0).numpy()
+    return torch.tensor([[np.random.choice(space) * random.choice([-1, 1]) for _ in range(cols)]
+                         for _ in range(rows)], dtype=torch.float32)
+
+
+G2_BIASES = {(3, 4): (3, 5, 5), (4, 3): (7, 9, 8), (2, 5): (1, 2, 2), (5, 2): (15, 17, 16)}
+
+
+def cmv(A, B, E, M, bA, bB, bR, tab, approx, s2n, qbma, gclip):
+    with contextlib.redirect_stdout(io.StringIO()):
+        return v9.custom_matmul_vectorize(
+            A, B, E, M, bA, bB, bR, tab, with_approx=approx, with_s2nn2s_opt=s2n,
+            golden_clip_OF=gclip, quant_btw_mult_accu=qbma)
+
+
+def gen_g2():
+    out, meta = {}, []
+    for (E, M), (bA, bB, bR) in G2_BIASES.items():
+        n = 256 if (E, M) == (3, 4) else 128
+        A = random_grid_tensor(E, M, bA, n, n, seed=5)
+        B = random_grid_tensor(E, M, bB, n, n, seed=5 if (E, M) == (3, 4) else 6)
+        fk = f"E{E}M{M}"
+        out[fk + "_A"] = A.numpy()
+        out[fk + "_B"] = B.numpy()
+        Ac, Bc = A[:64], B[:, :64]
+        At, Bt = A[:8, :64], B[:64, :8]
+        for (tname, wc, dn) in TABLE_VARIANTS[(E, M)]:
+            tab = table(E, M, wc, dn)
+            for approx in (True, False):
+                if not approx and tname != TABLE_VARIANTS[(E, M)][0][0]:
+                    continue  # table is irrelevant without approx
+                for s2n in (True, False):
+                    for qbma in (True, False):
+                        for gclip in (False, True):
+                            key = f"{fk}_{tname}_a{int(approx)}_s{int(s2n)}_q{int(qbma)}_g{int(gclip)}"
+                            C = cmv(Ac, Bc, E, M, bA, bB, bR, tab, approx, s2n, qbma, gclip)
+                            out[key + "_C"] = C.numpy()
+                            terms = torch.stack([cmv(At[:, k:k + 1], Bt[k:k + 1, :], E, M, bA, bB, bR,
+                                                     tab, approx, s2n, qbma, gclip)
+                                                 for k in range(At.shape[1])], dim=1)
+                            out[key + "_T"] = terms.numpy()
+                            meta.append(dict(key=key, fmt=fk, E=E, M=M, bA=bA, bB=bB, bR=bR,
+                                             table=tname, with_comp=wc, dnsmp=dn, approx=approx,
+                                             s2n=s2n, qbma=qbma, gclip=gclip))
+        for (tname, wc, dn) in TABLE_VARIANTS[(E, M)]:
+            out[f"{fk}_table_{tname}"] = table(E, M, wc, dn).numpy().astype(np.int32)
+    np.savez_compressed(os.path.join(HERE, "g2_matmul.npz"), **out)
+    return meta
+
+
+# ----------------------------------------------------------------------------- G3
+class _FakeOp:
+    """Minimal stand-in carrying the attributes approx_multiply reads."""
+
+    def __init__(self, params, approx_flag=True):
+        self.custom_approx_params = params
+        self.approx_flag = approx_flag
+        self.quantize_after_mult_and_add = False
+
+
+def approx_params(E, M, dnsmp, with_comp, approx, s2n, qbma, gclip=False):
+    return dict(expo_width=E, mant_width=M, dnsmp_factor=dnsmp, withComp=with_comp,
+                with_approx=approx, with_s2nn2s_opt=s2n, sim_hw_add_OFUF=False,
+                with_OF_opt=False, with_UF_opt=False, golden_clip_OF=gclip,
+                quant_btw_mult_accu=qbma, debug_mode=False, self_check_mode=False)
+
+
+def gen_g3():
+    A = np.loadtxt(os.path.join(REF, "debug_params/act.csv"), delimiter=",", dtype=np.float32)
+    B = np.loadtxt(os.path.join(REF, "debug_params/weight.csv"), delimiter=",", dtype=np.float32)
+    bA = np.loadtxt(os.path.join(REF, "debug_params/act_bias.csv"), delimiter=",", dtype=np.float32).reshape(1)
+    bB = np.loadtxt(os.path.join(REF, "debug_params/weight_bias.csv"), delimiter=",", dtype=np.float32).reshape(-1)
+    bR = np.array([5.0], dtype=np.float32)
+    out = dict(A=A, B=B, bA=bA, bB=bB, bR=bR)
+    meta = []
+    combos = [("comp3", True, 3, True, True, True), ("nocomp", False, 3, True, False, True),
+              ("nocomp", False, 3, True, True, False), ("comp4", True, 4, False, False, False),
+              ("comp3", True, 3, True, False, True)]
+    for (tname, wc, dn, approx, s2n, qbma) in combos:
+        op = _FakeOp(approx_params(3, 4, dn, wc, approx, s2n, qbma))
+        C = ac.QCustomBNConv2dTorch.approx_multiply(op, torch.from_numpy(A), torch.from_numpy(B),
+                                                    torch.from_numpy(bA), torch.from_numpy(bB),
+                                                    torch.from_numpy(bR))
+        key = f"{tname}_a{int(approx)}_s{int(s2n)}_q{int(qbma)}"
+        out[key + "_C"] = C.numpy()
+        meta.append(dict(key=key, table=tname, with_comp=wc, dnsmp=dn, approx=approx, s2n=s2n, qbma=qbma))
+    np.savez_compressed(os.path.join(HERE, "g3_debug.npz"), **out)
+    return meta
+
+
+# ----------------------------------------------------------------------------- G4
+def gen_g4():
+    out, meta = {}, []
+    gen = torch.Generator().manual_seed(77)
+    for (E, M), (bA, bB, bR) in G2_BIASES.items():
+        if (E, M) == (5, 2):
+            continue
+        A = random_grid_tensor(E, M, bA, 64, 9, seed=11)
+        A[torch.rand(A.shape, generator=gen) < 0.4] = 0.0  # ReLU-like zeros: exercise quirk F5
+        Bw = random_grid_tensor(E, M, bB, 9, 1, seed=12)
+        fk = f"E{E}M{M}"
+        out[fk + "_A"], out[fk + "_B"] = A.numpy(), Bw.numpy()
+        for (tname, wc, dn) in TABLE_VARIANTS[(E, M)]:
+            for approx in (True, False):
+                for s2n in (True, False):
+                    for qbma in (True, False):
+                        op = _FakeOp(approx_params(E, M, dn, wc, approx, s2n, qbma))
+                        xb = torch.tensor([float(bA)])
+                        yb = torch.tensor(float(bB))  # 0-dim, as weight_group_fp_bias.squeeze()
+                        rb = torch.tensor([float(bR)])
+                        C = ac.QCustomBNConv2dTorch.approx_multiply(op, A, Bw, xb, yb, rb)
+                        key = f"{fk}_{tname}_a{int(approx)}_s{int(s2n)}_q{int(qbma)}"
+                        out[key + "_C"] = C.numpy()
+                        terms = torch.stack([
+                            ac.QCustomBNConv2dTorch.approx_multiply(op, A[:, k:k + 1], Bw[k:k + 1, :],
+                                                                     xb, yb, rb)
+                            for k in range(A.shape[1])], dim=1)
+                        out[key + "_T"] = terms.numpy()
+                        meta.append(dict(key=key, fmt=fk, E=E, M=M, bA=bA, bB=bB, bR=bR, table=tname,
+                                         with_comp=wc, dnsmp=dn, approx=approx, s2n=s2n, qbma=qbma))
+    np.savez_compressed(os.path.join(HERE, "g4_tensorbias.npz"), **out)
+    return meta
+
+
+# ----------------------------------------------------------------------------- G5
+def qparams_for(E, M, approx_cfg, run_method):
+    return dict(
+        method=FPQuantizer, act_method=FPQuantizer, n_bits=8, n_bits_act=8,
+        per_channel_weights=True,
+        weight_range_method=RangeEstimators.current_minmax.cls, weight_range_options={},
+        act_range_method=RangeEstimators.allminmax.cls, act_range_options={},
+        quantize_input=True,
+        fp8_kwargs=dict(maxval=None, mantissa_bits=M, set_maxval=True, learn_maxval=False,
+                        learn_mantissa_bits=False, mse_include_mantissa_bits=False,
+                        allow_unsigned=False),
+        custom_approx_params=approx_cfg, run_method=run_method)
+
+
+def gen_g5():
+    out, meta = {}, []
+    torch.manual_seed(2024)
+    run_method = dict(approx_flag=True, quantize_after_mult_and_add=False,
+                      res_quantizer_flag=True, original_quantize_res=False)
+    cases = [
+        ("conv_e4m3_nocomp", (4, 3), dict(cin=8, cout=16, k=3, stride=1, pad=1, groups=1), False, True, True),
+        ("conv_e4m3_comp_s2", (4, 3), dict(cin=8, cout=16, k=3, stride=2, pad=1, groups=1), True, True, True),
+        ("conv_e3m4_comp3", (3, 4), dict(cin=6, cout=12, k=3, stride=1, pad=0, groups=1), True, False, True),
+        ("dwconv_e3m4_nocomp", (3, 4), dict(cin=8, cout=8, k=3, stride=1, pad=1, groups=8), False, True, True),
+        ("conv1x1_e2m5_comp3", (2, 5), dict(cin=16, cout=8, k=1, stride=1, pad=0, groups=1), True, True, False),
+        ("linear_e4m3_nocomp", (4, 3), dict(fin=32, fout=10), False, True, True),
+        ("linear_e3m4_comp3", (3, 4), dict(fin=24, fout=7), True, True, True),
+    ]
+    for (name, (E, M), shp, wc, s2n, qbma) in cases:
+        cfg = approx_params(E, M, 3, wc, True, s2n, qbma)
+        qp = qparams_for(E, M, cfg, dict(run_method))
+        if "fin" in shp:
+            mod = ac.QCustomLinearTorch(in_features=shp["fin"], out_features=shp["fout"], bias=True, **qp)
+            x_cal = torch.randn(6, shp["fin"])
+            x_ev = torch.randn(5, shp["fin"])
+        else:
+            mod = ac.QCustomBNConv2dTorch(in_channels=shp["cin"], out_channels=shp["cout"],
+                                          kernel_size=shp["k"], stride=shp["stride"], padding=shp["pad"],
+                                          groups=shp["groups"], bias=False, activation=nn.ReLU(), **qp)
+            with torch.no_grad():
+                mod.gamma.uniform_(0.5, 1.5)
+                mod.beta.uniform_(-0.2, 0.2)
+                mod.running_mean.uniform_(-0.1, 0.1)
+                mod.running_var.uniform_(0.5, 2.0)
+            x_cal = torch.relu(torch.randn(2, shp["cin"], 7, 7))
+            x_ev = torch.relu(torch.randn(2, shp["cin"], 7, 7))
+        with torch.no_grad():
+            mod.weight.normal_(0, 0.3)
+            if getattr(mod, "bias", None) is not None:
+                mod.bias.uniform_(-0.1, 0.1)
+        state = {k: v.clone() for k, v in mod.state_dict().items()}
+        mod.eval()
+        mod.quantized()
+        mod.estimate_ranges()
+        with torch.no_grad(), contextlib.redirect_stdout(io.StringIO()):
+            y_cal = mod(x_cal)
+        mod.fix_ranges()
+        with torch.no_grad(), contextlib.redirect_stdout(io.StringIO()):
+            y_ev = mod(x_ev)
+        for k, v in state.items():
+            out[f"{name}__state__{k}"] = v.numpy()
+        out[f"{name}__x_cal"] = x_cal.numpy()
+        out[f"{name}__x_ev"] = x_ev.numpy()
+        out[f"{name}__y_cal"] = y_cal.numpy()
+        out[f"{name}__y_ev"] = y_ev.numpy()
+        out[f"{name}__bA"] = mod.get_acts_fp_bias().reshape(-1).numpy()
+        out[f"{name}__bB"] = mod.get_weights_fp_bias().reshape(-1).numpy()
+        out[f"{name}__bR"] = mod.get_res_fp_bias().reshape(-1).numpy()
+        meta.append(dict(name=name, E=E, M=M, shape=shp, with_comp=wc, s2n=s2n, qbma=qbma,
+                         state_keys=list(state.keys())))
+    np.savez_compressed(os.path.join(HERE, "g5_operator.npz"), **out)
+    return meta
+
+
+def main():
+    torch.set_num_threads(os.cpu_count() or 1)
+    meta = dict(torch_version=torch.__version__, reference="revollllt/FP8_quantization@2024-11-08",
+                g1=gen_g1(), g2=gen_g2(), g3=gen_g3(), g4=gen_g4(), g5=gen_g5())
+    with open(os.path.join(HERE, "meta.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    sizes = {f: os.path.getsize(os.path.join(HERE, f)) for f in os.listdir(HERE) if f.endswith(".npz")}
+    print(json.dumps(sizes))
+
+
+if __name__ == "__main__":
+    main()
