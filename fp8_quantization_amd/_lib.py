@@ -1,0 +1,91 @@
+"""ctypes binding of libfp8approx.so (the gfx950 HIP library; C-ABI in include/fp8approx.h).
+
+There is no CPU or PyTorch fallback: if the library is missing or cannot be loaded, every
+entry point raises.  Device work needs HIP tensors; CPU tensors are rejected.
+"""
+import ctypes
+import os
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libfp8approx.so")
+
+APPROX, S2N, QBMA, GCLIP, TB = 1, 2, 4, 8, 16
+OK, EINVAL, EFORMAT, EHIP = 0, -1, -2, -3
+
+SYMBOLS = ("fp8a_version", "fp8a_last_error", "fp8a_decompose", "fp8a_quant", "fp8a_matmul_workspace_size",
+           "fp8a_matmul", "fp8a_terms", "fp8a_conv2d_workspace_size", "fp8a_conv2d", "fp8a_im2col",
+           "fp8a_fp8_quantize")
+
+_lib = None
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def load():
+    """Load (once) and return the ctypes handle; raise if the HIP library is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryMissing(
+            f"{LIB_PATH} not found: build it with `python -m fp8_quantization_amd.build_native` "
+            "(there is no CPU fallback for the approx-FP8 path)")
+    L = ctypes.CDLL(LIB_PATH)
+    P, I, I64, U, SZ = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_size_t
+    sig = {
+        "fp8a_version": ([], ctypes.c_char_p),
+        "fp8a_last_error": ([], ctypes.c_char_p),
+        "fp8a_decompose": ([P, I64, I64, I64, I, I, P, I64, U, P, P, P], I),
+        "fp8a_quant": ([P, I64, I, I, P, U, P, P], I),
+        "fp8a_matmul_workspace_size": ([], SZ),
+        "fp8a_matmul": ([P, I64, P, I64, I64, P, I64, I64, I64, I64, I, I, P, P, I64, P, P, U, P, SZ, P], I),
+        "fp8a_terms": ([P, I64, P, I64, I64, P, I64, I64, I64, I, I, P, P, I64, P, P, U, P], I),
+        "fp8a_conv2d_workspace_size": ([I64, I64, I64, I64, I64, I, I, I, I, I, I, I, I, I], SZ),
+        "fp8a_conv2d": ([P, P, P, I64, I64, I64, I64, I64, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P, U, P, SZ, P],
+                        I),
+        "fp8a_im2col": ([P, P, I64, I64, I64, I64, I, I, I, I, I, I, I, I, P], I),
+        "fp8a_fp8_quantize": ([P, I64, I64, P, I, I, I, I, P, P, P, P], I),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def version():
+    return load().fp8a_version().decode()
+
+
+def check(rc, what):
+    """Map a C-ABI return code onto the reference's exception types."""
+    if rc == OK:
+        return
+    msg = f"{what}: {load().fp8a_last_error().decode()}"
+    if rc == EINVAL:
+        raise AssertionError(msg)      # approx_matmul_whole_v9.py:20
+    if rc == EFORMAT:
+        raise ValueError(msg)          # approx_matmul_whole_v9.py:590
+    raise RuntimeError(msg)
+
+
+def stream_ptr(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def dev_ptr(t):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("fp8approx kernels need HIP device tensors (no CPU fallback)")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def host_ptr(t):
+    assert t.device.type == "cpu" and t.is_contiguous()
+    return ctypes.c_void_p(t.data_ptr())

@@ -1,0 +1,163 @@
+"""Drop-in approx operator classes (reference: approx/approx_calculation.py:551-1023).
+
+QCustomBNConv2dTorch, QCustomLinearTorch and QCustomConv2dTorch keep the reference's
+constructor contract (cls(**layer_args, activation=act, **qparams), with qparams carrying
+custom_approx_params and run_method) and its ``run_forward(x, weight, bias, offsets=None)``
+surface.  The arithmetic is one fused HIP launch per layer instead of the reference's
+per-group, per-output-column Python loop (approx_calculation.py:774-799):
+
+  * conv: im2col + approx GEMM + NCHW epilogue (fp8a_conv2d); single-output-channel groups
+    (depthwise) keep the reference's tensor-bias semantics (approx_calculation.py:800-809);
+  * linear: approx GEMM on x @ weight.t() consumed in place (fp8a_matmul).
+
+The behaviour lives in mixins so the same run_forward can sit on the reference's own
+QuantizationHijacker / BNFusedHijacker (see ``bind_operator_classes`` and INTEGRATION.md).
+"""
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from . import _lib
+from .approx_matmul import approx_conv2d, approx_matmul, make_flags
+from .error_tables import get_error_table_NN
+from .quantization.hijacker import QuantizationHijacker
+from .quantization.quantized_folded_bn import BNFusedHijacker
+
+__all__ = ["QCustomBNConv2dTorch", "QCustomLinearTorch", "QCustomConv2dTorch", "ApproxOpMixin",
+           "ApproxConv2dMixin", "ApproxLinearMixin", "ExactConv2dMixin", "bind_operator_classes"]
+
+
+class ApproxOpMixin:
+    """approx_multiply and its configuration plumbing (approx_calculation.py:749-814, 921-999)."""
+
+    def _approx_config(self):
+        p = self.custom_approx_params
+        E, M = p["expo_width"], p["mant_width"]
+        # get_error_table_NN runs first, as in the reference: unsupported formats raise
+        # ValueError even when approx_flag is off (approx_calculation.py:772)
+        table = get_error_table_NN(E, M, withComp=p["withComp"], dnsmp_factor=p["dnsmp_factor"])
+        flags = make_flags(p["with_approx"], p["with_s2nn2s_opt"], p["quant_btw_mult_accu"], p["golden_clip_OF"])
+        return E, M, table, flags
+
+    @staticmethod
+    def _default_bias(b, E, device):
+        # approx_calculation.py:766-767: a missing act/res bias falls back to 2^(E-1)
+        return b if b is not None else torch.tensor([2 ** (E - 1)], dtype=torch.int32, device=device)
+
+    def _qamaa_unsupported(self):
+        raise NotImplementedError("quantize_after_mult_and_add (qamaa) is SURVEY §8(f) next-4; not built yet")
+
+    def approx_multiply(self, x, y, x_bias, y_bias, res_bias):
+        """x [M, K] @ y [K, N] with the operator's approx configuration."""
+        E, M, table, flags = self._approx_config()
+        x_bias = self._default_bias(x_bias, E, x.device)
+        res_bias = self._default_bias(res_bias, E, x.device)
+        if y.shape[1] != 1:
+            if self.approx_flag:
+                return approx_matmul(x, y, E, M, x_bias, y_bias.reshape(-1), res_bias, table, flags=flags)
+            if self.quantize_after_mult_and_add:
+                self._qamaa_unsupported()
+            return x @ y
+        if self.approx_flag:  # single column: biases stay tensors -> tensor-bias semantics (F5)
+            return approx_matmul(x, y, E, M, x_bias, y_bias.reshape(-1), res_bias, table,
+                                 flags=flags | _lib.TB)
+        return x @ y
+
+    def multiply(self, x, y):
+        return torch.matmul(x, y)
+
+
+class ApproxConv2dMixin(ApproxOpMixin):
+    """run_forward of QCustomBNConv2dTorch (approx_calculation.py:822-917)."""
+
+    def im2col(self, input_data, kernel_height, kernel_width, stride, padding, dilation):
+        Bn, C, H, W = input_data.shape
+        Ho = (H + 2 * padding[0] - dilation[0] * (kernel_height - 1) - 1) // stride[0] + 1
+        Wo = (W + 2 * padding[1] - dilation[1] * (kernel_width - 1) - 1) // stride[1] + 1
+        x = input_data.contiguous().float()
+        out = torch.empty((Bn * Ho * Wo, C * kernel_height * kernel_width), dtype=torch.float32, device=x.device)
+        rc = _lib.load().fp8a_im2col(_lib.dev_ptr(x), _lib.dev_ptr(out), Bn, C, H, W, kernel_height, kernel_width,
+                                     stride[0], stride[1], padding[0], padding[1], dilation[0], dilation[1],
+                                     _lib.stream_ptr(x.device))
+        _lib.check(rc, "fp8a_im2col")
+        return out
+
+    def run_forward(self, x, weight, bias, offsets=None):
+        x = x.contiguous()
+        weight = weight.contiguous()
+        w_bias = self.get_weights_fp_bias()
+        a_bias = self.get_acts_fp_bias()
+        r_bias = self.get_res_fp_bias()
+        E, M, table, flags = self._approx_config()
+        if self.approx_flag:
+            if w_bias is None:  # the reference indexes weight_fp_bias[...] (approx_calculation.py:868)
+                raise TypeError("'NoneType' object is not subscriptable")
+            out = approx_conv2d(x.detach(), weight.detach(), E, M, self._default_bias(a_bias, E, x.device),
+                                w_bias.reshape(-1), self._default_bias(r_bias, E, x.device), table, flags=flags,
+                                stride=self.stride, padding=self.padding, dilation=self.dilation, groups=self.groups)
+        else:
+            if self.quantize_after_mult_and_add and self.out_channels // self.groups != 1:
+                self._qamaa_unsupported()
+            out = F.conv2d(x.detach(), weight.detach(), None, self.stride, self.padding, self.dilation, self.groups)
+        if bias is not None:
+            out += bias.view(1, -1, 1, 1)
+        return out
+
+
+class ExactConv2dMixin:
+    """run_forward of QCustomConv2dTorch: exact fp32 product (approx_calculation.py:660-719)."""
+
+    def run_forward(self, x, weight, bias, offsets=None):
+        out = F.conv2d(x.contiguous().detach(), weight.contiguous().detach(), None, self.stride, self.padding,
+                       self.dilation, self.groups)
+        if bias is not None:
+            out += bias.view(1, -1, 1, 1)
+        return out
+
+
+class ApproxLinearMixin(ApproxOpMixin):
+    """run_forward of QCustomLinearTorch (approx_calculation.py:1007-1023).
+
+    Like the reference, only 2-D inputs are accepted (a 3-D [B, T, K] input fails the
+    A.shape[1] == B.shape[0] assertion); set ``flatten_leading_dims = True`` on
+    the class or instance for the extension that folds leading dims into rows (ViT linears).
+    """
+    flatten_leading_dims = False
+
+    def run_forward(self, x, weight, bias, offsets=None):
+        x = x.contiguous()
+        weight = weight.contiguous()
+        lead = None
+        if x.dim() != 2:
+            if not self.flatten_leading_dims:
+                raise AssertionError(f"approx linear expects a 2-D input, got {tuple(x.shape)} (SURVEY F4)")
+            lead = x.shape[:-1]
+            x = x.reshape(-1, x.shape[-1])
+        out = self.approx_multiply(x.detach(), weight.detach().t(), self.get_acts_fp_bias(),
+                                   self.get_weights_fp_bias(), self.get_res_fp_bias())
+        if bias is not None:
+            out += bias
+        if lead is not None:
+            out = out.reshape(*lead, out.shape[-1])
+        return out
+
+
+def bind_operator_classes(hijacker_cls=QuantizationHijacker, bnfused_cls=BNFusedHijacker):
+    """Build the three operator classes on top of any hijacker implementation exposing the
+    reference surface (get_*_fp_bias, approx_flag, custom_approx_params, ...)."""
+    bn_conv = type("QCustomBNConv2dTorch", (ApproxConv2dMixin, bnfused_cls, nn.Conv2d), {})
+    linear = type("QCustomLinearTorch", (ApproxLinearMixin, hijacker_cls, nn.Linear), {})
+    conv = type("QCustomConv2dTorch", (ExactConv2dMixin, hijacker_cls, nn.Conv2d), {})
+    return bn_conv, linear, conv
+
+
+class QCustomBNConv2dTorch(ApproxConv2dMixin, BNFusedHijacker, nn.Conv2d):
+    pass
+
+
+class QCustomLinearTorch(ApproxLinearMixin, QuantizationHijacker, nn.Linear):
+    pass
+
+
+class QCustomConv2dTorch(ExactConv2dMixin, QuantizationHijacker, nn.Conv2d):
+    pass

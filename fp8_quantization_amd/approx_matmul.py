@@ -1,0 +1,271 @@
+"""Host side of the approx_v9 hot path: torch custom ops over the gfx950 C-ABI.
+
+Mirrors the reference module approx/approx_matmul_whole_v9.py (revollllt/FP8_quantization
+@ 2024-11-08): ``custom_matmul_vectorize`` keeps its signature and argument meaning
+(v9:10-18), ``quant_to_fp_any_vectorize_torch`` (v9:333) and ``float_to_fpany_absint_torch``
+(v9:233, here taking (E, M, bias) instead of a param dict) are the element codecs,
+``get_error_table_NN`` the table selection (v9:555).  All arithmetic runs in
+libfp8approx.so; these wrappers only marshal pointers, biases and flags.
+
+Bias typing follows the reference: Python ints select the int-bias semantics, int tensors the
+tensor-bias semantics (quirk F5 -- param_prepare's integer powers flush min_norm to 0), which
+is what approx_multiply passes for single-column products (approx_calculation.py:800-809).
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from .error_tables import get_error_table_NN  # noqa: F401  (re-exported, v9:555)
+
+__all__ = ["custom_matmul_vectorize", "approx_matmul", "approx_terms", "approx_conv2d",
+           "quant_to_fp_any_vectorize_torch", "float_to_fpany_absint_torch", "get_error_table_NN",
+           "make_flags", "fp8_fake_quantize"]
+
+
+def make_flags(with_approx=True, with_s2nn2s_opt=False, quant_btw_mult_accu=True, golden_clip_OF=False,
+               tensor_bias=False):
+    return ((_lib.APPROX if with_approx else 0) | (_lib.S2N if with_s2nn2s_opt else 0) |
+            (_lib.QBMA if quant_btw_mult_accu else 0) | (_lib.GCLIP if golden_clip_OF else 0) |
+            (_lib.TB if tensor_bias else 0))
+
+
+_BIAS_CACHE = {}
+
+
+def _bias_dev(b, device, n=None):
+    """Device int32 bias vector from an int or a (float/int) tensor; no host sync for tensors."""
+    if isinstance(b, torch.Tensor):
+        t = b.detach().reshape(-1)
+        if t.device != device:
+            t = t.to(device)
+        if t.dtype != torch.int32:
+            t = t.to(torch.int32)  # float biases are torch.round() outputs: exact
+        return t.contiguous()
+    key = (device, int(b))
+    t = _BIAS_CACHE.get(key)
+    if t is None:
+        t = torch.tensor([int(b)], dtype=torch.int32, device=device)
+        _BIAS_CACHE[key] = t
+    return t
+
+
+def _table_host(error_table_NN, mant_width, with_approx):
+    n = 2 ** mant_width
+    if error_table_NN is None or not with_approx:
+        return torch.zeros((n, n), dtype=torch.int32)
+    t = error_table_NN.detach()
+    if t.device.type != "cpu" or t.dtype != torch.int32 or not t.is_contiguous():
+        t = t.to(device="cpu", dtype=torch.int32).contiguous()  # host table: packed into kernargs
+    if t.shape != (n, n):
+        raise AssertionError(f"error table must be {n}x{n}, got {tuple(t.shape)}")
+    return t
+
+
+def _workspace(device, nbytes):
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+def _as_f32(x):
+    if x.dtype != torch.float32:
+        x = x.float()
+    return x
+
+
+# ----------------------------------------------------------------------------------- matmul
+@torch.library.custom_op("fp8approx::matmul", mutates_args=())
+def _matmul_op(A: torch.Tensor, B: torch.Tensor, bA: torch.Tensor, bB: torch.Tensor, bR: torch.Tensor,
+               table: torch.Tensor, E: int, M: int, flags: int) -> torch.Tensor:
+    L = _lib.load()
+    dev = A.device
+    if not A.is_contiguous() and A.stride(1) != 1:
+        A = A.contiguous()
+    Mr, K = A.shape
+    N = B.shape[1]
+    C = torch.empty((Mr, N), dtype=torch.float32, device=dev)
+    ws = _workspace(dev, L.fp8a_matmul_workspace_size())
+    bBs = 0 if bB.numel() == 1 else 1
+    rc = L.fp8a_matmul(_lib.dev_ptr(A), A.stride(0), _lib.dev_ptr(B), B.stride(0), B.stride(1),
+                       _lib.dev_ptr(C), N, Mr, N, K, E, M, _lib.dev_ptr(bA), _lib.dev_ptr(bB), bBs,
+                       _lib.dev_ptr(bR), _lib.host_ptr(table), flags, _lib.dev_ptr(ws), ws.numel(),
+                       _lib.stream_ptr(dev))
+    _lib.check(rc, "fp8a_matmul")
+    return C
+
+
+@_matmul_op.register_fake
+def _(A, B, bA, bB, bR, table, E, M, flags):
+    return A.new_empty((A.shape[0], B.shape[1]), dtype=torch.float32)
+
+
+def approx_matmul(A, B, E, M, bA, bB, bR, table=None, flags=None, **flag_kwargs):
+    """C[m, n] = sum_k approx_v9 term(A[m, k], B[k, n]) on the GPU.
+
+    A [M, K] and B [K, N] float32 device tensors (any strides with a unit stride dimension;
+    weight.t() views are consumed in place).  bB: int, 1-element or per-column [N] tensor.
+    """
+    if A.dim() != 2 or B.dim() != 2 or A.shape[1] != B.shape[0]:
+        raise AssertionError(f"approx_matmul: shape mismatch {tuple(A.shape)} @ {tuple(B.shape)}")  # v9:20
+    if flags is None:
+        flags = make_flags(**flag_kwargs)
+    A, B = _as_f32(A), _as_f32(B)
+    if B.stride(0) != 1 and B.stride(1) != 1:
+        B = B.contiguous()
+    dev = A.device
+    tab = _table_host(table, M, bool(flags & _lib.APPROX))
+    return _matmul_op(A, B, _bias_dev(bA, dev), _bias_dev(bB, dev), _bias_dev(bR, dev), tab, int(E), int(M),
+                      int(flags))
+
+
+def approx_terms(A, B, E, M, bA, bB, bR, table=None, flags=None, **flag_kwargs):
+    """Per-product terms T[m, k, n] (the values the reference sums at v9:113); parity tool."""
+    if A.shape[1] != B.shape[0]:
+        raise AssertionError("approx_terms: inner dimensions differ")
+    if flags is None:
+        flags = make_flags(**flag_kwargs)
+    L = _lib.load()
+    A, B = _as_f32(A), _as_f32(B)
+    dev = A.device
+    Mr, K = A.shape
+    N = B.shape[1]
+    T = torch.empty((Mr, K, N), dtype=torch.float32, device=dev)
+    bA_, bB_, bR_ = _bias_dev(bA, dev), _bias_dev(bB, dev), _bias_dev(bR, dev)
+    tab = _table_host(table, M, bool(flags & _lib.APPROX))
+    rc = L.fp8a_terms(_lib.dev_ptr(A), A.stride(0), _lib.dev_ptr(B), B.stride(0), B.stride(1), _lib.dev_ptr(T),
+                      Mr, N, K, int(E), int(M), _lib.dev_ptr(bA_), _lib.dev_ptr(bB_), 0 if bB_.numel() == 1 else 1,
+                      _lib.dev_ptr(bR_), _lib.host_ptr(tab), int(flags), _lib.stream_ptr(dev))
+    _lib.check(rc, "fp8a_terms")
+    return T
+
+
+def custom_matmul_vectorize(A, B, expo_width, mant_width, custom_bias_A, custom_bias_B, custom_bias_R,
+                            error_table_NN, with_approx=True, with_s2nn2s_opt=False, sim_hw_add_OFUF=False,
+                            with_OF_opt=False, with_UF_opt=False, golden_clip_OF=False, quant_btw_mult_accu=True,
+                            debug_mode=False, self_check_mode=False):
+    """Drop-in for approx_matmul_whole_v9.custom_matmul_vectorize (v9:10-169).
+
+    sim_hw_add_OFUF / with_OF_opt / with_UF_opt are accepted and ignored, as in v9.
+    """
+    assert A.shape[1] == B.shape[0]
+    tb = [isinstance(b, torch.Tensor) for b in (custom_bias_A, custom_bias_B, custom_bias_R)]
+    if any(tb) and not all(tb):
+        raise NotImplementedError("mixed int / tensor biases: pass all three the same way")
+    flags = make_flags(with_approx, with_s2nn2s_opt, quant_btw_mult_accu, golden_clip_OF, tensor_bias=all(tb))
+    out = approx_matmul(A, B, expo_width, mant_width, custom_bias_A, custom_bias_B, custom_bias_R,
+                        error_table_NN, flags=flags)
+    if self_check_mode:
+        golden = quant_to_fp_any_vectorize_torch(A.unsqueeze(2) * B.unsqueeze(0), expo_width, mant_width,
+                                                 custom_bias_R, clip_OF=golden_clip_OF) \
+            if quant_btw_mult_accu else A.unsqueeze(2) * B.unsqueeze(0)
+        err = (golden.sum(dim=1) - out).abs()
+        print("\n====== Self-Checking Mode ======")
+        print(f"MatMul Max  Error     : {err.max()}")
+        print(f"MatMul Mean Error     : {err.mean()}")
+        print(f"MatMul RMSE           : {torch.sqrt(torch.mean(err ** 2))}")
+    return out
+
+
+# ----------------------------------------------------------------------------------- codecs
+def _codec_bias(custom_bias, device):
+    if custom_bias is None:
+        raise NotImplementedError("pass the bias explicitly")
+    return _bias_dev(custom_bias, device), isinstance(custom_bias, torch.Tensor)
+
+
+def quant_to_fp_any_vectorize_torch(arr, expo_width, mant_width, custom_bias=None, clip_OF=True):
+    """Q_R (v9:333-362) on the GPU.  custom_bias None means the IEEE-style default 2^(E-1)-1."""
+    if custom_bias is None:
+        custom_bias = 2 ** (expo_width - 1) - 1
+    L = _lib.load()
+    x = _as_f32(arr).contiguous()
+    b, tb = _codec_bias(custom_bias, x.device)
+    out = torch.empty_like(x)
+    rc = L.fp8a_quant(_lib.dev_ptr(x), x.numel(), int(expo_width), int(mant_width), _lib.dev_ptr(b),
+                      make_flags(False, False, False, clip_OF, tb), _lib.dev_ptr(out), _lib.stream_ptr(x.device))
+    _lib.check(rc, "fp8a_quant")
+    return out
+
+
+def float_to_fpany_absint_torch(values, expo_width, mant_width, custom_bias, clip_OF=False):
+    """DEC (v9:233-291): returns (expo, mant) int32 tensors shaped like values."""
+    L = _lib.load()
+    x = _as_f32(values).contiguous()
+    b, tb = _codec_bias(custom_bias, x.device)
+    e = torch.empty(x.shape, dtype=torch.int32, device=x.device)
+    m = torch.empty_like(e)
+    rc = L.fp8a_decompose(_lib.dev_ptr(x), 1, x.numel(), x.numel(), int(expo_width), int(mant_width),
+                          _lib.dev_ptr(b), 0, make_flags(False, False, False, clip_OF, tb), _lib.dev_ptr(e),
+                          _lib.dev_ptr(m), _lib.stream_ptr(x.device))
+    _lib.check(rc, "fp8a_decompose")
+    return e, m
+
+
+# ----------------------------------------------------------------------------------- conv
+@torch.library.custom_op("fp8approx::conv2d", mutates_args=())
+def _conv2d_op(x: torch.Tensor, w: torch.Tensor, bA: torch.Tensor, bW: torch.Tensor, bR: torch.Tensor,
+               table: torch.Tensor, E: int, M: int, flags: int, stride: list[int], padding: list[int],
+               dilation: list[int], groups: int) -> torch.Tensor:
+    L = _lib.load()
+    x = x.contiguous()
+    w = w.contiguous()
+    Bn, Cin, H, W = x.shape
+    Cout, _, kh, kw = w.shape
+    sh, sw = stride
+    ph, pw = padding
+    dh, dw = dilation
+    Ho = (H + 2 * ph - dh * (kh - 1) - 1) // sh + 1
+    Wo = (W + 2 * pw - dw * (kw - 1) - 1) // sw + 1
+    y = torch.empty((Bn, Cout, Ho, Wo), dtype=torch.float32, device=x.device)
+    nbytes = L.fp8a_conv2d_workspace_size(Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups)
+    ws = _workspace(x.device, nbytes)
+    rc = L.fp8a_conv2d(_lib.dev_ptr(x), _lib.dev_ptr(w), _lib.dev_ptr(y), Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph,
+                       pw, dh, dw, groups, E, M, _lib.dev_ptr(bA), _lib.dev_ptr(bW), _lib.dev_ptr(bR),
+                       _lib.host_ptr(table), flags, _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(x.device))
+    _lib.check(rc, "fp8a_conv2d")
+    return y
+
+
+@_conv2d_op.register_fake
+def _(x, w, bA, bW, bR, table, E, M, flags, stride, padding, dilation, groups):
+    Bn, _, H, W = x.shape
+    Cout, _, kh, kw = w.shape
+    Ho = (H + 2 * padding[0] - dilation[0] * (kh - 1) - 1) // stride[0] + 1
+    Wo = (W + 2 * padding[1] - dilation[1] * (kw - 1) - 1) // stride[1] + 1
+    return x.new_empty((Bn, Cout, Ho, Wo))
+
+
+def approx_conv2d(x, w, E, M, bA, bW, bR, table=None, flags=None, stride=(1, 1), padding=(0, 0), dilation=(1, 1),
+                  groups=1, **flag_kwargs):
+    """approx_v9 convolution, NCHW in / NCHW out (pre-BN), K ordered (c, ky, kx) like the
+    reference im2col (approx_calculation.py:724-747); single-output-channel groups get the
+    tensor-bias semantics (approx_calculation.py:800-809).  bW: per output channel."""
+    if flags is None:
+        flags = make_flags(**flag_kwargs)
+    flags &= ~_lib.TB
+    dev = x.device
+    tab = _table_host(table, M, bool(flags & _lib.APPROX))
+    return _conv2d_op(_as_f32(x), _as_f32(w), _bias_dev(bA, dev), _bias_dev(bW, dev), _bias_dev(bR, dev), tab,
+                      int(E), int(M), int(flags), [int(s) for s in stride], [int(p) for p in padding],
+                      [int(d) for d in dilation], int(groups))
+
+
+# ----------------------------------------------------------------------------------- FP8 fake quant
+def fp8_fake_quantize(x, maxval, n_bits, mantissa_bits, sign_bits=1, per_row=False):
+    """quantize_to_fp8_ste_MM forward (fp8_quantizer.py:97-173): returns (values, float bias).
+
+    The bias has the reference's shape: [1] per tensor, [C, 1, ..., 1] per channel."""
+    L = _lib.load()
+    x = _as_f32(x).contiguous()
+    mx = _as_f32(maxval).reshape(-1).contiguous()
+    if mx.device != x.device:
+        mx = mx.to(x.device)
+    rows = mx.numel() if per_row else 1
+    out = torch.empty_like(x)
+    bias = torch.empty(rows, dtype=torch.float32, device=x.device)
+    rc = L.fp8a_fp8_quantize(_lib.dev_ptr(x), rows, x.numel() // rows, _lib.dev_ptr(mx), int(per_row), int(n_bits),
+                             int(mantissa_bits), int(sign_bits), _lib.dev_ptr(out), _lib.dev_ptr(bias), None,
+                             _lib.stream_ptr(x.device))
+    _lib.check(rc, "fp8a_fp8_quantize")
+    if per_row and rows > 1:
+        bias = bias.view([-1] + [1] * (x.dim() - 1))
+    return out, bias

@@ -1,0 +1,660 @@
+// fp8approx.hip -- MI355X (gfx950) kernels and C-ABI of the approx-FP8 matmul/conv engine.
+//
+// Hot path: approx_v9 (revollllt/FP8_quantization, approx/approx_matmul_whole_v9.py:10-169)
+// as a register-blocked VALU GEMM.  The approximate product cannot use MFMA (its mantissa
+// product depends on a per-pair error table and a per-product re-quantisation), so the kernel
+// is VALU-bound: 128x64 output tile per 256-thread workgroup, 8x4 outputs per thread, K staged
+// through LDS 16 deep.  Operands are decoded (sign / exponent / mantissa / table row) ONCE per
+// workgroup while staging; the inner loop costs ~10 VALU ops per product (14 with an error
+// table).  See DESIGN.md for the derivation and the exactness argument.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <string>
+
+#include "../../include/fp8approx.h"
+#include "fp8approx_device.h"
+
+namespace fp8a {
+
+// ------------------------------------------------------------------------- error handling
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+static int hip_check(const char *what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(FP8A_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+    return FP8A_OK;
+}
+
+// ------------------------------------------------------------------------- table packing
+// The error table (get_error_table_NN, v9:555-592) is a host constant; it is analysed on the
+// host and packed into the launch arguments so the hot loop reads one register per operand:
+//   TM_W1U  : entries in {0,1}   -> 1 bit / entry, 2^M bits per row      (E4M3)
+//   TM_W2S/U: entries in [-2,1] / [0,3] -> 2 bits / entry, R = 2^M*2/32 words per row
+//   TM_LUT  : anything else -> float LUT in LDS (E2M5 no-comp: entries up to 5)
+enum TMode : int { TM_NONE = 0, TM_W1U = 1, TM_W2S1 = 2, TM_W2U1 = 3, TM_W2S2 = 4, TM_W2U2 = 5, TM_LUT = 6 };
+
+struct TablePack {
+    uint32_t rows[64][2];  // packed rows for the bit modes (2^M <= 64)
+    int8_t raw[1024];      // the full table (2^M x 2^M), row-major; exact path and LUT mode
+};
+
+static int pack_table(const int32_t *table, int M, bool approx, TablePack &tp, int &mode) {
+    memset(&tp, 0, sizeof(tp));
+    mode = TM_NONE;
+    if (!approx || table == nullptr) return FP8A_OK;
+    const int n = 1 << M;
+    if (n * n > 1024) return fail(FP8A_EFORMAT, "error table larger than 32x32 (mant_width > 5)");
+    int lo = 0, hi = 0;
+    for (int i = 0; i < n * n; ++i) {
+        if (table[i] < -128 || table[i] > 127) return fail(FP8A_EINVAL, "error table entry out of int8 range");
+        tp.raw[i] = (int8_t)table[i];
+        lo = std::min(lo, table[i]);
+        hi = std::max(hi, table[i]);
+    }
+    if (lo == 0 && hi == 0) return FP8A_OK;
+    const int words2 = (n * 2 + 31) / 32;
+    if (lo >= 0 && hi <= 1 && n <= 32) {
+        mode = TM_W1U;
+        for (int i = 0; i < n; ++i)
+            for (int j = 0; j < n; ++j)
+                if (table[i * n + j]) tp.rows[i][0] |= 1u << j;
+    } else if (lo >= -2 && hi <= 1 && words2 <= 2) {
+        mode = words2 == 1 ? TM_W2S1 : TM_W2S2;
+    } else if (lo >= 0 && hi <= 3 && words2 <= 2) {
+        mode = words2 == 1 ? TM_W2U1 : TM_W2U2;
+    } else {
+        mode = TM_LUT;
+    }
+    if (mode >= TM_W2S1 && mode <= TM_W2U2) {
+        for (int i = 0; i < n; ++i)
+            for (int j = 0; j < n; ++j) {
+                const uint32_t code = (uint32_t)table[i * n + j] & 3u;
+                const int bit = j * 2;
+                tp.rows[i][bit >> 5] |= code << (bit & 31);
+            }
+    }
+    return FP8A_OK;
+}
+
+// ------------------------------------------------------------------------- GEMM arguments
+struct GemmArgs {
+    const float *A;
+    int64_t lda;
+    const float *B;
+    int64_t sbk, sbn;
+    float *C;
+    int64_t ldc;
+    int64_t M, N, K;
+    int E, Mw;
+    const int32_t *bA;
+    const int32_t *bB;
+    int64_t bBs;
+    const int32_t *bR;
+    uint32_t flags;
+    // output mapping: rowmajor C[m*ldc + n], or NCHW C[(m/hw)*ctot*hw + (coff+n)*hw + m%hw]
+    int nchw;
+    int64_t hw, ctot, coff;
+    uint32_t *flag;  // device word: set by the fast kernel when the exact kernel must run
+    TablePack tab;
+};
+
+constexpr int BM = 64, BN = 64, BK = 16, TM = 4, TN = 4, NT = 256;
+constexpr int AP = BM + 4, BP = BN + 4;
+
+__device__ __forceinline__ int64_t out_index(const GemmArgs &p, int64_t m, int64_t n) {
+    if (!p.nchw) return m * p.ldc + n;
+    const int64_t img = m / p.hw, pix = m - img * p.hw;
+    return (img * p.ctot + p.coff + n) * p.hw + pix;
+}
+
+// Fast-path operand decode straight from the float32 bit pattern (int-bias semantics).
+//   returns ok: x is exactly a value of the (M, b) grid (any exponent: A/B are decoded with
+//               clip_OF=False, v9:58-59) and |x| is 0 or in [2^-40, 2^40] (exactness window,
+//               DESIGN.md §3).  Otherwise the launch is flagged and the exact kernel reruns it.
+//   m        : the M-bit mantissa code = the top M bits of the fp32 mantissa (the s2n scale-up
+//               by 2^M, v9:53, leaves the fp32 mantissa untouched)
+//   c        : sign(x) * 2^floor(log2|x|): the scale of the error-table term.  Scale-up and
+//               scale-back of s2n cancel in it; without s2n a subnormal operand fails the
+//               reference's norm mask (v9:87), so c = 0 there, as for zeros.
+__device__ __forceinline__ bool stage_decode(float x, int M, uint32_t emn, bool s2n, float &c, uint32_t &m) {
+    const uint32_t u = __float_as_uint(x);
+    const uint32_t ua = u & 0x7FFFFFFFu;
+    const uint32_t ex = ua & 0x7F800000u;
+    const bool sub = ua < emn;  // |x| < min_norm = 2^(1-b)
+    const uint32_t sh = (uint32_t)(23 - M) + (sub ? ((emn - ex) >> 23) : 0u);
+    const bool grid = (sh < 24u) ? ((ua & ((1u << sh) - 1u)) == 0u) : (ua == 0u);
+    const bool win = (ua == 0u) || (ua >= 0x2B800000u /*2^-40*/ && ua <= 0x53800000u /*2^40*/);
+    m = (ua >> (23 - M)) & ((1u << M) - 1u);
+    c = (ua == 0u || (!s2n && sub)) ? 0.0f : __uint_as_float(u & 0xFF800000u);
+    return grid && win;
+}
+
+template <bool S2N, bool QBMA, bool GCLIP, int TMODE>
+__global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
+    constexpr bool TBL = TMODE != TM_NONE;
+    constexpr int R = (TMODE == TM_W2S2 || TMODE == TM_W2U2) ? 2 : 1;
+    constexpr bool SGN = (TMODE == TM_W2S1 || TMODE == TM_W2S2 || TMODE == TM_LUT);
+
+    __shared__ __attribute__((aligned(16))) float sA[BK][AP];
+    __shared__ __attribute__((aligned(16))) float sB[BK][BP];
+    __shared__ __attribute__((aligned(16))) float sAc[TBL ? BK : 1][AP];
+    __shared__ __attribute__((aligned(16))) uint32_t sAr[TBL ? R * BK : 1][AP];
+    __shared__ __attribute__((aligned(16))) float sBc[TBL ? BK : 1][BP];
+    __shared__ __attribute__((aligned(16))) uint32_t sBm[TBL ? BK : 1][BP];
+    __shared__ float sLut[TMODE == TM_LUT ? 1024 : 1];
+    __shared__ uint32_t sRows[TBL ? 64 * 2 : 1];
+
+    const int tid = threadIdx.x;
+    const int ty = tid >> 4, tx = tid & 15;
+    const int64_t num_mt = (p.M + BM - 1) / BM;
+    const int64_t bid = blockIdx.x;
+    const int64_t m0 = (bid % num_mt) * BM;   // consecutive blocks: same column tile, so the
+    const int64_t n0 = (bid / num_mt) * BN;   // B tile is shared by the 8 XCDs' L2s
+    const int M = p.Mw;
+    const int bA = *p.bA, bR = *p.bR;
+    const QC qc = make_qc(p.E, M, bR);
+    const uint32_t emnA = (uint32_t)(128 - bA) << 23;
+    const float ulpM = p2(-M);
+
+    if (TBL) {
+        const int n = 1 << M;
+        for (int i = tid; i < n * 2; i += NT) sRows[i] = p.tab.rows[i >> 1][i & 1];
+        if (TMODE == TM_LUT)
+            for (int i = tid; i < n * n; i += NT) sLut[i] = (float)p.tab.raw[i];
+        __syncthreads();
+    }
+
+    // B staging map: n-contiguous B reads along n, k-contiguous (W[N][K]) along k
+    const bool b_ncontig = (p.sbn == 1);
+    int bcol[4], bkk[4];
+    uint32_t emnB[4];
+    bool bias_ok = bR >= -40 && bR <= 80 && bA >= -100 && bA <= 100;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int e = tid + NT * r;
+        bcol[r] = b_ncontig ? (e & 63) : (e >> 4);
+        bkk[r] = b_ncontig ? (e >> 6) : (e & 15);
+        const int64_t n = n0 + bcol[r];
+        const int bb = (n < p.N) ? p.bB[n * p.bBs] : 0;
+        bias_ok = bias_ok && bb >= -100 && bb <= 100;
+        emnB[r] = (uint32_t)(128 - bb) << 23;
+    }
+
+    float acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = 0.0f;
+
+    for (int64_t k0 = 0; k0 < p.K; k0 += BK) {
+        bool bad = !bias_ok;
+        // ---- stage A (64 x 16): element e = tid + 256 r -> (row e>>4, kk e&15), k-contiguous
+#pragma unroll
+        for (int r = 0; r < (BM * BK) / NT; ++r) {
+            const int e = tid + NT * r;
+            const int row = e >> 4, kk = e & 15;
+            const int64_t m = m0 + row, k = k0 + kk;
+            const float x = (m < p.M && k < p.K) ? p.A[m * p.lda + k] : 0.0f;
+            float c;
+            uint32_t mc;
+            bad |= !stage_decode(x, M, emnA, S2N, c, mc);
+            sA[kk][row] = x;
+            if (TBL) {
+                sAc[kk][row] = c * ulpM;  // the 2^-M of mult_result_mant's table term (v9:182)
+                if (TMODE == TM_LUT) {
+                    sAr[kk][row] = mc << M;
+                } else {
+                    sAr[kk][row] = sRows[mc * 2];
+                    if (R == 2) sAr[BK + kk][row] = sRows[mc * 2 + 1];
+                }
+            }
+        }
+        // ---- stage B (16 x 64)
+#pragma unroll
+        for (int r = 0; r < (BN * BK) / NT; ++r) {
+            const int col = bcol[r], kk = bkk[r];
+            const int64_t n = n0 + col, k = k0 + kk;
+            const float x = (n < p.N && k < p.K) ? p.B[k * p.sbk + n * p.sbn] : 0.0f;
+            float c;
+            uint32_t mc;
+            bad |= !stage_decode(x, M, emnB[r], S2N, c, mc);
+            sB[kk][col] = x;
+            if (TBL) {
+                sBc[kk][col] = c;
+                sBm[kk][col] = (TMODE == TM_LUT || TMODE == TM_W1U) ? mc : mc * 2u;
+            }
+        }
+        // Off-grid operands / biases outside the exact window: flag the launch; the gated
+        // exact kernel that follows on the stream then recomputes the whole product.
+        const int anybad = __syncthreads_or(bad ? 1 : 0);
+        if (anybad && tid == 0) atomicOr(p.flag, 1u);
+
+        float tacc[TM][TN];  // per-k-tile partial sums (two-level accumulation)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) tacc[i][j] = 0.0f;
+
+#pragma unroll 2
+        for (int kk = 0; kk < BK; ++kk) {
+            const float4 a4 = *reinterpret_cast<const float4 *>(&sA[kk][ty * TM]);
+            const float4 b4 = *reinterpret_cast<const float4 *>(&sB[kk][tx * TN]);
+            const float a[TM] = {a4.x, a4.y, a4.z, a4.w};
+            const float b[TN] = {b4.x, b4.y, b4.z, b4.w};
+            if (!TBL) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        const float g = a[i] * b[j];
+                        tacc[i][j] += QBMA ? q_fast<GCLIP>(g, qc) : g;
+                    }
+            } else {
+                const float4 ac4 = *reinterpret_cast<const float4 *>(&sAc[kk][ty * TM]);
+                const uint4 ar4 = *reinterpret_cast<const uint4 *>(&sAr[kk][ty * TM]);
+                const uint4 ar4h = (R == 2) ? *reinterpret_cast<const uint4 *>(&sAr[BK + kk][ty * TM]) : make_uint4(0, 0, 0, 0);
+                const float4 bc4 = *reinterpret_cast<const float4 *>(&sBc[kk][tx * TN]);
+                const uint4 bm4 = *reinterpret_cast<const uint4 *>(&sBm[kk][tx * TN]);
+                const float ac[TM] = {ac4.x, ac4.y, ac4.z, ac4.w};
+                const uint32_t ar0[TM] = {ar4.x, ar4.y, ar4.z, ar4.w};
+                const uint32_t ar1[TM] = {ar4h.x, ar4h.y, ar4h.z, ar4h.w};
+                const float bc[TN] = {bc4.x, bc4.y, bc4.z, bc4.w};
+                const uint32_t bm[TN] = {bm4.x, bm4.y, bm4.z, bm4.w};
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        const float g = a[i] * b[j];
+                        const float cab = ac[i] * bc[j];
+                        float v0;
+                        if (TMODE == TM_W1U) {
+                            const int t = __builtin_amdgcn_sbfe((int)ar0[i], bm[j], 1);
+                            v0 = g - __uint_as_float(__float_as_uint(cab) & (uint32_t)t);
+                        } else if (TMODE == TM_LUT) {
+                            const float t = sLut[ar0[i] + bm[j]];
+                            v0 = __fmaf_rn(-t, cab, g);
+                        } else {
+                            const uint32_t w = (R == 2 && (bm[j] & 32u)) ? ar1[i] : ar0[i];
+                            const int t = SGN ? __builtin_amdgcn_sbfe((int)w, bm[j], 2)
+                                              : (int)__builtin_amdgcn_ubfe(w, bm[j], 2);
+                            v0 = __fmaf_rn(-(float)t, cab, g);
+                        }
+                        if (!S2N) v0 = (fabsf(g) >= qc.mnR) ? v0 : g;  // norm mask, v9:87
+                        if (S2N && QBMA && SGN) v0 = (g < 0.0f && g >= -qc.thr) ? fabsf(v0) : v0;  // F7
+                        tacc[i][j] += QBMA ? q_fast<GCLIP>(v0, qc) : v0;
+                    }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] += tacc[i][j];
+        __syncthreads();
+    }
+
+    // ---- epilogue
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int64_t m = m0 + ty * TM + i;
+        if (m >= p.M) continue;
+        const int64_t nb = n0 + tx * TN;
+        if (!p.nchw && nb + TN <= p.N && ((p.ldc & 3) == 0) && ((((uintptr_t)p.C) & 15) == 0)) {
+            *reinterpret_cast<float4 *>(&p.C[m * p.ldc + nb]) = make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                if (nb + j < p.N) p.C[out_index(p, m, nb + j)] = acc[i][j];
+        }
+    }
+}
+
+// Exact (reference-order) kernel: one thread per output (m, n), every term via exact_term.
+// Used for the tensor-bias (single-column) semantics and as the reference-path check.
+__global__ __launch_bounds__(256) void gemm_exact_kernel(const GemmArgs p) {
+    // Gate: after a fast launch, run only if it flagged off-grid operands (uniform per grid).
+    if (p.flag != nullptr && __hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= p.M * p.N) return;
+    const int64_t m = idx % p.M, n = idx / p.M;
+    const bool tb = p.flags & F_TB;
+    const DFmt fA = dfmt(p.E, p.Mw, *p.bA, tb), fR = dfmt(p.E, p.Mw, *p.bR, tb);
+    const DFmt fB = dfmt(p.E, p.Mw, p.bB[n * p.bBs], tb);
+    float s = 0.0f, part = 0.0f;
+    for (int64_t k = 0; k < p.K; ++k) {
+        part += exact_term(p.A[m * p.lda + k], p.B[k * p.sbk + n * p.sbn], fA, fB, fR, p.tab.raw, p.flags);
+        if ((k & 15) == 15) {
+            s += part;
+            part = 0.0f;
+        }
+    }
+    s += part;
+    p.C[out_index(p, m, n)] = s;
+}
+
+__global__ __launch_bounds__(256) void terms_kernel(const GemmArgs p, float *T) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= p.M * p.K * p.N) return;
+    const int64_t n = idx % p.N, k = (idx / p.N) % p.K, m = idx / (p.N * p.K);
+    const bool tb = p.flags & F_TB;
+    const DFmt fA = dfmt(p.E, p.Mw, *p.bA, tb), fR = dfmt(p.E, p.Mw, *p.bR, tb);
+    const DFmt fB = dfmt(p.E, p.Mw, p.bB[n * p.bBs], tb);
+    T[idx] = exact_term(p.A[m * p.lda + k], p.B[k * p.sbk + n * p.sbn], fA, fB, fR, p.tab.raw, p.flags);
+}
+
+__global__ __launch_bounds__(256) void decompose_kernel(const float *x, int64_t rows, int64_t cols, int64_t ld,
+                                                        int E, int M, const int32_t *bias, int64_t bs,
+                                                        uint32_t flags, int32_t *expo, int32_t *mant) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= rows * cols) return;
+    const int64_t r = idx / cols, c = idx - r * cols;
+    const DFmt f = dfmt(E, M, bias[r * bs], flags & F_TB);
+    int e, m;
+    exact_dec(x[r * ld + c], f, flags & F_GCLIP, e, m);
+    expo[idx] = e;
+    mant[idx] = m;
+}
+
+__global__ __launch_bounds__(256) void quant_kernel(const float *x, int64_t n, int E, int M, const int32_t *bias,
+                                                    uint32_t flags, float *out) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= n) return;
+    const DFmt f = dfmt(E, M, *bias, flags & F_TB);
+    out[idx] = exact_q(x[idx], f, flags & F_GCLIP);
+}
+
+// im2col, K ordered (c, ky, kx) like approx_calculation.py:738-745.
+__global__ __launch_bounds__(256) void im2col_kernel(const float *x, float *out, int64_t Bn, int64_t C, int64_t H,
+                                                     int64_t W, int kh, int kw, int sh, int sw, int ph, int pw,
+                                                     int dh, int dw, int64_t Ho, int64_t Wo) {
+    const int64_t K = C * kh * kw;
+    const int64_t total = Bn * Ho * Wo * K;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = idx % K, m = idx / K;
+        const int64_t kx = k % kw, ky = (k / kw) % kh, c = k / (kw * kh);
+        const int64_t wo = m % Wo, ho = (m / Wo) % Ho, b = m / (Wo * Ho);
+        const int64_t hi = ho * sh - ph + ky * dh, wi = wo * sw - pw + kx * dw;
+        float v = 0.0f;
+        if (hi >= 0 && hi < H && wi >= 0 && wi < W) v = x[((b * C + c) * H + hi) * W + wi];
+        out[idx] = v;
+    }
+}
+
+// Single-output-channel groups (depthwise): tensor-bias semantics, direct from NCHW x.
+__global__ __launch_bounds__(256) void conv_tb_direct_kernel(const float *x, const float *w, float *y, int64_t Bn,
+                                                             int64_t Cin, int64_t H, int64_t W, int64_t Cout,
+                                                             int kh, int kw, int sh, int sw, int ph, int pw, int dh,
+                                                             int dw, int groups, int64_t Ho, int64_t Wo, int E,
+                                                             int Mw, const int32_t *bA, const int32_t *bW,
+                                                             const int32_t *bR, TablePack tab, uint32_t flags) {
+    const int64_t total = Bn * Cout * Ho * Wo;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const int64_t wo = idx % Wo, ho = (idx / Wo) % Ho, co = (idx / (Wo * Ho)) % Cout, b = idx / (Wo * Ho * Cout);
+    const int64_t cpg = Cin / groups;   // input channels per group
+    const int64_t g = co / (Cout / groups);
+    const DFmt fA = dfmt(E, Mw, *bA, true), fR = dfmt(E, Mw, *bR, true), fB = dfmt(E, Mw, bW[co], true);
+    float s = 0.0f, part = 0.0f;
+    int cnt = 0;
+    for (int64_t c = 0; c < cpg; ++c)
+        for (int ky = 0; ky < kh; ++ky)
+            for (int kx = 0; kx < kw; ++kx) {
+                const int64_t hi = ho * sh - ph + ky * dh, wi = wo * sw - pw + kx * dw;
+                const float a = (hi >= 0 && hi < H && wi >= 0 && wi < W)
+                                    ? x[((b * Cin + g * cpg + c) * H + hi) * W + wi] : 0.0f;
+                const float bv = w[((co * cpg + c) * kh + ky) * kw + kx];
+                part += exact_term(a, bv, fA, fB, fR, tab.raw, flags | F_TB);
+                if (++cnt == 16) {
+                    s += part;
+                    part = 0.0f;
+                    cnt = 0;
+                }
+            }
+    y[idx] = s + part;
+}
+
+// FP8 fake quantizer (fp8_quantizer.py:97-173), one sign bit.
+__global__ __launch_bounds__(256) void fp8_quantize_kernel(const float *x, int64_t rows, int64_t inner,
+                                                           const float *maxval, int per_row, int E, int M,
+                                                           int sign_bits, float *out, float *bias_out,
+                                                           int32_t *ibias_out) {
+    const int64_t total = rows * inner;
+    const float cM = log2f(2.0f - p2(-M));
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = per_row ? idx / inner : 0;
+        const float mx = maxval[r];
+        const float bias = rintf((float)(1 << E) - log2f(mx) + cM - 1.0f);
+        const float v = x[idx];
+        const float xc = fminf(fmaxf(v, sign_bits ? -mx : 0.0f), mx);
+        int e;
+        frexpf(xc, &e);
+        const float ls = (xc == 0.0f) ? 1.0f : fmaxf((float)(e - 1) + bias, 1.0f);
+        const float sc = p2((int)(ls - (float)M - bias));
+        out[idx] = rintf(xc / sc) * sc;
+        if ((idx % inner) == 0) {
+            if (bias_out) bias_out[r] = bias;
+            if (ibias_out) ibias_out[r] = (int32_t)bias;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------- host dispatch
+template <bool S2N, bool QBMA, bool GCLIP>
+static void launch_fast_t(int mode, const GemmArgs &a, dim3 grid, hipStream_t s) {
+    switch (mode) {
+        case TM_NONE: gemm_fast_kernel<S2N, QBMA, GCLIP, TM_NONE><<<grid, NT, 0, s>>>(a); break;
+        case TM_W1U: gemm_fast_kernel<S2N, QBMA, GCLIP, TM_W1U><<<grid, NT, 0, s>>>(a); break;
+        case TM_W2S1: gemm_fast_kernel<S2N, QBMA, GCLIP, TM_W2S1><<<grid, NT, 0, s>>>(a); break;
+        case TM_W2U1: gemm_fast_kernel<S2N, QBMA, GCLIP, TM_W2U1><<<grid, NT, 0, s>>>(a); break;
+        case TM_W2S2: gemm_fast_kernel<S2N, QBMA, GCLIP, TM_W2S2><<<grid, NT, 0, s>>>(a); break;
+        case TM_W2U2: gemm_fast_kernel<S2N, QBMA, GCLIP, TM_W2U2><<<grid, NT, 0, s>>>(a); break;
+        default: gemm_fast_kernel<S2N, QBMA, GCLIP, TM_LUT><<<grid, NT, 0, s>>>(a); break;
+    }
+}
+
+static void launch_fast(int mode, const GemmArgs &a, hipStream_t s) {
+    const int64_t tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+    dim3 grid((unsigned)tiles);
+    const bool s2n = a.flags & F_S2N, q = a.flags & F_QBMA, gc = a.flags & F_GCLIP;
+    if (s2n) {
+        if (q) { gc ? launch_fast_t<true, true, true>(mode, a, grid, s) : launch_fast_t<true, true, false>(mode, a, grid, s); }
+        else   { gc ? launch_fast_t<true, false, true>(mode, a, grid, s) : launch_fast_t<true, false, false>(mode, a, grid, s); }
+    } else {
+        if (q) { gc ? launch_fast_t<false, true, true>(mode, a, grid, s) : launch_fast_t<false, true, false>(mode, a, grid, s); }
+        else   { gc ? launch_fast_t<false, false, true>(mode, a, grid, s) : launch_fast_t<false, false, false>(mode, a, grid, s); }
+    }
+}
+
+static int check_format(int E, int Mw) {
+    if (E < 1 || Mw < 1 || Mw > 5 || E > 6 || E + Mw > 8)
+        return fail(FP8A_EFORMAT, "Invalid combination of expo_width and mant_width");
+    return FP8A_OK;
+}
+
+constexpr size_t FLAG_BYTES = 256;  // workspace prefix holding the off-grid flag word
+
+// Fast tiled kernel + gated exact kernel (int-bias path), or the exact kernel alone (tb path).
+static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes, hipStream_t s) {
+    int rc = check_format(a.E, a.Mw);
+    if (rc) return rc;
+    if (a.M < 0 || a.N < 0 || a.K < 0) return fail(FP8A_EINVAL, "negative extent");
+    if (!a.A || !a.B || !a.C || !a.bA || !a.bB || !a.bR) return fail(FP8A_EINVAL, "null pointer");
+    if (a.M == 0 || a.N == 0) return FP8A_OK;
+    int mode;
+    rc = pack_table(table, a.Mw, a.flags & F_APPROX, a.tab, mode);
+    if (rc) return rc;
+    const int64_t total = a.M * a.N;
+    const unsigned eblocks = (unsigned)((total + 255) / 256);
+    if (a.flags & F_TB) {
+        a.flag = nullptr;
+        gemm_exact_kernel<<<eblocks, 256, 0, s>>>(a);
+        return hip_check("fp8a exact gemm launch");
+    }
+    if (ws == nullptr || ws_bytes < FLAG_BYTES) return fail(FP8A_EINVAL, "matmul workspace too small");
+    a.flag = (uint32_t *)ws;
+    if (hipMemsetAsync(ws, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a flag reset");
+    launch_fast(mode, a, s);
+    rc = hip_check("fp8a fast gemm launch");
+    if (rc) return rc;
+    gemm_exact_kernel<<<eblocks, 256, 0, s>>>(a);
+    return hip_check("fp8a gated exact gemm launch");
+}
+
+}  // namespace fp8a
+
+using namespace fp8a;
+
+extern "C" {
+
+const char *fp8a_version(void) { return "fp8approx gfx950 r1"; }
+
+const char *fp8a_last_error(void) { return g_err.c_str(); }
+
+int fp8a_decompose(const float *x, int64_t rows, int64_t cols, int64_t ld, int E, int M, const int32_t *bias,
+                   int64_t bias_stride, uint32_t flags, int32_t *expo, int32_t *mant, fp8a_stream_t stream) {
+    int rc = check_format(E, M);
+    if (rc) return rc;
+    if (rows < 0 || cols < 0 || ld < cols) return fail(FP8A_EINVAL, "bad decompose extents");
+    const int64_t total = rows * cols;
+    if (total == 0) return FP8A_OK;
+    decompose_kernel<<<(unsigned)((total + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+        x, rows, cols, ld, E, M, bias, bias_stride, flags, expo, mant);
+    return hip_check("fp8a_decompose");
+}
+
+int fp8a_quant(const float *x, int64_t n, int E, int M, const int32_t *bias, uint32_t flags, float *out,
+               fp8a_stream_t stream) {
+    int rc = check_format(E, M);
+    if (rc) return rc;
+    if (n <= 0) return FP8A_OK;
+    quant_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, n, E, M, bias, flags, out);
+    return hip_check("fp8a_quant");
+}
+
+static GemmArgs make_args(const float *A, int64_t lda, const float *B, int64_t sbk, int64_t sbn, float *C,
+                          int64_t ldc, int64_t M, int64_t N, int64_t K, int E, int Mw, const int32_t *bA,
+                          const int32_t *bB, int64_t bBs, const int32_t *bR, uint32_t flags) {
+    GemmArgs a;
+    memset(&a, 0, sizeof(a));
+    a.A = A; a.lda = lda; a.B = B; a.sbk = sbk; a.sbn = sbn; a.C = C; a.ldc = ldc;
+    a.M = M; a.N = N; a.K = K; a.E = E; a.Mw = Mw; a.bA = bA; a.bB = bB; a.bBs = bBs; a.bR = bR;
+    a.flags = flags; a.nchw = 0; a.hw = 1; a.ctot = N; a.coff = 0;
+    return a;
+}
+
+size_t fp8a_matmul_workspace_size(void) { return FLAG_BYTES; }
+
+int fp8a_matmul(const float *A, int64_t lda, const float *B, int64_t sbk, int64_t sbn, float *C, int64_t ldc,
+                int64_t M, int64_t N, int64_t K, int E, int Mw, const int32_t *bA, const int32_t *bB,
+                int64_t bB_stride, const int32_t *bR, const int32_t *table, uint32_t flags, void *workspace,
+                size_t workspace_bytes, fp8a_stream_t stream) {
+    if (lda < K || ldc < N) return fail(FP8A_EINVAL, "leading dimension smaller than extent");
+    GemmArgs a = make_args(A, lda, B, sbk, sbn, C, ldc, M, N, K, E, Mw, bA, bB, bB_stride, bR, flags);
+    return run_gemm(a, table, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int fp8a_terms(const float *A, int64_t lda, const float *B, int64_t sbk, int64_t sbn, float *T, int64_t M,
+               int64_t N, int64_t K, int E, int Mw, const int32_t *bA, const int32_t *bB, int64_t bB_stride,
+               const int32_t *bR, const int32_t *table, uint32_t flags, fp8a_stream_t stream) {
+    int rc = check_format(E, Mw);
+    if (rc) return rc;
+    GemmArgs a = make_args(A, lda, B, sbk, sbn, nullptr, 0, M, N, K, E, Mw, bA, bB, bB_stride, bR, flags);
+    int mode;
+    rc = pack_table(table, Mw, flags & F_APPROX, a.tab, mode);
+    if (rc) return rc;
+    const int64_t total = M * N * K;
+    if (total == 0) return FP8A_OK;
+    terms_kernel<<<(unsigned)((total + 255) / 256), 256, 0, (hipStream_t)stream>>>(a, T);
+    return hip_check("fp8a_terms");
+}
+
+int fp8a_im2col(const float *x, float *out, int64_t Bn, int64_t Cin, int64_t H, int64_t W, int kh, int kw, int sh,
+                int sw, int ph, int pw, int dh, int dw, fp8a_stream_t stream) {
+    const int64_t Ho = (H + 2 * ph - dh * (kh - 1) - 1) / sh + 1;
+    const int64_t Wo = (W + 2 * pw - dw * (kw - 1) - 1) / sw + 1;
+    if (Ho <= 0 || Wo <= 0) return fail(FP8A_EINVAL, "empty convolution output");
+    const int64_t total = Bn * Ho * Wo * Cin * kh * kw;
+    if (total == 0) return FP8A_OK;
+    const int64_t blocks = std::min<int64_t>((total + 255) / 256, 65536);
+    im2col_kernel<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(x, out, Bn, Cin, H, W, kh, kw, sh, sw, ph, pw,
+                                                                     dh, dw, Ho, Wo);
+    return hip_check("fp8a_im2col");
+}
+
+size_t fp8a_conv2d_workspace_size(int64_t Bn, int64_t Cin, int64_t H, int64_t W, int64_t Cout, int kh, int kw,
+                                  int sh, int sw, int ph, int pw, int dh, int dw, int groups) {
+    if (groups <= 0 || Cout % groups != 0 || Cin % groups != 0) return 0;
+    if (Cout / groups == 1) return 0;  // direct tensor-bias kernel, no im2col image
+    const int64_t Ho = (H + 2 * ph - dh * (kh - 1) - 1) / sh + 1;
+    const int64_t Wo = (W + 2 * pw - dw * (kw - 1) - 1) / sw + 1;
+    if (Ho <= 0 || Wo <= 0) return 0;
+    return FLAG_BYTES + (size_t)(Bn * Ho * Wo) * (size_t)(Cin * kh * kw) * sizeof(float);
+}
+
+int fp8a_conv2d(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
+                int64_t Cout, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw, int groups, int E,
+                int Mw, const int32_t *bA, const int32_t *bW, const int32_t *bR, const int32_t *table,
+                uint32_t flags, void *workspace, size_t workspace_bytes, fp8a_stream_t stream) {
+    hipStream_t s = (hipStream_t)stream;
+    int rc = check_format(E, Mw);
+    if (rc) return rc;
+    if (groups <= 0 || Cout % groups != 0 || Cin % groups != 0) return fail(FP8A_EINVAL, "bad groups");
+    const int64_t Ho = (H + 2 * ph - dh * (kh - 1) - 1) / sh + 1;
+    const int64_t Wo = (W + 2 * pw - dw * (kw - 1) - 1) / sw + 1;
+    if (Ho <= 0 || Wo <= 0) return fail(FP8A_EINVAL, "empty convolution output");
+    const int64_t cog = Cout / groups, cig = Cin / groups;
+    const int64_t Mrows = Bn * Ho * Wo, Ktot = Cin * kh * kw, Kg = cig * kh * kw;
+    if (Mrows == 0) return FP8A_OK;
+    if (cog == 1) {
+        TablePack tp;
+        int mode;
+        rc = pack_table(table, Mw, flags & F_APPROX, tp, mode);
+        if (rc) return rc;
+        const int64_t total = Bn * Cout * Ho * Wo;
+        conv_tb_direct_kernel<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(
+            x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups, Ho, Wo, E, Mw, bA, bW, bR, tp,
+            flags | F_TB);
+        return hip_check("fp8a_conv2d (tensor-bias groups)");
+    }
+    const size_t need = fp8a_conv2d_workspace_size(Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups);
+    if (workspace == nullptr || workspace_bytes < need) return fail(FP8A_EINVAL, "conv2d workspace too small");
+    float *col = (float *)((char *)workspace + FLAG_BYTES);
+    rc = fp8a_im2col(x, col, Bn, Cin, H, W, kh, kw, sh, sw, ph, pw, dh, dw, stream);
+    if (rc) return rc;
+    for (int g = 0; g < groups; ++g) {
+        GemmArgs a = make_args(col + g * Kg, Ktot, w + g * cog * Kg, 1, Kg, y, 0, Mrows, cog, Kg, E, Mw, bA,
+                               bW + g * cog, 1, bR, flags & ~F_TB);
+        a.nchw = 1;
+        a.hw = Ho * Wo;
+        a.ctot = Cout;
+        a.coff = g * cog;
+        rc = run_gemm(a, table, workspace, FLAG_BYTES, s);
+        if (rc) return rc;
+    }
+    return FP8A_OK;
+}
+
+int fp8a_fp8_quantize(const float *x, int64_t rows, int64_t inner, const float *maxval, int per_row, int n_bits,
+                      int Mbits, int sign_bits, float *out, float *bias_out, int32_t *ibias_out,
+                      fp8a_stream_t stream) {
+    const int E = n_bits - sign_bits - Mbits;
+    if (Mbits < 1 || E < 1) return fail(FP8A_EFORMAT, "bad FP8 quantizer format");
+    const int64_t total = rows * inner;
+    if (total <= 0) return FP8A_OK;
+    const int64_t blocks = std::min<int64_t>((total + 255) / 256, 65536);
+    fp8_quantize_kernel<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(x, rows, inner, maxval, per_row, E,
+                                                                           Mbits, sign_bits, out, bias_out, ibias_out);
+    return hip_check("fp8a_fp8_quantize");
+}
+
+}  // extern "C"

@@ -1,0 +1,154 @@
+// fp8approx_device.h -- device-side arithmetic of the approx_v9 FP8 multiplier for gfx950.
+//
+// Two families of functions:
+//   * exact_*  : a literal float32 restatement of the reference op sequence
+//                (approx/approx_matmul_whole_v9.py).  Every reference torch op is one IEEE
+//                float32 op here (the library is compiled with -ffp-contract=off), so each
+//                product term is bit-identical to the reference.  Used for the tensor-bias
+//                (single-column) path, for off-grid operand tiles and for fp8a_terms.
+//   * q_fast   : a branch-free Q_R on the float32 bit pattern (8 VALU ops), valid for the
+//                int-bias path; exactness argument in DESIGN.md §3.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fp8a {
+
+enum : uint32_t { F_APPROX = 1u, F_S2N = 2u, F_QBMA = 4u, F_GCLIP = 8u, F_TB = 16u };
+
+__device__ __forceinline__ float p2(int k) { return ldexpf(1.0f, k); }
+
+// param_prepare (v9:189-229).  Int bias: Python float powers.  Tensor bias (tb): 2**(negative)
+// is an integer power and evaluates to 0 (quirk F5).
+struct DFmt {
+    float mn;   // min_norm
+    float mx;   // max_norm
+    int b, M, maxe, maxm;
+};
+
+__device__ __forceinline__ DFmt dfmt(int E, int M, int b, bool tb) {
+    DFmt f;
+    f.b = b;
+    f.M = M;
+    f.maxe = (1 << E) - 1;
+    f.maxm = (1 << M) - 1;
+    const float frac = 2.0f - p2(-M);
+    if (!tb) {
+        f.mn = p2(1 - b);
+        f.mx = ldexpf(frac, f.maxe - b);
+    } else {
+        f.mn = (1 - b >= 0) ? p2(1 - b) : 0.0f;
+        f.mx = (f.maxe - b >= 0) ? p2(f.maxe - b) * frac : 0.0f;
+    }
+    return f;
+}
+
+// float_to_fpany_absint_torch (v9:233-291).
+__device__ __forceinline__ void exact_dec(float x, const DFmt &f, bool clip, int &expo, int &mant) {
+    int e;
+    const float fr = frexpf(x, &e);
+    const bool sub = fabsf(x) < f.mn;
+    const float t = sub ? fabsf(fr) * p2(e + (f.b - 1 + f.M)) : (fabsf(fr) * 2.0f - 1.0f) * p2(f.M);
+    float r = rintf(t);
+    r = (r > (float)f.maxm) ? (float)f.maxm : r;
+    mant = (int)r;
+    expo = sub ? 0 : e + (f.b - 1);
+    if (clip && ((x < -f.mx) || (x > f.mx))) {
+        expo = f.maxe;
+        mant = f.maxm;
+    }
+}
+
+// fpany_absint_to_float_torch (v9:295-329).
+__device__ __forceinline__ float exact_rec(float sign, int expo, int mant, const DFmt &f) {
+    const float ms = (float)mant * p2(-f.M);
+    const float v = (expo == 0) ? p2(1 - f.b) * ms : p2(expo - f.b) * (1.0f + ms);
+    return v * sign;
+}
+
+// quant_to_fp_any_vectorize_torch, Q_R (v9:333-362).
+__device__ __forceinline__ float exact_q(float x, const DFmt &f, bool clip) {
+    int e, m;
+    exact_dec(x, f, clip, e, m);
+    return exact_rec(x < 0.0f ? -1.0f : 1.0f, e, m, f);
+}
+
+// One product term of custom_matmul_vectorize (v9:29-108).  tab: int8 [2^M][2^M].
+__device__ __forceinline__ float exact_term(float a, float b, const DFmt &fA, const DFmt &fB,
+                                            const DFmt &fR, const int8_t *tab, uint32_t flags) {
+    const bool s2n = flags & F_S2N, qbma = flags & F_QBMA, gclip = flags & F_GCLIP;
+    const int M = fA.M;
+    float g = a * b;
+    const bool zero = (g == 0.0f);
+    if (qbma) g = exact_q(g, fR, gclip);
+    const bool as = fabsf(a) < fA.mn, bs = fabsf(b) < fB.mn;
+    const float scale = (float)(1 << M);
+    float a2 = a, b2 = b;
+    if (s2n) {
+        if (as) a2 = a * scale;
+        if (bs) b2 = b * scale;
+    }
+    int eA, mA, eB, mB;
+    exact_dec(a2, fA, false, eA, mA);
+    exact_dec(b2, fB, false, eB, mB);
+    const int aexp = eA + eB - (fA.b + fB.b - fR.b);
+    const float sgn = (g < 0.0f) ? -1.0f : 1.0f;
+    const float ulp = p2(-M);
+    float mp = (1.0f + (float)mA * ulp) * (1.0f + (float)mB * ulp);
+    if (flags & F_APPROX) {
+        const int n = 1 << M;
+        const int ia = mA < 0 ? mA + n : mA, ib = mB < 0 ? mB + n : mB;
+        mp = mp - ulp * (float)tab[ia * n + ib];
+    }
+    float v;
+    if (s2n) {
+        v = p2(aexp - fR.b) * mp * sgn;
+        if (as) v = v / scale;
+        if (bs) v = v / scale;
+        if (zero) v = 0.0f;
+    } else {
+        const bool norm = (eA > 0) && (eB > 0) && (fabsf(g) >= fR.mn);
+        v = norm ? p2(aexp - fR.b) * mp * sgn : g;
+    }
+    if (qbma) v = exact_q(v, fR, gclip);
+    return v;
+}
+
+// ---------------------------------------------------------------------------- fast path
+// Q_R for the int-bias path on the float32 bit pattern.  For |x| in binade e:
+//   step  = 2^(max(e, e_min) - M)               (e_min = 1 - bR: subnormal grid below it)
+//   bound = 2^e (2 - 2^-M) - ulp                (pre-clamp: rounding can no longer carry
+//                                                past the largest M-bit mantissa, F6)
+//   r     = ((min(|x|, bound) + C) - C),  C = 2^(max(e, e_min) + 23 - M)   (RNE at `step`)
+struct QC {
+    uint32_t emn;   // exponent field of 2^(1 - bR)
+    uint32_t kb;    // ((2^M - 1) << (23 - M)) - 1
+    uint32_t kc;    // (23 - M) << 23
+    float maxnorm;  // max_norm(bR) (golden_clip_OF)
+    float mnR;      // min_norm(bR)
+    float thr;      // largest |g| that Q_R flushes to 0: 2^(-bR - M)
+};
+
+__device__ __forceinline__ QC make_qc(int E, int M, int bR) {
+    QC q;
+    q.emn = (uint32_t)(127 + 1 - bR) << 23;
+    q.kb = ((((1u << M) - 1u)) << (23 - M)) - 1u;
+    q.kc = (uint32_t)(23 - M) << 23;
+    q.maxnorm = ldexpf(2.0f - p2(-M), (1 << E) - 1 - bR);
+    q.mnR = p2(1 - bR);
+    q.thr = p2(-bR - M);
+    return q;
+}
+
+template <bool GCLIP>
+__device__ __forceinline__ float q_fast(float x, const QC &q) {
+    const uint32_t ex = __float_as_uint(x) & 0x7F800000u;
+    float xa = fminf(fabsf(x), __uint_as_float(ex + q.kb));
+    if (GCLIP) xa = fminf(xa, q.maxnorm);
+    const uint32_t ee = ex > q.emn ? ex : q.emn;
+    const float c = __uint_as_float(ee + q.kc);
+    const float r = (xa + c) - c;
+    return copysignf(r, x);
+}
+
+}  // namespace fp8a

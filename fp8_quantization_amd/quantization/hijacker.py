@@ -1,0 +1,98 @@
+"""QuantizationHijacker (reference: quantization/hijacker.py:32-151).
+
+forward() keeps the reference's ordering exactly (hijacker.py:77-115):
+  act-quant input -> quantize weights -> [calibration / original_quantize_res: run_forward
+  + res_quantizer] -> [qamaa: run_forward] -> [approx: run_forward] -> activation ->
+  [output act-quant].  The ValueError for approx/qamaa without res_quantizer_flag is kept.
+"""
+import copy
+
+from torch import nn
+
+from .base_quantized_classes import QuantizedModule
+from .quantization_manager import QuantizationManager
+from .range_estimators import CurrentMinMaxEstimator
+
+activations_set = [nn.ReLU, nn.ReLU6, nn.Hardtanh, nn.Sigmoid, nn.Tanh, nn.GELU, nn.PReLU, nn.SiLU, nn.Hardswish,
+                   nn.Hardsigmoid]
+
+
+class QuantizationHijacker(QuantizedModule):
+    def __init__(self, *args, activation: nn.Module = None, **kwargs):
+        super().__init__(*args, **kwargs)
+        if activation:
+            assert isinstance(activation, tuple(activations_set)), str(activation)
+        self.activation_function = copy.deepcopy(activation) if activation else None
+        mk = dict(qmethod=self.act_method, init=self.act_range_method, qparams=self.act_qparams,
+                  range_estim_params=self.act_range_options)
+        self.activation_quantizer = QuantizationManager(**mk)
+        self.res_quantizer = QuantizationManager(**mk)
+        if self.weight_range_method is CurrentMinMaxEstimator:
+            w_init = dict(percentile=self.percentile)
+        else:
+            w_init = self.weight_range_options
+        self.weight_quantizer = QuantizationManager(qmethod=self.method, init=self.weight_range_method,
+                                                    per_channel=self.per_channel_weights, qparams=self.weight_qparams,
+                                                    range_estim_params=w_init)
+
+    def _check_res_flag(self):
+        if (self.quantize_after_mult_and_add or self.approx_flag) and not self.res_quantizer_flag:
+            raise ValueError("quantize_after_mult_and_add or approx_flag is set but res_quantizer_flag is not set. "
+                             "you need to set res_quantizer_flag to True if you want to use "
+                             "quantize_after_mult_and_add or approx_flag")
+
+    def _core(self, x, offsets=None):
+        """Shared part of QuantizationHijacker.forward and BNFusedHijacker.forward."""
+        qa = self._qa()
+        if self.quantize_input and qa:
+            x = self.activation_quantizer(x)
+        weight, bias = self.get_params()
+        res = None
+        if not self.fix_ranges_flag or self.original_quantize_res:
+            res = self.run_forward(x, weight, bias, offsets=offsets)
+            if self.quantize_input and qa and self.res_quantizer_flag:
+                res = self.res_quantizer(res)
+        if self.res_quantizer_flag and self.quantize_after_mult_and_add:
+            res = self.run_forward(x, weight, bias)
+        if self.res_quantizer_flag and self.approx_flag:
+            res = self.run_forward(x, weight, bias, offsets=offsets)
+        self._check_res_flag()
+        return res, qa
+
+    def _epilogue(self, res, qa):
+        if self.activation_function is not None:
+            res = self.activation_function(res)
+        if not self.quantize_input and qa:
+            res = self.activation_quantizer(res)
+        return res
+
+    def forward(self, x, offsets=None):
+        res, qa = self._core(x, offsets)
+        return self._epilogue(res, qa)
+
+    def get_params(self):
+        weight, bias = self.get_weight_bias()
+        if self._qw():
+            weight = self.quantize_weights(weight)
+        return weight, bias
+
+    def quantize_weights(self, weights):
+        return self.weight_quantizer(weights)
+
+    def get_weights_fp_bias(self):
+        return self.weight_quantizer.get_fp_bias()
+
+    def get_acts_fp_bias(self):
+        return self.activation_quantizer.get_fp_bias()
+
+    def get_res_fp_bias(self):
+        return self.res_quantizer.get_fp_bias()
+
+    def get_weight_bias(self):
+        return self.weight, getattr(self, "bias", None)
+
+    def run_forward(self, x, weight, bias, offsets=None):
+        raise NotImplementedError()
+
+    def extra_repr(self):
+        return f"{super().extra_repr()}-{'input' if self.quantize_input else 'output'}"

@@ -1,0 +1,123 @@
+/*
+ * fp8approx.h -- C-ABI of the MI355X (gfx950) approx-FP8 matmul/conv engine.
+ *
+ * Drop-in boundary for the approx_v9 hot path of revollllt/FP8_quantization @ 2024-11-08.
+ * Plain pointers and sizes only; every entry point is asynchronous on the given HIP stream,
+ * allocates nothing and never synchronises the host (biases are DEVICE int32 scalars/arrays, so
+ * a whole forward needs no .item() round trip -- unlike approx_calculation.py:780).
+ *
+ * Return codes: 0 ok; FP8A_EINVAL (shape/stride contract broken: the reference's
+ * AssertionError, approx_matmul_whole_v9.py:20); FP8A_EFORMAT (unsupported (E, M): the
+ * reference's ValueError, approx_matmul_whole_v9.py:590); FP8A_EHIP (HIP launch failure).
+ * fp8a_last_error() gives a message for the last failure on the calling thread.
+ *
+ * Flags (same bit values the oracle uses):
+ */
+#ifndef FP8APPROX_H
+#define FP8APPROX_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FP8A_APPROX 1u  /* with_approx: subtract the error table            v9:178-184 */
+#define FP8A_S2N    2u  /* with_s2nn2s_opt: subnormal scale-up / scale-back v9:51-81   */
+#define FP8A_QBMA   4u  /* quant_btw_mult_accu: Q_R before and after mult    v9:35,107 */
+#define FP8A_GCLIP  8u  /* golden_clip_OF: Q_R clips overflow to max_norm   v9:283-286 */
+#define FP8A_TB     16u /* biases are int tensors (single-column call): quirk F5,
+                           approx_calculation.py:800-809 / v9:202                      */
+
+#define FP8A_OK       0
+#define FP8A_EINVAL  -1
+#define FP8A_EFORMAT -2
+#define FP8A_EHIP    -3
+
+typedef void *fp8a_stream_t; /* a hipStream_t (NULL = default stream) */
+
+/* Library identification, e.g. "fp8approx gfx950 r1". */
+const char *fp8a_version(void);
+/* Message describing the last non-zero return on this thread ("" if none). */
+const char *fp8a_last_error(void);
+
+/*
+ * Element decomposition DEC of float_to_fpany_absint_torch (approx_matmul_whole_v9.py:233-291)
+ * over a rows x cols matrix with row stride ld.  bias: device int32, bias_stride 0 = one bias
+ * for all elements, 1 = one bias per ROW (per-channel weights).  flags: FP8A_TB selects the
+ * tensor-bias variant of param_prepare (v9:189-229); FP8A_GCLIP selects clip_OF.
+ * Writes expo/mant (int32, dense rows x cols).
+ */
+int fp8a_decompose(const float *x, int64_t rows, int64_t cols, int64_t ld, int E, int M,
+                   const int32_t *bias, int64_t bias_stride, uint32_t flags,
+                   int32_t *expo, int32_t *mant, fp8a_stream_t stream);
+
+/* Q_R = quant_to_fp_any_vectorize_torch (v9:333-362) elementwise over n floats. */
+int fp8a_quant(const float *x, int64_t n, int E, int M, const int32_t *bias, uint32_t flags,
+               float *out, fp8a_stream_t stream);
+
+/*
+ * Replaces custom_matmul_vectorize (approx_matmul_whole_v9.py:10-169) as driven by
+ * approx_multiply's per-column loop (approx_calculation.py:749-814 / 921-999):
+ *   C[m, n] = sum_k term(A[m, k], B(k, n)),   B(k, n) = B[k * sbk + n * sbn]
+ * with bA (device int32 [1]), bB (device int32, bB_stride 0 = shared, 1 = per column), bR
+ * (device int32 [1]).  table: HOST int32 [2^M][2^M] error table (get_error_table_NN,
+ * v9:555-592) or NULL for all-zero; it is packed into the launch arguments, so the call stays
+ * asynchronous.  C is row-major with leading dimension ldc.  workspace: device scratch of at
+ * least fp8a_matmul_workspace_size() bytes (holds the off-grid flag that gates the exact
+ * re-computation when an operand is not exactly representable in its FP8 code).
+ */
+size_t fp8a_matmul_workspace_size(void);
+int fp8a_matmul(const float *A, int64_t lda, const float *B, int64_t sbk, int64_t sbn,
+                float *C, int64_t ldc, int64_t M, int64_t N, int64_t K, int E, int Mw,
+                const int32_t *bA, const int32_t *bB, int64_t bB_stride, const int32_t *bR,
+                const int32_t *table, uint32_t flags, void *workspace, size_t workspace_bytes,
+                fp8a_stream_t stream);
+
+/*
+ * Per-product terms (debug / parity): T[m, k, n] = the value the reference sums at v9:113.
+ * Same arguments as fp8a_matmul; T is dense [M][K][N].
+ */
+int fp8a_terms(const float *A, int64_t lda, const float *B, int64_t sbk, int64_t sbn, float *T,
+               int64_t M, int64_t N, int64_t K, int E, int Mw, const int32_t *bA,
+               const int32_t *bB, int64_t bB_stride, const int32_t *bR, const int32_t *table,
+               uint32_t flags, fp8a_stream_t stream);
+
+/*
+ * Replaces QCustomBNConv2dTorch.run_forward (approx_calculation.py:822-917) minus the conv
+ * bias: x NCHW [Bn, Cin, H, W], w [Cout, Cin/groups, kh, kw], y NCHW [Bn, Cout, Ho, Wo].
+ * bW: device int32 per output channel (weight_quantizer.custom_bias).  Groups whose output
+ * block has a single channel (depthwise) take the tensor-bias semantics (FP8A_TB) exactly as
+ * the reference does (approx_calculation.py:800-809), other groups the int-bias semantics.
+ * workspace: device scratch of fp8a_conv2d_workspace_size() bytes (im2col image).
+ */
+size_t fp8a_conv2d_workspace_size(int64_t Bn, int64_t Cin, int64_t H, int64_t W, int64_t Cout,
+                                  int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw,
+                                  int groups);
+int fp8a_conv2d(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H,
+                int64_t W, int64_t Cout, int kh, int kw, int sh, int sw, int ph, int pw, int dh,
+                int dw, int groups, int E, int Mw, const int32_t *bA, const int32_t *bW,
+                const int32_t *bR, const int32_t *table, uint32_t flags, void *workspace,
+                size_t workspace_bytes, fp8a_stream_t stream);
+
+/* The reference's im2col (approx_calculation.py:724-747): out [Bn*Ho*Wo, Cin*kh*kw]. */
+int fp8a_im2col(const float *x, float *out, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
+                int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw,
+                fp8a_stream_t stream);
+
+/*
+ * FP8 fake quantizer forward value, quantize_to_fp8_ste_MM (fp8_quantizer.py:97-173),
+ * E = n_bits - sign_bits - Mbits, clamp range [-maxval, maxval] (sign_bits 1) or [0, maxval]:
+ * x viewed as [rows, inner]; maxval device float [rows] if per_row else [1].  Writes out (same shape) and, if bias_out != NULL, the float bias
+ * round(2^E - log2(maxval) + log2(2 - 2^-M) - 1) per row (or [1]) and, if ibias_out != NULL,
+ * the same bias as int32 (what approx_multiply feeds the matmul, approx_calculation.py:768).
+ */
+int fp8a_fp8_quantize(const float *x, int64_t rows, int64_t inner, const float *maxval,
+                      int per_row, int n_bits, int Mbits, int sign_bits, float *out,
+                      float *bias_out, int32_t *ibias_out, fp8a_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FP8APPROX_H */

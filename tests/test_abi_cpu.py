@@ -1,0 +1,54 @@
+"""C-ABI surface checks that need no GPU: the library loads and exports every entry point
+include/fp8approx.h declares; host-side argument validation reports the reference's errors."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from fp8_quantization_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "fp8approx.h")).read()
+    return sorted(set(re.findall(r"\b(fp8a_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_symbols_match_binding_table():
+    assert declared_symbols() == sorted(_lib.SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.load()
+    for name in declared_symbols():
+        assert hasattr(L, name), name
+        assert ctypes.cast(getattr(L, name), ctypes.c_void_p).value
+
+
+def test_version_string():
+    assert _lib.version().startswith("fp8approx gfx950")
+
+
+def test_workspace_queries_are_host_only():
+    L = _lib.load()
+    assert L.fp8a_matmul_workspace_size() >= 4
+    # depthwise (single output channel per group): direct kernel, no im2col image
+    assert L.fp8a_conv2d_workspace_size(2, 8, 6, 6, 8, 3, 3, 1, 1, 1, 1, 1, 1, 8) == 0
+    n = L.fp8a_conv2d_workspace_size(2, 3, 8, 8, 4, 3, 3, 1, 1, 1, 1, 1, 1, 1)
+    assert n >= 2 * 8 * 8 * 27 * 4
+
+
+def test_bad_format_maps_to_value_error():
+    L = _lib.load()
+    rc = L.fp8a_quant(None, 0, 0, 3, None, 0, None, None)  # E = 0: rejected before any launch
+    with pytest.raises(ValueError):
+        _lib.check(rc, "fp8a_quant")
+
+
+def test_bad_extent_maps_to_assertion_error():
+    L = _lib.load()
+    rc = L.fp8a_matmul(None, 2, None, 1, 1, None, 4, 3, 4, 5, 4, 3, None, None, 0, None, None, 0, None, 0, None)
+    with pytest.raises(AssertionError):
+        _lib.check(rc, "fp8a_matmul")
