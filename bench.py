@@ -1,0 +1,214 @@
+#!/usr/bin/env python
+"""Headline benchmark: ImageNet-val images/s of ResNet-18 FP8 approx_v9 (BASELINE.json metric).
+
+One step = one forward of ResNet-18 (20 approx convs + approx fc, BN, ReLU, pools, FP8
+activation / weight / result quantizers) over a batch of synthetic ImageNet-shaped images
+(3x224x224) already resident in HBM, in the reference's eval protocol
+(run_method approx_flag + res_quantizer_flag, ranges fixed after one calibration batch),
+E4M3, dnsmp_factor=3, with_s2nn2s_opt, quant_btw_mult_accu.  Random-init weights (no network
+for checkpoints), synthetic data (no ImageNet here).
+
+N>1 (torch.distributed.run, one rank per GPU, RCCL): the validation batch is sharded --
+each rank runs its own B images (weak scaling) and the logits are all-gathered once per step,
+as the validate driver does.
+
+Prints ONE JSON line (rank 0).  `roofline` is for the dominant kernel family, the fused
+approx GEMM/conv launches (fp8a_conv2d / fp8a_matmul), timed with HIP events on the stream
+they run on; `cpu_baseline` is the vectorised torch restatement of the reference's op sequence
+(oracle/v9_torch_port.py, cost within ~5 % of the reference on identical inputs) on a bounded
+sample of the same workload.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "ImageNet val images/sec, ResNet-18 FP8 approx_v9; top-1 delta vs reference"
+FP32_VALU_PEAK_TFLOPS = 157.3  # MI355X fp32 vector (= fp32 MFMA) peak, MI355X_MICROARCH.md
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=256, help="images per GPU per step")
+    ap.add_argument("--cal-batch", type=int, default=64)
+    ap.add_argument("--with-comp", action="store_true", help="withComp=True (E4M3: all-zero error table)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-columns", type=int, default=2, help="output columns per layer in the CPU sample")
+    ap.add_argument("--arch", default="resnet18", choices=["resnet18", "resnet50"])
+    return ap.parse_args()
+
+
+def synthetic_images(n, seed, device):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    # ImageNet-normalised statistics: roughly N(0, 1) per channel
+    return torch.randn((n, 3, 224, 224), generator=g).to(device)
+
+
+def pmc_traffic(round_tag="r01"):
+    """Per-launch HBM bytes of the approx GEMM kernel from a committed rocprofv3 PMC summary
+    (profiles/pmc_<round>.json, produced by tools/pmc_summary.py), else None."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{round_tag}.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get("gemm_fast_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(shapes, table, cols):
+    """Reference-cost CPU throughput on a bounded sample: for every distinct approx layer
+    shape of ONE image, time `cols` output columns of the torch port, scale by the layer's
+    column count; images/s = 1 / projected seconds per image."""
+    from oracle import v9_torch_port as port
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    fa, fb = port._fmt(4, 3, 12), port._fmt(4, 3, 19)
+    g = torch.Generator().manual_seed(7)
+    per_img, measured, cache = 0.0, 0.0, {}
+    for (_, Mi, K, N, groups) in shapes:
+        key = (Mi, K)
+        if key not in cache:
+            A = port._q(torch.randn((Mi, K), generator=g).relu(), fa, True)
+            B = port._q(torch.randn((K, cols), generator=g) * 0.05, fb, True)
+            t0 = time.perf_counter()
+            for c in range(cols):
+                port.column(A, B[:, c:c + 1], 4, 3, 12, 19, 15, table, approx=True, s2n=True, qbma=True)
+            dt = (time.perf_counter() - t0) / cols
+            cache[key] = dt
+            measured += dt * cols
+        per_img += cache[key] * N * groups
+    return dict(value=1.0 / per_img, unit="images/s", cores=threads, kind="port",
+                sample=(f"1 image: {cols} output columns of each of {len(cache)} distinct approx layer shapes "
+                        f"(torch port of the v9 op sequence, {measured:.1f} s measured), scaled by each layer's "
+                        f"output-column count; {per_img:.1f} s/img projected"))
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.manual_seed(0)
+
+    import fp8_quantization_amd as fa
+    from fp8_quantization_amd import approx_matmul as am
+    from fp8_quantization_amd.error_tables import get_error_table_NN
+    from fp8_quantization_amd.resnet_workload import (approx_layer_shapes, approx_macs_per_image, resnet18_approx,
+                                                      resnet50_approx)
+
+    fa._lib.load()
+    cfg = dict(expo_width=4, mant_width=3, dnsmp_factor=3, withComp=args.with_comp, with_approx=True,
+               with_s2nn2s_opt=True, quant_btw_mult_accu=True)
+    build = resnet18_approx if args.arch == "resnet18" else resnet50_approx
+    model = build(**cfg).to(dev).eval()
+
+    # calibration (one batch, identical on every rank), then fixed ranges -- image_net.py:76-91
+    with torch.no_grad():
+        shapes, hooks = approx_layer_shapes(model)
+        model.quantized()
+        model.estimate_ranges()
+        model(synthetic_images(args.cal_batch, 1234, dev))
+        model.fix_ranges()
+        for h in hooks:
+            h.remove()
+    shapes = shapes[:len(shapes) // 2]  # estimate mode runs each approx layer twice
+    macs_img = approx_macs_per_image(shapes)
+
+    x = synthetic_images(args.batch, 10 + rank, dev)
+    gathered = torch.empty((world * args.batch, 1000), device=dev) if world > 1 else None
+
+    def step():
+        logits = model(x)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, logits.contiguous())
+        return logits
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        am._PROFILE = []
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        prof, am._PROFILE = am._PROFILE, None
+
+    op_ms = sum(s.elapsed_time(e) for (s, e, _) in prof)
+    op_macs = sum(m for (_, _, m) in prof)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    images = world * args.batch * args.steps
+
+    if rank == 0:
+        launches = len(prof)
+        avg_s = op_ms / 1e3 / launches
+        achieved = 2.0 * (op_macs / launches) / avg_s / 1e12
+        res = {
+            "metric": METRIC,
+            "value": images / elapsed,
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{args.arch} E4M3 approx_v9 forward (dnsmp_factor=3, withComp={args.with_comp}, "
+                            "with_s2nn2s_opt, quant_btw_mult_accu, res_quantizer, fixed ranges), "
+                            "ImageNet-shaped synthetic batch, random-init weights",
+                "global_batch": world * args.batch,
+                "per_gpu_batch": args.batch,
+                "image_hw": 224,
+                "approx_macs_per_image": macs_img,
+                "parallelism": f"dp{world}",
+            },
+            "roofline": {
+                "bound": "valu",
+                "kernel": "gemm_fast_kernel (fused implicit-GEMM approx conv / linear)",
+                "achieved": achieved,
+                "peak": FP32_VALU_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": achieved / FP32_VALU_PEAK_TFLOPS,
+                "traffic": pmc_traffic(),
+                "algorithmic": f"2 FLOP per approx-MAC; {op_macs / launches:.4g} approx-MAC per launch avg over "
+                               f"{launches} launches, {avg_s * 1e3:.3f} ms avg launch (HIP events)",
+                "approx_macs_per_s": op_macs / (op_ms / 1e3),
+                "gemm_share_of_step": op_ms / 1e3 / elapsed,
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(shapes, get_error_table_NN(4, 3, args.with_comp, 3), args.cpu_columns)
+            res["speedup_vs_cpu_baseline"] = res["value"] / res["cpu_baseline"]["value"]
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -32,6 +32,25 @@ def make_flags(with_approx=True, with_s2nn2s_opt=False, quant_btw_mult_accu=True
 
 _BIAS_CACHE = {}
 
+# bench.py sets this to a list to time every approx launch with HIP events on the current
+# stream: entries (start_event, end_event, approx_MACs).  None = no instrumentation.
+_PROFILE = None
+
+
+def _prof_start():
+    if _PROFILE is None:
+        return None
+    ev = torch.cuda.Event(enable_timing=True)
+    ev.record()
+    return ev
+
+
+def _prof_end(start, macs):
+    if start is not None:
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        _PROFILE.append((start, ev, int(macs)))
+
 
 def _bias_dev(b, device, n=None):
     """Device int32 bias vector from an int or a (float/int) tensor; no host sync for tensors."""
@@ -113,8 +132,13 @@ def approx_matmul(A, B, E, M, bA, bB, bR, table=None, flags=None, **flag_kwargs)
         B = B.contiguous()
     dev = A.device
     tab = _table_host(table, M, bool(flags & _lib.APPROX))
-    return _matmul_op(A, B, _bias_dev(bA, dev), _bias_dev(bB, dev), _bias_dev(bR, dev), tab, int(E), int(M),
-                      int(flags))
+    bB_ = _bias_dev(bB, dev)
+    if bB_.numel() not in (1, B.shape[1]):
+        raise AssertionError(f"approx_matmul: {bB_.numel()} column biases for {B.shape[1]} columns")
+    ev = _prof_start()
+    C = _matmul_op(A, B, _bias_dev(bA, dev), bB_, _bias_dev(bR, dev), tab, int(E), int(M), int(flags))
+    _prof_end(ev, A.shape[0] * A.shape[1] * B.shape[1])
+    return C
 
 
 def approx_terms(A, B, E, M, bA, bB, bR, table=None, flags=None, **flag_kwargs):
@@ -244,9 +268,17 @@ def approx_conv2d(x, w, E, M, bA, bW, bR, table=None, flags=None, stride=(1, 1),
     flags &= ~_lib.TB
     dev = x.device
     tab = _table_host(table, M, bool(flags & _lib.APPROX))
-    return _conv2d_op(_as_f32(x), _as_f32(w), _bias_dev(bA, dev), _bias_dev(bW, dev), _bias_dev(bR, dev), tab,
-                      int(E), int(M), int(flags), [int(s) for s in stride], [int(p) for p in padding],
-                      [int(d) for d in dilation], int(groups))
+    bW_ = _bias_dev(bW, dev)
+    if bW_.numel() == 1:
+        bW_ = bW_.expand(w.shape[0]).contiguous()
+    if bW_.numel() != w.shape[0]:
+        raise AssertionError(f"approx_conv2d: {bW_.numel()} weight biases for {w.shape[0]} output channels")
+    ev = _prof_start()
+    y = _conv2d_op(_as_f32(x), _as_f32(w), _bias_dev(bA, dev), bW_, _bias_dev(bR, dev), tab,
+                   int(E), int(M), int(flags), [int(s) for s in stride], [int(p) for p in padding],
+                   [int(d) for d in dilation], int(groups))
+    _prof_end(ev, y.shape[0] * y.shape[2] * y.shape[3] * w.shape[0] * w.shape[1] * w.shape[2] * w.shape[3])
+    return y
 
 
 # ----------------------------------------------------------------------------------- FP8 fake quant

@@ -104,8 +104,27 @@ struct GemmArgs {
     int nchw;
     int64_t hw, ctot, coff;
     uint32_t *flag;  // device word: set by the fast kernel when the exact kernel must run
+    // implicit-GEMM convolution: A(m, k) gathered from NCHW x (no im2col image), m = (b, ho, wo),
+    // k = (c, ky, kx) within the group -- the reference's im2col order (approx_calculation.py:745)
+    int conv;
+    const float *X;
+    int64_t Cin, H, W, Ho, Wo, cbase;
+    int kh, kw, sh, sw, ph, pw, dh, dw;
+    uint32_t kk_mul, kk_shift, kw_mul, kw_shift;  // fast division by kh*kw and by kw
     TablePack tab;
 };
+
+// n / d for 0 <= n < 2^31 via one mulhi: q = (mulhi(n, mul) + n) >> shift (Granlund-Montgomery).
+static void fastdiv_params(uint32_t d, uint32_t &mul, uint32_t &shift) {
+    uint32_t l = 0;
+    while ((1ull << l) < d) ++l;
+    shift = l;
+    mul = (uint32_t)(((1ull << 32) * ((1ull << l) - d)) / d + 1);
+}
+
+__device__ __forceinline__ uint32_t fastdiv(uint32_t n, uint32_t mul, uint32_t shift) {
+    return (__umulhi(n, mul) + n) >> shift;
+}
 
 constexpr int BM = 64, BN = 64, BK = 16, TM = 4, TN = 4, NT = 256;
 constexpr int AP = BM + 4, BP = BN + 4;
@@ -189,6 +208,20 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
         emnB[r] = (uint32_t)(128 - bb) << 23;
     }
 
+    // implicit-conv row of this thread (fixed across k tiles)
+    bool crow_ok = false;
+    int64_t cxoff = 0, chi0 = 0, cwi0 = 0;
+    if (p.conv) {
+        const int64_t m = m0 + (tid & 63);
+        crow_ok = m < p.M;
+        const int64_t hw = p.Ho * p.Wo;
+        const int64_t img = crow_ok ? m / hw : 0, pix = crow_ok ? m - img * hw : 0;
+        const int64_t ho = pix / p.Wo, wo = pix - ho * p.Wo;
+        cxoff = (img * p.Cin + p.cbase) * p.H * p.W;
+        chi0 = ho * p.sh - p.ph;
+        cwi0 = wo * p.sw - p.pw;
+    }
+
     float acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -197,13 +230,30 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
 
     for (int64_t k0 = 0; k0 < p.K; k0 += BK) {
         bool bad = !bias_ok;
-        // ---- stage A (64 x 16): element e = tid + 256 r -> (row e>>4, kk e&15), k-contiguous
+        // ---- stage A (64 x 16)
 #pragma unroll
         for (int r = 0; r < (BM * BK) / NT; ++r) {
-            const int e = tid + NT * r;
-            const int row = e >> 4, kk = e & 15;
-            const int64_t m = m0 + row, k = k0 + kk;
-            const float x = (m < p.M && k < p.K) ? p.A[m * p.lda + k] : 0.0f;
+            int row, kk;
+            float x = 0.0f;
+            if (!p.conv) {  // matrix A: lanes along k (row-major A is k-contiguous)
+                const int e = tid + NT * r;
+                row = e >> 4;
+                kk = e & 15;
+                const int64_t m = m0 + row, k = k0 + kk;
+                if (m < p.M && k < p.K) x = p.A[m * p.lda + k];
+            } else {        // implicit im2col: lanes along m (consecutive output pixels)
+                row = tid & 63;
+                kk = (tid >> 6) + 4 * r;
+                const int64_t k = k0 + kk;
+                if (crow_ok && k < p.K) {
+                    const uint32_t c = fastdiv((uint32_t)k, p.kk_mul, p.kk_shift);
+                    const uint32_t t = (uint32_t)k - c * (uint32_t)(p.kh * p.kw);
+                    const uint32_t ky = fastdiv(t, p.kw_mul, p.kw_shift);
+                    const uint32_t kx = t - ky * (uint32_t)p.kw;
+                    const int64_t hi = chi0 + (int64_t)ky * p.dh, wi = cwi0 + (int64_t)kx * p.dw;
+                    if (hi >= 0 && hi < p.H && wi >= 0 && wi < p.W) x = p.X[cxoff + ((int64_t)c * p.H + hi) * p.W + wi];
+                }
+            }
             float c;
             uint32_t mc;
             bad |= !stage_decode(x, M, emnA, S2N, c, mc);
@@ -319,6 +369,17 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
 
 // Exact (reference-order) kernel: one thread per output (m, n), every term via exact_term.
 // Used for the tensor-bias (single-column) semantics and as the reference-path check.
+// A(m, k) for the exact kernels: matrix or implicit im2col.
+__device__ __forceinline__ float load_A(const GemmArgs &p, int64_t m, int64_t k) {
+    if (!p.conv) return p.A[m * p.lda + k];
+    const int64_t hw = p.Ho * p.Wo, img = m / hw, pix = m - img * hw;
+    const int64_t ho = pix / p.Wo, wo = pix - ho * p.Wo;
+    const int64_t taps = (int64_t)p.kh * p.kw, c = k / taps, t = k - c * taps, ky = t / p.kw, kx = t - ky * p.kw;
+    const int64_t hi = ho * p.sh - p.ph + ky * p.dh, wi = wo * p.sw - p.pw + kx * p.dw;
+    if (hi < 0 || hi >= p.H || wi < 0 || wi >= p.W) return 0.0f;
+    return p.X[((img * p.Cin + p.cbase + c) * p.H + hi) * p.W + wi];
+}
+
 __global__ __launch_bounds__(256) void gemm_exact_kernel(const GemmArgs p) {
     // Gate: after a fast launch, run only if it flagged off-grid operands (uniform per grid).
     if (p.flag != nullptr && __hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
@@ -330,7 +391,7 @@ __global__ __launch_bounds__(256) void gemm_exact_kernel(const GemmArgs p) {
     const DFmt fB = dfmt(p.E, p.Mw, p.bB[n * p.bBs], tb);
     float s = 0.0f, part = 0.0f;
     for (int64_t k = 0; k < p.K; ++k) {
-        part += exact_term(p.A[m * p.lda + k], p.B[k * p.sbk + n * p.sbn], fA, fB, fR, p.tab.raw, p.flags);
+        part += exact_term(load_A(p, m, k), p.B[k * p.sbk + n * p.sbn], fA, fB, fR, p.tab.raw, p.flags);
         if ((k & 15) == 15) {
             s += part;
             part = 0.0f;
@@ -488,8 +549,15 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     int rc = check_format(a.E, a.Mw);
     if (rc) return rc;
     if (a.M < 0 || a.N < 0 || a.K < 0) return fail(FP8A_EINVAL, "negative extent");
-    if (!a.A || !a.B || !a.C || !a.bA || !a.bB || !a.bR) return fail(FP8A_EINVAL, "null pointer");
     if (a.M == 0 || a.N == 0) return FP8A_OK;
+    if (a.K == 0) {  // empty inner dimension: the reference's sum over an empty axis is 0
+        if (a.nchw) return fail(FP8A_EINVAL, "empty convolution window");
+        if (hipMemset2DAsync(a.C, a.ldc * sizeof(float), 0, a.N * sizeof(float), a.M, s) != hipSuccess)
+            return hip_check("fp8a zero fill");
+        return FP8A_OK;
+    }
+    if ((!a.A && !a.conv) || (a.conv && !a.X) || !a.B || !a.C || !a.bA || !a.bB || !a.bR)
+        return fail(FP8A_EINVAL, "null pointer");
     int mode;
     rc = pack_table(table, a.Mw, a.flags & F_APPROX, a.tab, mode);
     if (rc) return rc;
@@ -598,7 +666,8 @@ size_t fp8a_conv2d_workspace_size(int64_t Bn, int64_t Cin, int64_t H, int64_t W,
     const int64_t Ho = (H + 2 * ph - dh * (kh - 1) - 1) / sh + 1;
     const int64_t Wo = (W + 2 * pw - dw * (kw - 1) - 1) / sw + 1;
     if (Ho <= 0 || Wo <= 0) return 0;
-    return FLAG_BYTES + (size_t)(Bn * Ho * Wo) * (size_t)(Cin * kh * kw) * sizeof(float);
+    (void)Bn; (void)Cin;
+    return FLAG_BYTES;  // implicit GEMM: only the off-grid flag word
 }
 
 int fp8a_conv2d(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
@@ -628,17 +697,22 @@ int fp8a_conv2d(const float *x, const float *w, float *y, int64_t Bn, int64_t Ci
     }
     const size_t need = fp8a_conv2d_workspace_size(Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups);
     if (workspace == nullptr || workspace_bytes < need) return fail(FP8A_EINVAL, "conv2d workspace too small");
-    float *col = (float *)((char *)workspace + FLAG_BYTES);
-    rc = fp8a_im2col(x, col, Bn, Cin, H, W, kh, kw, sh, sw, ph, pw, dh, dw, stream);
-    if (rc) return rc;
+    if (Kg >= (1ll << 31)) return fail(FP8A_EINVAL, "conv2d window too large");
+    (void)Ktot;
     for (int g = 0; g < groups; ++g) {
-        GemmArgs a = make_args(col + g * Kg, Ktot, w + g * cog * Kg, 1, Kg, y, 0, Mrows, cog, Kg, E, Mw, bA,
-                               bW + g * cog, 1, bR, flags & ~F_TB);
+        GemmArgs a = make_args(nullptr, 0, w + g * cog * Kg, 1, Kg, y, 0, Mrows, cog, Kg, E, Mw, bA, bW + g * cog, 1,
+                               bR, flags & ~F_TB);
         a.nchw = 1;
         a.hw = Ho * Wo;
         a.ctot = Cout;
         a.coff = g * cog;
-        rc = run_gemm(a, table, workspace, FLAG_BYTES, s);
+        a.conv = 1;
+        a.X = x;
+        a.Cin = Cin; a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo; a.cbase = g * cig;
+        a.kh = kh; a.kw = kw; a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw; a.dh = dh; a.dw = dw;
+        fastdiv_params((uint32_t)(kh * kw), a.kk_mul, a.kk_shift);
+        fastdiv_params((uint32_t)kw, a.kw_mul, a.kw_shift);
+        rc = run_gemm(a, table, workspace, workspace_bytes, s);
         if (rc) return rc;
     }
     return FP8A_OK;

@@ -142,9 +142,10 @@ __device__ __forceinline__ QC make_qc(int E, int M, int bR) {
 
 template <bool GCLIP>
 __device__ __forceinline__ float q_fast(float x, const QC &q) {
-    const uint32_t ex = __float_as_uint(x) & 0x7F800000u;
-    float xa = fminf(fabsf(x), __uint_as_float(ex + q.kb));
-    if (GCLIP) xa = fminf(xa, q.maxnorm);
+    float xa = fabsf(x);
+    if (GCLIP) xa = fminf(xa, q.maxnorm);  // clip_OF first: the step comes from the clipped binade
+    const uint32_t ex = __float_as_uint(xa) & 0x7F800000u;
+    xa = fminf(xa, __uint_as_float(ex + q.kb));
     const uint32_t ee = ex > q.emn ? ex : q.emn;
     const float c = __uint_as_float(ee + q.kc);
     const float r = (xa + c) - c;
