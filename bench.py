@@ -105,7 +105,7 @@ def main():
     torch.manual_seed(0)
 
     import fp8_quantization_amd as fa
-    from fp8_quantization_amd import approx_matmul as am
+    from fp8_quantization_amd import approx_ops as am
     from fp8_quantization_amd.error_tables import get_error_table_NN
     from fp8_quantization_amd.resnet_workload import (approx_layer_shapes, approx_macs_per_image, resnet18_approx,
                                                       resnet50_approx)

@@ -18,7 +18,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from . import _lib
-from .approx_matmul import approx_conv2d, approx_matmul, make_flags
+from .approx_ops import approx_conv2d, approx_matmul, make_flags
 from .error_tables import get_error_table_NN
 from .quantization.hijacker import QuantizationHijacker
 from .quantization.quantized_folded_bn import BNFusedHijacker

@@ -8,7 +8,7 @@ custom_bias (set by every forward), set_quant_range / fix_ranges.
 import torch
 from torch import nn
 
-from ..approx_matmul import fp8_fake_quantize
+from ..approx_ops import fp8_fake_quantize
 
 
 def quantize_to_fp8_ste_MM(x_float, n_bits, maxval, num_mantissa_bits, sign_bits):

@@ -6,7 +6,7 @@ import torch
 from torch import nn
 
 from fp8_quantization_amd import _lib
-from fp8_quantization_amd.approx_matmul import make_flags
+from fp8_quantization_amd.approx_ops import make_flags
 from fp8_quantization_amd.error_tables import get_error_table_NN
 from tests import golden_io as gio
 
