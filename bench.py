@@ -125,7 +125,6 @@ def main():
         model.fix_ranges()
         for h in hooks:
             h.remove()
-    shapes = shapes[:len(shapes) // 2]  # estimate mode runs each approx layer twice
     macs_img = approx_macs_per_image(shapes)
 
     x = synthetic_images(args.batch, 10 + rank, dev)

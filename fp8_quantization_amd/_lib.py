@@ -9,7 +9,7 @@ import os
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libfp8approx.so")
+LIB_PATH = os.environ.get("FP8A_LIB_PATH") or os.path.join(HERE, "lib", "libfp8approx.so")
 
 APPROX, S2N, QBMA, GCLIP, TB = 1, 2, 4, 8, 16
 OK, EINVAL, EFORMAT, EHIP = 0, -1, -2, -3

@@ -34,18 +34,22 @@ def up_to_date():
     return all(os.path.getmtime(d) <= t for d in DEPS)
 
 
-def build(force=False, verbose=False):
-    if not force and up_to_date():
+EXTRA = os.environ.get("FP8A_HIPCC_FLAGS", "-fno-slp-vectorize").split()
+
+
+def build(force=False, verbose=False, out=None, extra=None):
+    out = out or OUT
+    if not force and out == OUT and up_to_date():
         return OUT
-    os.makedirs(OUT_DIR, exist_ok=True)
-    tmp = OUT + ".tmp"
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    tmp = out + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
-           "-Wall", "-o", tmp, SRC]
+           "-Wall"] + (EXTRA if extra is None else extra) + ["-o", tmp, SRC]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, OUT)
-    return OUT
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":

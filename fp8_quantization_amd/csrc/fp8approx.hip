@@ -381,24 +381,26 @@ __device__ __forceinline__ float load_A(const GemmArgs &p, int64_t m, int64_t k)
 }
 
 __global__ __launch_bounds__(256) void gemm_exact_kernel(const GemmArgs p) {
-    // Gate: after a fast launch, run only if it flagged off-grid operands (uniform per grid).
+    // Gate: after a fast launch, run only if it flagged off-grid operands (uniform per grid;
+    // the grid is capped, so the no-op case costs one small launch).
     if (p.flag != nullptr && __hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= p.M * p.N) return;
-    const int64_t m = idx % p.M, n = idx / p.M;
     const bool tb = p.flags & F_TB;
     const DFmt fA = dfmt(p.E, p.Mw, *p.bA, tb), fR = dfmt(p.E, p.Mw, *p.bR, tb);
-    const DFmt fB = dfmt(p.E, p.Mw, p.bB[n * p.bBs], tb);
-    float s = 0.0f, part = 0.0f;
-    for (int64_t k = 0; k < p.K; ++k) {
-        part += exact_term(load_A(p, m, k), p.B[k * p.sbk + n * p.sbn], fA, fB, fR, p.tab.raw, p.flags);
-        if ((k & 15) == 15) {
-            s += part;
-            part = 0.0f;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < p.M * p.N;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t m = idx % p.M, n = idx / p.M;
+        const DFmt fB = dfmt(p.E, p.Mw, p.bB[n * p.bBs], tb);
+        float s = 0.0f, part = 0.0f;
+        for (int64_t k = 0; k < p.K; ++k) {
+            part += exact_term(load_A(p, m, k), p.B[k * p.sbk + n * p.sbn], fA, fB, fR, p.tab.raw, p.flags);
+            if ((k & 15) == 15) {
+                s += part;
+                part = 0.0f;
+            }
         }
+        s += part;
+        p.C[out_index(p, m, n)] = s;
     }
-    s += part;
-    p.C[out_index(p, m, n)] = s;
 }
 
 __global__ __launch_bounds__(256) void terms_kernel(const GemmArgs p, float *T) {
@@ -562,7 +564,7 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     rc = pack_table(table, a.Mw, a.flags & F_APPROX, a.tab, mode);
     if (rc) return rc;
     const int64_t total = a.M * a.N;
-    const unsigned eblocks = (unsigned)((total + 255) / 256);
+    const unsigned eblocks = (unsigned)std::min<int64_t>((total + 255) / 256, 4096);
     if (a.flags & F_TB) {
         a.flag = nullptr;
         gemm_exact_kernel<<<eblocks, 256, 0, s>>>(a);

@@ -142,13 +142,14 @@ __device__ __forceinline__ QC make_qc(int E, int M, int bR) {
 
 template <bool GCLIP>
 __device__ __forceinline__ float q_fast(float x, const QC &q) {
-    float xa = fabsf(x);
-    if (GCLIP) xa = fminf(xa, q.maxnorm);  // clip_OF first: the step comes from the clipped binade
-    const uint32_t ex = __float_as_uint(xa) & 0x7F800000u;
-    xa = fminf(xa, __uint_as_float(ex + q.kb));
-    const uint32_t ee = ex > q.emn ? ex : q.emn;
+    // |x| and the bound are non-negative floats: compare them as integers (no canonicalisation)
+    uint32_t xa = __float_as_uint(x) & 0x7FFFFFFFu;
+    if (GCLIP) xa = min(xa, __float_as_uint(q.maxnorm));  // clip_OF first: step from the clipped binade
+    const uint32_t ex = GCLIP ? (xa & 0x7F800000u) : (__float_as_uint(x) & 0x7F800000u);
+    xa = min(xa, ex + q.kb);
+    const uint32_t ee = max(ex, q.emn);
     const float c = __uint_as_float(ee + q.kc);
-    const float r = (xa + c) - c;
+    const float r = (__uint_as_float(xa) + c) - c;
     return copysignf(r, x);
 }
 

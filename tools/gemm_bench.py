@@ -1,0 +1,84 @@
+#!/usr/bin/env python
+"""Per-layer throughput of the approx conv/GEMM kernel on the ResNet-18 layer shapes.
+
+    python tools/gemm_bench.py [--batch 256] [--mode w1u|none|w2s|lut] [--reps 5]
+
+Times fp8a_conv2d (implicit GEMM) with HIP events on the current stream, random FP8-grid
+operands of realistic magnitude; prints one JSON line per layer and a total.
+FP8A_LIB_PATH selects an alternative build of libfp8approx.so (A/B of kernel variants).
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+RESNET18 = [  # (name, cin, cout, k, stride, pad, H_in at 224)
+    ("conv1", 3, 64, 7, 2, 3, 224), ("l1.c", 64, 64, 3, 1, 1, 56), ("l2.c1", 64, 128, 3, 2, 1, 56),
+    ("l2.c2", 128, 128, 3, 1, 1, 28), ("l2.ds", 64, 128, 1, 2, 0, 56), ("l3.c1", 128, 256, 3, 2, 1, 28),
+    ("l3.c2", 256, 256, 3, 1, 1, 14), ("l3.ds", 128, 256, 1, 2, 0, 28), ("l4.c1", 256, 512, 3, 2, 1, 14),
+    ("l4.c2", 512, 512, 3, 1, 1, 7), ("l4.ds", 256, 512, 1, 2, 0, 14)]
+COUNT = {"conv1": 1, "l1.c": 4, "l2.c1": 1, "l2.c2": 3, "l2.ds": 1, "l3.c1": 1, "l3.c2": 3, "l3.ds": 1, "l4.c1": 1,
+         "l4.c2": 3, "l4.ds": 1}
+MODES = {"w1u": (4, 3, False), "none": (4, 3, True), "w2s": (3, 4, True), "w2u": (3, 4, False),
+         "lut": (2, 5, False), "w2s2": (2, 5, True)}
+
+
+def grid(rng, E, M, shape, bias, zero_frac):
+    emax = 2 ** E - 1
+    expo = rng.integers(max(0, emax - 8), emax + 1, size=shape)
+    mant = rng.integers(0, 2 ** M, size=shape)
+    v = np.where(expo == 0, np.ldexp(mant / 2 ** M, 1 - bias), np.ldexp(1.0 + mant / 2 ** M, expo - bias))
+    v = v * rng.choice([-1.0, 1.0], size=shape)
+    v[rng.random(shape) < zero_frac] = 0.0
+    return torch.from_numpy(v.astype(np.float32))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--mode", default="w1u", choices=sorted(MODES))
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--layers", default="")
+    args = ap.parse_args()
+    import fp8_quantization_amd as fa
+    from fp8_quantization_amd.error_tables import get_error_table_NN
+    dev = "cuda:0"
+    E, M, wc = MODES[args.mode]
+    tab = get_error_table_NN(E, M, wc, 3)
+    fl = fa.make_flags(with_approx=True, with_s2nn2s_opt=True, quant_btw_mult_accu=True)
+    rng = np.random.default_rng(0)
+    tot_t, tot_mac = 0.0, 0
+    for (name, cin, cout, k, s, p, h) in RESNET18:
+        if args.layers and name not in args.layers.split(","):
+            continue
+        x = grid(rng, E, M, (args.batch, cin, h, h), 2 ** (E - 1) + 3, 0.5).to(dev)
+        w = grid(rng, E, M, (cout, cin, k, k), 2 ** (E - 1) + 8, 0.0).to(dev)
+        bW = torch.full((cout,), 2 ** (E - 1) + 8, dtype=torch.int32, device=dev)
+        args_ = dict(flags=fl, stride=(s, s), padding=(p, p))
+        y = fa.approx_conv2d(x, w, E, M, 2 ** (E - 1) + 3, bW, 2 ** (E - 1) + 6, tab, **args_)
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(args.reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            fa.approx_conv2d(x, w, E, M, 2 ** (E - 1) + 3, bW, 2 ** (E - 1) + 6, tab, **args_)
+            b.record()
+            b.synchronize()
+            ts.append(a.elapsed_time(b) / 1e3)
+        t = float(np.median(ts))
+        macs = y.shape[0] * y.shape[2] * y.shape[3] * cout * cin * k * k
+        tot_t += t * COUNT[name]
+        tot_mac += macs * COUNT[name]
+        print(json.dumps(dict(layer=name, M=y.shape[0] * y.shape[2] * y.shape[3], K=cin * k * k, N=cout,
+                              ms=t * 1e3, tmacs=macs / t / 1e12)), flush=True)
+    print(json.dumps(dict(total_ms=tot_t * 1e3, tmacs=tot_mac / tot_t / 1e12, mode=args.mode,
+                          lib=os.environ.get("FP8A_LIB_PATH", "default"))), flush=True)
+
+
+if __name__ == "__main__":
+    main()
