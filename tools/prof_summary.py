@@ -1,0 +1,74 @@
+#!/usr/bin/env python
+"""Summarise rocprofv3 CSV output for the approx GEMM kernel (profiles/ evidence).
+
+    python tools/prof_summary.py --trace DIR/..._kernel_trace.csv --stats DIR/..._kernel_stats.csv \
+        [--pmc DIR/..._counter_collection.csv ...] --timed-launches N --out profiles/rocprof_r01
+
+Writes <out>.json (machine-readable) and <out>.txt (human-readable).  The timed-region
+average takes the LAST N dispatches of gemm_fast_kernel (bench.py's timed steps come last).
+PMC counters are averaged per dispatch of gemm_fast_kernel; HBM traffic per launch =
+(FETCH_SIZE + WRITE_SIZE) * 1024 bytes -- rocprofv3's KB units; on gfx950 FETCH_SIZE is
+calibrated only for 16-B-per-lane streaming reads (MI355X_MICROARCH.md §HBM), these loads
+are 4 B per lane, so the read side is reported raw and marked uncalibrated.
+"""
+import argparse
+import collections
+import csv
+import json
+
+KERNEL = "gemm_fast_kernel"
+
+
+def read_csv(path):
+    with open(path, newline="") as f:
+        return list(csv.DictReader(f))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--trace", required=True)
+    ap.add_argument("--stats")
+    ap.add_argument("--pmc", nargs="*", default=[])
+    ap.add_argument("--timed-launches", type=int, required=True)
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--note", default="")
+    a = ap.parse_args()
+
+    rows = [r for r in read_csv(a.trace) if KERNEL in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    timed = rows[-a.timed_launches:]
+    durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in timed]
+    res = dict(kernel=KERNEL, all_dispatches=len(rows), timed_dispatches=len(timed),
+               timed_avg_ns=sum(durs) / max(1, len(durs)), timed_total_ns=sum(durs),
+               vgpr=timed[-1]["VGPR_Count"] if timed else None, lds=timed[-1]["LDS_Block_Size"] if timed else None,
+               note=a.note)
+    if a.stats:
+        res["stats_top"] = [dict(name=r["Name"][:120], calls=int(r["Calls"]), avg_ns=float(r["AverageNs"]),
+                                 pct=float(r["Percentage"])) for r in read_csv(a.stats)[:8]]
+    counters = collections.defaultdict(list)
+    for p in a.pmc:
+        for r in read_csv(p):
+            if KERNEL in r.get("Kernel_Name", ""):
+                counters[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    if counters:
+        res["pmc_avg_per_dispatch"] = {k: sum(v) / len(v) for k, v in counters.items()}
+        pm = res["pmc_avg_per_dispatch"]
+        if "FETCH_SIZE" in pm and "WRITE_SIZE" in pm:
+            res["gemm_fast_bytes_per_launch"] = (pm["FETCH_SIZE"] + pm["WRITE_SIZE"]) * 1024.0
+            res["traffic_note"] = "FETCH_SIZE uncalibrated for 4-byte-per-lane loads (raw KB x 1024)"
+        if "SQ_INSTS_VALU" in pm and "SQ_WAVES" in pm:
+            res["valu_instr_per_wave"] = pm["SQ_INSTS_VALU"] / pm["SQ_WAVES"]
+    with open(a.out + ".json", "w") as f:
+        json.dump(res, f, indent=1)
+    with open(a.out + ".txt", "w") as f:
+        f.write(f"rocprofv3 summary, {KERNEL}\n{a.note}\n")
+        for k, v in res.items():
+            if k != "stats_top":
+                f.write(f"{k}: {v}\n")
+        for s in res.get("stats_top", []):
+            f.write(f"  {s['pct']:6.2f}%  {s['calls']:6d} calls  {s['avg_ns'] / 1e3:10.1f} us avg  {s['name']}\n")
+    print(json.dumps({k: v for k, v in res.items() if k != "stats_top"}))
+
+
+if __name__ == "__main__":
+    main()
