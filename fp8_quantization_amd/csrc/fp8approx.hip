@@ -228,32 +228,49 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = 0.0f;
 
-    for (int64_t k0 = 0; k0 < p.K; k0 += BK) {
-        bool bad = !bias_ok;
-        // ---- stage A (64 x 16)
+    // per-thread staging slots (fixed across k tiles)
+    int arow[(BM * BK) / NT], akk[(BM * BK) / NT];
+#pragma unroll
+    for (int r = 0; r < (BM * BK) / NT; ++r) {
+        const int e = tid + NT * r;
+        arow[r] = p.conv ? (tid & 63) : (e >> 4);       // conv: lanes along m (consecutive pixels)
+        akk[r] = p.conv ? ((tid >> 6) + 4 * r) : (e & 15);  // matrix: lanes along k (row-major A)
+    }
+    float xa[(BM * BK) / NT], xb[(BN * BK) / NT];
+    // global -> registers for the tile at k0 (issued one tile ahead of its use)
+    auto load_tile = [&](int64_t k0) {
 #pragma unroll
         for (int r = 0; r < (BM * BK) / NT; ++r) {
-            int row, kk;
             float x = 0.0f;
-            if (!p.conv) {  // matrix A: lanes along k (row-major A is k-contiguous)
-                const int e = tid + NT * r;
-                row = e >> 4;
-                kk = e & 15;
-                const int64_t m = m0 + row, k = k0 + kk;
+            const int64_t k = k0 + akk[r];
+            if (!p.conv) {
+                const int64_t m = m0 + arow[r];
                 if (m < p.M && k < p.K) x = p.A[m * p.lda + k];
-            } else {        // implicit im2col: lanes along m (consecutive output pixels)
-                row = tid & 63;
-                kk = (tid >> 6) + 4 * r;
-                const int64_t k = k0 + kk;
-                if (crow_ok && k < p.K) {
-                    const uint32_t c = fastdiv((uint32_t)k, p.kk_mul, p.kk_shift);
-                    const uint32_t t = (uint32_t)k - c * (uint32_t)(p.kh * p.kw);
-                    const uint32_t ky = fastdiv(t, p.kw_mul, p.kw_shift);
-                    const uint32_t kx = t - ky * (uint32_t)p.kw;
-                    const int64_t hi = chi0 + (int64_t)ky * p.dh, wi = cwi0 + (int64_t)kx * p.dw;
-                    if (hi >= 0 && hi < p.H && wi >= 0 && wi < p.W) x = p.X[cxoff + ((int64_t)c * p.H + hi) * p.W + wi];
-                }
+            } else if (crow_ok && k < p.K) {  // implicit im2col
+                const uint32_t c = fastdiv((uint32_t)k, p.kk_mul, p.kk_shift);
+                const uint32_t t = (uint32_t)k - c * (uint32_t)(p.kh * p.kw);
+                const uint32_t ky = fastdiv(t, p.kw_mul, p.kw_shift);
+                const uint32_t kx = t - ky * (uint32_t)p.kw;
+                const int64_t hi = chi0 + (int64_t)ky * p.dh, wi = cwi0 + (int64_t)kx * p.dw;
+                if (hi >= 0 && hi < p.H && wi >= 0 && wi < p.W) x = p.X[cxoff + ((int64_t)c * p.H + hi) * p.W + wi];
             }
+            xa[r] = x;
+        }
+#pragma unroll
+        for (int r = 0; r < (BN * BK) / NT; ++r) {
+            const int64_t n = n0 + bcol[r], k = k0 + bkk[r];
+            xb[r] = (n < p.N && k < p.K) ? p.B[k * p.sbk + n * p.sbn] : 0.0f;
+        }
+    };
+    load_tile(0);
+
+    for (int64_t k0 = 0; k0 < p.K; k0 += BK) {
+        bool bad = !bias_ok;
+        // ---- decode + stage A (64 x 16)
+#pragma unroll
+        for (int r = 0; r < (BM * BK) / NT; ++r) {
+            const int row = arow[r], kk = akk[r];
+            const float x = xa[r];
             float c;
             uint32_t mc;
             bad |= !stage_decode(x, M, emnA, S2N, c, mc);
@@ -268,12 +285,11 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
                 }
             }
         }
-        // ---- stage B (16 x 64)
+        // ---- decode + stage B (16 x 64)
 #pragma unroll
         for (int r = 0; r < (BN * BK) / NT; ++r) {
             const int col = bcol[r], kk = bkk[r];
-            const int64_t n = n0 + col, k = k0 + kk;
-            const float x = (n < p.N && k < p.K) ? p.B[k * p.sbk + n * p.sbn] : 0.0f;
+            const float x = xb[r];
             float c;
             uint32_t mc;
             bad |= !stage_decode(x, M, emnB[r], S2N, c, mc);
@@ -287,6 +303,7 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
         // exact kernel that follows on the stream then recomputes the whole product.
         const int anybad = __syncthreads_or(bad ? 1 : 0);
         if (anybad && tid == 0) atomicOr(p.flag, 1u);
+        if (k0 + BK < p.K) load_tile(k0 + BK);  // next tile's loads fly during this tile's math
 
         float tacc[TM][TN];  // per-k-tile partial sums (two-level accumulation)
 #pragma unroll
@@ -323,21 +340,24 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j) {
-                        const float g = a[i] * b[j];
+                        // v0 = a*b - t*cA*cB is exactly representable, so one
+                        // fused op yields it; g = a*b is formed only where a mask needs it.
                         const float cab = ac[i] * bc[j];
-                        float v0;
+                        float tc;  // t * cA * cB
                         if (TMODE == TM_W1U) {
                             const int t = __builtin_amdgcn_sbfe((int)ar0[i], bm[j], 1);
-                            v0 = g - __uint_as_float(__float_as_uint(cab) & (uint32_t)t);
+                            tc = __uint_as_float(__float_as_uint(cab) & (uint32_t)t);
                         } else if (TMODE == TM_LUT) {
-                            const float t = sLut[ar0[i] + bm[j]];
-                            v0 = __fmaf_rn(-t, cab, g);
+                            tc = sLut[ar0[i] + bm[j]] * cab;
                         } else {
                             const uint32_t w = (R == 2 && (bm[j] & 32u)) ? ar1[i] : ar0[i];
                             const int t = SGN ? __builtin_amdgcn_sbfe((int)w, bm[j], 2)
                                               : (int)__builtin_amdgcn_ubfe(w, bm[j], 2);
-                            v0 = __fmaf_rn(-(float)t, cab, g);
+                            tc = (float)t * cab;
                         }
+                        float v0 = __fmaf_rn(a[i], b[j], -tc);
+                        constexpr bool NEED_G = !S2N || (QBMA && SGN);
+                        const float g = NEED_G ? a[i] * b[j] : 0.0f;
                         if (!S2N) v0 = (fabsf(g) >= qc.mnR) ? v0 : g;  // norm mask, v9:87
                         if (S2N && QBMA && SGN) v0 = (g < 0.0f && g >= -qc.thr) ? fabsf(v0) : v0;  // F7
                         tacc[i][j] += QBMA ? q_fast<GCLIP>(v0, qc) : v0;

@@ -122,8 +122,9 @@ __device__ __forceinline__ float exact_term(float a, float b, const DFmt &fA, co
 //   r     = ((min(|x|, bound) + C) - C),  C = 2^(max(e, e_min) + 23 - M)   (RNE at `step`)
 struct QC {
     uint32_t emn;   // exponent field of 2^(1 - bR)
-    uint32_t kb;    // ((2^M - 1) << (23 - M)) - 1
-    uint32_t kc;    // (23 - M) << 23
+    float kb;       // (2 - 2^-M - 2^-22): bound = 2^e * kb sits in (max - step/2, max] of binade e
+    float kc;       // 2^(23 - M): C = 2^max(e, e_min) * kc has ulp(C) = step
+    float cmin;     // 2^(e_min) * kc
     float maxnorm;  // max_norm(bR) (golden_clip_OF)
     float mnR;      // min_norm(bR)
     float thr;      // largest |g| that Q_R flushes to 0: 2^(-bR - M)
@@ -132,24 +133,25 @@ struct QC {
 __device__ __forceinline__ QC make_qc(int E, int M, int bR) {
     QC q;
     q.emn = (uint32_t)(127 + 1 - bR) << 23;
-    q.kb = ((((1u << M) - 1u)) << (23 - M)) - 1u;
-    q.kc = (uint32_t)(23 - M) << 23;
+    q.kb = 2.0f - p2(-M) - p2(-22);
+    q.kc = p2(23 - M);
+    q.cmin = p2(1 - bR + 23 - M);
     q.maxnorm = ldexpf(2.0f - p2(-M), (1 << E) - 1 - bR);
     q.mnR = p2(1 - bR);
     q.thr = p2(-bR - M);
     return q;
 }
 
+// All intermediate floats come out of float arithmetic (canonical), so min/max need no
+// canonicalisation: 8 VALU ops (and, mul, min, mul, max, add, sub, bfi).
 template <bool GCLIP>
 __device__ __forceinline__ float q_fast(float x, const QC &q) {
-    // |x| and the bound are non-negative floats: compare them as integers (no canonicalisation)
-    uint32_t xa = __float_as_uint(x) & 0x7FFFFFFFu;
-    if (GCLIP) xa = min(xa, __float_as_uint(q.maxnorm));  // clip_OF first: step from the clipped binade
-    const uint32_t ex = GCLIP ? (xa & 0x7F800000u) : (__float_as_uint(x) & 0x7F800000u);
-    xa = min(xa, ex + q.kb);
-    const uint32_t ee = max(ex, q.emn);
-    const float c = __uint_as_float(ee + q.kc);
-    const float r = (__uint_as_float(xa) + c) - c;
+    float xa = fabsf(x);
+    if (GCLIP) xa = fminf(xa, q.maxnorm);  // clip_OF first: the step comes from the clipped binade
+    const float pe = __uint_as_float(__float_as_uint(GCLIP ? xa : x) & 0x7F800000u);  // 2^floor(log2|x|)
+    xa = fminf(xa, pe * q.kb);
+    const float c = fmaxf(pe * q.kc, q.cmin);
+    const float r = (xa + c) - c;
     return copysignf(r, x);
 }
 
