@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--cal-batch", type=int, default=64)
     ap.add_argument("--with-comp", action="store_true", help="withComp=True (E4M3: all-zero error table)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-columns", type=int, default=2, help="output columns per layer in the CPU sample")
+    ap.add_argument("--cpu-columns", type=int, default=48, help="output columns per layer in the CPU sample")
     ap.add_argument("--arch", default="resnet18", choices=["resnet18", "resnet50"])
     return ap.parse_args()
 
@@ -80,15 +80,16 @@ def cpu_baseline(shapes, table, cols):
         if key not in cache:
             A = port._q(torch.randn((Mi, K), generator=g).relu(), fa, True)
             B = port._q(torch.randn((K, cols), generator=g) * 0.05, fb, True)
+            nc = min(cols, N)
             t0 = time.perf_counter()
-            for c in range(cols):
+            for c in range(nc):
                 port.column(A, B[:, c:c + 1], 4, 3, 12, 19, 15, table, approx=True, s2n=True, qbma=True)
-            dt = (time.perf_counter() - t0) / cols
+            dt = (time.perf_counter() - t0) / nc
             cache[key] = dt
-            measured += dt * cols
+            measured += dt * nc
         per_img += cache[key] * N * groups
     return dict(value=1.0 / per_img, unit="images/s", cores=threads, kind="port",
-                sample=(f"1 image: {cols} output columns of each of {len(cache)} distinct approx layer shapes "
+                sample=(f"1 image: up to {cols} output columns of each of {len(cache)} distinct approx layer shapes "
                         f"(torch port of the v9 op sequence, {measured:.1f} s measured), scaled by each layer's "
                         f"output-column count; {per_img:.1f} s/img projected"))
 
@@ -106,6 +107,7 @@ def main():
 
     import fp8_quantization_amd as fa
     from fp8_quantization_amd import approx_ops as am
+    from fp8_quantization_amd.distributed import broadcast_quant_state, gather_logits
     from fp8_quantization_amd.error_tables import get_error_table_NN
     from fp8_quantization_amd.resnet_workload import (approx_layer_shapes, approx_macs_per_image, resnet18_approx,
                                                       resnet50_approx)
@@ -125,16 +127,13 @@ def main():
         model.fix_ranges()
         for h in hooks:
             h.remove()
+        broadcast_quant_state(model, src=0)  # identical bA/bB/bR on every rank
     macs_img = approx_macs_per_image(shapes)
 
-    x = synthetic_images(args.batch, 10 + rank, dev)
-    gathered = torch.empty((world * args.batch, 1000), device=dev) if world > 1 else None
+    x = synthetic_images(args.batch, 10 + rank, dev)  # this rank's shard of the validation batch
 
     def step():
-        logits = model(x)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, logits.contiguous())
-        return logits
+        return gather_logits(model(x))  # one RCCL all-gather of logits per step (N > 1)
 
     with torch.no_grad():
         for _ in range(args.warmup):
