@@ -372,23 +372,48 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
     }
 
     // ---- epilogue
+    const int64_t nb = n0 + tx * TN;
+    if (!p.nchw) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-        const int64_t m = m0 + ty * TM + i;
-        if (m >= p.M) continue;
-        const int64_t nb = n0 + tx * TN;
-        if (!p.nchw && nb + TN <= p.N && ((p.ldc & 3) == 0) && ((((uintptr_t)p.C) & 15) == 0)) {
-            *reinterpret_cast<float4 *>(&p.C[m * p.ldc + nb]) = make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
-        } else {
+        for (int i = 0; i < TM; ++i) {
+            const int64_t m = m0 + ty * TM + i;
+            if (m >= p.M) continue;
+            if (nb + TN <= p.N && ((p.ldc & 3) == 0) && ((((uintptr_t)p.C) & 15) == 0)) {
+                *reinterpret_cast<float4 *>(&p.C[m * p.ldc + nb]) =
+                    make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    if (nb + j < p.N) p.C[m * p.ldc + nb + j] = acc[i][j];
+            }
+        }
+    } else {
+        // NCHW: the thread's 4 rows are 4 consecutive pixels; when they lie in one image and
+        // start 16-B aligned, each output channel gets one float4 store.
+        const int64_t mb = m0 + ty * TM;
+        const int64_t img = mb / p.hw, pix = mb - img * p.hw;
+        const bool vec = (pix + TM <= p.hw) && (mb + TM <= p.M) && ((p.hw & 3) == 0) &&
+                         ((((uintptr_t)p.C) & 15) == 0);
+        if (vec) {
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-                if (nb + j < p.N) p.C[out_index(p, m, nb + j)] = acc[i][j];
+                if (nb + j < p.N)
+                    *reinterpret_cast<float4 *>(&p.C[(img * p.ctot + p.coff + nb + j) * p.hw + pix]) =
+                        make_float4(acc[0][j], acc[1][j], acc[2][j], acc[3][j]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int64_t m = mb + i;
+                if (m >= p.M) continue;
+                const int64_t im = m / p.hw, px = m - im * p.hw;
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    if (nb + j < p.N) p.C[(im * p.ctot + p.coff + nb + j) * p.hw + px] = acc[i][j];
+            }
         }
     }
 }
 
-// Exact (reference-order) kernel: one thread per output (m, n), every term via exact_term.
-// Used for the tensor-bias (single-column) semantics and as the reference-path check.
 // A(m, k) for the exact kernels: matrix or implicit im2col.
 __device__ __forceinline__ float load_A(const GemmArgs &p, int64_t m, int64_t k) {
     if (!p.conv) return p.A[m * p.lda + k];

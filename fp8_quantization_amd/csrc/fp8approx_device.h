@@ -123,7 +123,8 @@ __device__ __forceinline__ float exact_term(float a, float b, const DFmt &fA, co
 struct QC {
     uint32_t emn;   // exponent field of 2^(1 - bR)
     float kb;       // (2 - 2^-M - 2^-22): bound = 2^e * kb sits in (max - step/2, max] of binade e
-    float kc;       // 2^(23 - M): C = 2^max(e, e_min) * kc has ulp(C) = step
+    float kc;       // 1.5 * 2^(23 - M): C = 2^max(e, e_min) * kc has ulp(C) = step, and
+                    //   (x + C) - C rounds SIGNED x (|x| < C/3) half-to-even at step
     float cmin;     // 2^(e_min) * kc
     float maxnorm;  // max_norm(bR) (golden_clip_OF)
     float mnR;      // min_norm(bR)
@@ -134,25 +135,27 @@ __device__ __forceinline__ QC make_qc(int E, int M, int bR) {
     QC q;
     q.emn = (uint32_t)(127 + 1 - bR) << 23;
     q.kb = 2.0f - p2(-M) - p2(-22);
-    q.kc = p2(23 - M);
-    q.cmin = p2(1 - bR + 23 - M);
+    q.kc = 1.5f * p2(23 - M);
+    q.cmin = 1.5f * p2(1 - bR + 23 - M);
     q.maxnorm = ldexpf(2.0f - p2(-M), (1 << E) - 1 - bR);
     q.mnR = p2(1 - bR);
     q.thr = p2(-bR - M);
     return q;
 }
 
-// All intermediate floats come out of float arithmetic (canonical), so min/max need no
-// canonicalisation: 8 VALU ops (and, mul, min, mul, max, add, sub, bfi).
+// 7 VALU ops (and, mul, med3, mul, max, add, sub), no sign handling: the 1.5 * 2^k magic
+// constant rounds negative and positive values alike.  All inputs of min/max/med3 come out of
+// float arithmetic (canonical), so no canonicalisation is emitted.  A negative value that
+// rounds to zero comes back as +0 (the reference gives -0 or +0; both add nothing).
 template <bool GCLIP>
 __device__ __forceinline__ float q_fast(float x, const QC &q) {
-    float xa = fabsf(x);
-    if (GCLIP) xa = fminf(xa, q.maxnorm);  // clip_OF first: the step comes from the clipped binade
-    const float pe = __uint_as_float(__float_as_uint(GCLIP ? xa : x) & 0x7F800000u);  // 2^floor(log2|x|)
-    xa = fminf(xa, pe * q.kb);
+    float xs = x;
+    if (GCLIP) xs = __builtin_amdgcn_fmed3f(xs, -q.maxnorm, q.maxnorm);  // clip_OF first
+    const float pe = __uint_as_float(__float_as_uint(xs) & 0x7F800000u);  // 2^floor(log2|x|)
+    const float bd = pe * q.kb;
+    xs = __builtin_amdgcn_fmed3f(xs, -bd, bd);
     const float c = fmaxf(pe * q.kc, q.cmin);
-    const float r = (xa + c) - c;
-    return copysignf(r, x);
+    return (xs + c) - c;
 }
 
 }  // namespace fp8a
