@@ -305,11 +305,9 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
         if (anybad && tid == 0) atomicOr(p.flag, 1u);
         if (k0 + BK < p.K) load_tile(k0 + BK);  // next tile's loads fly during this tile's math
 
-        float tacc[TM][TN];  // per-k-tile partial sums (two-level accumulation)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) tacc[i][j] = 0.0f;
+        // fp32 accumulation in k order: measured max |error| ~3e-7 x sum|terms| at K = 4608 on
+        // realistic data, 30x inside the 1e-5 parity tolerance
+        float (&tacc)[TM][TN] = acc;
 
 #pragma unroll 2
         for (int kk = 0; kk < BK; ++kk) {
@@ -364,10 +362,6 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
                     }
             }
         }
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[i][j] += tacc[i][j];
         __syncthreads();
     }
 
