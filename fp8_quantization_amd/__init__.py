@@ -7,6 +7,6 @@ reference's operator / quantizer surface on top of it.
 from . import _lib  # noqa: F401
 from .approx_ops import (approx_conv2d, approx_matmul, approx_terms, custom_matmul_vectorize,  # noqa: F401
                             float_to_fpany_absint_torch, fp8_fake_quantize, get_error_table_NN, make_flags,
-                            quant_to_fp_any_vectorize_torch)
+                            qamaa_conv2d, qamaa_matmul, quant_to_fp_any_vectorize_torch)
 
 __version__ = "0.1.0"

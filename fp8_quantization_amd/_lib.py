@@ -16,7 +16,7 @@ OK, EINVAL, EFORMAT, EHIP = 0, -1, -2, -3
 
 SYMBOLS = ("fp8a_version", "fp8a_last_error", "fp8a_decompose", "fp8a_quant", "fp8a_matmul_workspace_size",
            "fp8a_matmul", "fp8a_terms", "fp8a_conv2d_workspace_size", "fp8a_conv2d", "fp8a_im2col",
-           "fp8a_fp8_quantize")
+           "fp8a_fp8_quantize", "fp8a_matmul_qamaa", "fp8a_conv2d_qamaa")
 
 _lib = None
 
@@ -49,6 +49,8 @@ def load():
                         I),
         "fp8a_im2col": ([P, P, I64, I64, I64, I64, I, I, I, I, I, I, I, I, P], I),
         "fp8a_fp8_quantize": ([P, I64, I64, P, I, I, I, I, P, P, P, P], I),
+        "fp8a_matmul_qamaa": ([P, I64, P, I64, I64, P, I64, I64, I64, P, I, I, I, P], I),
+        "fp8a_conv2d_qamaa": ([P, P, P, I64, I64, I64, I64, I64, I, I, I, I, I, I, I, I, I, P, I, I, I, P], I),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -18,7 +18,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from . import _lib
-from .approx_ops import approx_conv2d, approx_matmul, make_flags
+from .approx_ops import _res_quant_params, approx_conv2d, approx_matmul, make_flags, qamaa_conv2d, qamaa_matmul
 from .error_tables import get_error_table_NN
 from .quantization.hijacker import QuantizationHijacker
 from .quantization.quantized_folded_bn import BNFusedHijacker
@@ -44,8 +44,8 @@ class ApproxOpMixin:
         # approx_calculation.py:766-767: a missing act/res bias falls back to 2^(E-1)
         return b if b is not None else torch.tensor([2 ** (E - 1)], dtype=torch.int32, device=device)
 
-    def _qamaa_unsupported(self):
-        raise NotImplementedError("quantize_after_mult_and_add (qamaa) is SURVEY §8(f) next-4; not built yet")
+    def _qamaa_params(self):
+        return _res_quant_params(self.res_quantizer)
 
     def approx_multiply(self, x, y, x_bias, y_bias, res_bias):
         """x [M, K] @ y [K, N] with the operator's approx configuration."""
@@ -55,8 +55,8 @@ class ApproxOpMixin:
         if y.shape[1] != 1:
             if self.approx_flag:
                 return approx_matmul(x, y, E, M, x_bias, y_bias.reshape(-1), res_bias, table, flags=flags)
-            if self.quantize_after_mult_and_add:
-                self._qamaa_unsupported()
+            if self.quantize_after_mult_and_add:  # approx_calculation.py:787-795
+                return qamaa_matmul(x, y, *self._qamaa_params())
             return x @ y
         if self.approx_flag:  # single column: biases stay tensors -> tensor-bias semantics (F5)
             return approx_matmul(x, y, E, M, x_bias, y_bias.reshape(-1), res_bias, table,
@@ -95,9 +95,10 @@ class ApproxConv2dMixin(ApproxOpMixin):
             out = approx_conv2d(x.detach(), weight.detach(), E, M, self._default_bias(a_bias, E, x.device),
                                 w_bias.reshape(-1), self._default_bias(r_bias, E, x.device), table, flags=flags,
                                 stride=self.stride, padding=self.padding, dilation=self.dilation, groups=self.groups)
-        else:
-            if self.quantize_after_mult_and_add and self.out_channels // self.groups != 1:
-                self._qamaa_unsupported()
+        elif self.quantize_after_mult_and_add and self.out_channels // self.groups != 1:
+            out = qamaa_conv2d(x.detach(), weight.detach(), *self._qamaa_params(), stride=self.stride,
+                               padding=self.padding, dilation=self.dilation, groups=self.groups)
+        else:  # exact product (also qamaa's single-column groups, approx_calculation.py:810-811)
             out = F.conv2d(x.detach(), weight.detach(), None, self.stride, self.padding, self.dilation, self.groups)
         if bias is not None:
             out += bias.view(1, -1, 1, 1)

@@ -18,7 +18,7 @@ import torch
 from . import _lib
 from .error_tables import get_error_table_NN  # noqa: F401  (re-exported, v9:555)
 
-__all__ = ["custom_matmul_vectorize", "approx_matmul", "approx_terms", "approx_conv2d",
+__all__ = ["custom_matmul_vectorize", "approx_matmul", "approx_terms", "approx_conv2d", "qamaa_matmul", "qamaa_conv2d",
            "quant_to_fp_any_vectorize_torch", "float_to_fpany_absint_torch", "get_error_table_NN",
            "make_flags", "fp8_fake_quantize"]
 
@@ -301,3 +301,55 @@ def fp8_fake_quantize(x, maxval, n_bits, mantissa_bits, sign_bits=1, per_row=Fal
     if per_row and rows > 1:
         bias = bias.view([-1] + [1] * (x.dim() - 1))
     return out, bias
+
+
+# ----------------------------------------------------------------------------------- qamaa
+def _res_quant_params(res_quantizer):
+    """(maxval device tensor, n_bits, mantissa bits, sign bits) of a res QuantizationManager /
+    FPQuantizer, as approx_multiply reads them (approx_calculation.py:790-794)."""
+    q = getattr(res_quantizer, "quantizer", res_quantizer)
+    mb = q.mantissa_bits
+    mb = int(torch.clamp(torch.round(torch.as_tensor(mb, dtype=torch.float32)), 1, q.n_bits - q.sign_bits).item()) \
+        if isinstance(mb, torch.Tensor) else int(mb)
+    return q.maxval, int(q.n_bits), mb, int(q.sign_bits)
+
+
+def qamaa_matmul(A, B, maxval, n_bits, mantissa_bits, sign_bits=1):
+    """quantize_after_mult_and_add: fq(sum_k fq(A[m,k] * B[k,n])) on the GPU."""
+    if A.dim() != 2 or B.dim() != 2 or A.shape[1] != B.shape[0]:
+        raise AssertionError(f"qamaa_matmul: shape mismatch {tuple(A.shape)} @ {tuple(B.shape)}")
+    L = _lib.load()
+    A, B = _as_f32(A), _as_f32(B)
+    if A.stride(1) != 1:
+        A = A.contiguous()
+    if B.stride(0) != 1 and B.stride(1) != 1:
+        B = B.contiguous()
+    mx = _as_f32(maxval).reshape(-1).to(A.device).contiguous()
+    C = torch.empty((A.shape[0], B.shape[1]), dtype=torch.float32, device=A.device)
+    ev = _prof_start()
+    rc = L.fp8a_matmul_qamaa(_lib.dev_ptr(A), A.stride(0), _lib.dev_ptr(B), B.stride(0), B.stride(1),
+                             _lib.dev_ptr(C), A.shape[0], B.shape[1], A.shape[1], _lib.dev_ptr(mx), int(n_bits),
+                             int(mantissa_bits), int(sign_bits), _lib.stream_ptr(A.device))
+    _lib.check(rc, "fp8a_matmul_qamaa")
+    _prof_end(ev, A.shape[0] * A.shape[1] * B.shape[1])
+    return C
+
+
+def qamaa_conv2d(x, w, maxval, n_bits, mantissa_bits, sign_bits=1, stride=(1, 1), padding=(0, 0),
+                 dilation=(1, 1), groups=1):
+    """Convolution form of qamaa (groups with > 1 output channel)."""
+    L = _lib.load()
+    x = _as_f32(x).contiguous()
+    w = _as_f32(w).contiguous()
+    Bn, Cin, H, W = x.shape
+    Cout, _, kh, kw = w.shape
+    Ho = (H + 2 * padding[0] - dilation[0] * (kh - 1) - 1) // stride[0] + 1
+    Wo = (W + 2 * padding[1] - dilation[1] * (kw - 1) - 1) // stride[1] + 1
+    mx = _as_f32(maxval).reshape(-1).to(x.device).contiguous()
+    y = torch.empty((Bn, Cout, Ho, Wo), dtype=torch.float32, device=x.device)
+    rc = L.fp8a_conv2d_qamaa(_lib.dev_ptr(x), _lib.dev_ptr(w), _lib.dev_ptr(y), Bn, Cin, H, W, Cout, kh, kw,
+                             stride[0], stride[1], padding[0], padding[1], dilation[0], dilation[1], groups,
+                             _lib.dev_ptr(mx), int(n_bits), int(mantissa_bits), int(sign_bits),
+                             _lib.stream_ptr(x.device))
+    _lib.check(rc, "fp8a_conv2d_qamaa")
+    return y

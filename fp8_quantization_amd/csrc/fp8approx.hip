@@ -40,7 +40,8 @@ static int hip_check(const char *what) {
 //   TM_W1U  : entries in {0,1}   -> 1 bit / entry, 2^M bits per row      (E4M3)
 //   TM_W2S/U: entries in [-2,1] / [0,3] -> 2 bits / entry, R = 2^M*2/32 words per row
 //   TM_LUT  : anything else -> float LUT in LDS (E2M5 no-comp: entries up to 5)
-enum TMode : int { TM_NONE = 0, TM_W1U = 1, TM_W2S1 = 2, TM_W2U1 = 3, TM_W2S2 = 4, TM_W2U2 = 5, TM_LUT = 6 };
+enum TMode : int { TM_NONE = 0, TM_W1U = 1, TM_W2S1 = 2, TM_W2U1 = 3, TM_W2S2 = 4, TM_W2U2 = 5, TM_LUT = 6,
+                   TM_QAMAA = 7 /* quantize_after_mult_and_add: term = fq(a*b), no decode */ };
 
 struct TablePack {
     uint32_t rows[64][2];  // packed rows for the bit modes (2^M <= 64)
@@ -111,6 +112,9 @@ struct GemmArgs {
     int64_t Cin, H, W, Ho, Wo, cbase;
     int kh, kw, sh, sw, ph, pw, dh, dw;
     uint32_t kk_mul, kk_shift, kw_mul, kw_shift;  // fast division by kh*kw and by kw
+    // qamaa: the res quantizer's FP8 fake quantizer (fp8_quantizer.py:97-173) per product
+    const float *qmax;
+    int qE, qM, qsign;
     TablePack tab;
 };
 
@@ -159,7 +163,8 @@ __device__ __forceinline__ bool stage_decode(float x, int M, uint32_t emn, bool 
 
 template <bool S2N, bool QBMA, bool GCLIP, int TMODE>
 __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
-    constexpr bool TBL = TMODE != TM_NONE;
+    constexpr bool QAMAA = TMODE == TM_QAMAA;
+    constexpr bool TBL = TMODE != TM_NONE && !QAMAA;
     constexpr int R = (TMODE == TM_W2S2 || TMODE == TM_W2U2) ? 2 : 1;
     constexpr bool SGN = (TMODE == TM_W2S1 || TMODE == TM_W2S2 || TMODE == TM_LUT);
 
@@ -179,8 +184,10 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
     const int64_t m0 = (bid % num_mt) * BM;   // consecutive blocks: same column tile, so the
     const int64_t n0 = (bid / num_mt) * BN;   // B tile is shared by the 8 XCDs' L2s
     const int M = p.Mw;
-    const int bA = *p.bA, bR = *p.bR;
+    const int bA = QAMAA ? 0 : *p.bA, bR = QAMAA ? 0 : *p.bR;
     const QC qc = make_qc(p.E, M, bR);
+    FQ fq;
+    if (QAMAA) fq = make_fq(*p.qmax, p.qE, p.qM, p.qsign);
     const uint32_t emnA = (uint32_t)(128 - bA) << 23;
     const float ulpM = p2(-M);
 
@@ -203,7 +210,7 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
         bcol[r] = b_ncontig ? (e & 63) : (e >> 4);
         bkk[r] = b_ncontig ? (e >> 6) : (e & 15);
         const int64_t n = n0 + bcol[r];
-        const int bb = (n < p.N) ? p.bB[n * p.bBs] : 0;
+        const int bb = (!QAMAA && n < p.N) ? p.bB[n * p.bBs] : 0;
         bias_ok = bias_ok && bb >= -100 && bb <= 100;
         emnB[r] = (uint32_t)(128 - bb) << 23;
     }
@@ -273,7 +280,7 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
             const float x = xa[r];
             float c;
             uint32_t mc;
-            bad |= !stage_decode(x, M, emnA, S2N, c, mc);
+            if (!QAMAA) bad |= !stage_decode(x, M, emnA, S2N, c, mc);
             sA[kk][row] = x;
             if (TBL) {
                 sAc[kk][row] = c * ulpM;  // the 2^-M of mult_result_mant's table term (v9:182)
@@ -292,7 +299,7 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
             const float x = xb[r];
             float c;
             uint32_t mc;
-            bad |= !stage_decode(x, M, emnB[r], S2N, c, mc);
+            if (!QAMAA) bad |= !stage_decode(x, M, emnB[r], S2N, c, mc);
             sB[kk][col] = x;
             if (TBL) {
                 sBc[kk][col] = c;
@@ -315,7 +322,12 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
             const float4 b4 = *reinterpret_cast<const float4 *>(&sB[kk][tx * TN]);
             const float a[TM] = {a4.x, a4.y, a4.z, a4.w};
             const float b[TN] = {b4.x, b4.y, b4.z, b4.w};
-            if (!TBL) {
+            if (QAMAA) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) tacc[i][j] += fq_fast(a[i] * b[j], fq);
+            } else if (!TBL) {
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -560,7 +572,8 @@ static void launch_fast_t(int mode, const GemmArgs &a, dim3 grid, hipStream_t s)
         case TM_W2U1: gemm_fast_kernel<S2N, QBMA, GCLIP, TM_W2U1><<<grid, NT, 0, s>>>(a); break;
         case TM_W2S2: gemm_fast_kernel<S2N, QBMA, GCLIP, TM_W2S2><<<grid, NT, 0, s>>>(a); break;
         case TM_W2U2: gemm_fast_kernel<S2N, QBMA, GCLIP, TM_W2U2><<<grid, NT, 0, s>>>(a); break;
-        default: gemm_fast_kernel<S2N, QBMA, GCLIP, TM_LUT><<<grid, NT, 0, s>>>(a); break;
+        case TM_LUT: gemm_fast_kernel<S2N, QBMA, GCLIP, TM_LUT><<<grid, NT, 0, s>>>(a); break;
+        default: gemm_fast_kernel<false, false, false, TM_QAMAA><<<grid, NT, 0, s>>>(a); break;
     }
 }
 
@@ -586,7 +599,10 @@ static int check_format(int E, int Mw) {
 constexpr size_t FLAG_BYTES = 256;  // workspace prefix holding the off-grid flag word
 
 // Fast tiled kernel + gated exact kernel (int-bias path), or the exact kernel alone (tb path).
+static int run_qamaa(GemmArgs &a, hipStream_t s);
+
 static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes, hipStream_t s) {
+    if (a.qmax) return run_qamaa(a, s);
     int rc = check_format(a.E, a.Mw);
     if (rc) return rc;
     if (a.M < 0 || a.N < 0 || a.K < 0) return fail(FP8A_EINVAL, "negative extent");
@@ -617,6 +633,22 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     if (rc) return rc;
     gemm_exact_kernel<<<eblocks, 256, 0, s>>>(a);
     return hip_check("fp8a gated exact gemm launch");
+}
+
+// qamaa: term = fq(a*b) (no operand decode: exact for any fp32 inputs), then fq(sum) in place.
+static int run_qamaa(GemmArgs &a, hipStream_t s) {
+    if (a.M < 0 || a.N < 0 || a.K < 0) return fail(FP8A_EINVAL, "negative extent");
+    if (a.M == 0 || a.N == 0) return FP8A_OK;
+    if (a.qM < 1 || a.qE < 1) return fail(FP8A_EFORMAT, "bad qamaa quantizer format");
+    if (!a.nchw && a.ldc != a.N) return fail(FP8A_EINVAL, "qamaa output must be dense");
+    if (a.K == 0) {
+        if (hipMemsetAsync(a.C, 0, (size_t)a.M * a.N * sizeof(float), s) != hipSuccess) return hip_check("fill");
+    } else {
+        launch_fast(TM_QAMAA, a, s);
+        int rc = hip_check("fp8a qamaa gemm launch");
+        if (rc) return rc;
+    }
+    return FP8A_OK;
 }
 
 }  // namespace fp8a
@@ -757,6 +789,50 @@ int fp8a_conv2d(const float *x, const float *w, float *y, int64_t Bn, int64_t Ci
         if (rc) return rc;
     }
     return FP8A_OK;
+}
+
+int fp8a_matmul_qamaa(const float *A, int64_t lda, const float *B, int64_t sbk, int64_t sbn, float *C, int64_t M,
+                      int64_t N, int64_t K, const float *maxval, int n_bits, int Mbits, int sign_bits,
+                      fp8a_stream_t stream) {
+    if (lda < K) return fail(FP8A_EINVAL, "leading dimension smaller than extent");
+    if (!A || !B || !C || !maxval) return fail(FP8A_EINVAL, "null pointer");
+    GemmArgs a = make_args(A, lda, B, sbk, sbn, C, N, M, N, K, 1, 1, nullptr, nullptr, 0, nullptr, 0);
+    a.qmax = maxval;
+    a.qM = Mbits;
+    a.qE = n_bits - sign_bits - Mbits;
+    a.qsign = sign_bits;
+    int rc = run_qamaa(a, (hipStream_t)stream);
+    if (rc) return rc;
+    return fp8a_fp8_quantize(C, 1, M * N, maxval, 0, n_bits, Mbits, sign_bits, C, nullptr, nullptr, stream);
+}
+
+int fp8a_conv2d_qamaa(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
+                      int64_t Cout, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw, int groups,
+                      const float *maxval, int n_bits, int Mbits, int sign_bits, fp8a_stream_t stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (groups <= 0 || Cout % groups != 0 || Cin % groups != 0) return fail(FP8A_EINVAL, "bad groups");
+    if (Cout / groups == 1)
+        return fail(FP8A_EINVAL, "single-output-channel groups take the exact product in the reference "
+                                 "(approx_calculation.py:810-811): not a qamaa launch");
+    const int64_t Ho = (H + 2 * ph - dh * (kh - 1) - 1) / sh + 1;
+    const int64_t Wo = (W + 2 * pw - dw * (kw - 1) - 1) / sw + 1;
+    if (Ho <= 0 || Wo <= 0) return fail(FP8A_EINVAL, "empty convolution output");
+    const int64_t cog = Cout / groups, cig = Cin / groups, Kg = cig * kh * kw, Mrows = Bn * Ho * Wo;
+    for (int g = 0; g < groups; ++g) {
+        GemmArgs a = make_args(nullptr, 0, w + g * cog * Kg, 1, Kg, y, 0, Mrows, cog, Kg, 1, 1, nullptr, nullptr, 0,
+                               nullptr, 0);
+        a.nchw = 1; a.hw = Ho * Wo; a.ctot = Cout; a.coff = g * cog;
+        a.conv = 1; a.X = x;
+        a.Cin = Cin; a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo; a.cbase = g * cig;
+        a.kh = kh; a.kw = kw; a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw; a.dh = dh; a.dw = dw;
+        fastdiv_params((uint32_t)(kh * kw), a.kk_mul, a.kk_shift);
+        fastdiv_params((uint32_t)kw, a.kw_mul, a.kw_shift);
+        a.qmax = maxval; a.qM = Mbits; a.qE = n_bits - sign_bits - Mbits; a.qsign = sign_bits;
+        int rc = run_qamaa(a, s);
+        if (rc) return rc;
+    }
+    return fp8a_fp8_quantize(y, 1, Bn * Cout * Ho * Wo, maxval, 0, n_bits, Mbits, sign_bits, y, nullptr, nullptr,
+                             stream);
 }
 
 int fp8a_fp8_quantize(const float *x, int64_t rows, int64_t inner, const float *maxval, int per_row, int n_bits,

@@ -158,4 +158,30 @@ __device__ __forceinline__ float q_fast(float x, const QC &q) {
     return (xs + c) - c;
 }
 
+// quantize_to_fp8_ste_MM (fp8_quantizer.py:97-173) as the qamaa per-product quantizer, for a
+// per-tensor maxval: xc = clamp(x, [-]maxval, maxval); step = 2^(max(floor(log2|xc|), 1-bias) - M);
+// round half-even; unlike Q_R the rounding MAY carry into the next binade.  6 VALU ops.
+struct FQ {
+    float lo, hi;   // clamp range
+    float kc;       // 1.5 * 2^(23 - M)
+    float cmin;     // 1.5 * 2^(1 - bias + 23 - M)
+};
+
+__device__ __forceinline__ FQ make_fq(float mx, int E, int M, int sign_bits) {
+    FQ f;
+    const float bias = rintf((float)(1 << E) - log2f(mx) + log2f(2.0f - p2(-M)) - 1.0f);
+    f.hi = mx;
+    f.lo = sign_bits ? -mx : 0.0f;
+    f.kc = 1.5f * p2(23 - M);
+    f.cmin = 1.5f * p2((int)(1.0f - bias) + 23 - M);
+    return f;
+}
+
+__device__ __forceinline__ float fq_fast(float x, const FQ &f) {
+    const float xc = __builtin_amdgcn_fmed3f(x, f.lo, f.hi);
+    const float pe = __uint_as_float(__float_as_uint(xc) & 0x7F800000u);
+    const float c = fmaxf(pe * f.kc, f.cmin);
+    return (xc + c) - c;
+}
+
 }  // namespace fp8a

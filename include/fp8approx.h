@@ -101,6 +101,22 @@ int fp8a_conv2d(const float *x, const float *w, float *y, int64_t Bn, int64_t Ci
                 const int32_t *bR, const int32_t *table, uint32_t flags, void *workspace,
                 size_t workspace_bytes, fp8a_stream_t stream);
 
+/*
+ * quantize_after_mult_and_add (qamaa) path of approx_multiply (approx_calculation.py:787-795):
+ *   C = fq(sum_k fq(A[m,k] * B(k,n))),  fq = quantize_to_fp8_ste_MM with the res quantizer's
+ *   n_bits / mantissa bits / sign bits and per-tensor maxval (device float [1]).
+ * C is dense [M][N].  Exact for any fp32 inputs (no operand decode).
+ */
+int fp8a_matmul_qamaa(const float *A, int64_t lda, const float *B, int64_t sbk, int64_t sbn,
+                      float *C, int64_t M, int64_t N, int64_t K, const float *maxval, int n_bits,
+                      int Mbits, int sign_bits, fp8a_stream_t stream);
+/* Convolution form (groups with > 1 output channel; single-output-channel groups take the
+ * reference's exact product and are not launched here). */
+int fp8a_conv2d_qamaa(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H,
+                      int64_t W, int64_t Cout, int kh, int kw, int sh, int sw, int ph, int pw,
+                      int dh, int dw, int groups, const float *maxval, int n_bits, int Mbits,
+                      int sign_bits, fp8a_stream_t stream);
+
 /* The reference's im2col (approx_calculation.py:724-747): out [Bn*Ho*Wo, Cin*kh*kw]. */
 int fp8a_im2col(const float *x, float *out, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
                 int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw,

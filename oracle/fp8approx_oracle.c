@@ -178,6 +178,36 @@ void orc_matmul(const float *A, int64_t lda, const float *B, int64_t ldb, float 
     }
 }
 
+/* One quantize_to_fp8_ste_MM value (fp8_quantizer.py:111-154), bias given. */
+static float orc_fq1(float v, float mx, float bias, int M, int sign_bits) {
+    float xc = fminf(fmaxf(v, sign_bits ? -mx : 0.0f), mx);
+    int e;
+    frexpf(xc, &e);
+    float ls = (xc == 0.0f) ? 1.0f : fmaxf((float)(e - 1) + bias, 1.0f);
+    float sc = ldexpf(1.0f, (int)(ls - (float)M - bias));
+    return rintf(xc / sc) * sc;
+}
+
+static float orc_fq_bias(float mx, int E, int M) {
+    return rintf((float)(1 << E) - log2f(mx) + log2f(2.0f - ldexpf(1.0f, -M)) - 1.0f);
+}
+
+/* quantize_after_mult_and_add (approx_calculation.py:787-795): C = fq(sum_k fq(a*b)).
+ * The sum is accumulated in float32 in k order (the GPU kernel's order), so C is comparable
+ * bit for bit; Cpre (nullable) receives the pre-quantisation sums. */
+void orc_matmul_qamaa(const float *A, int64_t lda, const float *B, int64_t ldb, float *C, float *Cpre,
+                      int Mr, int N, int K, float mx, int n_bits, int M, int sign_bits) {
+    int E = n_bits - sign_bits - M;
+    float bias = orc_fq_bias(mx, E, M);
+    for (int m = 0; m < Mr; ++m)
+        for (int n = 0; n < N; ++n) {
+            float s = 0.0f;
+            for (int k = 0; k < K; ++k) s += orc_fq1(A[m * lda + k] * B[k * ldb + n], mx, bias, M, sign_bits);
+            if (Cpre) Cpre[m * N + n] = s;
+            C[m * N + n] = orc_fq1(s, mx, bias, M, sign_bits);
+        }
+}
+
 /* quantize_to_fp8_ste_MM forward value (fp8_quantizer.py:97-173) for a per-tensor or
  * per-row maxval: bias = round(2^E - log2(maxval) + log2(2 - 2^-M) - 1), then
  * round-half-even onto the grid 2^(max(floor(log2|x|)+bias, 1) - M - bias).

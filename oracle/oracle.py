@@ -35,6 +35,8 @@ def lib():
         L.orc_terms.argtypes = [P, I64, P, I64, P, I, I, I, I, I, I, P, I, P, U]
         L.orc_matmul.argtypes = [P, I64, P, I64, P, I64, I, I, I, I, I, I, P, I, P, U, P]
         L.orc_fp8_fake_quant.argtypes = [P, I64, I64, P, I, I, I, P, P]
+        L.orc_matmul_qamaa.argtypes = [P, I64, P, I64, P, P, I, I, I, ctypes.c_float, I, I, I]
+        L.orc_matmul_qamaa.restype = None
         for f in (L.orc_decompose, L.orc_quant, L.orc_terms, L.orc_matmul, L.orc_fp8_fake_quant):
             f.restype = None
         _lib = L
@@ -111,3 +113,15 @@ def fp8_fake_quant(x, maxval, E, M, per_row=False):
     lib().orc_fp8_fake_quant(x2.ctypes.data, rows, x2.shape[1], mx.ctypes.data, int(per_row), E, M,
                              out.ctypes.data, bias.ctypes.data)
     return out.reshape(x.shape), bias
+
+
+def matmul_qamaa(A, B, maxval, n_bits, M, sign_bits=1):
+    """(C, Cpre): fq(sum fq(a*b)) with float32 k-order sums, and the sums before the final fq."""
+    A, B = _f32(A), _f32(B)
+    Mr, K = A.shape
+    N = B.shape[1]
+    C = np.empty((Mr, N), np.float32)
+    Cp = np.empty((Mr, N), np.float32)
+    lib().orc_matmul_qamaa(A.ctypes.data, K, B.ctypes.data, N, C.ctypes.data, Cp.ctypes.data, Mr, N, K,
+                           float(maxval), n_bits, M, sign_bits)
+    return C, Cp

@@ -272,6 +272,38 @@ def gen_g4():
     return meta
 
 
+# ----------------------------------------------------------------------------- G6
+class _FakeResQ:
+    """The attributes approx_multiply's qamaa branch reads (approx_calculation.py:790-794)."""
+
+    def __init__(self, maxval, M):
+        self.quantizer = types.SimpleNamespace(n_bits=8, maxval=torch.tensor([maxval]),
+                                               mantissa_bits=torch.tensor([float(M)]), sign_bits=1)
+
+
+def gen_g6():
+    """quantize_after_mult_and_add: per-product FP8 fake quant, sum, fake quant."""
+    out, meta = {}, []
+    for (E, M), (bA, bB, bR) in G2_BIASES.items():
+        if (E, M) == (5, 2):
+            continue
+        fk = f"E{E}M{M}"
+        A = random_grid_tensor(E, M, bA, 48, 96, seed=21)
+        B = random_grid_tensor(E, M, bB, 96, 24, seed=22)
+        out[fk + "_A"], out[fk + "_B"] = A.numpy(), B.numpy()
+        for mx in (0.75, 3.0, 40.0):
+            op = _FakeOp(approx_params(E, M, 3, True, True, True, True), approx_flag=False)
+            op.quantize_after_mult_and_add = True
+            op.res_quantizer = _FakeResQ(mx, M)
+            C = ac.QCustomBNConv2dTorch.approx_multiply(op, A, B, torch.tensor([float(bA)]),
+                                                        torch.full((24,), float(bB)), torch.tensor([float(bR)]))
+            key = f"{fk}_mx{mx}"
+            out[key + "_C"] = C.numpy()
+            meta.append(dict(key=key, fmt=fk, E=E, M=M, maxval=mx))
+    np.savez_compressed(os.path.join(HERE, "g6_qamaa.npz"), **out)
+    return meta
+
+
 # ----------------------------------------------------------------------------- G5
 def qparams_for(E, M, approx_cfg, run_method):
     return dict(
@@ -349,7 +381,7 @@ def gen_g5():
 def main():
     torch.set_num_threads(os.cpu_count() or 1)
     meta = dict(torch_version=torch.__version__, reference="revollllt/FP8_quantization@2024-11-08",
-                g1=gen_g1(), g2=gen_g2(), g3=gen_g3(), g4=gen_g4(), g5=gen_g5())
+                g1=gen_g1(), g2=gen_g2(), g3=gen_g3(), g4=gen_g4(), g5=gen_g5(), g6=gen_g6())
     with open(os.path.join(HERE, "meta.json"), "w") as f:
         json.dump(meta, f, indent=1)
     sizes = {f: os.path.getsize(os.path.join(HERE, f)) for f in os.listdir(HERE) if f.endswith(".npz")}

@@ -291,3 +291,33 @@ def test_fp8_fake_quantize_matches_oracle(M):
     y1, b1 = fa().fp8_fake_quantize(t(x), t(mx[:1]), 8, M, per_row=False)
     yr1, br1 = orc.fp8_fake_quant(x, mx[:1], 7 - M, M, per_row=False)
     np.testing.assert_array_equal(y1.cpu().numpy().view(np.uint32), yr1.view(np.uint32))
+
+
+# ------------------------------------------------------------------------------ qamaa
+@pytest.mark.parametrize("case", META["g6"], ids=lambda c: c["key"])
+def test_qamaa_matmul(case):
+    """Bit-exact vs the oracle (same float32 k-order sums); vs the reference identical up to
+    one FP8 step where its torch-order sum straddles a rounding boundary (none in G6)."""
+    g = gio.load("g6_qamaa.npz")
+    A, B = g[case["fmt"] + "_A"], g[case["fmt"] + "_B"]
+    mx = torch.tensor([case["maxval"]], device=DEV)
+    C = fa().qamaa_matmul(t(A), t(B), mx, 8, case["M"]).cpu().numpy()
+    Cref, _ = orc.matmul_qamaa(A, B, case["maxval"], 8, case["M"])
+    np.testing.assert_array_equal(C, Cref)
+    np.testing.assert_array_equal(C, g[case["key"] + "_C"])
+
+
+@pytest.mark.parametrize("groups", [1, 2])
+def test_qamaa_conv2d(groups):
+    rng = np.random.default_rng(11 + groups)
+    x = _grid_operands(rng, 3, 4, 2 * 8, 100, 6, zero_frac=0.4).reshape(2, 8, 10, 10)
+    w = _grid_operands(rng, 3, 4, 12, (8 // groups) * 9, 8).reshape(12, 8 // groups, 3, 3)
+    y = fa().qamaa_conv2d(t(x), t(w), torch.tensor([2.5], device=DEV), 8, 4, stride=(1, 1), padding=(1, 1),
+                          groups=groups).cpu().numpy()
+    cols = _im2col_np(x, 3, 3, 1, 1, 1)
+    cog, Kg = 12 // groups, (8 // groups) * 9
+    for gi in range(groups):
+        Cref, _ = orc.matmul_qamaa(cols[:, gi * Kg:(gi + 1) * Kg], w[gi * cog:(gi + 1) * cog].reshape(cog, -1).T, 2.5,
+                                   8, 4)
+        got = y[:, gi * cog:(gi + 1) * cog].transpose(0, 2, 3, 1).reshape(-1, cog)
+        np.testing.assert_array_equal(got, Cref)

@@ -76,3 +76,20 @@ def test_g4_tensor_bias_terms_bitexact(case):
     np.testing.assert_array_equal(np.abs(T), np.abs(ref_T))
     C, S = orc.matmul(A, B, case["E"], case["M"], case["bA"], case["bB"], case["bR"], tab, fl, with_abs=True)
     assert np.all(np.abs(C - g[key + "_C"]) <= gio.sum_tolerance(S))
+
+
+@pytest.mark.parametrize("case", META["g6"], ids=lambda c: c["key"])
+def test_g6_qamaa(case):
+    """qamaa vs the reference: identical wherever the pre-quantisation sums agree; where the
+    reference's torch sum order and the k-order sum straddle an FP8 rounding boundary the
+    outputs may differ by one FP8 step (both are correct roundings of sums equal within
+    fp32 summation error)."""
+    g = gio.load("g6_qamaa.npz")
+    A, B = g[case["fmt"] + "_A"], g[case["fmt"] + "_B"]
+    C, Cpre = orc.matmul_qamaa(A, B, case["maxval"], 8, case["M"])
+    ref = g[case["key"] + "_C"]
+    diff = C != ref
+    assert diff.mean() < 0.02, diff.mean()
+    if diff.any():
+        step = np.ldexp(1.0, np.floor(np.log2(np.abs(ref[diff]) + 1e-30)).astype(int) - case["M"])
+        assert np.all(np.abs(C[diff] - ref[diff]) <= step * 1.0001)
