@@ -17,7 +17,7 @@ from .quantization.base_quantized_classes import QuantizedActivation, QuantizedM
 
 
 def approx_qparams(expo_width=4, mant_width=3, dnsmp_factor=3, withComp=False, with_approx=True,
-                   with_s2nn2s_opt=True, quant_btw_mult_accu=True, golden_clip_OF=False, n_bits=8):
+                   with_s2nn2s_opt=True, quant_btw_mult_accu=True, golden_clip_OF=False, n_bits=8, run_method=None):
     """qparams exactly as the reference scripts build them (utils/click_options.py:544-606,
     scripts/generated_scripts.py): per-channel current_minmax weights, allminmax activations,
     quantize_input, FP8 quantizer with set_maxval, approx + res_quantizer run method."""
@@ -32,8 +32,8 @@ def approx_qparams(expo_width=4, mant_width=3, dnsmp_factor=3, withComp=False, w
                                   sim_hw_add_OFUF=False, with_OF_opt=False, with_UF_opt=False,
                                   golden_clip_OF=golden_clip_OF, quant_btw_mult_accu=quant_btw_mult_accu,
                                   debug_mode=False, self_check_mode=False),
-        run_method=dict(approx_flag=True, quantize_after_mult_and_add=False, res_quantizer_flag=True,
-                        original_quantize_res=False))
+        run_method=dict(run_method) if run_method else dict(
+            approx_flag=True, quantize_after_mult_and_add=False, res_quantizer_flag=True, original_quantize_res=False))
 
 
 def _conv(qp, cin, cout, k, stride, pad, relu):

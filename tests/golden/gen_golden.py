@@ -323,8 +323,12 @@ def gen_g5():
     torch.manual_seed(2024)
     run_method = dict(approx_flag=True, quantize_after_mult_and_add=False,
                       res_quantizer_flag=True, original_quantize_res=False)
+    qamaa_rm = dict(approx_flag=False, quantize_after_mult_and_add=True, res_quantizer_flag=True,
+                    original_quantize_res=False)
     cases = [
         ("conv_e4m3_nocomp", (4, 3), dict(cin=8, cout=16, k=3, stride=1, pad=1, groups=1), False, True, True),
+        ("qamaa_conv_e3m4", (3, 4), dict(cin=6, cout=10, k=3, stride=1, pad=1, groups=1), False, True, True),
+        ("qamaa_linear_e4m3", (4, 3), dict(fin=20, fout=9), False, True, True),
         ("conv_e4m3_comp_s2", (4, 3), dict(cin=8, cout=16, k=3, stride=2, pad=1, groups=1), True, True, True),
         ("conv_e3m4_comp3", (3, 4), dict(cin=6, cout=12, k=3, stride=1, pad=0, groups=1), True, False, True),
         ("dwconv_e3m4_nocomp", (3, 4), dict(cin=8, cout=8, k=3, stride=1, pad=1, groups=8), False, True, True),
@@ -334,7 +338,8 @@ def gen_g5():
     ]
     for (name, (E, M), shp, wc, s2n, qbma) in cases:
         cfg = approx_params(E, M, 3, wc, True, s2n, qbma)
-        qp = qparams_for(E, M, cfg, dict(run_method))
+        rm = qamaa_rm if name.startswith("qamaa") else run_method
+        qp = qparams_for(E, M, cfg, dict(rm))
         if "fin" in shp:
             mod = ac.QCustomLinearTorch(in_features=shp["fin"], out_features=shp["fout"], bias=True, **qp)
             x_cal = torch.randn(6, shp["fin"])
@@ -372,7 +377,7 @@ def gen_g5():
         out[f"{name}__bA"] = mod.get_acts_fp_bias().reshape(-1).numpy()
         out[f"{name}__bB"] = mod.get_weights_fp_bias().reshape(-1).numpy()
         out[f"{name}__bR"] = mod.get_res_fp_bias().reshape(-1).numpy()
-        meta.append(dict(name=name, E=E, M=M, shape=shp, with_comp=wc, s2n=s2n, qbma=qbma,
+        meta.append(dict(name=name, E=E, M=M, shape=shp, with_comp=wc, s2n=s2n, qbma=qbma, run_method=rm,
                          state_keys=list(state.keys())))
     np.savez_compressed(os.path.join(HERE, "g5_operator.npz"), **out)
     return meta

@@ -33,7 +33,8 @@ def test_operator_estimate_fix_approx(case):
     g = gio.load("g5_operator.npz")
     name = case["name"]
     qp = approx_qparams(expo_width=case["E"], mant_width=case["M"], dnsmp_factor=3, withComp=case["with_comp"],
-                        with_s2nn2s_opt=case["s2n"], quant_btw_mult_accu=case["qbma"])
+                        with_s2nn2s_opt=case["s2n"], quant_btw_mult_accu=case["qbma"],
+                        run_method=case.get("run_method"))
     mod = _build(case, qp)
     state = {k: torch.from_numpy(g[f"{name}__state__{k}"]) for k in case["state_keys"]}
     missing, unexpected = mod.load_state_dict(state, strict=False)
