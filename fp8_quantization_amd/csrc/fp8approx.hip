@@ -3,10 +3,11 @@
 // Hot path: approx_v9 (revollllt/FP8_quantization, approx/approx_matmul_whole_v9.py:10-169)
 // as a register-blocked VALU GEMM.  The approximate product cannot use MFMA (its mantissa
 // product depends on a per-pair error table and a per-product re-quantisation), so the kernel
-// is VALU-bound: 128x64 output tile per 256-thread workgroup, 8x4 outputs per thread, K staged
+// is VALU-bound: 64x64 output tile per 256-thread workgroup, 4x4 outputs per thread, K staged
 // through LDS 16 deep.  Operands are decoded (sign / exponent / mantissa / table row) ONCE per
-// workgroup while staging; the inner loop costs ~10 VALU ops per product (14 with an error
-// table).  See DESIGN.md for the derivation and the exactness argument.
+// workgroup while staging; the inner loop costs 8 VALU ops per product without an error table,
+// 11 with the E4M3 table, 14 with E3M4/E2M5 compensation tables.  See DESIGN.md for the
+// derivation and the exactness argument.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -96,6 +97,8 @@ struct GemmArgs {
     int64_t ldc;
     int64_t M, N, K;
     int E, Mw;
+    uint32_t kexp, kdc;  // 0x7F800000 and (23 - Mw) << 23 as launch arguments: opaque SGPR operands
+                         // keep q_fast at one v_and_or_b32 / one v_add_u32 (see make_qc)
     const int32_t *bA;
     const int32_t *bB;
     int64_t bBs;
@@ -185,7 +188,7 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
     const int64_t n0 = (bid / num_mt) * BN;   // B tile is shared by the 8 XCDs' L2s
     const int M = p.Mw;
     const int bA = QAMAA ? 0 : *p.bA, bR = QAMAA ? 0 : *p.bR;
-    const QC qc = make_qc(p.E, M, bR);
+    const QC qc = make_qc(p.E, M, bR, p.kexp, p.kdc);
     FQ fq;
     if (QAMAA) fq = make_fq(*p.qmax, p.qE, p.qM, p.qsign);
     const uint32_t emnA = (uint32_t)(128 - bA) << 23;
@@ -333,7 +336,7 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
 #pragma unroll
                     for (int j = 0; j < TN; ++j) {
                         const float g = a[i] * b[j];
-                        tacc[i][j] += QBMA ? q_fast<GCLIP>(g, qc) : g;
+                        tacc[i][j] += QBMA ? q_fast<GCLIP, true>(g, qc) : g;
                     }
             } else {
                 const float4 ac4 = *reinterpret_cast<const float4 *>(&sAc[kk][ty * TM]);
@@ -353,23 +356,31 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
                         // v0 = a*b - t*cA*cB is exactly representable, so one
                         // fused op yields it; g = a*b is formed only where a mask needs it.
                         const float cab = ac[i] * bc[j];
-                        float tc;  // t * cA * cB
+                        constexpr bool NEED_G = !S2N || (QBMA && SGN);
+                        // g = a*b is exact (two (M+1)-bit significands); formed only where a mask
+                        // needs it, and then the table term is folded into one fma on it
+                        const float g = NEED_G ? a[i] * b[j] : 0.0f;
+                        float v0;
                         if (TMODE == TM_W1U) {
                             const int t = __builtin_amdgcn_sbfe((int)ar0[i], bm[j], 1);
-                            tc = __uint_as_float(__float_as_uint(cab) & (uint32_t)t);
-                        } else if (TMODE == TM_LUT) {
-                            tc = sLut[ar0[i] + bm[j]] * cab;
+                            const float tc = __uint_as_float(__float_as_uint(cab) & (uint32_t)t);
+                            v0 = NEED_G ? g - tc : __fmaf_rn(a[i], b[j], -tc);
                         } else {
-                            const uint32_t w = (R == 2 && (bm[j] & 32u)) ? ar1[i] : ar0[i];
-                            const int t = SGN ? __builtin_amdgcn_sbfe((int)w, bm[j], 2)
-                                              : (int)__builtin_amdgcn_ubfe(w, bm[j], 2);
-                            tc = (float)t * cab;
+                            float tf;  // the table entry
+                            if (TMODE == TM_LUT) {
+                                tf = sLut[ar0[i] + bm[j]];
+                            } else {
+                                const uint32_t w = (R == 2 && (bm[j] & 32u)) ? ar1[i] : ar0[i];
+                                const int t = SGN ? (int)__builtin_amdgcn_sbfe((int)w, bm[j], 2)
+                                                  : (int)__builtin_amdgcn_ubfe(w, bm[j], 2);
+                                tf = (float)t;
+                            }
+                            v0 = NEED_G ? __fmaf_rn(-tf, cab, g) : __fmaf_rn(a[i], b[j], -(tf * cab));
                         }
-                        float v0 = __fmaf_rn(a[i], b[j], -tc);
-                        constexpr bool NEED_G = !S2N || (QBMA && SGN);
-                        const float g = NEED_G ? a[i] * b[j] : 0.0f;
                         if (!S2N) v0 = (fabsf(g) >= qc.mnR) ? v0 : g;  // norm mask, v9:87
-                        if (S2N && QBMA && SGN) v0 = (g < 0.0f && g >= -qc.thr) ? fabsf(v0) : v0;  // F7
+                        // F7: the sign comes from Q_R(g), which is -0 (sign +1) for g in [-thr, 0);
+                        // v0 has g's sign, so for every g >= -thr the term is |v0|
+                        if (S2N && QBMA && SGN) v0 = (g >= -qc.thr) ? fabsf(v0) : v0;
                         tacc[i][j] += QBMA ? q_fast<GCLIP>(v0, qc) : v0;
                     }
             }
@@ -688,7 +699,8 @@ static GemmArgs make_args(const float *A, int64_t lda, const float *B, int64_t s
     GemmArgs a;
     memset(&a, 0, sizeof(a));
     a.A = A; a.lda = lda; a.B = B; a.sbk = sbk; a.sbn = sbn; a.C = C; a.ldc = ldc;
-    a.M = M; a.N = N; a.K = K; a.E = E; a.Mw = Mw; a.bA = bA; a.bB = bB; a.bBs = bBs; a.bR = bR;
+    a.M = M; a.N = N; a.K = K; a.E = E; a.Mw = Mw; a.kexp = 0x7F800000u; a.kdc = (uint32_t)(23 - Mw) << 23;
+    a.bA = bA; a.bB = bB; a.bBs = bBs; a.bR = bR;
     a.flags = flags; a.nchw = 0; a.hw = 1; a.ctot = N; a.coff = 0;
     return a;
 }

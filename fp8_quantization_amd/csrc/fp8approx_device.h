@@ -6,7 +6,7 @@
 //                float32 op here (the library is compiled with -ffp-contract=off), so each
 //                product term is bit-identical to the reference.  Used for the tensor-bias
 //                (single-column) path, for off-grid operand tiles and for fp8a_terms.
-//   * q_fast   : a branch-free Q_R on the float32 bit pattern (8 VALU ops), valid for the
+//   * q_fast   : a branch-free Q_R on the float32 bit pattern (6-7 VALU ops), valid for the
 //                int-bias path; exactness argument in DESIGN.md §3.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -122,39 +122,68 @@ __device__ __forceinline__ float exact_term(float a, float b, const DFmt &fA, co
 //   r     = ((min(|x|, bound) + C) - C),  C = 2^(max(e, e_min) + 23 - M)   (RNE at `step`)
 struct QC {
     uint32_t emn;   // exponent field of 2^(1 - bR)
-    float kb;       // (2 - 2^-M - 2^-22): bound = 2^e * kb sits in (max - step/2, max] of binade e
-    float kc;       // 1.5 * 2^(23 - M): C = 2^max(e, e_min) * kc has ulp(C) = step, and
-                    //   (x + C) - C rounds SIGNED x (|x| < C/3) half-to-even at step
-    float cmin;     // 2^(e_min) * kc
+    uint32_t kexp;  // 0x7F800000
+    uint32_t kbm;   // mantissa field of kb = 2 - 2^-M - 2^-22: bound = 2^e * kb = (x & EXP) | kbm
+                    //   sits in (max - step/2, max] of binade e
+    uint32_t dc;    // (23 - M) << 23: C = bound * 2^(23-M) has ulp(C) = step, C/step is even and
+                    //   C +- 2^(e+1) stays in C's binade, so (x + C) - C rounds SIGNED x half-to-even
+    uint32_t cmin;  // bits of 2^(e_min) * 1.5 * 2^(23 - M): the subnormal grid's C
+    float kb;       // 2 - 2^-M - 2^-22 (float form)
+    float kc;       // 1.5 * 2^(23 - M) (float form: C = 2^max(e, e_min) * kc)
+    float cminf;    // 2^(e_min) * kc (float form)
     float maxnorm;  // max_norm(bR) (golden_clip_OF)
     float mnR;      // min_norm(bR)
     float thr;      // largest |g| that Q_R flushes to 0: 2^(-bR - M)
 };
 
-__device__ __forceinline__ QC make_qc(int E, int M, int bR) {
+// kexp = 0x7F800000 and kdc = (23 - M) << 23 arrive as launch arguments: as literals the
+// selector splits (x & EXP) | kbm into two ops (gfx9 VOP3 takes no literal) and re-associates
+// the add of kdc into two adds.  Call once per kernel, outside loops.
+__device__ __forceinline__ QC make_qc(int E, int M, int bR, uint32_t kexp, uint32_t kdc) {
     QC q;
     q.emn = (uint32_t)(127 + 1 - bR) << 23;
+    // kbm lives in a VGPR: with kexp it would be the second scalar operand of v_and_or_b32,
+    // which gfx9's one-constant-bus-read rule forbids, and the selector would emit and + or
+    const uint32_t kbm = __float_as_uint(2.0f - p2(-M) - p2(-22)) & 0x007FFFFFu;
+    asm("v_mov_b32 %0, %1" : "=v"(q.kbm) : "s"(kbm));
+    q.kexp = kexp;
+    q.dc = kdc;
+    q.cmin = __float_as_uint(1.5f * p2(1 - bR + 23 - M));
     q.kb = 2.0f - p2(-M) - p2(-22);
     q.kc = 1.5f * p2(23 - M);
-    q.cmin = 1.5f * p2(1 - bR + 23 - M);
+    q.cminf = 1.5f * p2(1 - bR + 23 - M);
     q.maxnorm = ldexpf(2.0f - p2(-M), (1 << E) - 1 - bR);
     q.mnR = p2(1 - bR);
     q.thr = p2(-bR - M);
     return q;
 }
 
-// 7 VALU ops (and, mul, med3, mul, max, add, sub), no sign handling: the 1.5 * 2^k magic
-// constant rounds negative and positive values alike.  All inputs of min/max/med3 come out of
-// float arithmetic (canonical), so no canonicalisation is emitted.  A negative value that
-// rounds to zero comes back as +0 (the reference gives -0 or +0; both add nothing).
-template <bool GCLIP>
+// Two equivalent instruction forms, picked per kernel by measurement (tools/q_variants.hip and
+// tools/gemm_bench.py A/B on MI355X):
+//   BITS = false, float form, 7 VALU ops (and, mul, med3, mul, max, add, sub): one int->float
+//     hand-off per product; 1-2 % faster where an error-table term precedes it;
+//   BITS = true, bit form, 6 VALU ops (and_or, med3, add_u32, max_u32, add, sub): one op fewer
+//     but three half-rate ops and three int<->float hand-offs; 3 % faster with no table.
+// No sign handling in either: the magic constant rounds negative and positive values alike.
+// All min/max/med3 inputs are canonical (float arithmetic or positive bit patterns), so no
+// canonicalisation is emitted.  Zero gives C = the subnormal grid's C, i.e. 0.  A negative value
+// that rounds to zero comes back as +0 (the reference gives -0 or +0; both add nothing).
+template <bool GCLIP, bool BITS = false>
 __device__ __forceinline__ float q_fast(float x, const QC &q) {
     float xs = x;
     if (GCLIP) xs = __builtin_amdgcn_fmed3f(xs, -q.maxnorm, q.maxnorm);  // clip_OF first
-    const float pe = __uint_as_float(__float_as_uint(xs) & 0x7F800000u);  // 2^floor(log2|x|)
-    const float bd = pe * q.kb;
-    xs = __builtin_amdgcn_fmed3f(xs, -bd, bd);
-    const float c = fmaxf(pe * q.kc, q.cmin);
+    float c;
+    if (BITS) {
+        const uint32_t bdb = (__float_as_uint(xs) & q.kexp) | q.kbm;  // 2^floor(log2|x|) * kb
+        const float bd = __uint_as_float(bdb);
+        xs = __builtin_amdgcn_fmed3f(xs, -bd, bd);
+        c = __uint_as_float(max(bdb + q.dc, q.cmin));
+    } else {
+        const float pe = __uint_as_float(__float_as_uint(xs) & 0x7F800000u);  // 2^floor(log2|x|)
+        const float bd = pe * q.kb;
+        xs = __builtin_amdgcn_fmed3f(xs, -bd, bd);
+        c = fmaxf(pe * q.kc, q.cminf);
+    }
     return (xs + c) - c;
 }
 
