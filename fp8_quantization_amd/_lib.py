@@ -15,7 +15,7 @@ APPROX, S2N, QBMA, GCLIP, TB = 1, 2, 4, 8, 16
 OK, EINVAL, EFORMAT, EHIP = 0, -1, -2, -3
 
 SYMBOLS = ("fp8a_version", "fp8a_last_error", "fp8a_decompose", "fp8a_quant", "fp8a_matmul_workspace_size",
-           "fp8a_matmul", "fp8a_terms", "fp8a_conv2d_workspace_size", "fp8a_conv2d", "fp8a_im2col",
+           "fp8a_matmul_workspace_size_mnk", "fp8a_matmul", "fp8a_terms", "fp8a_conv2d_workspace_size", "fp8a_conv2d", "fp8a_im2col",
            "fp8a_fp8_quantize", "fp8a_matmul_qamaa", "fp8a_conv2d_qamaa")
 
 _lib = None
@@ -42,6 +42,7 @@ def load():
         "fp8a_decompose": ([P, I64, I64, I64, I, I, P, I64, U, P, P, P], I),
         "fp8a_quant": ([P, I64, I, I, P, U, P, P], I),
         "fp8a_matmul_workspace_size": ([], SZ),
+        "fp8a_matmul_workspace_size_mnk": ([I64, I64, I64], SZ),
         "fp8a_matmul": ([P, I64, P, I64, I64, P, I64, I64, I64, I64, I, I, P, P, I64, P, P, U, P, SZ, P], I),
         "fp8a_terms": ([P, I64, P, I64, I64, P, I64, I64, I64, I, I, P, P, I64, P, P, U, P], I),
         "fp8a_conv2d_workspace_size": ([I64, I64, I64, I64, I64, I, I, I, I, I, I, I, I, I], SZ),

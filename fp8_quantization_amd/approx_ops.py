@@ -102,7 +102,7 @@ def _matmul_op(A: torch.Tensor, B: torch.Tensor, bA: torch.Tensor, bB: torch.Ten
     Mr, K = A.shape
     N = B.shape[1]
     C = torch.empty((Mr, N), dtype=torch.float32, device=dev)
-    ws = _workspace(dev, L.fp8a_matmul_workspace_size())
+    ws = _workspace(dev, L.fp8a_matmul_workspace_size_mnk(Mr, N, K))
     bBs = 0 if bB.numel() == 1 else 1
     rc = L.fp8a_matmul(_lib.dev_ptr(A), A.stride(0), _lib.dev_ptr(B), B.stride(0), B.stride(1),
                        _lib.dev_ptr(C), N, Mr, N, K, E, M, _lib.dev_ptr(bA), _lib.dev_ptr(bB), bBs,

@@ -66,9 +66,13 @@ int fp8a_quant(const float *x, int64_t n, int E, int M, const int32_t *bias, uin
  * v9:555-592) or NULL for all-zero; it is packed into the launch arguments, so the call stays
  * asynchronous.  C is row-major with leading dimension ldc.  workspace: device scratch of at
  * least fp8a_matmul_workspace_size() bytes (holds the off-grid flag that gates the exact
- * re-computation when an operand is not exactly representable in its FP8 code).
+ * re-computation when an operand is not exactly representable in its FP8 code); a workspace
+ * of fp8a_matmul_workspace_size_mnk(M, N, K) bytes also holds split-K partial sums, which the
+ * launch then uses when the shape fills the GPU in a fractional number of waves (the partials
+ * are summed in a fixed order: results stay deterministic).
  */
 size_t fp8a_matmul_workspace_size(void);
+size_t fp8a_matmul_workspace_size_mnk(int64_t M, int64_t N, int64_t K);
 int fp8a_matmul(const float *A, int64_t lda, const float *B, int64_t sbk, int64_t sbn,
                 float *C, int64_t ldc, int64_t M, int64_t N, int64_t K, int E, int Mw,
                 const int32_t *bA, const int32_t *bB, int64_t bB_stride, const int32_t *bR,
@@ -90,7 +94,9 @@ int fp8a_terms(const float *A, int64_t lda, const float *B, int64_t sbk, int64_t
  * bW: device int32 per output channel (weight_quantizer.custom_bias).  Groups whose output
  * block has a single channel (depthwise) take the tensor-bias semantics (FP8A_TB) exactly as
  * the reference does (approx_calculation.py:800-809), other groups the int-bias semantics.
- * workspace: device scratch of fp8a_conv2d_workspace_size() bytes (im2col image).
+ * workspace: device scratch of fp8a_conv2d_workspace_size() bytes (the off-grid flag word
+ * and split-K partial sums; no im2col image: the GEMM gathers its operand rows from x).  A
+ * smaller workspace that still holds the flag word runs without split-K.
  */
 size_t fp8a_conv2d_workspace_size(int64_t Bn, int64_t Cin, int64_t H, int64_t W, int64_t Cout,
                                   int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw,

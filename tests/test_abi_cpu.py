@@ -34,6 +34,11 @@ def test_version_string():
 def test_workspace_queries_are_host_only():
     L = _lib.load()
     assert L.fp8a_matmul_workspace_size() >= 4
+    # split-K sizing is host logic (no device: 256 CUs assumed): a fraction-of-a-wave shape
+    # gets room for partial sums, a many-wave shape does not
+    flag = L.fp8a_matmul_workspace_size()
+    assert L.fp8a_matmul_workspace_size_mnk(12544, 512, 4608) > flag
+    assert L.fp8a_matmul_workspace_size_mnk(3211264, 64, 147) == flag
     # depthwise (single output channel per group): direct kernel, no im2col image
     assert L.fp8a_conv2d_workspace_size(2, 8, 6, 6, 8, 3, 3, 1, 1, 1, 1, 1, 1, 8) == 0
     # implicit-GEMM conv: only the off-grid flag word, independent of the batch

@@ -212,6 +212,28 @@ def test_ragged_shapes_all_table_modes(shape, fmt):
         assert_sums_close(C, Cref, S, f"{shape} {fmt} s2n={s2n}")
 
 
+@pytest.mark.parametrize("shape", [(256, 2048, 128), (100, 1000, 70), (64, 4608, 64)])
+def test_split_k_matmul(shape):
+    """Shapes that fill the GPU in a fraction of a wave take split-K (partials summed in a
+    fixed order): sums within tolerance and bit-identical across calls."""
+    from fp8_quantization_amd import _lib
+    Mr, K, N = shape
+    assert _lib.load().fp8a_matmul_workspace_size_mnk(Mr, N, K) > 256, "shape expected to split"
+    E, M = 4, 3
+    rng = np.random.default_rng(Mr + K + N)
+    A = _grid_operands(rng, E, M, Mr, K, 10, zero_frac=0.4)
+    B = _grid_operands(rng, E, M, K, N, 13)
+    bB = rng.integers(12, 15, size=N).astype(np.int32)
+    tab = g2_table("E4M3", "nocomp")
+    fl = orc.flags_of(approx=True, s2n=True, qbma=True)
+    run = lambda: fa().approx_matmul(t(A), t(B), E, M, 10, t(bB, torch.int32), 12, torch.as_tensor(tab),
+                                     flags=fl).cpu().numpy()
+    C1, C2 = run(), run()
+    assert np.array_equal(C1.view(np.uint32), C2.view(np.uint32)), "split-K result not deterministic"
+    Cref, S = orc.matmul(A, B, E, M, 10, bB, 12, tab, fl, with_abs=True)
+    assert_sums_close(C1, Cref, S, f"split-K {shape}")
+
+
 def test_empty_inner_dimension_gives_zeros():
     A = torch.zeros((5, 0), device=DEV)
     B = torch.zeros((0, 3), device=DEV)
@@ -231,6 +253,8 @@ def _im2col_np(x, kh, kw, stride, pad, dil):
     dict(cin=16, cout=32, k=3, s=1, p=1, g=1, hw=14),
     dict(cin=16, cout=24, k=1, s=2, p=0, g=1, hw=15),
     dict(cin=8, cout=16, k=3, s=1, p=1, g=4, hw=9),      # grouped, 4 out channels per group
+    dict(cin=128, cout=64, k=3, s=1, p=1, g=1, hw=7),    # split-K, hw=49 (scalar reduce)
+    dict(cin=256, cout=64, k=3, s=1, p=1, g=2, hw=8),    # split-K, grouped, hw=64 (float4 reduce)
 ])
 def test_conv2d_int_bias_groups(cfg):
     rng = np.random.default_rng(cfg["cin"] * 7 + cfg["cout"])
