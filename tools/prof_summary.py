@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--timed-launches", type=int, required=True)
     ap.add_argument("--out", required=True)
     ap.add_argument("--note", default="")
+    ap.add_argument("--pmc-json", default="", help="also write the per-launch PMC summary bench.py reads")
     a = ap.parse_args()
 
     rows = [r for r in read_csv(a.trace) if KERNEL in r["Kernel_Name"]]
@@ -58,6 +59,24 @@ def main():
             res["traffic_note"] = "FETCH_SIZE uncalibrated for 4-byte-per-lane loads (raw KB x 1024)"
         if "SQ_INSTS_VALU" in pm and "SQ_WAVES" in pm:
             res["valu_instr_per_wave"] = pm["SQ_INSTS_VALU"] / pm["SQ_WAVES"]
+    if counters and a.pmc_json:
+        pm = res["pmc_avg_per_dispatch"]
+        pj = dict(source="rocprofv3 --kernel-trace --pmc (separate passes per counter group, "
+                         "--kernel-include-regex gemm_fast) on bench.py --steps 2 --warmup 1",
+                  note="per gemm_fast_kernel dispatch, averaged; FETCH_SIZE/WRITE_SIZE in KB (x1024 = bytes); "
+                       "FETCH_SIZE uncalibrated for 4-byte-per-lane loads (MI355X_MICROARCH.md HBM section)")
+        if "FETCH_SIZE" in pm and "WRITE_SIZE" in pm:
+            pj.update(gemm_fast_bytes_per_launch=(pm["FETCH_SIZE"] + pm["WRITE_SIZE"]) * 1024.0,
+                      fetch_kb=pm["FETCH_SIZE"], write_kb=pm["WRITE_SIZE"])
+        if "SQ_INSTS_VALU" in pm and "GRBM_GUI_ACTIVE" in pm:
+            # GRBM_GUI_ACTIVE is summed over the 8 XCDs; 1024 SIMDs; a wave64 VALU op issues in 2 cycles
+            cyc = pm["GRBM_GUI_ACTIVE"] / 8.0
+            pj.update(valu_instr_per_simd_cycle=pm["SQ_INSTS_VALU"] / 1024.0 / cyc,
+                      valu_issue_fraction=2.0 * pm["SQ_INSTS_VALU"] / 1024.0 / cyc,
+                      gui_cycles_per_xcd=cyc,
+                      effective_clock_ghz=cyc / res["timed_avg_ns"] if res.get("timed_avg_ns") else None)
+        with open(a.pmc_json, "w") as f:
+            json.dump(pj, f, indent=1)
     with open(a.out + ".json", "w") as f:
         json.dump(res, f, indent=1)
     with open(a.out + ".txt", "w") as f:
