@@ -20,6 +20,10 @@
 #define ORC_QBMA   4u  /* quant_btw_mult_accu        */
 #define ORC_GCLIP  8u  /* golden_clip_OF             */
 #define ORC_TB     16u /* biases passed as int tensors (single-column call) */
+#define ORC_V5     32u /* superseded integer-adder model, approx_matmul_whole_v5.py         */
+#define ORC_OFUF   64u /* v5 sim_hw_add_OFUF                                               */
+#define ORC_OF    128u /* v5 with_OF_opt                                                   */
+#define ORC_UF    256u /* v5 with_UF_opt                                                   */
 
 /* torch float32 pow(2.0, k) for an int32 exponent: correctly rounded 2^k (0 below
  * 2^-150, inf above 2^127).  Used wherever the reference writes 2.0**(int tensor) or
@@ -86,9 +90,40 @@ static float orc_q1(float x, const orc_fmt *p, int clip) {
     return orc_rec1(sign, e, m, p);
 }
 
+/* One product term of the v5 integer-adder model (approx_matmul_whole_v5.py:10-183),
+ * generalised to per-operand biases: A and B decode with clip_OF=True (v5:22, 27-49), the
+ * product is the integer sum of the two (expo << M | mant) codes minus (bA + bB - bR) << M
+ * (v5:56-59 with B_neg, v5:162: with one bias b that is b << M) plus the compensation table
+ * entry; optionally wrapped like a hardware adder of E+M bits (v5:165-178); decoded with bR
+ * (v5:285-313: expo = floor(r / 2^M), mant = r mod 2^M, so a zero operand gives a NONZERO
+ * term) and signed with sign(a) * sign(b) (v5:108-111).  The whole v5 call uses one
+ * custom_bias for A, B and the result (bA = bB = bR). */
+static float orc_term_v5(float a, float b, int M, const orc_fmt *pA, const orc_fmt *pB,
+                         const orc_fmt *pR, const int32_t *table, unsigned flags) {
+    const int E = pA->E, n = 1 << M;
+    int32_t eA, mA, eB, mB;
+    orc_dec1(a, pA, 1, &eA, &mA);
+    orc_dec1(b, pB, 1, &eB, &mB);
+    int32_t r = eA * n + mA + eB * n + mB - (pA->b + pB->b - pR->b) * n + table[mA * n + mB];
+    if (flags & ORC_OFUF) {                                         /* v5:165-178 */
+        const int32_t maxi = (1 << (E + M)) - 1, mod = 1 << (E + M);
+        int of = r > maxi, uf = r < 0;
+        r = ((r % mod) + mod) % mod;                                /* torch %: sign of divisor */
+        if ((flags & ORC_OF) && of) r = maxi;
+        if ((flags & ORC_UF) && uf) r = r % n;
+    }
+    int32_t expo = (r >= 0) ? r / n : -((-r + n - 1) / n);          /* floor division */
+    int32_t mant = r - expo * n;
+    float ms = (float)mant / (float)n;
+    float v = (expo == 0) ? pow2f(1 - pR->b) * ms : pow2f(expo - pR->b) * (1.0f + ms);
+    float sign = ((a < 0.0f) ? -1.0f : 1.0f) * ((b < 0.0f) ? -1.0f : 1.0f);
+    return v * sign;
+}
+
 /* One product term of custom_matmul_vectorize, v9:29-108, for element (a, b). */
 static float orc_term1(float a, float b, int M, const orc_fmt *pA, const orc_fmt *pB,
                        const orc_fmt *pR, const int32_t *table, unsigned flags) {
+    if (flags & ORC_V5) return orc_term_v5(a, b, M, pA, pB, pR, table, flags);
     const int s2n = (flags & ORC_S2N) != 0, qbma = (flags & ORC_QBMA) != 0;
     const int gclip = (flags & ORC_GCLIP) != 0, approx = (flags & ORC_APPROX) != 0;
     float g = a * b;                                                /* v9:30 */

@@ -15,6 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 APPROX, S2N, QBMA, GCLIP, TB = 1, 2, 4, 8, 16
+V5, OFUF, OF_OPT, UF_OPT = 32, 64, 128, 256
 
 _lib = None
 
@@ -54,6 +55,11 @@ def _i32(x):
 def flags_of(approx=True, s2n=False, qbma=True, gclip=False, tb=False):
     return (APPROX if approx else 0) | (S2N if s2n else 0) | (QBMA if qbma else 0) | \
         (GCLIP if gclip else 0) | (TB if tb else 0)
+
+
+def flags_v5(ofuf=False, of_opt=False, uf_opt=False):
+    """v5 integer-adder model (approx_matmul_whole_v5.py) with its OF/UF switches."""
+    return V5 | (OFUF if ofuf else 0) | (OF_OPT if of_opt else 0) | (UF_OPT if uf_opt else 0)
 
 
 def decompose(x, E, M, b, tb=False, clip=False):

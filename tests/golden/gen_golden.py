@@ -16,6 +16,13 @@ Fixture groups:
   g4_tensorbias.npz single-column (tensor-bias) calls, quirk F5 (approx_calculation.py:800-809)
   g5_operator.npz   QCustomBNConv2dTorch / QCustomLinearTorch through estimate->fix->approx
                     (quantized_folded_bn.py:30-83, hijacker.py:77-115)
+  g6_qamaa.npz      the quantize_after_mult_and_add branch of approx_multiply
+                    (approx_calculation.py:787-795)
+  g7_v5.npz         the superseded integer-adder model with live sim_hw_add_OFUF /
+                    with_OF_opt / with_UF_opt semantics (approx_matmul_whole_v5.py:10-183,
+                    tables :362-550); v5's with_OF_opt line names a global `A` that only the
+                    module's own __main__ defines, so the generator sets one (a CPU tensor, used
+                    for its .device only) to let that branch run
 
 Usage:  python tests/golden/gen_golden.py      (about a minute on 8 cores)
 """
@@ -62,6 +69,7 @@ def _install_shim():
 _install_shim()
 import approx.approx_matmul_whole_v9 as v9  # noqa: E402  (reference, unmodified)
 import approx.approx_calculation as ac  # noqa: E402
+import approx.approx_matmul_whole_v5 as v5  # noqa: E402  (reference, unmodified)
 from quantization.quantizers.fp8_quantizer import FPQuantizer  # noqa: E402
 from quantization.range_estimators import RangeEstimators  # noqa: E402
 
@@ -304,6 +312,64 @@ def gen_g6():
     return meta
 
 
+# ----------------------------------------------------------------------------- G7
+V5_TABLES = {(4, 3): [3], (3, 4): [3, 4], (2, 5): [3, 4, 5]}
+V5_FLAGS = [(False, False, False), (True, False, False), (True, True, False), (True, False, True),
+            (True, True, True)]
+
+
+def v5_operands(E, M, b, rows, cols, rng):
+    """Grid codes over the whole exponent range plus out-of-range and off-grid values:
+    zeros, subnormals, values above max_norm (clipped by v5's clip_OF=True decode)."""
+    expo = rng.integers(0, 2 ** E, size=(rows, cols))
+    mant = rng.integers(0, 2 ** M, size=(rows, cols))
+    v = np.where(expo == 0, np.ldexp(mant / 2 ** M, 1 - b), np.ldexp(1.0 + mant / 2 ** M, expo - b))
+    r = rng.random((rows, cols))
+    v = np.where(r < 0.1, 0.0, v)
+    big = 2.0 ** (2 ** E - 1 - b) * rng.uniform(2.0, 8.0, size=(rows, cols))
+    v = np.where((r >= 0.1) & (r < 0.15), big, v)
+    off = np.ldexp(rng.uniform(1.0, 2.0, size=(rows, cols)), rng.integers(-b - 2, 2 ** E - b, size=(rows, cols)))
+    v = np.where((r >= 0.15) & (r < 0.25), off, v)
+    v = v * rng.choice([-1.0, 1.0], size=(rows, cols))
+    return torch.tensor(v, dtype=torch.float32)
+
+
+def v5_call(A, B, E, M, b, tab, ofuf, of, uf):
+    v5.A = torch.zeros(1)  # the global v5's with_OF_opt branch reads (see module docstring)
+    with contextlib.redirect_stdout(io.StringIO()):
+        return v5.custom_matmul_vectorize(A, B, E, M, custom_bias=b, comp_table_NN=tab, sim_hw_add_OFUF=ofuf,
+                                          with_OF_opt=of, with_UF_opt=uf, golden_clip_OF=False)
+
+
+def gen_g7():
+    out, meta = {}, []
+    rng = np.random.default_rng(77)
+    for (E, M), dns in V5_TABLES.items():
+        fk = f"E{E}M{M}"
+        tabs = [("zero", torch.zeros((2 ** M, 2 ** M), dtype=torch.int32))]
+        for d in dns:
+            t = v5.get_comp_table_NN(E, M, True, d, "cpu")
+            out[f"{fk}_table_d{d}"] = t.numpy().astype(np.int32)
+            tabs.append((f"d{d}", t))
+        for b in (None, 2 ** (E - 1) + 2):
+            bb = 2 ** (E - 1) - 1 if b is None else b
+            A = v5_operands(E, M, bb, 24, 40, rng)
+            B = v5_operands(E, M, bb, 40, 16, rng)
+            bk = f"{fk}_b{bb}"
+            out[bk + "_A"], out[bk + "_B"] = A.numpy(), B.numpy()
+            At, Bt = A[:6], B[:, :6]
+            for tname, tab in tabs:
+                for (ofuf, of, uf) in V5_FLAGS:
+                    key = f"{bk}_{tname}_s{int(ofuf)}{int(of)}{int(uf)}"
+                    out[key + "_C"] = v5_call(A, B, E, M, b, tab, ofuf, of, uf).numpy()
+                    out[key + "_T"] = torch.stack([v5_call(At[:, k:k + 1], Bt[k:k + 1, :], E, M, b, tab, ofuf, of, uf)
+                                                   for k in range(At.shape[1])], dim=1).numpy()
+                    meta.append(dict(key=key, fmt=fk, E=E, M=M, bias=bb, default_bias=b is None, table=tname,
+                                     ofuf=ofuf, of_opt=of, uf_opt=uf))
+    np.savez_compressed(os.path.join(HERE, "g7_v5.npz"), **out)
+    return meta
+
+
 # ----------------------------------------------------------------------------- G5
 def qparams_for(E, M, approx_cfg, run_method):
     return dict(
@@ -386,7 +452,7 @@ def gen_g5():
 def main():
     torch.set_num_threads(os.cpu_count() or 1)
     meta = dict(torch_version=torch.__version__, reference="revollllt/FP8_quantization@2024-11-08",
-                g1=gen_g1(), g2=gen_g2(), g3=gen_g3(), g4=gen_g4(), g5=gen_g5(), g6=gen_g6())
+                g1=gen_g1(), g2=gen_g2(), g3=gen_g3(), g4=gen_g4(), g5=gen_g5(), g6=gen_g6(), g7=gen_g7())
     with open(os.path.join(HERE, "meta.json"), "w") as f:
         json.dump(meta, f, indent=1)
     sizes = {f: os.path.getsize(os.path.join(HERE, f)) for f in os.listdir(HERE) if f.endswith(".npz")}

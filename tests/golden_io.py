@@ -24,3 +24,13 @@ def flags_from(c, tb=False):
 def sum_tolerance(abs_sum):
     """|c - c_hat| <= 1e-5 * sum_k |v_k| + tiny (summation order differs)."""
     return 1e-5 * abs_sum + 1e-30
+
+
+def v5_case(c):
+    """(A, B, table, flags) of a G7 (approx_matmul_whole_v5) case."""
+    g = load("g7_v5.npz")
+    bk = c["key"].rsplit("_", 2)[0]
+    M = c["M"]
+    tab = np.zeros((2 ** M, 2 ** M), np.int32) if c["table"] == "zero" else g[f"{c['fmt']}_table_{c['table']}"]
+    flags = 32 | (64 if c["ofuf"] else 0) | (128 if c["of_opt"] else 0) | (256 if c["uf_opt"] else 0)
+    return g[bk + "_A"], g[bk + "_B"], np.ascontiguousarray(tab, np.int32), flags

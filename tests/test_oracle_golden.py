@@ -93,3 +93,18 @@ def test_g6_qamaa(case):
     if diff.any():
         step = np.ldexp(1.0, np.floor(np.log2(np.abs(ref[diff]) + 1e-30)).astype(int) - case["M"])
         assert np.all(np.abs(C[diff] - ref[diff]) <= step * 1.0001)
+
+
+@pytest.mark.parametrize("case", META["g7"], ids=lambda c: c["key"])
+def test_g7_v5_integer_adder_terms_bitexact_and_sums(case):
+    """v5 integer-adder model with sim_hw_add_OFUF / with_OF_opt / with_UF_opt (SURVEY §8(f)
+    next-4): per-product terms bit-exact, sums within the accumulation tolerance."""
+    g = gio.load("g7_v5.npz")
+    A, B, tab, fl = gio.v5_case(case)
+    E, M, b = case["E"], case["M"], case["bias"]
+    T = orc.terms(A[:6], B[:, :6], E, M, b, b, b, tab, fl)
+    Tr = g[case["key"] + "_T"]
+    same = (T.view(np.uint32) == Tr.view(np.uint32)) | ((T == 0) & (Tr == 0))
+    assert same.all(), f"{np.count_nonzero(~same)} terms differ"
+    C, S = orc.matmul(A, B, E, M, b, b, b, tab, fl, with_abs=True)
+    assert np.all(np.abs(C.astype(np.float64) - g[case["key"] + "_C"]) <= gio.sum_tolerance(S))
