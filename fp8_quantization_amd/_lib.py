@@ -12,6 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FP8A_LIB_PATH") or os.path.join(HERE, "lib", "libfp8approx.so")
 
 APPROX, S2N, QBMA, GCLIP, TB = 1, 2, 4, 8, 16
+V5, OFUF, OF_OPT, UF_OPT = 32, 64, 128, 256  # v5 integer-adder model (include/fp8approx.h)
 OK, EINVAL, EFORMAT, EHIP = 0, -1, -2, -3
 
 SYMBOLS = ("fp8a_version", "fp8a_last_error", "fp8a_decompose", "fp8a_quant", "fp8a_matmul_workspace_size",

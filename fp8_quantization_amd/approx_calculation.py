@@ -18,8 +18,9 @@ import torch.nn.functional as F
 from torch import nn
 
 from . import _lib
-from .approx_ops import _res_quant_params, approx_conv2d, approx_matmul, make_flags, qamaa_conv2d, qamaa_matmul
-from .error_tables import get_error_table_NN
+from .approx_ops import (_res_quant_params, approx_conv2d, approx_matmul, make_flags, make_flags_v5, qamaa_conv2d,
+                         qamaa_matmul)
+from .error_tables import get_comp_table_NN_v5, get_error_table_NN
 from .quantization.hijacker import QuantizationHijacker
 from .quantization.quantized_folded_bn import BNFusedHijacker
 
@@ -33,6 +34,14 @@ class ApproxOpMixin:
     def _approx_config(self):
         p = self.custom_approx_params
         E, M = p["expo_width"], p["mant_width"]
+        if p.get("approx_version", 9) == 5:
+            # opt-in extension: the v5 integer-adder model with live sim_hw_add_OFUF /
+            # with_OF_opt / with_UF_opt (approx_v5.py); without withComp, the zero table the v5
+            # harness passes for "no compensation"
+            table = get_comp_table_NN_v5(E, M, True, p["dnsmp_factor"]) if p["withComp"] else \
+                torch.zeros((2 ** M, 2 ** M), dtype=torch.int32)
+            return E, M, table, make_flags_v5(p.get("sim_hw_add_OFUF", False), p.get("with_OF_opt", False),
+                                              p.get("with_UF_opt", False))
         # get_error_table_NN runs first, as in the reference: unsupported formats raise
         # ValueError even when approx_flag is off (approx_calculation.py:772)
         table = get_error_table_NN(E, M, withComp=p["withComp"], dnsmp_factor=p["dnsmp_factor"])
@@ -59,8 +68,8 @@ class ApproxOpMixin:
                 return qamaa_matmul(x, y, *self._qamaa_params())
             return x @ y
         if self.approx_flag:  # single column: biases stay tensors -> tensor-bias semantics (F5)
-            return approx_matmul(x, y, E, M, x_bias, y_bias.reshape(-1), res_bias, table,
-                                 flags=flags | _lib.TB)
+            tb = 0 if flags & _lib.V5 else _lib.TB  # (v5 never had tensor-bias semantics)
+            return approx_matmul(x, y, E, M, x_bias, y_bias.reshape(-1), res_bias, table, flags=flags | tb)
         return x @ y
 
     def multiply(self, x, y):

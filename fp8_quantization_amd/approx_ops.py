@@ -20,7 +20,7 @@ from .error_tables import get_error_table_NN  # noqa: F401  (re-exported, v9:555
 
 __all__ = ["custom_matmul_vectorize", "approx_matmul", "approx_terms", "approx_conv2d", "qamaa_matmul", "qamaa_conv2d",
            "quant_to_fp_any_vectorize_torch", "float_to_fpany_absint_torch", "get_error_table_NN",
-           "make_flags", "fp8_fake_quantize"]
+           "make_flags", "make_flags_v5", "fp8_fake_quantize"]
 
 
 def make_flags(with_approx=True, with_s2nn2s_opt=False, quant_btw_mult_accu=True, golden_clip_OF=False,
@@ -28,6 +28,16 @@ def make_flags(with_approx=True, with_s2nn2s_opt=False, quant_btw_mult_accu=True
     return ((_lib.APPROX if with_approx else 0) | (_lib.S2N if with_s2nn2s_opt else 0) |
             (_lib.QBMA if quant_btw_mult_accu else 0) | (_lib.GCLIP if golden_clip_OF else 0) |
             (_lib.TB if tensor_bias else 0))
+
+
+def make_flags_v5(sim_hw_add_OFUF=False, with_OF_opt=False, with_UF_opt=False):
+    """Flags of the v5 integer-adder model (approx_matmul_whole_v5.py:155-183)."""
+    return (_lib.V5 | (_lib.OFUF if sim_hw_add_OFUF else 0) | (_lib.OF_OPT if with_OF_opt else 0) |
+            (_lib.UF_OPT if with_UF_opt else 0))
+
+
+def _uses_table(flags):
+    return bool(flags & (_lib.APPROX | _lib.V5))
 
 
 _BIAS_CACHE = {}
@@ -131,7 +141,7 @@ def approx_matmul(A, B, E, M, bA, bB, bR, table=None, flags=None, **flag_kwargs)
     if B.stride(0) != 1 and B.stride(1) != 1:
         B = B.contiguous()
     dev = A.device
-    tab = _table_host(table, M, bool(flags & _lib.APPROX))
+    tab = _table_host(table, M, _uses_table(flags))
     bB_ = _bias_dev(bB, dev)
     if bB_.numel() not in (1, B.shape[1]):
         raise AssertionError(f"approx_matmul: {bB_.numel()} column biases for {B.shape[1]} columns")
@@ -154,7 +164,7 @@ def approx_terms(A, B, E, M, bA, bB, bR, table=None, flags=None, **flag_kwargs):
     N = B.shape[1]
     T = torch.empty((Mr, K, N), dtype=torch.float32, device=dev)
     bA_, bB_, bR_ = _bias_dev(bA, dev), _bias_dev(bB, dev), _bias_dev(bR, dev)
-    tab = _table_host(table, M, bool(flags & _lib.APPROX))
+    tab = _table_host(table, M, _uses_table(flags))
     rc = L.fp8a_terms(_lib.dev_ptr(A), A.stride(0), _lib.dev_ptr(B), B.stride(0), B.stride(1), _lib.dev_ptr(T),
                       Mr, N, K, int(E), int(M), _lib.dev_ptr(bA_), _lib.dev_ptr(bB_), 0 if bB_.numel() == 1 else 1,
                       _lib.dev_ptr(bR_), _lib.host_ptr(tab), int(flags), _lib.stream_ptr(dev))
@@ -267,7 +277,7 @@ def approx_conv2d(x, w, E, M, bA, bW, bR, table=None, flags=None, stride=(1, 1),
         flags = make_flags(**flag_kwargs)
     flags &= ~_lib.TB
     dev = x.device
-    tab = _table_host(table, M, bool(flags & _lib.APPROX))
+    tab = _table_host(table, M, _uses_table(flags))
     bW_ = _bias_dev(bW, dev)
     if bW_.numel() == 1:
         bW_ = bW_.expand(w.shape[0]).contiguous()

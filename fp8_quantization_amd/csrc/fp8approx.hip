@@ -44,7 +44,8 @@ static int hip_check(const char *what) {
 //   TM_W2S/U: entries in [-2,1] / [0,3] -> 2 bits / entry, R = 2^M*2/32 words per row
 //   TM_LUT  : anything else -> float LUT in LDS (E2M5 no-comp: entries up to 5)
 enum TMode : int { TM_NONE = 0, TM_W1U = 1, TM_W2S1 = 2, TM_W2U1 = 3, TM_W2S2 = 4, TM_W2U2 = 5, TM_LUT = 6,
-                   TM_QAMAA = 7 /* quantize_after_mult_and_add: term = fq(a*b), no decode */ };
+                   TM_QAMAA = 7 /* quantize_after_mult_and_add: term = fq(a*b), no decode */,
+                   TM_V5 = 8 /* v5 integer-adder model: code sum + compensation LUT, OF/UF wrap */ };
 
 struct TablePack {
     uint32_t rows[64][2];  // packed rows for the bit modes (2^M <= 64)
@@ -175,6 +176,7 @@ __device__ __forceinline__ bool stage_decode(float x, int M, uint32_t emn, bool 
 template <bool S2N, bool QBMA, bool GCLIP, int TMODE>
 __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
     constexpr bool QAMAA = TMODE == TM_QAMAA;
+    constexpr bool V5 = TMODE == TM_V5;
     constexpr bool TBL = TMODE != TM_NONE && !QAMAA;
     constexpr int R = (TMODE == TM_W2S2 || TMODE == TM_W2U2) ? 2 : 1;
     constexpr bool SGN = (TMODE == TM_W2S1 || TMODE == TM_W2S2 || TMODE == TM_LUT);
@@ -186,6 +188,7 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
     __shared__ __attribute__((aligned(16))) float sBc[TBL ? BK : 1][BP];
     __shared__ __attribute__((aligned(16))) uint32_t sBm[TBL ? BK : 1][BP];
     __shared__ float sLut[TMODE == TM_LUT ? 1024 : 1];
+    __shared__ int32_t sLutI[V5 ? 1024 : 1];
     __shared__ uint32_t sRows[TBL ? 64 * 2 : 1];
 
     const int tid = threadIdx.x;
@@ -209,6 +212,8 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
         for (int i = tid; i < n * 2; i += NT) sRows[i] = p.tab.rows[i >> 1][i & 1];
         if (TMODE == TM_LUT)
             for (int i = tid; i < n * n; i += NT) sLut[i] = (float)p.tab.raw[i];
+        if (V5)
+            for (int i = tid; i < n * n; i += NT) sLutI[i] = p.tab.raw[i];
         __syncthreads();
     }
 
@@ -216,6 +221,7 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
     const bool b_ncontig = (p.sbn == 1);
     int bcol[4], bkk[4];
     uint32_t emnB[4];
+    int bbv[4];
     bool bias_ok = bR >= -40 && bR <= 80 && bA >= -100 && bA <= 100;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -225,7 +231,17 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
         const int64_t n = n0 + bcol[r];
         const int bb = (!QAMAA && n < p.N) ? p.bB[n * p.bBs] : 0;
         bias_ok = bias_ok && bb >= -100 && bb <= 100;
+        // v5: every decoded term 2^(e - bR) (1 + m/2^M) stays a normal float, so the ldexp form
+        // below equals the reference's pow(2, e - bR) * (1 + m/2^M)
+        if (V5) bias_ok = bias_ok && bA + bb <= 120;
         emnB[r] = (uint32_t)(128 - bb) << 23;
+        bbv[r] = V5 ? bb : 0;
+    }
+    DFmt fA5 = {};
+    int32_t v5max = 0;
+    if (V5) {
+        fA5 = dfmt(p.E, M, bA, false);
+        v5max = ((1 << p.E) << M) - 1;
     }
 
     // implicit-conv row of this thread (fixed across k tiles)
@@ -293,6 +309,14 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
             const float x = xa[r];
             float c;
             uint32_t mc;
+            if (V5) {  // exact decode with clip_OF (v5:22, 27-38): any fp32 input
+                int e, m;
+                exact_dec(x, fA5, true, e, m);
+                sA[kk][row] = __int_as_float((e << M) + m);
+                sAc[kk][row] = __uint_as_float(x < 0.0f ? 0x80000000u : 0u);
+                sAr[kk][row] = (uint32_t)m << M;
+                continue;
+            }
             if (!QAMAA) bad |= !stage_decode(x, M, emnA, S2N, c, mc);
             sA[kk][row] = x;
             if (TBL) {
@@ -312,6 +336,14 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
             const float x = xb[r];
             float c;
             uint32_t mc;
+            if (V5) {  // B code with the product's exponent offset folded in: -(bA + bB - bR) << M
+                int e, m;
+                exact_dec(x, dfmt(p.E, M, bbv[r], false), true, e, m);
+                sB[kk][col] = __int_as_float(((e - (bA + bbv[r] - bR)) << M) + m);
+                sBc[kk][col] = __uint_as_float(x < 0.0f ? 0x80000000u : 0u);
+                sBm[kk][col] = (uint32_t)m;
+                continue;
+            }
             if (!QAMAA) bad |= !stage_decode(x, M, emnB[r], S2N, c, mc);
             sB[kk][col] = x;
             if (TBL) {
@@ -329,8 +361,11 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
         // realistic data, 30x inside the 1e-5 parity tolerance
         float (&tacc)[TM][TN] = acc;
 
+        // v5 terms of zero operands are not zero (the code sum of a zero is still decoded), so
+        // the zero padding of a ragged last K-tile must not be summed there
+        const int kk_end = V5 ? (int)min<int64_t>(BK, kend - k0) : BK;
 #pragma unroll 2
-        for (int kk = 0; kk < BK; ++kk) {
+        for (int kk = 0; kk < kk_end; ++kk) {
             const float4 a4 = *reinterpret_cast<const float4 *>(&sA[kk][ty * TM]);
             const float4 b4 = *reinterpret_cast<const float4 *>(&sB[kk][tx * TN]);
             const float a[TM] = {a4.x, a4.y, a4.z, a4.w};
@@ -340,6 +375,29 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j) tacc[i][j] += fq_fast(a[i] * b[j], fq);
+            } else if (V5) {
+                const float4 ac4 = *reinterpret_cast<const float4 *>(&sAc[kk][ty * TM]);
+                const uint4 ar4 = *reinterpret_cast<const uint4 *>(&sAr[kk][ty * TM]);
+                const float4 bc4 = *reinterpret_cast<const float4 *>(&sBc[kk][tx * TN]);
+                const uint4 bm4 = *reinterpret_cast<const uint4 *>(&sBm[kk][tx * TN]);
+                const uint32_t as[TM] = {__float_as_uint(ac4.x), __float_as_uint(ac4.y), __float_as_uint(ac4.z),
+                                         __float_as_uint(ac4.w)};
+                const uint32_t bs[TN] = {__float_as_uint(bc4.x), __float_as_uint(bc4.y), __float_as_uint(bc4.z),
+                                         __float_as_uint(bc4.w)};
+                const uint32_t ar[TM] = {ar4.x, ar4.y, ar4.z, ar4.w};
+                const uint32_t bm[TN] = {bm4.x, bm4.y, bm4.z, bm4.w};
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        int32_t r = __float_as_int(a[i]) + __float_as_int(b[j]) + sLutI[ar[i] + bm[j]];
+                        r = v5_ofuf(r, v5max, M, p.flags);
+                        const int32_t e = r >> M, m = r & ((1 << M) - 1);
+                        // expo 0: m * 2^(1-bR-M); else (2^M + m) * 2^(e-bR-M) (also for e < 0)
+                        const float v = (e == 0) ? ldexpf((float)m, 1 - bR - M)
+                                                 : ldexpf((float)(m + (1 << M)), e - bR - M);
+                        tacc[i][j] += __uint_as_float(__float_as_uint(v) ^ as[i] ^ bs[j]);
+                    }
             } else if (!TBL) {
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
@@ -646,6 +704,10 @@ static void launch_fast_t(int mode, const GemmArgs &a, dim3 grid, hipStream_t s)
 static void launch_fast(int mode, const GemmArgs &a, hipStream_t s) {
     const int64_t tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
     dim3 grid((unsigned)(tiles * a.splits));
+    if (mode == TM_V5) {  // the v5 model has no s2n / qbma / golden-clip variants
+        gemm_fast_kernel<false, false, false, TM_V5><<<grid, NT, 0, s>>>(a);
+        return;
+    }
     const bool s2n = a.flags & F_S2N, q = a.flags & F_QBMA, gc = a.flags & F_GCLIP;
     if (s2n) {
         if (q) { gc ? launch_fast_t<true, true, true>(mode, a, grid, s) : launch_fast_t<true, true, false>(mode, a, grid, s); }
@@ -741,8 +803,11 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     if ((!a.A && !a.conv) || (a.conv && !a.X) || !a.B || !a.C || !a.bA || !a.bB || !a.bR)
         return fail(FP8A_EINVAL, "null pointer");
     int mode;
-    rc = pack_table(table, a.Mw, a.flags & F_APPROX, a.tab, mode);
+    const bool v5 = a.flags & F_V5;
+    if (v5 && (a.flags & F_TB)) return fail(FP8A_EINVAL, "the v5 model has no tensor-bias semantics");
+    rc = pack_table(table, a.Mw, v5 || (a.flags & F_APPROX), a.tab, mode);
     if (rc) return rc;
+    if (v5) mode = TM_V5;
     const int64_t total = a.M * a.N;
     const unsigned eblocks = (unsigned)std::min<int64_t>((total + 255) / 256, 4096);
     if (a.flags & F_TB) {
@@ -858,7 +923,7 @@ int fp8a_terms(const float *A, int64_t lda, const float *B, int64_t sbk, int64_t
     if (rc) return rc;
     GemmArgs a = make_args(A, lda, B, sbk, sbn, nullptr, 0, M, N, K, E, Mw, bA, bB, bB_stride, bR, flags);
     int mode;
-    rc = pack_table(table, Mw, flags & F_APPROX, a.tab, mode);
+    rc = pack_table(table, Mw, (flags & (F_APPROX | F_V5)) != 0, a.tab, mode);
     if (rc) return rc;
     const int64_t total = M * N * K;
     if (total == 0) return FP8A_OK;
@@ -882,7 +947,6 @@ int fp8a_im2col(const float *x, float *out, int64_t Bn, int64_t Cin, int64_t H, 
 size_t fp8a_conv2d_workspace_size(int64_t Bn, int64_t Cin, int64_t H, int64_t W, int64_t Cout, int kh, int kw,
                                   int sh, int sw, int ph, int pw, int dh, int dw, int groups) {
     if (groups <= 0 || Cout % groups != 0 || Cin % groups != 0) return 0;
-    if (Cout / groups == 1) return 0;  // direct tensor-bias kernel, no im2col image
     const int64_t Ho = (H + 2 * ph - dh * (kh - 1) - 1) / sh + 1;
     const int64_t Wo = (W + 2 * pw - dw * (kw - 1) - 1) / sw + 1;
     if (Ho <= 0 || Wo <= 0) return 0;
@@ -906,7 +970,7 @@ int fp8a_conv2d(const float *x, const float *w, float *y, int64_t Bn, int64_t Ci
     const int64_t cog = Cout / groups, cig = Cin / groups;
     const int64_t Mrows = Bn * Ho * Wo, Ktot = Cin * kh * kw, Kg = cig * kh * kw;
     if (Mrows == 0) return FP8A_OK;
-    if (cog == 1) {
+    if (cog == 1 && !(flags & F_V5)) {  // v5 never had tensor-bias semantics: it takes the GEMM path
         TablePack tp;
         int mode;
         rc = pack_table(table, Mw, flags & F_APPROX, tp, mode);

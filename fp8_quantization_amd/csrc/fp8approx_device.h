@@ -14,7 +14,9 @@
 
 namespace fp8a {
 
-enum : uint32_t { F_APPROX = 1u, F_S2N = 2u, F_QBMA = 4u, F_GCLIP = 8u, F_TB = 16u };
+enum : uint32_t { F_APPROX = 1u, F_S2N = 2u, F_QBMA = 4u, F_GCLIP = 8u, F_TB = 16u,
+                  // superseded integer-adder model (approx_matmul_whole_v5.py) and its switches
+                  F_V5 = 32u, F_OFUF = 64u, F_OF = 128u, F_UF = 256u };
 
 __device__ __forceinline__ float p2(int k) { return ldexpf(1.0f, k); }
 
@@ -73,9 +75,41 @@ __device__ __forceinline__ float exact_q(float x, const DFmt &f, bool clip) {
     return exact_rec(x < 0.0f ? -1.0f : 1.0f, e, m, f);
 }
 
+// v5 adder wrap (approx_mult_new, v5:163-178): an (E+M)-bit hardware adder; overflow to
+// max_norm_int with with_OF_opt, underflow to (r mod 2^M) with with_UF_opt.
+__device__ __forceinline__ int32_t v5_ofuf(int32_t r, int32_t maxi, int M, uint32_t flags) {
+    if (flags & F_OFUF) {
+        const bool of = r > maxi, uf = r < 0;
+        r &= maxi;  // mod 2^(E+M), two's complement: torch's % with a positive modulus
+        if ((flags & F_OF) && of) r = maxi;
+        if ((flags & F_UF) && uf) r &= (1 << M) - 1;
+    }
+    return r;
+}
+
+// One term of the v5 integer-adder model (approx_matmul_whole_v5.py:10-183), per-operand
+// biases (v5 itself uses one custom_bias for A, B and the result): operands decode with
+// clip_OF = True, the product is the sum of the (expo << M | mant) codes minus
+// (bA + bB - bR) << M plus the compensation entry, decoded with floor division (a zero
+// operand gives a nonzero term), signed with sign(a) * sign(b).
+__device__ __forceinline__ float exact_term_v5(float a, float b, const DFmt &fA, const DFmt &fB, const DFmt &fR,
+                                               const int8_t *tab, uint32_t flags) {
+    const int M = fA.M, n = 1 << M;
+    int eA, mA, eB, mB;
+    exact_dec(a, fA, true, eA, mA);
+    exact_dec(b, fB, true, eB, mB);
+    int32_t r = (eA + eB - (fA.b + fB.b - fR.b)) * n + mA + mB + tab[mA * n + mB];
+    r = v5_ofuf(r, ((fA.maxe + 1) << M) - 1, M, flags);
+    const int32_t expo = r >> M, mant = r & (n - 1);  // floor division / modulo by 2^M
+    const float ms = (float)mant * p2(-M);
+    const float v = (expo == 0) ? p2(1 - fR.b) * ms : p2(expo - fR.b) * (1.0f + ms);
+    return v * (((a < 0.0f) ? -1.0f : 1.0f) * ((b < 0.0f) ? -1.0f : 1.0f));
+}
+
 // One product term of custom_matmul_vectorize (v9:29-108).  tab: int8 [2^M][2^M].
 __device__ __forceinline__ float exact_term(float a, float b, const DFmt &fA, const DFmt &fB,
                                             const DFmt &fR, const int8_t *tab, uint32_t flags) {
+    if (flags & F_V5) return exact_term_v5(a, b, fA, fB, fR, tab, flags);
     const bool s2n = flags & F_S2N, qbma = flags & F_QBMA, gclip = flags & F_GCLIP;
     const int M = fA.M;
     float g = a * b;

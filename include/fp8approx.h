@@ -29,6 +29,15 @@ extern "C" {
 #define FP8A_GCLIP  8u  /* golden_clip_OF: Q_R clips overflow to max_norm   v9:283-286 */
 #define FP8A_TB     16u /* biases are int tensors (single-column call): quirk F5,
                            approx_calculation.py:800-809 / v9:202                      */
+/* The superseded integer-adder model (approx_matmul_whole_v5.py:10-183), opt-in: the term is
+ * the sum of the operands' (expo << M | mant) codes minus (bA + bB - bR) << M plus the
+ * compensation table entry (v5 tables, added), decoded with bR and signed.  The table argument
+ * is then the v5 compensation table.  v9 accepts but ignores the OF/UF switches;
+ * here they act as in v5 (approx_mult_new, v5:155-183). */
+#define FP8A_V5     32u  /* use the v5 model                                    v5:10-183 */
+#define FP8A_OFUF   64u  /* sim_hw_add_OFUF: wrap the code sum mod 2^(E+M)      v5:165-171 */
+#define FP8A_OF_OPT 128u /* with_OF_opt: overflow -> max_norm_int               v5:173-174 */
+#define FP8A_UF_OPT 256u /* with_UF_opt: underflow -> (sum mod 2^M)             v5:176-177 */
 
 #define FP8A_OK       0
 #define FP8A_EINVAL  -1

@@ -39,8 +39,9 @@ def test_workspace_queries_are_host_only():
     flag = L.fp8a_matmul_workspace_size()
     assert L.fp8a_matmul_workspace_size_mnk(12544, 512, 4608) > flag
     assert L.fp8a_matmul_workspace_size_mnk(3211264, 64, 147) == flag
-    # depthwise (single output channel per group): direct kernel, no im2col image
-    assert L.fp8a_conv2d_workspace_size(2, 8, 6, 6, 8, 3, 3, 1, 1, 1, 1, 1, 1, 8) == 0
+    # depthwise (single output channel per group): no im2col image; the flag word only (the
+    # v9 tensor-bias kernel needs none, the v5 mode takes the GEMM path)
+    assert L.fp8a_conv2d_workspace_size(2, 8, 6, 6, 8, 3, 3, 1, 1, 1, 1, 1, 1, 8) == flag
     # implicit-GEMM conv: only the off-grid flag word, independent of the batch
     n = L.fp8a_conv2d_workspace_size(2, 3, 8, 8, 4, 3, 3, 1, 1, 1, 1, 1, 1, 1)
     assert n == L.fp8a_conv2d_workspace_size(256, 3, 224, 224, 4, 3, 3, 1, 1, 1, 1, 1, 1, 1) >= 4
