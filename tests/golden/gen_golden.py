@@ -23,6 +23,10 @@ Fixture groups:
                     tables :362-550); v5's with_OF_opt line names a global `A` that only the
                     module's own __main__ defines, so the generator sets one (a CPU tensor, used
                     for its .device only) to let that branch run
+  g8_mbv2.npz       model level: the reference's QuantizedMobileNetV2
+                    (models/mobilenet_v2_quantized_approx.py) over its float MobileNetV2
+                    (width 0.25, 32x32, 10 classes, random weights and BN statistics) through
+                    estimate -> fix -> approx: the initial state, every layer's biases, logits
 
 Usage:  python tests/golden/gen_golden.py      (about a minute on 8 cores)
 """
@@ -370,6 +374,63 @@ def gen_g7():
     return meta
 
 
+# ----------------------------------------------------------------------------- G8
+def gen_g8():
+    # models/__init__.py imports every wrapper, some of which need torchvision (absent here):
+    # register the package without running its __init__, then import the two modules unmodified
+    if "models" not in sys.modules:
+        pkg = types.ModuleType("models")
+        pkg.__path__ = [os.path.join(REF, "models")]
+        sys.modules["models"] = pkg
+    from models.mobilenet_v2 import MobileNetV2 as RefMobileNetV2  # reference, unmodified
+    from models.mobilenet_v2_quantized_approx import QuantizedMobileNetV2 as RefQuantizedMobileNetV2
+    out, meta = {}, []
+    run_method = dict(approx_flag=True, quantize_after_mult_and_add=False, res_quantizer_flag=True,
+                      original_quantize_res=False)
+    for (name, (E, M), wc) in [("mbv2_e4m3", (4, 3), False)]:
+        torch.manual_seed(88)
+        fp = RefMobileNetV2(n_class=10, input_size=32, width_mult=0.25)
+        with torch.no_grad():
+            for m in fp.modules():
+                if isinstance(m, nn.BatchNorm2d):
+                    m.weight.uniform_(0.5, 1.5)
+                    m.bias.uniform_(-0.2, 0.2)
+                    m.running_mean.uniform_(-0.1, 0.1)
+                    m.running_var.uniform_(0.5, 2.0)
+                elif isinstance(m, nn.Linear):
+                    m.weight.normal_(0, 0.1)
+                    m.bias.uniform_(-0.1, 0.1)
+        qp = qparams_for(E, M, approx_params(E, M, 3, wc, True, True, True), dict(run_method))
+        with contextlib.redirect_stdout(io.StringIO()):
+            model = RefQuantizedMobileNetV2(fp, input_size=(1, 3, 32, 32), **qp)
+        state = {k: v.clone() for k, v in model.state_dict().items()}
+        x_cal = torch.randn(4, 3, 32, 32)
+        x_ev = torch.randn(3, 3, 32, 32)
+        model.eval()
+        model.quantized()
+        model.estimate_ranges()
+        with torch.no_grad(), contextlib.redirect_stdout(io.StringIO()):
+            model(x_cal)
+        model.fix_ranges()
+        with torch.no_grad(), contextlib.redirect_stdout(io.StringIO()):
+            logits = model(x_ev)
+        for k, v in state.items():
+            out[f"{name}__state__{k}"] = v.numpy()
+        biases = []
+        for lname, mod in model.named_modules():
+            if isinstance(mod, (ac.QCustomBNConv2dTorch, ac.QCustomLinearTorch)):
+                out[f"{name}__bA__{lname}"] = mod.get_acts_fp_bias().reshape(-1).numpy()
+                out[f"{name}__bB__{lname}"] = mod.get_weights_fp_bias().reshape(-1).numpy()
+                out[f"{name}__bR__{lname}"] = mod.get_res_fp_bias().reshape(-1).numpy()
+                biases.append(lname)
+        out[f"{name}__x_cal"], out[f"{name}__x_ev"] = x_cal.numpy(), x_ev.numpy()
+        out[f"{name}__logits"] = logits.numpy()
+        meta.append(dict(name=name, E=E, M=M, with_comp=wc, width_mult=0.25, input_size=32, n_class=10,
+                         state_keys=list(state.keys()), approx_layers=biases))
+    np.savez_compressed(os.path.join(HERE, "g8_mbv2.npz"), **out)
+    return meta
+
+
 # ----------------------------------------------------------------------------- G5
 def qparams_for(E, M, approx_cfg, run_method):
     return dict(
@@ -452,7 +513,7 @@ def gen_g5():
 def main():
     torch.set_num_threads(os.cpu_count() or 1)
     meta = dict(torch_version=torch.__version__, reference="revollllt/FP8_quantization@2024-11-08",
-                g1=gen_g1(), g2=gen_g2(), g3=gen_g3(), g4=gen_g4(), g5=gen_g5(), g6=gen_g6(), g7=gen_g7())
+                g1=gen_g1(), g2=gen_g2(), g3=gen_g3(), g4=gen_g4(), g5=gen_g5(), g6=gen_g6(), g7=gen_g7(), g8=gen_g8())
     with open(os.path.join(HERE, "meta.json"), "w") as f:
         json.dump(meta, f, indent=1)
     sizes = {f: os.path.getsize(os.path.join(HERE, f)) for f in os.listdir(HERE) if f.endswith(".npz")}

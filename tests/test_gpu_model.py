@@ -1,0 +1,46 @@
+"""Model-level parity (G8): the reference's QuantizedMobileNetV2 (width 0.25, 32x32, E4M3
+approx_v9, random weights and BN statistics) rebuilt from the drop-in operators, given the
+reference's initial state, goes through estimate -> fix -> approx on the GPU.
+
+Bars: every approx layer's bA / per-channel bB / bR identical (calibration reproduced through
+the whole network); logits within a summation-order tolerance; top-1 identical."""
+import numpy as np
+import pytest
+import torch
+
+from tests import golden_io as gio
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.mark.parametrize("case", gio.meta()["g8"], ids=lambda c: c["name"])
+def test_mobilenet_v2_model_level(case):
+    from fp8_quantization_amd.approx_calculation import QCustomBNConv2dTorch, QCustomLinearTorch
+    from fp8_quantization_amd.mobilenet_workload import mobilenet_v2_approx
+    g = gio.load("g8_mbv2.npz")
+    name = case["name"]
+    m = mobilenet_v2_approx(input_size=case["input_size"], width_mult=case["width_mult"], n_class=case["n_class"],
+                            expo_width=case["E"], mant_width=case["M"], withComp=case["with_comp"])
+    state = {k: torch.from_numpy(g[f"{name}__state__{k}"]) for k in case["state_keys"]}
+    missing, unexpected = torch.nn.Module.load_state_dict(m, state, strict=False)
+    assert not unexpected and not missing, (missing, unexpected)
+    m = m.to(DEV).eval()
+    m.quantized()
+    m.estimate_ranges()
+    with torch.no_grad():
+        m(torch.from_numpy(g[f"{name}__x_cal"]).to(DEV))
+    m.fix_ranges()
+    with torch.no_grad():
+        logits = m(torch.from_numpy(g[f"{name}__x_ev"]).to(DEV)).cpu().numpy()
+    mods = dict(m.named_modules())
+    for lname in case["approx_layers"]:
+        mod = mods[lname]
+        assert isinstance(mod, (QCustomBNConv2dTorch, QCustomLinearTorch))
+        for key, get in (("bA", mod.get_acts_fp_bias), ("bB", mod.get_weights_fp_bias), ("bR", mod.get_res_fp_bias)):
+            np.testing.assert_array_equal(get().reshape(-1).cpu().numpy(), g[f"{name}__{key}__{lname}"],
+                                          err_msg=f"{lname} {key}")
+    ref = g[f"{name}__logits"]
+    assert logits.shape == ref.shape
+    assert np.max(np.abs(logits - ref)) <= 1e-3 * np.abs(ref).max(), np.max(np.abs(logits - ref))
+    assert np.array_equal(logits.argmax(1), ref.argmax(1))

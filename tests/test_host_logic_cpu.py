@@ -86,3 +86,30 @@ def test_cpu_tensors_are_rejected_not_computed():
     from fp8_quantization_amd import approx_matmul
     with pytest.raises(RuntimeError):
         approx_matmul(torch.ones(2, 3), torch.ones(3, 2), 4, 3, 7, 7, 7, None, with_approx=True)
+
+
+def test_quantized_mobilenet_v2_matches_reference_module_tree():
+    """The module swap (fold_bn / quantize_sequential / quantize_model) applied to the float
+    MobileNetV2 gives the reference QuantizedMobileNetV2's exact state_dict layout (G8)."""
+    from fp8_quantization_amd.approx_calculation import QCustomBNConv2dTorch, QCustomLinearTorch
+    from fp8_quantization_amd.mobilenet_workload import mobilenet_v2_approx
+    c = gio.meta()["g8"][0]
+    g = gio.load("g8_mbv2.npz")
+    m = mobilenet_v2_approx(input_size=c["input_size"], width_mult=c["width_mult"], n_class=c["n_class"],
+                            expo_width=c["E"], mant_width=c["M"], withComp=c["with_comp"])
+    sd = m.state_dict()
+    assert set(sd) == set(c["state_keys"])
+    for k in c["state_keys"]:
+        assert tuple(sd[k].shape) == g[f"{c['name']}__state__{k}"].shape, k
+    names = [n for n, mod in m.named_modules() if isinstance(mod, (QCustomBNConv2dTorch, QCustomLinearTorch))]
+    assert names == c["approx_layers"]
+
+
+def test_module_swap_rejects_layers_outside_the_approx_path():
+    import pytest
+    from torch import nn
+
+    from fp8_quantization_amd.model_wrap import quantize_model
+    from fp8_quantization_amd.resnet_workload import approx_qparams
+    with pytest.raises(NotImplementedError):
+        quantize_model(nn.Sequential(nn.Conv1d(3, 4, 3)), **approx_qparams())
