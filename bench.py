@@ -44,14 +44,42 @@ def parse():
     ap.add_argument("--with-comp", action="store_true", help="withComp=True (E4M3: all-zero error table)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-columns", type=int, default=48, help="output columns per layer in the CPU sample")
-    ap.add_argument("--arch", default="resnet18", choices=["resnet18", "resnet50"])
+    ap.add_argument("--arch", default="resnet18", choices=["resnet18", "resnet50", "mobilenet_v2", "vit_fc"],
+                    help="resnet18 = the headline (BASELINE configs[1]); the others are BASELINE configs 3-5 "
+                         "measured the same way (vit_fc: the 768x3072 QCustomLinearTorch on [B, 197, 768])")
+    ap.add_argument("--expo-width", type=int, default=4)
+    ap.add_argument("--mant-width", type=int, default=3)
     return ap.parse_args()
 
 
-def synthetic_images(n, seed, device):
+def synthetic_images(n, seed, device, shape=(3, 224, 224)):
     g = torch.Generator(device="cpu").manual_seed(seed)
-    # ImageNet-normalised statistics: roughly N(0, 1) per channel
-    return torch.randn((n, 3, 224, 224), generator=g).to(device)
+    # ImageNet-normalised statistics: roughly N(0, 1) per channel (ViT fc: token features)
+    return torch.randn((n,) + tuple(shape), generator=g).to(device)
+
+
+def build_workload(arch, cfg):
+    """(model, per-image input shape, description) of a BASELINE config."""
+    from fp8_quantization_amd import resnet_workload as rw
+    if arch == "resnet18":
+        return rw.resnet18_approx(**cfg), (3, 224, 224), "resnet18"
+    if arch == "resnet50":
+        return rw.resnet50_approx(**cfg), (3, 224, 224), "resnet50"
+    if arch == "mobilenet_v2":
+        from fp8_quantization_amd.mobilenet_workload import mobilenet_v2_approx
+        return mobilenet_v2_approx(**cfg), (3, 224, 224), "mobilenet_v2"
+    from fp8_quantization_amd.approx_calculation import QCustomLinearTorch
+    from fp8_quantization_amd.model_wrap import QuantizedModel
+
+    class VitFc(QuantizedModel):  # vit_quantized_approx's intermediate dense: 768 -> 3072 on 197 tokens
+        def __init__(self):
+            super().__init__((1, 197, 768))
+            self.fc1 = QCustomLinearTorch(in_features=768, out_features=3072, bias=True, **rw.approx_qparams(**cfg))
+            self.fc1.flatten_leading_dims = True  # the reference asserts on 3-D inputs (SURVEY F4)
+
+        def forward(self, x):
+            return self.fc1(x)
+    return VitFc(), (197, 768), "vit_b16 fc1 (768x3072 QCustomLinearTorch, 197 tokens/image)"
 
 
 def pmc_traffic(round_tag="r01"):
@@ -109,28 +137,27 @@ def main():
     from fp8_quantization_amd import approx_ops as am
     from fp8_quantization_amd.distributed import broadcast_quant_state, gather_logits
     from fp8_quantization_amd.error_tables import get_error_table_NN
-    from fp8_quantization_amd.resnet_workload import (approx_layer_shapes, approx_macs_per_image, resnet18_approx,
-                                                      resnet50_approx)
+    from fp8_quantization_amd.resnet_workload import approx_layer_shapes, approx_macs_per_image
 
     fa._lib.load()
-    cfg = dict(expo_width=4, mant_width=3, dnsmp_factor=3, withComp=args.with_comp, with_approx=True,
-               with_s2nn2s_opt=True, quant_btw_mult_accu=True)
-    build = resnet18_approx if args.arch == "resnet18" else resnet50_approx
-    model = build(**cfg).to(dev).eval()
+    cfg = dict(expo_width=args.expo_width, mant_width=args.mant_width, dnsmp_factor=3, withComp=args.with_comp,
+               with_approx=True, with_s2nn2s_opt=True, quant_btw_mult_accu=True)
+    model, in_shape, arch_desc = build_workload(args.arch, cfg)
+    model = model.to(dev).eval()
 
     # calibration (one batch, identical on every rank), then fixed ranges -- image_net.py:76-91
     with torch.no_grad():
         shapes, hooks = approx_layer_shapes(model)
         model.quantized()
         model.estimate_ranges()
-        model(synthetic_images(args.cal_batch, 1234, dev))
+        model(synthetic_images(args.cal_batch, 1234, dev, in_shape))
         model.fix_ranges()
         for h in hooks:
             h.remove()
         broadcast_quant_state(model, src=0)  # identical bA/bB/bR on every rank
     macs_img = approx_macs_per_image(shapes)
 
-    x = synthetic_images(args.batch, 10 + rank, dev)  # this rank's shard of the validation batch
+    x = synthetic_images(args.batch, 10 + rank, dev, in_shape)  # this rank's shard of the validation batch
 
     def step():
         return gather_logits(model(x))  # one RCCL all-gather of logits per step (N > 1)
@@ -177,12 +204,12 @@ def main():
             "dtype": "fp32",
             "data": "synthetic",
             "config": {
-                "workload": f"{args.arch} E4M3 approx_v9 forward (dnsmp_factor=3, withComp={args.with_comp}, "
-                            "with_s2nn2s_opt, quant_btw_mult_accu, res_quantizer, fixed ranges), "
-                            "ImageNet-shaped synthetic batch, random-init weights",
+                "workload": f"{arch_desc} E{args.expo_width}M{args.mant_width} approx_v9 forward (dnsmp_factor=3, "
+                            f"withComp={args.with_comp}, with_s2nn2s_opt, quant_btw_mult_accu, res_quantizer, fixed "
+                            "ranges), ImageNet-shaped synthetic batch, random-init weights",
                 "global_batch": world * args.batch,
                 "per_gpu_batch": args.batch,
-                "image_hw": 224,
+                "input_shape_per_image": list(in_shape),
                 "approx_macs_per_image": macs_img,
                 "parallelism": f"dp{world}",
             },
@@ -200,7 +227,7 @@ def main():
                 "gemm_share_of_step": op_ms / 1e3 / elapsed,
             },
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and (args.expo_width, args.mant_width) == (4, 3):
             res["cpu_baseline"] = cpu_baseline(shapes, get_error_table_NN(4, 3, args.with_comp, 3), args.cpu_columns)
             res["speedup_vs_cpu_baseline"] = res["value"] / res["cpu_baseline"]["value"]
         print(json.dumps(res), flush=True)

@@ -1,19 +1,22 @@
 """ResNet-18 / ResNet-50 built from the drop-in approx operators (bench workload).
 
-Mirrors the module structure QuantizedResNet gives torchvision's ResNet in the reference
-(models/resnet_quantized_approx.py:11-130 + quantize_model / fold_bn,
-approx/replace_operations_with_approx_ops.py:263-384): every conv+BN pair becomes a
-QCustomBNConv2dTorch (approx), the fc a QCustomLinearTorch (approx), each residual block
-quantizes its output, the average pool re-uses the last block's activation quantizer without
-updating its range.  torchvision is not installed and pretrained weights need the network, so
-weights are random (kaiming, as torchvision initialises them); shapes are the real ones.
+The float network has torchvision's ResNet layout and parameter names (conv1 / bn1 / relu /
+maxpool / layer1-4 of BasicBlock or Bottleneck / avgpool / fc, so a torchvision checkpoint
+loads with ``load_float_weights``), and QuantizedResNet wraps it exactly the way the
+reference's models/resnet_quantized_approx.py:11-130 does: the stem and every block's
+conv+BN(+ReLU) become QCustomBNConv2dTorch through ``quantize_model`` (fold_bn), each block
+re-quantizes its output (QuantizedBlock), the average pool re-uses the last block's quantizer
+without updating its range, and the fc is a QCustomLinearTorch.  The quantized model's
+state_dict therefore has the reference's keys.  torchvision is not installed and pretrained
+weights need the network, so by default weights are random (torchvision's initialisation).
 """
 import torch
 from torch import nn
 
 from .approx_calculation import QCustomBNConv2dTorch, QCustomLinearTorch
+from .model_wrap import Flattener, QuantizedActivationWrapper, QuantizedModel, quantize_model
 from .quantization import FPQuantizer, RangeEstimators
-from .quantization.base_quantized_classes import QuantizedActivation, QuantizedModule
+from .quantization.base_quantized_classes import FP32Acts, QuantizedActivation
 
 
 def approx_qparams(expo_width=4, mant_width=3, dnsmp_factor=3, withComp=False, with_approx=True,
@@ -37,28 +40,113 @@ def approx_qparams(expo_width=4, mant_width=3, dnsmp_factor=3, withComp=False, w
 
 
 def _conv(qp, cin, cout, k, stride, pad, relu):
+    """One stand-alone approx conv + BN (+ ReLU) operator (tests)."""
     m = QCustomBNConv2dTorch(in_channels=cin, out_channels=cout, kernel_size=k, stride=stride, padding=pad,
                              bias=False, activation=nn.ReLU() if relu else None, **qp)
     nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
     return m
 
 
-class ApproxBlock(QuantizedActivation):
-    """QuantizedBlock (models/resnet_quantized_approx.py:11-41) for Basic / Bottleneck blocks."""
+# ------------------------------------------------------------------------- float ResNet (torchvision layout)
+class BasicBlock(nn.Module):
+    expansion = 1
 
-    def __init__(self, qp, cin, planes, stride, bottleneck):
-        super().__init__(**{k: v for k, v in qp.items() if k not in ("custom_approx_params",)})
-        exp = 4 if bottleneck else 1
-        if bottleneck:
-            feats = [_conv(qp, cin, planes, 1, 1, 0, True), _conv(qp, planes, planes, 3, stride, 1, True),
-                     _conv(qp, planes, planes * exp, 1, 1, 0, False)]
+    def __init__(self, cin, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(cin, planes, 3, stride, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.relu = nn.ReLU(inplace=True)
+        self.conv2 = nn.Conv2d(planes, planes, 3, 1, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x):
+        idt = x if self.downsample is None else self.downsample(x)
+        out = self.relu(self.bn1(self.conv1(x)))
+        return self.relu(self.bn2(self.conv2(out)) + idt)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(cin, planes, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, stride, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.conv3 = nn.Conv2d(planes, planes * 4, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * 4)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x):
+        idt = x if self.downsample is None else self.downsample(x)
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.relu(self.bn2(self.conv2(out)))
+        return self.relu(self.bn3(self.conv3(out)) + idt)
+
+
+class ResNet(nn.Module):
+    def __init__(self, block, layers, num_classes=1000):
+        super().__init__()
+        self.inplanes = 64
+        self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(3, 2, 1)
+        self.layer1 = self._layer(block, 64, layers[0], 1)
+        self.layer2 = self._layer(block, 128, layers[1], 2)
+        self.layer3 = self._layer(block, 256, layers[2], 2)
+        self.layer4 = self._layer(block, 512, layers[3], 2)
+        self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
+        self.fc = nn.Linear(512 * block.expansion, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.constant_(m.weight, 1)
+                nn.init.constant_(m.bias, 0)
+
+    def _layer(self, block, planes, n, stride):
+        down = None
+        if stride != 1 or self.inplanes != planes * block.expansion:
+            down = nn.Sequential(nn.Conv2d(self.inplanes, planes * block.expansion, 1, stride, bias=False),
+                                 nn.BatchNorm2d(planes * block.expansion))
+        blocks = [block(self.inplanes, planes, stride, down)]
+        self.inplanes = planes * block.expansion
+        blocks += [block(self.inplanes, planes) for _ in range(1, n)]
+        return nn.Sequential(*blocks)
+
+    def forward(self, x):
+        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        return self.fc(torch.flatten(self.avgpool(x), 1))
+
+
+def load_float_weights(model_fp, path):
+    """Load a torchvision-format float checkpoint (state dict) without executing pickled code."""
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    model_fp.load_state_dict(sd.get("state_dict", sd) if isinstance(sd, dict) else sd)
+    return model_fp
+
+
+# ------------------------------------------------------------------------- quantized wrappers
+class QuantizedBlock(QuantizedActivation):
+    """resnet_quantized_approx.py:11-41."""
+
+    def __init__(self, block, **quant_params):
+        super().__init__(**quant_params)
+        if isinstance(block, Bottleneck):
+            feats = nn.Sequential(block.conv1, block.bn1, block.relu, block.conv2, block.bn2, block.relu, block.conv3,
+                                  block.bn3)
         else:
-            feats = [_conv(qp, cin, planes, 3, stride, 1, True), _conv(qp, planes, planes, 3, 1, 1, False)]
-        self.features = nn.Sequential(*feats)
-        self.downsample = _conv(qp, cin, planes * exp, 1, stride, 0, False) if (stride != 1 or cin != planes * exp) \
-            else None
-        self.relu = nn.ReLU()
-        self.out_channels = planes * exp
+            feats = nn.Sequential(block.conv1, block.bn1, block.relu, block.conv2, block.bn2)
+        self.features = quantize_model(feats, **quant_params)
+        self.downsample = quantize_model(block.downsample, **quant_params) if block.downsample else None
+        self.relu = block.relu
 
     def forward(self, x):
         residual = x if self.downsample is None else self.downsample(x)
@@ -67,64 +155,41 @@ class ApproxBlock(QuantizedActivation):
         return self.quantize_activations(self.relu(out))
 
 
-class TiedAvgPool(QuantizedActivation):
-    """QuantizedActivationWrapper(avgpool, tie_activation_quantizers=True) (autoquant_utils.py:125-163)."""
+class QuantizedResNet(QuantizedModel):
+    """resnet_quantized_approx.py:44-130 (quant_setup None / "all" / "FP_logits")."""
 
-    def __init__(self, qp, input_quantizer):
-        super().__init__(**{k: v for k, v in qp.items() if k not in ("custom_approx_params",)})
-        self.activation_quantizer = input_quantizer
-        self.layer = nn.AdaptiveAvgPool2d((1, 1))
-
-    def forward(self, x):
-        x = self.layer(x)
-        return self.activation_quantizer.quantizer(x) if self._qa() else x
-
-
-class ApproxResNet(nn.Module):
-    def __init__(self, qp, layers=(2, 2, 2, 2), bottleneck=False, num_classes=1000):
-        super().__init__()
-        feats = [_conv(qp, 3, 64, 7, 2, 3, True), nn.MaxPool2d(3, 2, 1)]
-        cin = 64
-        for i, (planes, n) in enumerate(zip((64, 128, 256, 512), layers)):
-            blocks = []
-            for b in range(n):
-                blk = ApproxBlock(qp, cin, planes, 2 if (b == 0 and i > 0) else 1, bottleneck)
-                cin = blk.out_channels
-                blocks.append(blk)
-            feats.append(nn.Sequential(*blocks))
-        self.features = nn.Sequential(*feats)
-        self.avgpool = TiedAvgPool(qp, self.features[-1][-1].activation_quantizer)
-        self.fc = QCustomLinearTorch(in_features=cin, out_features=num_classes, bias=True, **qp)
-        bound = 1.0 / cin ** 0.5
-        nn.init.uniform_(self.fc.weight, -bound, bound)
-        nn.init.uniform_(self.fc.bias, -bound, bound)
+    def __init__(self, resnet, input_size=(1, 3, 224, 224), quant_setup=None, **quant_params):
+        super().__init__(input_size)
+        specials = {BasicBlock: QuantizedBlock, Bottleneck: QuantizedBlock}
+        feats = nn.Sequential(resnet.conv1, resnet.bn1, resnet.relu, resnet.maxpool, resnet.layer1, resnet.layer2,
+                              resnet.layer3, resnet.layer4)
+        self.features = quantize_model(feats, specials=specials, **quant_params)
+        self.avgpool = QuantizedActivationWrapper(resnet.avgpool, tie_activation_quantizers=True,
+                                                  input_quantizer=self.features[-1][-1].activation_quantizer,
+                                                  **quant_params)
+        self.flattener = Flattener()
+        self.fc = quantize_model(resnet.fc, **quant_params)
+        if quant_setup == "FP_logits":
+            self.fc.activation_quantizer = FP32Acts()
+        elif quant_setup is not None and quant_setup != "all":
+            raise ValueError("Quantization setup '{}' not supported for Resnet".format(quant_setup))
 
     def forward(self, x):
-        x = self.avgpool(self.features(x))
-        return self.fc(x.reshape(x.shape[0], -1))
-
-    # QuantizedModel-style switches (base_quantized_model.py)
-    def _each(self, fn):
-        for m in self.modules():
-            if isinstance(m, QuantizedModule):
-                fn(m)
-
-    def quantized(self):
-        self._each(lambda m: m.quantized())
-
-    def estimate_ranges(self):
-        self._each(lambda m: m.estimate_ranges())
-
-    def fix_ranges(self):
-        self._each(lambda m: m.fix_ranges())
+        return self.fc(self.flattener(self.avgpool(self.features(x))))
 
 
-def resnet18_approx(**cfg):
-    return ApproxResNet(approx_qparams(**cfg), (2, 2, 2, 2), bottleneck=False)
+def resnet18_approx(weights=None, **cfg):
+    fp = ResNet(BasicBlock, (2, 2, 2, 2))
+    if weights:
+        load_float_weights(fp, weights)
+    return QuantizedResNet(fp, **approx_qparams(**cfg))
 
 
-def resnet50_approx(**cfg):
-    return ApproxResNet(approx_qparams(**cfg), (3, 4, 6, 3), bottleneck=True)
+def resnet50_approx(weights=None, **cfg):
+    fp = ResNet(Bottleneck, (3, 4, 6, 3))
+    if weights:
+        load_float_weights(fp, weights)
+    return QuantizedResNet(fp, **approx_qparams(**cfg))
 
 
 def approx_layer_shapes(model, image_hw=224):
@@ -132,14 +197,13 @@ def approx_layer_shapes(model, image_hw=224):
     shapes, hooks = [], []
 
     def conv_hook(mod, inp, out):
-        x = inp[0]
         cog = mod.out_channels // mod.groups
         K = (mod.in_channels // mod.groups) * mod.kernel_size[0] * mod.kernel_size[1]
         shapes.append((type(mod).__name__, out.shape[2] * out.shape[3], K, cog, mod.groups))
-        del x
 
-    def lin_hook(mod, inp, out):
-        shapes.append((type(mod).__name__, 1, mod.in_features, mod.out_features, 1))
+    def lin_hook(mod, inp, out):  # rows per image: 1 for [B, K], T for token inputs [B, T, K]
+        rows = inp[0].numel() // (mod.in_features * inp[0].shape[0])
+        shapes.append((type(mod).__name__, rows, mod.in_features, mod.out_features, 1))
 
     for m in model.modules():
         if isinstance(m, QCustomBNConv2dTorch):
