@@ -122,7 +122,7 @@ def mini_test_batches(n_batches_total, num_batches=10, start_index=5, step=300):
     return out
 
 
-def build_model(arch, weights, cfg):
+def build_model(arch, weights, cfg, image_size=224):
     from . import resnet_workload as rw
     if arch == "resnet18":
         return rw.resnet18_approx(weights=weights, **cfg)
@@ -130,11 +130,11 @@ def build_model(arch, weights, cfg):
         return rw.resnet50_approx(weights=weights, **cfg)
     if arch == "mobilenet_v2":
         from .mobilenet_workload import MobileNetV2, QuantizedMobileNetV2
-        fp = MobileNetV2()
+        fp = MobileNetV2(input_size=image_size)  # its head pools with AvgPool2d(input_size // 32)
         if weights:
             sd = torch.load(weights, map_location="cpu", weights_only=True)
             fp.load_state_dict(sd.get("state_dict", sd))
-        return QuantizedMobileNetV2(fp, **rw.approx_qparams(**cfg))
+        return QuantizedMobileNetV2(fp, input_size=(1, 3, image_size, image_size), **rw.approx_qparams(**cfg))
     raise ValueError(f"unknown architecture {arch}")
 
 
@@ -196,7 +196,7 @@ def main(argv=None):
     if args.no_approx:
         cfg["run_method"] = dict(approx_flag=False, quantize_after_mult_and_add=False, res_quantizer_flag=True,
                                  original_quantize_res=False)
-    model = build_model(args.arch, args.weights, cfg).to(dev).eval()
+    model = build_model(args.arch, args.weights, cfg, args.image_size).to(dev).eval()
 
     # calibration on rank 0, ranges broadcast (identical biases everywhere)
     model.estimate_ranges()
