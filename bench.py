@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--arch", default="resnet18", choices=["resnet18", "resnet50", "mobilenet_v2", "vit_fc"],
                     help="resnet18 = the headline (BASELINE configs[1]); the others are BASELINE configs 3-5 "
                          "measured the same way (vit_fc: the 768x3072 QCustomLinearTorch on [B, 197, 768])")
+    ap.add_argument("--bn-stats-batches", type=int, default=4,
+                    help="synthetic batches that set the random-init float model's BN statistics (0 = keep the "
+                         "default (0, 1) statistics)")
     ap.add_argument("--expo-width", type=int, default=4)
     ap.add_argument("--mant-width", type=int, default=3)
     return ap.parse_args()
@@ -58,16 +61,17 @@ def synthetic_images(n, seed, device, shape=(3, 224, 224)):
     return torch.randn((n,) + tuple(shape), generator=g).to(device)
 
 
-def build_workload(arch, cfg):
+def build_workload(arch, cfg, bn_batches=0, device=None):
     """(model, per-image input shape, description) of a BASELINE config."""
     from fp8_quantization_amd import resnet_workload as rw
+    bn = dict(bn_stats_batches=bn_batches, device=device)
     if arch == "resnet18":
-        return rw.resnet18_approx(**cfg), (3, 224, 224), "resnet18"
+        return rw.resnet18_approx(**bn, **cfg), (3, 224, 224), "resnet18"
     if arch == "resnet50":
-        return rw.resnet50_approx(**cfg), (3, 224, 224), "resnet50"
+        return rw.resnet50_approx(**bn, **cfg), (3, 224, 224), "resnet50"
     if arch == "mobilenet_v2":
         from fp8_quantization_amd.mobilenet_workload import mobilenet_v2_approx
-        return mobilenet_v2_approx(**cfg), (3, 224, 224), "mobilenet_v2"
+        return mobilenet_v2_approx(**bn, **cfg), (3, 224, 224), "mobilenet_v2"
     from fp8_quantization_amd.approx_calculation import QCustomLinearTorch
     from fp8_quantization_amd.model_wrap import QuantizedModel
 
@@ -142,7 +146,7 @@ def main():
     fa._lib.load()
     cfg = dict(expo_width=args.expo_width, mant_width=args.mant_width, dnsmp_factor=3, withComp=args.with_comp,
                with_approx=True, with_s2nn2s_opt=True, quant_btw_mult_accu=True)
-    model, in_shape, arch_desc = build_workload(args.arch, cfg)
+    model, in_shape, arch_desc = build_workload(args.arch, cfg, args.bn_stats_batches, dev)
     model = model.to(dev).eval()
 
     # calibration (one batch, identical on every rank), then fixed ranges -- image_net.py:76-91
@@ -206,7 +210,9 @@ def main():
             "config": {
                 "workload": f"{arch_desc} E{args.expo_width}M{args.mant_width} approx_v9 forward (dnsmp_factor=3, "
                             f"withComp={args.with_comp}, with_s2nn2s_opt, quant_btw_mult_accu, res_quantizer, fixed "
-                            "ranges), ImageNet-shaped synthetic batch, random-init weights",
+                            "ranges), ImageNet-shaped synthetic batch, random-init weights"
+                            + (f" with BN statistics estimated on {args.bn_stats_batches} synthetic batches"
+                               if args.bn_stats_batches and args.arch != "vit_fc" else ""),
                 "global_batch": world * args.batch,
                 "per_gpu_batch": args.batch,
                 "input_shape_per_image": list(in_shape),

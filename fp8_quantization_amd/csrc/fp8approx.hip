@@ -153,7 +153,8 @@ __device__ __forceinline__ int64_t out_index(const GemmArgs &p, int64_t m, int64
 
 // Fast-path operand decode straight from the float32 bit pattern (int-bias semantics).
 //   returns ok: x is exactly a value of the (M, b) grid (any exponent: A/B are decoded with
-//               clip_OF=False, v9:58-59) and |x| is 0 or in [2^-40, 2^40] (exactness window,
+//               clip_OF=False, v9:58-59) and |x| is 0 or in [2^-62, 2^50] (exactness window:
+//               every product and table term a normal float, every Q_R constant finite,
 //               DESIGN.md §3).  Otherwise the launch is flagged and the exact kernel reruns it.
 //   m        : the M-bit mantissa code = the top M bits of the fp32 mantissa (the s2n scale-up
 //               by 2^M, v9:53, leaves the fp32 mantissa untouched)
@@ -167,7 +168,7 @@ __device__ __forceinline__ bool stage_decode(float x, int M, uint32_t emn, bool 
     const bool sub = ua < emn;  // |x| < min_norm = 2^(1-b)
     const uint32_t sh = (uint32_t)(23 - M) + (sub ? ((emn - ex) >> 23) : 0u);
     const bool grid = (sh < 24u) ? ((ua & ((1u << sh) - 1u)) == 0u) : (ua == 0u);
-    const bool win = (ua == 0u) || (ua >= 0x2B800000u /*2^-40*/ && ua <= 0x53800000u /*2^40*/);
+    const bool win = (ua == 0u) || (ua >= 0x20800000u /*2^-62*/ && ua <= 0x58800000u /*2^50*/);
     m = (ua >> (23 - M)) & ((1u << M) - 1u);
     c = (ua == 0u || (!s2n && sub)) ? 0.0f : __uint_as_float(u & 0xFF800000u);
     return grid && win;
@@ -222,7 +223,8 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
     int bcol[4], bkk[4];
     uint32_t emnB[4];
     int bbv[4];
-    bool bias_ok = bR >= -40 && bR <= 80 && bA >= -100 && bA <= 100;
+    // Q_R constants 2^(1-bR), 2^(-bR-M), 1.5 * 2^(1-bR+23-M) stay normal; decode fields fit
+    bool bias_ok = bR >= -100 && bR <= 120 && bA >= -100 && bA <= 120;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int e = tid + NT * r;
@@ -230,7 +232,7 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
         bkk[r] = b_ncontig ? (e >> 6) : (e & 15);
         const int64_t n = n0 + bcol[r];
         const int bb = (!QAMAA && n < p.N) ? p.bB[n * p.bBs] : 0;
-        bias_ok = bias_ok && bb >= -100 && bb <= 100;
+        bias_ok = bias_ok && bb >= -100 && bb <= 120;
         // v5: every decoded term 2^(e - bR) (1 + m/2^M) stays a normal float, so the ldexp form
         // below equals the reference's pow(2, e - bR) * (1 + m/2^M)
         if (V5) bias_ok = bias_ok && bA + bb <= 120;
@@ -633,31 +635,126 @@ __global__ __launch_bounds__(256) void conv_tb_direct_kernel(const float *x, con
                                                              int kh, int kw, int sh, int sw, int ph, int pw, int dh,
                                                              int dw, int groups, int64_t Ho, int64_t Wo, int E,
                                                              int Mw, const int32_t *bA, const int32_t *bW,
-                                                             const int32_t *bR, TablePack tab, uint32_t flags) {
+                                                             const int32_t *bR, TablePack tab, uint32_t flags,
+                                                             const uint32_t *gate) {
+    // after conv_tb_fast_kernel: run only if it flagged inputs outside its exactness window
+    if (gate != nullptr && __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
     const int64_t total = Bn * Cout * Ho * Wo;
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= total) return;
-    const int64_t wo = idx % Wo, ho = (idx / Wo) % Ho, co = (idx / (Wo * Ho)) % Cout, b = idx / (Wo * Ho * Cout);
     const int64_t cpg = Cin / groups;   // input channels per group
-    const int64_t g = co / (Cout / groups);
-    const DFmt fA = dfmt(E, Mw, *bA, true), fR = dfmt(E, Mw, *bR, true), fB = dfmt(E, Mw, bW[co], true);
-    float s = 0.0f, part = 0.0f;
-    int cnt = 0;
-    for (int64_t c = 0; c < cpg; ++c)
-        for (int ky = 0; ky < kh; ++ky)
-            for (int kx = 0; kx < kw; ++kx) {
-                const int64_t hi = ho * sh - ph + ky * dh, wi = wo * sw - pw + kx * dw;
-                const float a = (hi >= 0 && hi < H && wi >= 0 && wi < W)
-                                    ? x[((b * Cin + g * cpg + c) * H + hi) * W + wi] : 0.0f;
-                const float bv = w[((co * cpg + c) * kh + ky) * kw + kx];
-                part += exact_term(a, bv, fA, fB, fR, tab.raw, flags | F_TB);
-                if (++cnt == 16) {
-                    s += part;
-                    part = 0.0f;
-                    cnt = 0;
+    const DFmt fA = dfmt(E, Mw, *bA, true), fR = dfmt(E, Mw, *bR, true);
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t wo = idx % Wo, ho = (idx / Wo) % Ho, co = (idx / (Wo * Ho)) % Cout, b = idx / (Wo * Ho * Cout);
+        const int64_t g = co / (Cout / groups);
+        const DFmt fB = dfmt(E, Mw, bW[co], true);
+        float s = 0.0f, part = 0.0f;
+        int cnt = 0;
+        for (int64_t c = 0; c < cpg; ++c)
+            for (int ky = 0; ky < kh; ++ky)
+                for (int kx = 0; kx < kw; ++kx) {
+                    const int64_t hi = ho * sh - ph + ky * dh, wi = wo * sw - pw + kx * dw;
+                    const float a = (hi >= 0 && hi < H && wi >= 0 && wi < W)
+                                        ? x[((b * Cin + g * cpg + c) * H + hi) * W + wi] : 0.0f;
+                    const float bv = w[((co * cpg + c) * kh + ky) * kw + kx];
+                    part += exact_term(a, bv, fA, fB, fR, tab.raw, flags | F_TB);
+                    if (++cnt == 16) {
+                        s += part;
+                        part = 0.0f;
+                        cnt = 0;
+                    }
                 }
+        y[idx] = s + part;
+    }
+}
+
+// Single-output-channel groups (depthwise) with the tensor-bias semantics, fast form.
+// With int32-tensor biases >= 2 the reference's param_prepare yields min_norm = 0 (quirk F5):
+// no operand or result is subnormal, every nonzero value decodes at its own binade.  For
+// exactly representable operands (M-bit mantissa at their binade, |x| in [2^-62, 2^50]) and
+// with_s2nn2s_opt on, golden_clip_OF off, the term is then
+//   v0 = a*b - T[mA][mB] * cA * cB * 2^-M                         (exact, as in the GEMM)
+//   sign quirk F7: Q_R(g) is 0 only in the binade 2^-bR (expo 0, mantissa rounding to 0), where
+//                  a negative g gives the term |v0|
+//   Q_R, tb form: round at the value's own binade with the F6 clamp, except in the binade
+//                  [2^-bR, 2^(1-bR)) (expo field 0), whose decode is 2^(1-bR) * m / 2^M, i.e.
+//                  2 * (Q(x) - sign * 2^-bR)
+// Anything else sets the gate word and conv_tb_direct_kernel recomputes the launch exactly.
+// One thread per output pixel; grid (pixel chunks, Cout, Bn); the channel's decoded weights and
+// the error table live in LDS.
+constexpr int TBF_MAXK = 512;
+
+__global__ __launch_bounds__(256) void conv_tb_fast_kernel(const float *x, const float *w, float *y, int64_t Cin,
+                                                           int64_t H, int64_t W, int64_t Cout, int kh, int kw,
+                                                           int sh, int sw, int ph, int pw, int dh, int dw, int groups,
+                                                           int64_t Ho, int64_t Wo, int Mw, const int32_t *bA,
+                                                           const int32_t *bW, const int32_t *bR, TablePack tab,
+                                                           uint32_t flags, uint32_t *gate) {
+    __shared__ float sw_v[TBF_MAXK], sw_c[TBF_MAXK];
+    __shared__ int32_t sw_m[TBF_MAXK];
+    __shared__ float sT[1024];
+    const int64_t co = blockIdx.y, img = blockIdx.z;
+    const int64_t cpg = Cin / groups, g = co / (Cout / groups);
+    const int K = (int)(cpg * kh * kw), M = Mw, n = 1 << M;
+    const int a_b = *bA, r_b = *bR, w_b = bW[co];
+    const bool approx = flags & F_APPROX, qbma = flags & F_QBMA;
+    bool bad = !(a_b >= 2 && w_b >= 2 && r_b >= 2 && a_b <= 120 && w_b <= 120 && r_b <= 120 && K <= TBF_MAXK);
+    const uint32_t offgrid = (1u << (23 - M)) - 1u;
+    for (int i = threadIdx.x; i < n * n; i += blockDim.x) sT[i] = approx ? (float)tab.raw[i] : 0.0f;
+    for (int k = threadIdx.x; k < K && k < TBF_MAXK; k += blockDim.x) {
+        const float v = w[co * K + k];
+        const uint32_t ua = __float_as_uint(v) & 0x7FFFFFFFu;
+        bad |= (ua != 0u) && ((ua & offgrid) != 0u || ua < 0x20800000u || ua > 0x58800000u);
+        sw_v[k] = v;
+        sw_c[k] = __uint_as_float(__float_as_uint(v) & 0xFF800000u) * p2(-M);  // cB * 2^-M (0 for zeros)
+        sw_m[k] = (int32_t)((ua >> (23 - M)) & (uint32_t)(n - 1));
+    }
+    __syncthreads();
+    // Q_R constants (tb form: no subnormal floor)
+    const float kb = 2.0f - p2(-M) - p2(-22), kc = 1.5f * p2(23 - M);
+    const uint32_t q0exp = (uint32_t)(127 - r_b) << 23;             // exponent field of 2^-bR
+    const float zlo = p2(-r_b), zhi = p2(-r_b) * (1.0f + p2(-M - 1));  // |g| where Q_R(g) == 0
+    const int64_t pix = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = pix < Ho * Wo;
+    const int64_t ho = live ? pix / Wo : 0, wo = live ? pix - ho * Wo : 0;
+    float acc = 0.0f;
+    int k = 0;
+    for (int64_t c = 0; c < cpg; ++c) {
+        const float *xc = x + ((img * Cin + g * cpg + c) * H) * W;
+        for (int ky = 0; ky < kh; ++ky) {
+            const int64_t hi = ho * sh - ph + (int64_t)ky * dh;
+            for (int kx = 0; kx < kw; ++kx, ++k) {
+                const int64_t wi = wo * sw - pw + (int64_t)kx * dw;
+                const float a = (live && hi >= 0 && hi < H && wi >= 0 && wi < W) ? xc[hi * W + wi] : 0.0f;
+                const uint32_t ua = __float_as_uint(a) & 0x7FFFFFFFu;
+                bad |= (ua != 0u) && ((ua & offgrid) != 0u || ua < 0x20800000u || ua > 0x58800000u);
+                const float cA = __uint_as_float(__float_as_uint(a) & 0xFF800000u);
+                const int mA = (int)((ua >> (23 - M)) & (uint32_t)(n - 1));
+                const float b = sw_v[k];
+                const float gq = a * b;  // exact
+                float v = __fmaf_rn(-sT[mA * n + sw_m[k]], cA * sw_c[k], gq);
+                // F7: Q_R(g) == 0 (so the sign is +) only for |g| in [2^-bR, 2^-bR (1 + 2^-(M+1))]
+                const float ag = fabsf(gq);
+                if (gq < 0.0f && ag >= zlo && ag <= zhi) v = fabsf(v);
+                if (qbma) {
+                    const uint32_t pb = __float_as_uint(v) & 0x7F800000u;
+                    const float pe = __uint_as_float(pb);
+                    const float bd = pe * kb;
+                    const float xs = __builtin_amdgcn_fmed3f(v, -bd, bd);
+                    const float cc = pe * kc;
+                    float r = (xs + cc) - cc;
+                    if (pb == q0exp) r = 2.0f * (r - copysignf(pe, v));  // expo field 0: 2^(1-bR) m / 2^M
+                    v = r;
+                }
+                acc += v;
             }
-    y[idx] = s + part;
+        }
+    }
+    const bool anybad = __syncthreads_or(bad ? 1 : 0);
+    if (anybad) {
+        if (threadIdx.x == 0) atomicOr(gate, 1u);
+        return;
+    }
+    if (live) y[((img * Cout + co) * Ho + ho) * Wo + wo] = acc;
 }
 
 // FP8 fake quantizer (fp8_quantizer.py:97-173), one sign bit.
@@ -976,9 +1073,27 @@ int fp8a_conv2d(const float *x, const float *w, float *y, int64_t Bn, int64_t Ci
         rc = pack_table(table, Mw, flags & F_APPROX, tp, mode);
         if (rc) return rc;
         const int64_t total = Bn * Cout * Ho * Wo;
-        conv_tb_direct_kernel<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(
-            x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups, Ho, Wo, E, Mw, bA, bW, bR, tp,
-            flags | F_TB);
+        uint32_t *gate = nullptr;
+        // fast form: needs s2n on and golden_clip_OF off (else every launch would fall back)
+        const bool fast_ok = (flags & F_S2N) && !(flags & F_GCLIP) && workspace != nullptr &&
+                             workspace_bytes >= FLAG_BYTES && Cout <= 65535 && Bn <= 65535;
+        if (fast_ok) {
+            gate = (uint32_t *)workspace;
+            if (hipMemsetAsync(gate, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a gate reset");
+            dim3 grid((unsigned)((Ho * Wo + 255) / 256), (unsigned)Cout, (unsigned)Bn);
+            conv_tb_fast_kernel<<<grid, 256, 0, s>>>(x, w, y, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups,
+                                                     Ho, Wo, Mw, bA, bW, bR, tp, flags | F_TB, gate);
+            rc = hip_check("fp8a_conv2d (tensor-bias groups, fast)");
+            if (rc) return rc;
+        }
+        const unsigned eb = (unsigned)(fast_ok ? std::min<int64_t>((total + 255) / 256, 4096) : (total + 255) / 256);
+        if (fast_ok) {  // gated, grid-capped: a no-op launch unless the fast kernel flagged
+            conv_tb_direct_kernel<<<eb, 256, 0, s>>>(x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw,
+                                                    groups, Ho, Wo, E, Mw, bA, bW, bR, tp, flags | F_TB, gate);
+        } else {
+            conv_tb_direct_kernel<<<eb, 256, 0, s>>>(x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw,
+                                                     groups, Ho, Wo, E, Mw, bA, bW, bR, tp, flags | F_TB, nullptr);
+        }
         return hip_check("fp8a_conv2d (tensor-bias groups)");
     }
     // (a workspace below fp8a_conv2d_workspace_size but holding the flag word runs unsplit)

@@ -113,7 +113,9 @@ class QuantizedMobileNetV2(QuantizedModel):
         return self.classifier(self.flattener(self.features(x)))
 
 
-def mobilenet_v2_approx(input_size=224, width_mult=1.0, n_class=1000, **cfg):
-    from .resnet_workload import approx_qparams
+def mobilenet_v2_approx(input_size=224, width_mult=1.0, n_class=1000, bn_stats_batches=0, device=None, **cfg):
+    from .resnet_workload import approx_qparams, estimate_bn_statistics
     fp = MobileNetV2(n_class=n_class, input_size=input_size, width_mult=width_mult)
+    if bn_stats_batches:
+        estimate_bn_statistics(fp, bn_stats_batches, input_shape=(3, input_size, input_size), device=device)
     return QuantizedMobileNetV2(fp, input_size=(1, 3, input_size, input_size), **approx_qparams(**cfg))

@@ -126,6 +126,29 @@ class ResNet(nn.Module):
         return self.fc(torch.flatten(self.avgpool(x), 1))
 
 
+def estimate_bn_statistics(model_fp, batches=4, batch_size=32, input_shape=(3, 224, 224), device=None, seed=0):
+    """Give a random-init float model trained-like activation ranges: BN running statistics
+    become the cumulative mean / variance of its own activations on synthetic ImageNet-normalised
+    inputs (what BN statistics are after training).  Without this, eval-mode BN with the
+    default (0, 1) statistics lets activations shrink geometrically through a random network
+    (MobileNetV2: ~2^-40 by the head), far from any trained model's FP8 ranges."""
+    dev = device or next(model_fp.parameters()).device
+    model_fp.to(dev)
+    bns = [m for m in model_fp.modules() if isinstance(m, nn.modules.batchnorm._BatchNorm)]
+    for m in bns:
+        m.reset_running_stats()
+        m.momentum = None  # cumulative average
+    model_fp.train()
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    with torch.no_grad():
+        for _ in range(batches):
+            model_fp(torch.randn((batch_size,) + tuple(input_shape), generator=g).to(dev))
+    model_fp.eval()
+    for m in bns:
+        m.momentum = 0.1
+    return model_fp
+
+
 def load_float_weights(model_fp, path):
     """Load a torchvision-format float checkpoint (state dict) without executing pickled code."""
     sd = torch.load(path, map_location="cpu", weights_only=True)
@@ -178,17 +201,21 @@ class QuantizedResNet(QuantizedModel):
         return self.fc(self.flattener(self.avgpool(self.features(x))))
 
 
-def resnet18_approx(weights=None, **cfg):
+def resnet18_approx(weights=None, bn_stats_batches=0, device=None, **cfg):
     fp = ResNet(BasicBlock, (2, 2, 2, 2))
     if weights:
         load_float_weights(fp, weights)
+    elif bn_stats_batches:
+        estimate_bn_statistics(fp, bn_stats_batches, device=device)
     return QuantizedResNet(fp, **approx_qparams(**cfg))
 
 
-def resnet50_approx(weights=None, **cfg):
+def resnet50_approx(weights=None, bn_stats_batches=0, device=None, **cfg):
     fp = ResNet(Bottleneck, (3, 4, 6, 3))
     if weights:
         load_float_weights(fp, weights)
+    elif bn_stats_batches:
+        estimate_bn_statistics(fp, bn_stats_batches, device=device)
     return QuantizedResNet(fp, **approx_qparams(**cfg))
 
 

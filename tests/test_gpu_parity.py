@@ -302,6 +302,50 @@ def test_depthwise_conv_tensor_bias_semantics():
             assert_sums_close(got, Cref, S, f"channel {c} s2n={s2n}")
 
 
+@pytest.mark.parametrize("fmt", [(4, 3, "nocomp"), (3, 4, "comp3"), (2, 5, "comp3"), (3, 4, "nocomp")])
+@pytest.mark.parametrize("qbma", [True, False])
+def test_depthwise_fast_tensor_bias_per_term_bitexact(fmt, qbma):
+    """1x1 depthwise: every output is ONE tensor-bias term, so the fast depthwise kernel is
+    checked term by term against the oracle, including the expo-0 binade of Q_R and the F7
+    band (products near 2^-bR), zeros and every table mode."""
+    E, M, tname = fmt
+    rng = np.random.default_rng(E * 10 + M + int(qbma))
+    bA, bW_, bR = 2 ** (E - 1) + 3, 2 ** (E - 1) + 6, 2 ** (E - 1) + 4
+    C = 64
+    x = _grid_operands(rng, E, M, 4 * C, 50, bA, zero_frac=0.2, scale_bins=12).reshape(4, C, 5, 10)
+    w = _grid_operands(rng, E, M, C, 1, bW_, scale_bins=12).reshape(C, 1, 1, 1)
+    # steer some products into the binade [2^-bR, 2^(1-bR)) and onto the F7 band
+    w[:8, 0, 0, 0] = np.float32(2.0 ** -bR) / np.where(x[0, :8, 0, 0] == 0, 1, x[0, :8, 0, 0])
+    w = np.where(np.isfinite(w), w, 0).astype(np.float32)
+    bW = np.full(C, bW_, np.int32)
+    tab = g2_table(f"E{E}M{M}", tname)
+    fl = orc.flags_of(approx=True, s2n=True, qbma=qbma)
+    y = fa().approx_conv2d(t(x), t(w), E, M, torch.tensor([bA], device=DEV), t(bW, torch.int32),
+                           torch.tensor([bR], device=DEV), torch.as_tensor(tab), flags=fl, groups=C).cpu().numpy()
+    for c in range(C):
+        ref = orc.terms(x[:, c].reshape(-1, 1), w[c].reshape(1, 1), E, M, bA, bW[c:c + 1], bR, tab, fl | orc.TB)
+        assert_terms_equal(y[:, c].reshape(-1), ref.reshape(-1), f"channel {c}")
+
+
+def test_depthwise_fast_falls_back_on_off_grid_inputs():
+    rng = np.random.default_rng(11)
+    E, M = 4, 3
+    x = _grid_operands(rng, E, M, 2 * 16, 49, 9, zero_frac=0.3).reshape(2, 16, 7, 7)
+    x[1, 3, 2, 2] = 0.123456  # not an E4M3 value
+    w = _grid_operands(rng, E, M, 16, 9, 12).reshape(16, 1, 3, 3)
+    bW = np.full(16, 12, np.int32)
+    tab = g2_table("E4M3", "nocomp")
+    fl = orc.flags_of(approx=True, s2n=True, qbma=True)
+    y = fa().approx_conv2d(t(x), t(w), E, M, torch.tensor([9], device=DEV), t(bW, torch.int32),
+                           torch.tensor([10], device=DEV), torch.as_tensor(tab), flags=fl, padding=(1, 1),
+                           groups=16).cpu().numpy()
+    cols = _im2col_np(x, 3, 3, 1, 1, 1)
+    for c in range(16):
+        Cref, S = orc.matmul(cols[:, c * 9:(c + 1) * 9], w[c].reshape(9, 1), E, M, 9, 12, 10, tab, fl | orc.TB,
+                             with_abs=True)
+        assert_sums_close(y[:, c].reshape(-1, 1), Cref, S, f"channel {c}")
+
+
 # ------------------------------------------------------------------------------ FP8 fake quant
 @pytest.mark.parametrize("M", [3, 4, 5, 2])
 def test_fp8_fake_quantize_matches_oracle(M):
