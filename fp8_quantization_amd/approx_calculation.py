@@ -91,9 +91,13 @@ class ApproxConv2dMixin(ApproxOpMixin):
         _lib.check(rc, "fp8a_im2col")
         return out
 
-    def run_forward(self, x, weight, bias, offsets=None):
+    supports_bn_act_epilogue = True
+
+    def run_forward(self, x, weight, bias, offsets=None, epilogue=None):
         x = x.contiguous()
         weight = weight.contiguous()
+        if epilogue is not None and (bias is not None or not self.approx_flag):
+            raise AssertionError("the fused BN epilogue needs the approx product without a conv bias")
         w_bias = self.get_weights_fp_bias()
         a_bias = self.get_acts_fp_bias()
         r_bias = self.get_res_fp_bias()
@@ -103,7 +107,8 @@ class ApproxConv2dMixin(ApproxOpMixin):
                 raise TypeError("'NoneType' object is not subscriptable")
             out = approx_conv2d(x.detach(), weight.detach(), E, M, self._default_bias(a_bias, E, x.device),
                                 w_bias.reshape(-1), self._default_bias(r_bias, E, x.device), table, flags=flags,
-                                stride=self.stride, padding=self.padding, dilation=self.dilation, groups=self.groups)
+                                stride=self.stride, padding=self.padding, dilation=self.dilation, groups=self.groups,
+                                epilogue=epilogue)
         elif self.quantize_after_mult_and_add and self.out_channels // self.groups != 1:
             out = qamaa_conv2d(x.detach(), weight.detach(), *self._qamaa_params(), stride=self.stride,
                                padding=self.padding, dilation=self.dilation, groups=self.groups)

@@ -12,15 +12,17 @@ tensor-bias semantics (quirk F5 -- param_prepare's integer powers flush min_norm
 is what approx_multiply passes for single-column products (approx_calculation.py:800-809).
 """
 import ctypes
+from typing import Optional
 
 import torch
+from torch import nn
 
 from . import _lib
 from .error_tables import get_error_table_NN  # noqa: F401  (re-exported, v9:555)
 
 __all__ = ["custom_matmul_vectorize", "approx_matmul", "approx_terms", "approx_conv2d", "qamaa_matmul", "qamaa_conv2d",
            "quant_to_fp_any_vectorize_torch", "float_to_fpany_absint_torch", "get_error_table_NN",
-           "make_flags", "make_flags_v5", "fp8_fake_quantize"]
+           "make_flags", "make_flags_v5", "fp8_fake_quantize", "bn_act_epilogue"]
 
 
 def make_flags(with_approx=True, with_s2nn2s_opt=False, quant_btw_mult_accu=True, golden_clip_OF=False,
@@ -238,7 +240,8 @@ def float_to_fpany_absint_torch(values, expo_width, mant_width, custom_bias, cli
 @torch.library.custom_op("fp8approx::conv2d", mutates_args=())
 def _conv2d_op(x: torch.Tensor, w: torch.Tensor, bA: torch.Tensor, bW: torch.Tensor, bR: torch.Tensor,
                table: torch.Tensor, E: int, M: int, flags: int, stride: list[int], padding: list[int],
-               dilation: list[int], groups: int) -> torch.Tensor:
+               dilation: list[int], groups: int, bn: Optional[torch.Tensor] = None, act: int = 0,
+               act_lo: float = 0.0, act_hi: float = 0.0) -> torch.Tensor:
     L = _lib.load()
     x = x.contiguous()
     w = w.contiguous()
@@ -252,15 +255,26 @@ def _conv2d_op(x: torch.Tensor, w: torch.Tensor, bA: torch.Tensor, bW: torch.Ten
     y = torch.empty((Bn, Cout, Ho, Wo), dtype=torch.float32, device=x.device)
     nbytes = L.fp8a_conv2d_workspace_size(Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups)
     ws = _workspace(x.device, nbytes)
-    rc = L.fp8a_conv2d(_lib.dev_ptr(x), _lib.dev_ptr(w), _lib.dev_ptr(y), Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph,
-                       pw, dh, dw, groups, E, M, _lib.dev_ptr(bA), _lib.dev_ptr(bW), _lib.dev_ptr(bR),
-                       _lib.host_ptr(table), flags, _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(x.device))
-    _lib.check(rc, "fp8a_conv2d")
+    if bn is None:
+        rc = L.fp8a_conv2d(_lib.dev_ptr(x), _lib.dev_ptr(w), _lib.dev_ptr(y), Bn, Cin, H, W, Cout, kh, kw, sh, sw,
+                           ph, pw, dh, dw, groups, E, M, _lib.dev_ptr(bA), _lib.dev_ptr(bW), _lib.dev_ptr(bR),
+                           _lib.host_ptr(table), flags, _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(x.device))
+        _lib.check(rc, "fp8a_conv2d")
+        return y
+    if bn.shape != (Cout, 2) or bn.dtype != torch.float32 or not bn.is_contiguous() or bn.device != x.device:
+        raise AssertionError(f"approx_conv2d: epilogue parameters must be contiguous float32 [{Cout}, 2] "
+                             f"on {x.device}, got {tuple(bn.shape)} {bn.dtype} on {bn.device}")
+    rc = L.fp8a_conv2d_bn_act(_lib.dev_ptr(x), _lib.dev_ptr(w), _lib.dev_ptr(y), Bn, Cin, H, W, Cout, kh, kw, sh, sw,
+                              ph, pw, dh, dw, groups, E, M, _lib.dev_ptr(bA), _lib.dev_ptr(bW), _lib.dev_ptr(bR),
+                              _lib.host_ptr(table), flags, _lib.dev_ptr(bn), int(act), float(act_lo), float(act_hi),
+                              _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(x.device))
+    _lib.check(rc, "fp8a_conv2d_bn_act")
     return y
 
 
 @_conv2d_op.register_fake
-def _(x, w, bA, bW, bR, table, E, M, flags, stride, padding, dilation, groups):
+def _(x, w, bA, bW, bR, table, E, M, flags, stride, padding, dilation, groups, bn=None, act=0, act_lo=0.0,
+      act_hi=0.0):
     Bn, _, H, W = x.shape
     Cout, _, kh, kw = w.shape
     Ho = (H + 2 * padding[0] - dilation[0] * (kh - 1) - 1) // stride[0] + 1
@@ -269,10 +283,14 @@ def _(x, w, bA, bW, bR, table, E, M, flags, stride, padding, dilation, groups):
 
 
 def approx_conv2d(x, w, E, M, bA, bW, bR, table=None, flags=None, stride=(1, 1), padding=(0, 0), dilation=(1, 1),
-                  groups=1, **flag_kwargs):
+                  groups=1, epilogue=None, **flag_kwargs):
     """approx_v9 convolution, NCHW in / NCHW out (pre-BN), K ordered (c, ky, kx) like the
     reference im2col (approx_calculation.py:724-747); single-output-channel groups get the
-    tensor-bias semantics (approx_calculation.py:800-809).  bW: per output channel."""
+    tensor-bias semantics (approx_calculation.py:800-809).  bW: per output channel.
+
+    epilogue: optional ``(scale_shift [Cout, 2] float32 device tensor, act, lo, hi)`` fusing
+    the layer's eval-mode BatchNorm (y * scale + shift) and a clamp activation into the
+    kernel's store (fp8a_conv2d_bn_act, include/fp8approx.h); see ``bn_act_epilogue``."""
     if flags is None:
         flags = make_flags(**flag_kwargs)
     flags &= ~_lib.TB
@@ -286,9 +304,33 @@ def approx_conv2d(x, w, E, M, bA, bW, bR, table=None, flags=None, stride=(1, 1),
     ev = _prof_start()
     y = _conv2d_op(_as_f32(x), _as_f32(w), _bias_dev(bA, dev), bW_, _bias_dev(bR, dev), tab,
                    int(E), int(M), int(flags), [int(s) for s in stride], [int(p) for p in padding],
-                   [int(d) for d in dilation], int(groups))
+                   [int(d) for d in dilation], int(groups), *(epilogue or ()))
     _prof_end(ev, y.shape[0] * y.shape[2] * y.shape[3] * w.shape[0] * w.shape[1] * w.shape[2] * w.shape[3])
     return y
+
+
+def bn_act_epilogue(running_mean, running_var, gamma, beta, eps, activation=None):
+    """Epilogue parameters for approx_conv2d: eval-mode F.batch_norm as one scale/shift per
+    channel (scale = gamma / sqrt(var + eps), shift = beta - mean * scale, the transform ATen's
+    eval batch norm applies) and ReLU / ReLU6 / Hardtanh as a clamp.  Returns None when the
+    activation is not a clamp (the caller then runs it unfused)."""
+    if activation is None:
+        act, lo, hi = 0, 0.0, 0.0
+    elif type(activation) is nn.ReLU:
+        act, lo, hi = 1, 0.0, float("inf")
+    elif type(activation) is nn.ReLU6:
+        act, lo, hi = 1, 0.0, 6.0
+    elif type(activation) is nn.Hardtanh:
+        act, lo, hi = 1, float(activation.min_val), float(activation.max_val)
+    else:
+        return None
+    with torch.no_grad():
+        invstd = 1.0 / torch.sqrt(running_var.float() + eps)
+        scale = invstd * gamma.float() if gamma is not None else invstd
+        shift = -running_mean.float() * scale
+        if beta is not None:
+            shift = shift + beta.float()
+        return torch.stack((scale, shift), dim=1).contiguous(), act, lo, hi
 
 
 # ----------------------------------------------------------------------------------- FP8 fake quant

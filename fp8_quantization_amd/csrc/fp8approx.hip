@@ -127,8 +127,22 @@ struct GemmArgs {
     // qamaa: the res quantizer's FP8 fake quantizer (fp8_quantizer.py:97-173) per product
     const float *qmax;
     int qE, qM, qsign;
+    // fused eval-mode BatchNorm + activation epilogue (BNFusedHijacker: F.batch_norm then ReLU /
+    // ReLU6 / Hardtanh): per output channel {scale, shift}; ep_act clamps to [ep_lo, ep_hi]
+    const float2 *ep;
+    int ep_act;
+    float ep_lo, ep_hi;
     TablePack tab;
 };
+
+// y = x * scale + shift with scale = gamma * invstd, shift = beta - mean * scale (ATen's eval
+// batch-norm transform), then the activation clamp; c = output channel
+__device__ __forceinline__ float epi(const float2 *ep, int act, float lo, float hi, int64_t c, float x) {
+    if (ep == nullptr) return x;
+    const float2 e = ep[c];
+    const float v = __fmaf_rn(x, e.x, e.y);
+    return act ? fminf(fmaxf(v, lo), hi) : v;
+}
 
 // n / d for 0 <= n < 2^31 via one mulhi: q = (mulhi(n, mul) + n) >> shift (Granlund-Montgomery).
 static void fastdiv_params(uint32_t d, uint32_t &mul, uint32_t &shift) {
@@ -463,6 +477,14 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
     float *const C = partial ? p.part + split * p.M * p.N : p.C;
     const int64_t ldc = partial ? p.N : p.ldc, ctot = partial ? p.N : p.ctot, coff = partial ? 0 : p.coff;
     const int64_t nb = n0 + tx * TN;
+    if (!partial && p.ep != nullptr) {  // fused BN + activation (split-K applies it in the reduction)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int64_t ch = p.coff + min<int64_t>(nb + j, p.N - 1);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) acc[i][j] = epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, ch, acc[i][j]);
+        }
+    }
     if (!p.nchw) {
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
@@ -523,9 +545,22 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs p) {
             if (p.nchw) {
                 const int64_t img = q / (p.N * p.hw), rem = q - img * p.N * p.hw, n = rem / p.hw, pix = rem - n * p.hw;
                 o = (img * p.ctot + p.coff + n) * p.hw + pix;
+                if (p.ep) {  // the 4 values share channel coff + n (hw % 4 == 0)
+                    const int64_t ch = p.coff + n;
+                    acc.x = epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, ch, acc.x);
+                    acc.y = epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, ch, acc.y);
+                    acc.z = epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, ch, acc.z);
+                    acc.w = epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, ch, acc.w);
+                }
             } else {
                 const int64_t m = q / p.N, n = q - m * p.N;
                 o = m * p.ldc + n;
+                if (p.ep) {
+                    acc.x = epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, p.coff + n, acc.x);
+                    acc.y = epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, p.coff + n + 1, acc.y);
+                    acc.z = epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, p.coff + n + 2, acc.z);
+                    acc.w = epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, p.coff + n + 3, acc.w);
+                }
             }
             *reinterpret_cast<float4 *>(p.C + o) = acc;
         }
@@ -534,15 +569,17 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs p) {
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < MN; q += stride) {
         float acc = p.part[q];
         for (int sp = 1; sp < S; ++sp) acc += p.part[sp * MN + q];
-        int64_t o;
+        int64_t o, ch;
         if (p.nchw) {
             const int64_t img = q / (p.N * p.hw), rem = q - img * p.N * p.hw, n = rem / p.hw, pix = rem - n * p.hw;
             o = (img * p.ctot + p.coff + n) * p.hw + pix;
+            ch = p.coff + n;
         } else {
             const int64_t m = q / p.N, n = q - m * p.N;
             o = m * p.ldc + n;
+            ch = p.coff + n;
         }
-        p.C[o] = acc;
+        p.C[o] = epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, ch, acc);
     }
 }
 
@@ -576,7 +613,7 @@ __global__ __launch_bounds__(256) void gemm_exact_kernel(const GemmArgs p) {
             }
         }
         s += part;
-        p.C[out_index(p, m, n)] = s;
+        p.C[out_index(p, m, n)] = epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, p.coff + n, s);
     }
 }
 
@@ -636,7 +673,8 @@ __global__ __launch_bounds__(256) void conv_tb_direct_kernel(const float *x, con
                                                              int dw, int groups, int64_t Ho, int64_t Wo, int E,
                                                              int Mw, const int32_t *bA, const int32_t *bW,
                                                              const int32_t *bR, TablePack tab, uint32_t flags,
-                                                             const uint32_t *gate) {
+                                                             const uint32_t *gate, const float2 *ep, int ep_act,
+                                                             float ep_lo, float ep_hi) {
     // after conv_tb_fast_kernel: run only if it flagged inputs outside its exactness window
     if (gate != nullptr && __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
     const int64_t total = Bn * Cout * Ho * Wo;
@@ -663,7 +701,7 @@ __global__ __launch_bounds__(256) void conv_tb_direct_kernel(const float *x, con
                         cnt = 0;
                     }
                 }
-        y[idx] = s + part;
+        y[idx] = epi(ep, ep_act, ep_lo, ep_hi, co, s + part);
     }
 }
 
@@ -688,7 +726,8 @@ __global__ __launch_bounds__(256) void conv_tb_fast_kernel(const float *x, const
                                                            int sh, int sw, int ph, int pw, int dh, int dw, int groups,
                                                            int64_t Ho, int64_t Wo, int Mw, const int32_t *bA,
                                                            const int32_t *bW, const int32_t *bR, TablePack tab,
-                                                           uint32_t flags, uint32_t *gate) {
+                                                           uint32_t flags, uint32_t *gate, const float2 *ep,
+                                                           int ep_act, float ep_lo, float ep_hi) {
     __shared__ float sw_v[TBF_MAXK], sw_c[TBF_MAXK];
     __shared__ int32_t sw_m[TBF_MAXK];
     __shared__ float sT[1024];
@@ -754,7 +793,7 @@ __global__ __launch_bounds__(256) void conv_tb_fast_kernel(const float *x, const
         if (threadIdx.x == 0) atomicOr(gate, 1u);
         return;
     }
-    if (live) y[((img * Cout + co) * Ho + ho) * Wo + wo] = acc;
+    if (live) y[((img * Cout + co) * Ho + ho) * Wo + wo] = epi(ep, ep_act, ep_lo, ep_hi, co, acc);
 }
 
 // FP8 fake quantizer (fp8_quantizer.py:97-173), one sign bit.
@@ -1057,6 +1096,17 @@ int fp8a_conv2d(const float *x, const float *w, float *y, int64_t Bn, int64_t Ci
                 int64_t Cout, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw, int groups, int E,
                 int Mw, const int32_t *bA, const int32_t *bW, const int32_t *bR, const int32_t *table,
                 uint32_t flags, void *workspace, size_t workspace_bytes, fp8a_stream_t stream) {
+    return fp8a_conv2d_bn_act(x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups, E, Mw, bA, bW, bR,
+                              table, flags, nullptr, 0, 0.0f, 0.0f, workspace, workspace_bytes, stream);
+}
+
+int fp8a_conv2d_bn_act(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
+                       int64_t Cout, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw, int groups,
+                       int E, int Mw, const int32_t *bA, const int32_t *bW, const int32_t *bR, const int32_t *table,
+                       uint32_t flags, const float *bn, int act, float act_lo, float act_hi, void *workspace,
+                       size_t workspace_bytes, fp8a_stream_t stream) {
+    const float2 *ep = reinterpret_cast<const float2 *>(bn);
+    if (ep && (((uintptr_t)bn) & 7) != 0) return fail(FP8A_EINVAL, "bn parameters must be 8-byte aligned");
     hipStream_t s = (hipStream_t)stream;
     int rc = check_format(E, Mw);
     if (rc) return rc;
@@ -1082,17 +1132,20 @@ int fp8a_conv2d(const float *x, const float *w, float *y, int64_t Bn, int64_t Ci
             if (hipMemsetAsync(gate, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a gate reset");
             dim3 grid((unsigned)((Ho * Wo + 255) / 256), (unsigned)Cout, (unsigned)Bn);
             conv_tb_fast_kernel<<<grid, 256, 0, s>>>(x, w, y, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups,
-                                                     Ho, Wo, Mw, bA, bW, bR, tp, flags | F_TB, gate);
+                                                     Ho, Wo, Mw, bA, bW, bR, tp, flags | F_TB, gate, ep, act, act_lo,
+                                                     act_hi);
             rc = hip_check("fp8a_conv2d (tensor-bias groups, fast)");
             if (rc) return rc;
         }
         const unsigned eb = (unsigned)(fast_ok ? std::min<int64_t>((total + 255) / 256, 4096) : (total + 255) / 256);
         if (fast_ok) {  // gated, grid-capped: a no-op launch unless the fast kernel flagged
             conv_tb_direct_kernel<<<eb, 256, 0, s>>>(x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw,
-                                                    groups, Ho, Wo, E, Mw, bA, bW, bR, tp, flags | F_TB, gate);
+                                                    groups, Ho, Wo, E, Mw, bA, bW, bR, tp, flags | F_TB, gate, ep,
+                                                    act, act_lo, act_hi);
         } else {
             conv_tb_direct_kernel<<<eb, 256, 0, s>>>(x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw,
-                                                     groups, Ho, Wo, E, Mw, bA, bW, bR, tp, flags | F_TB, nullptr);
+                                                     groups, Ho, Wo, E, Mw, bA, bW, bR, tp, flags | F_TB, nullptr, ep,
+                                                     act, act_lo, act_hi);
         }
         return hip_check("fp8a_conv2d (tensor-bias groups)");
     }
@@ -1113,6 +1166,7 @@ int fp8a_conv2d(const float *x, const float *w, float *y, int64_t Bn, int64_t Ci
         a.kh = kh; a.kw = kw; a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw; a.dh = dh; a.dw = dw;
         fastdiv_params((uint32_t)(kh * kw), a.kk_mul, a.kk_shift);
         fastdiv_params((uint32_t)kw, a.kw_mul, a.kw_shift);
+        a.ep = ep; a.ep_act = act; a.ep_lo = act_lo; a.ep_hi = act_hi;
         rc = run_gemm(a, table, workspace, workspace_bytes, s);
         if (rc) return rc;
     }

@@ -41,8 +41,10 @@ class QuantizationHijacker(QuantizedModule):
                              "you need to set res_quantizer_flag to True if you want to use "
                              "quantize_after_mult_and_add or approx_flag")
 
-    def _core(self, x, offsets=None):
-        """Shared part of QuantizationHijacker.forward and BNFusedHijacker.forward."""
+    def _core(self, x, offsets=None, epilogue=None):
+        """Shared part of QuantizationHijacker.forward and BNFusedHijacker.forward.  epilogue
+        (BNFusedHijacker's fused BN + activation) goes to the approx product only; the caller
+        guarantees that product is the only one this forward runs."""
         qa = self._qa()
         if self.quantize_input and qa:
             x = self.activation_quantizer(x)
@@ -55,12 +57,15 @@ class QuantizationHijacker(QuantizedModule):
         if self.res_quantizer_flag and self.quantize_after_mult_and_add:
             res = self.run_forward(x, weight, bias)
         if self.res_quantizer_flag and self.approx_flag:
-            res = self.run_forward(x, weight, bias, offsets=offsets)
+            if epilogue is not None:
+                res = self.run_forward(x, weight, bias, offsets=offsets, epilogue=epilogue)
+            else:
+                res = self.run_forward(x, weight, bias, offsets=offsets)
         self._check_res_flag()
         return res, qa
 
-    def _epilogue(self, res, qa):
-        if self.activation_function is not None:
+    def _epilogue(self, res, qa, activation_done=False):
+        if self.activation_function is not None and not activation_done:
             res = self.activation_function(res)
         if not self.quantize_input and qa:
             res = self.activation_quantizer(res)

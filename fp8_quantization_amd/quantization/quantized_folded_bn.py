@@ -2,7 +2,16 @@
 
 Same state machine as QuantizationHijacker, then F.batch_norm with the layer's own running
 statistics (BN is applied after the approx product, not folded into the weights).
+
+Fused epilogue (MI355X-side, same result within fp32 rounding): when the forward reduces to one
+approx product followed by eval-mode batch norm -- eval mode, fixed ranges, approx_flag +
+res_quantizer_flag, no original_quantize_res / qamaa -- the batch norm and a clamp activation
+(ReLU / ReLU6 / Hardtanh) run inside the conv kernel's store instead of as two more passes over
+the output (fp8a_conv2d_bn_act).  ``fuse_bn_act = False`` on the class or instance, or
+FP8A_FUSE_BN=0 in the environment, keeps the unfused sequence.
 """
+import os
+
 import torch
 import torch.nn.functional as F
 from torch import nn
@@ -12,6 +21,8 @@ from .hijacker import QuantizationHijacker
 
 
 class BNFusedHijacker(QuantizationHijacker):
+    fuse_bn_act = os.environ.get("FP8A_FUSE_BN", "1") != "0"
+
     def __init__(self, *args, **kwargs):
         kwargs.pop("bias", None)
         super().__init__(*args, **kwargs, bias=False)
@@ -24,7 +35,27 @@ class BNFusedHijacker(QuantizationHijacker):
         self.epsilon = kwargs.get("eps", 1e-5)
         self.bias = None
 
+    def _fused_epilogue(self):
+        """(scale_shift, act, lo, hi) for the kernel epilogue, or None when the forward is not
+        the single-product eval form (see module doc) or the activation is not a clamp."""
+        if (not self.fuse_bn_act or self.training or not self.fix_ranges_flag or self.original_quantize_res
+                or self.quantize_after_mult_and_add or not self.approx_flag or not self.res_quantizer_flag
+                or not getattr(self, "supports_bn_act_epilogue", False)):
+            return None
+        from ..approx_ops import bn_act_epilogue
+        ts = (self.running_mean, self.running_var, self.gamma, self.beta)
+        key = tuple((t._version, t.data_ptr(), t.device) for t in ts) + (self.epsilon, id(self.activation_function))
+        cached = getattr(self, "_bn_act_cache", None)
+        if cached is None or cached[0] != key:
+            cached = (key, bn_act_epilogue(*ts, self.epsilon, self.activation_function))
+            self._bn_act_cache = cached
+        return cached[1]
+
     def forward(self, x):
+        ep = self._fused_epilogue()
+        if ep is not None:
+            res, qa = self._core(x, epilogue=ep)
+            return self._epilogue(res, qa, activation_done=True)
         res, qa = self._core(x)
         res = F.batch_norm(res, self.running_mean, self.running_var, self.gamma, self.beta, self.training,
                            self.momentum, self.epsilon)

@@ -117,6 +117,22 @@ int fp8a_conv2d(const float *x, const float *w, float *y, int64_t Bn, int64_t Ci
                 size_t workspace_bytes, fp8a_stream_t stream);
 
 /*
+ * fp8a_conv2d with the layer's eval-mode BatchNorm and activation fused into the epilogue
+ * (BNFusedHijacker.forward: F.batch_norm after run_forward, then the activation,
+ * quantization/quantized_folded_bn.py:30-83): y = acc * scale + shift per output channel, with
+ * scale = gamma / sqrt(running_var + eps) and shift = beta - running_mean * scale (the eval-mode
+ * transform ATen applies), then clamped to [act_lo, act_hi] when act != 0 (ReLU: [0, inf],
+ * ReLU6: [0, 6], Hardtanh: [min_val, max_val]).  bn: device float [Cout][2] = {scale, shift},
+ * 8-byte aligned, or NULL (plain fp8a_conv2d).
+ */
+int fp8a_conv2d_bn_act(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin,
+                       int64_t H, int64_t W, int64_t Cout, int kh, int kw, int sh, int sw, int ph,
+                       int pw, int dh, int dw, int groups, int E, int Mw, const int32_t *bA,
+                       const int32_t *bW, const int32_t *bR, const int32_t *table, uint32_t flags,
+                       const float *bn, int act, float act_lo, float act_hi, void *workspace,
+                       size_t workspace_bytes, fp8a_stream_t stream);
+
+/*
  * quantize_after_mult_and_add (qamaa) path of approx_multiply (approx_calculation.py:787-795):
  *   C = fq(sum_k fq(A[m,k] * B(k,n))),  fq = quantize_to_fp8_ste_MM with the res quantizer's
  *   n_bits / mantissa bits / sign bits and per-tensor maxval (device float [1]).

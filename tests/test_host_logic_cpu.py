@@ -113,3 +113,40 @@ def test_module_swap_rejects_layers_outside_the_approx_path():
     from fp8_quantization_amd.resnet_workload import approx_qparams
     with pytest.raises(NotImplementedError):
         quantize_model(nn.Sequential(nn.Conv1d(3, 4, 3)), **approx_qparams())
+
+
+def test_bn_act_epilogue_eligibility_and_parameters():
+    """BNFusedHijacker hands BN + clamp activation to the kernel only in the single-product
+    eval form (quantized_folded_bn.py module doc); the scale/shift pair is ATen's eval transform."""
+    from fp8_quantization_amd.approx_calculation import QCustomBNConv2dTorch
+    from fp8_quantization_amd.approx_ops import bn_act_epilogue
+    conv = QCustomBNConv2dTorch(in_channels=4, out_channels=8, kernel_size=3, padding=1, bias=False,
+                                activation=nn.ReLU6(), **_qparams())
+    with torch.no_grad():
+        conv.running_mean.uniform_(-1, 1)
+        conv.running_var.uniform_(0.5, 2)
+        conv.gamma.uniform_(0.5, 1.5)
+        conv.beta.uniform_(-1, 1)
+    conv.eval()
+    assert conv._fused_epilogue() is None            # ranges not fixed yet
+    conv.fix_ranges_flag = True
+    ss, act, lo, hi = conv._fused_epilogue()
+    assert (act, lo, hi) == (1, 0.0, 6.0) and ss.shape == (8, 2)
+    y = torch.randn(3, 8, 5, 5)
+    bn = torch.nn.functional.batch_norm(y, conv.running_mean, conv.running_var, conv.gamma, conv.beta, False, 0.1,
+                                        conv.epsilon)
+    torch.testing.assert_close(y * ss[:, 0].view(1, -1, 1, 1) + ss[:, 1].view(1, -1, 1, 1), bn, rtol=1e-5,
+                               atol=1e-5)
+    conv.train()
+    assert conv._fused_epilogue() is None
+    conv.eval()
+    conv.original_quantize_res = True
+    assert conv._fused_epilogue() is None
+    conv.original_quantize_res = False
+    conv.fuse_bn_act = False
+    assert conv._fused_epilogue() is None
+    conv.fuse_bn_act = True
+    conv.activation_function = nn.GELU()
+    assert conv._fused_epilogue() is None            # not a clamp: BN + GELU stay unfused
+    assert bn_act_epilogue(conv.running_mean, conv.running_var, None, None, 1e-5, nn.ReLU())[1:] == \
+        (1, 0.0, float("inf"))
