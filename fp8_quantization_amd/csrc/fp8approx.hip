@@ -45,7 +45,8 @@ static int hip_check(const char *what) {
 //   TM_LUT  : anything else -> float LUT in LDS (E2M5 no-comp: entries up to 5)
 enum TMode : int { TM_NONE = 0, TM_W1U = 1, TM_W2S1 = 2, TM_W2U1 = 3, TM_W2S2 = 4, TM_W2U2 = 5, TM_LUT = 6,
                    TM_QAMAA = 7 /* quantize_after_mult_and_add: term = fq(a*b), no decode */,
-                   TM_V5 = 8 /* v5 integer-adder model: code sum + compensation LUT, OF/UF wrap */ };
+                   TM_V5 = 8 /* v5 integer-adder model: code sum + compensation LUT, OF/UF wrap */,
+                   TM_F8 = 9 /* E4M3 with s2n + qbma, table in {0,1}: LDS term LUT + hardware fp8 Q_R */ };
 
 struct TablePack {
     uint32_t rows[64][2];  // packed rows for the bit modes (2^M <= 64)
@@ -192,16 +193,20 @@ template <bool S2N, bool QBMA, bool GCLIP, int TMODE>
 __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
     constexpr bool QAMAA = TMODE == TM_QAMAA;
     constexpr bool V5 = TMODE == TM_V5;
-    constexpr bool TBL = TMODE != TM_NONE && !QAMAA;
+    constexpr bool F8 = TMODE == TM_F8;
+    constexpr bool TBL = TMODE != TM_NONE && !QAMAA && !F8;
     constexpr int R = (TMODE == TM_W2S2 || TMODE == TM_W2U2) ? 2 : 1;
     constexpr bool SGN = (TMODE == TM_W2S1 || TMODE == TM_W2S2 || TMODE == TM_LUT);
 
     __shared__ __attribute__((aligned(16))) float sA[BK][AP];
     __shared__ __attribute__((aligned(16))) float sB[BK][BP];
     __shared__ __attribute__((aligned(16))) float sAc[TBL ? BK : 1][AP];
-    __shared__ __attribute__((aligned(16))) uint32_t sAr[TBL ? R * BK : 1][AP];
+    __shared__ __attribute__((aligned(16))) uint32_t sAr[(TBL || F8) ? R * BK : 1][AP];
     __shared__ __attribute__((aligned(16))) float sBc[TBL ? BK : 1][BP];
-    __shared__ __attribute__((aligned(16))) uint32_t sBm[TBL ? BK : 1][BP];
+    __shared__ __attribute__((aligned(16))) uint32_t sBm[(TBL || F8) ? BK : 1][BP];
+    // F8: the normalised term V'(sign a, m_a, m_b) = min(sig_a sig_b - T[m_a][m_b] 2^-M, top of
+    // its binade), 17 rows (2 signs x 8 codes + a zero row) x 2 copies x 8 (see F8_ROW)
+    __shared__ __attribute__((aligned(16))) float sF8[F8 ? 17 * 16 : 1];
     __shared__ float sLut[TMODE == TM_LUT ? 1024 : 1];
     __shared__ int32_t sLutI[V5 ? 1024 : 1];
     __shared__ uint32_t sRows[TBL ? 64 * 2 : 1];
@@ -222,6 +227,29 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
     const uint32_t emnA = (uint32_t)(128 - bA) << 23;
     const float ulpM = p2(-M);
 
+    // F8 Q_R: the result grid of bias bR (floor step 2^(-2-bR), binades from 2^(1-bR)) is the
+    // OCP e4m3 grid scaled by 2^(7-bR), so Q_R(y) = 2^(7-bR) * cvt_fp8(y / 2^(7-bR)) (RNE) for y
+    // already clamped to Q_R's bound (the clamp scales with y's binade, so it is folded into the
+    // LUT value V'), except beyond the e4m3 range (NaN: flagged in the epilogue, the exact kernel
+    // reruns the launch)
+    const float f8S = F8 ? __uint_as_float((uint32_t)min(max(134 - bR, 1), 254) << 23) : 0.0f;
+    if (F8) {
+        for (int e = tid; e < 17 * 16; e += NT) {
+            const int r = e >> 4, mb = e & 7;  // both 8-entry copies of a row hold the same values
+            float v = 0.0f;
+            if (r < 16) {
+                const int ma = r & 7;
+                const float t = (float)p.tab.raw[ma * 8 + mb];
+                v = __fmaf_rn(1.0f + 0.125f * ma, 1.0f + 0.125f * mb, -t * 0.125f);  // exact
+                // Q_R's pre-clamp bound 2^e (2 - 2^-M - 2^-22) (QC::kb): the mantissa saturates
+                // instead of carrying, and on the subnormal grid the top tie rounds down
+                v = fminf(v, __uint_as_float(__float_as_uint(v) & 0x7F800000u) * (1.875f - p2(-22)));
+                if (r >= 8) v = -v;
+            }
+            sF8[e] = v;
+        }
+        __syncthreads();
+    }
     if (TBL) {
         const int n = 1 << M;
         for (int i = tid; i < n * 2; i += NT) sRows[i] = p.tab.rows[i >> 1][i & 1];
@@ -333,6 +361,19 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
                 sAr[kk][row] = (uint32_t)m << M;
                 continue;
             }
+            if (F8) {
+                // cvt scale 2^(7-bR) / |c| (applied to x' = V' * c_b inside the conversion) and the
+                // byte offset of the LUT row; rows with ty even / odd read copies on disjoint banks
+                bad |= !stage_decode(x, M, emnA, true, c, mc);
+                const uint32_t cb = __float_as_uint(c);
+                const int se = 261 - bR - (int)((cb >> 23) & 0xFFu);
+                const bool zero = (cb & 0x7FFFFFFFu) == 0u;
+                bad |= !zero && (se < 1 || se > 254);
+                sA[kk][row] = zero ? f8S : __uint_as_float((uint32_t)min(max(se, 1), 254) << 23);
+                const uint32_t rr = zero ? 16u : ((cb >> 31) * 8u + mc);
+                sAr[kk][row] = (rr * 16u + (uint32_t)((row >> 2) & 1) * 8u) * 4u;
+                continue;
+            }
             if (!QAMAA) bad |= !stage_decode(x, M, emnA, S2N, c, mc);
             sA[kk][row] = x;
             if (TBL) {
@@ -358,6 +399,12 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
                 sB[kk][col] = __int_as_float(((e - (bA + bbv[r] - bR)) << M) + m);
                 sBc[kk][col] = __uint_as_float(x < 0.0f ? 0x80000000u : 0u);
                 sBm[kk][col] = (uint32_t)m;
+                continue;
+            }
+            if (F8) {
+                bad |= !stage_decode(x, M, emnB[r], true, c, mc);
+                sB[kk][col] = c;  // sign(b) 2^floor(log2|b|), 0 for b = 0
+                sBm[kk][col] = mc * 4u;
                 continue;
             }
             if (!QAMAA) bad |= !stage_decode(x, M, emnB[r], S2N, c, mc);
@@ -391,6 +438,30 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j) tacc[i][j] += fq_fast(a[i] * b[j], fq);
+            } else if (F8) {
+                // a = scales, b = c_b; term = Q_R(V' * c_a * c_b) via the scaled fp8 round trip
+                const uint4 ia4 = *reinterpret_cast<const uint4 *>(&sAr[kk][ty * TM]);
+                const uint4 ib4 = *reinterpret_cast<const uint4 *>(&sBm[kk][tx * TN]);
+                const uint32_t ia[TM] = {ia4.x, ia4.y, ia4.z, ia4.w};
+                const uint32_t ib[TN] = {ib4.x, ib4.y, ib4.z, ib4.w};
+                const char *lut = reinterpret_cast<const char *>(sF8);
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    float xv[TN];
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        xv[j] = *reinterpret_cast<const float *>(lut + (ia[i] + ib[j])) * b[j];
+                    typedef short s2 __attribute__((ext_vector_type(2)));
+                    s2 code = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32((s2){0, 0}, xv[0], xv[1], a[i], false);
+                    code = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(code, xv[2], xv[3], a[i], true);
+                    const uint32_t cu = __builtin_bit_cast(uint32_t, code);
+                    const auto lo = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(cu, f8S, false);
+                    const auto hi = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(cu, f8S, true);
+                    tacc[i][0] += lo[0];
+                    tacc[i][1] += lo[1];
+                    tacc[i][2] += hi[0];
+                    tacc[i][3] += hi[1];
+                }
             } else if (V5) {
                 const float4 ac4 = *reinterpret_cast<const float4 *>(&sAc[kk][ty * TM]);
                 const uint4 ar4 = *reinterpret_cast<const uint4 *>(&sAr[kk][ty * TM]);
@@ -472,6 +543,14 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
         __syncthreads();
     }
 
+    if (F8) {  // a term beyond the e4m3 range came back NaN: the exact kernel reruns the launch
+        bool nan = false;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) nan |= __builtin_isnan(acc[i][j]);
+        if (__syncthreads_or(nan ? 1 : 0) && tid == 0) atomicOr(p.flag, 1u);
+    }
     // ---- epilogue (a split-K partial goes to its slice of the workspace, same layout)
     const bool partial = p.splits > 1;
     float *const C = partial ? p.part + split * p.M * p.N : p.C;
@@ -844,6 +923,10 @@ static void launch_fast(int mode, const GemmArgs &a, hipStream_t s) {
         gemm_fast_kernel<false, false, false, TM_V5><<<grid, NT, 0, s>>>(a);
         return;
     }
+    if (mode == TM_F8) {  // s2n + qbma, no golden clip (selected in run_gemm)
+        gemm_fast_kernel<true, true, false, TM_F8><<<grid, NT, 0, s>>>(a);
+        return;
+    }
     const bool s2n = a.flags & F_S2N, q = a.flags & F_QBMA, gc = a.flags & F_GCLIP;
     if (s2n) {
         if (q) { gc ? launch_fast_t<true, true, true>(mode, a, grid, s) : launch_fast_t<true, true, false>(mode, a, grid, s); }
@@ -944,6 +1027,12 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     rc = pack_table(table, a.Mw, v5 || (a.flags & F_APPROX), a.tab, mode);
     if (rc) return rc;
     if (v5) mode = TM_V5;
+    // E4M3 with a {0,1} (or no) table, s2n and per-product quantization: the LUT + hardware-fp8
+    // form (FP8A_NO_F8=1 keeps the arithmetic form, for comparison)
+    static const bool no_f8 = getenv("FP8A_NO_F8") != nullptr;
+    if (!v5 && !no_f8 && a.E == 4 && a.Mw == 3 && (mode == TM_NONE || mode == TM_W1U) && (a.flags & F_S2N) &&
+        (a.flags & F_QBMA) && !(a.flags & F_GCLIP) && !(a.flags & F_TB))
+        mode = TM_F8;
     const int64_t total = a.M * a.N;
     const unsigned eblocks = (unsigned)std::min<int64_t>((total + 255) / 256, 4096);
     if (a.flags & F_TB) {

@@ -1,0 +1,115 @@
+"""The E4M3 LUT + hardware-fp8 form of the fast kernel (TM_F8).
+
+For E4M3 with s2n and per-product quantization and a {0,1} (or no) error table, the term
+Q_R(a*b - T*c_a*c_b*2^-M) is computed as a clamped LDS table value V'(sign a, m_a, m_b) times
+c_b, rounded by the gfx950 scaled fp8 conversion.  Checked here:
+  * every one of the 256 x 256 E4M3 code pairs as a K = 1 product (one term per output),
+    bit-exact against the oracle, for several bias triples, with the launch's fallback flag
+    read back to prove the fast form (not the exact kernel) produced them;
+  * terms beyond the e4m3 range raise the flag and the exact kernel's result is returned;
+  * sums at realistic shapes stay within the 1e-5 * sum|term| bar.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as orc
+from tests import golden_io as gio
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device")
+    from fp8_quantization_amd import _lib
+    _lib.load()
+
+
+def _all_codes(bias):
+    """The 256 E4M3 values of the given bias (both zeros included)."""
+    e = np.repeat(np.arange(16), 8)
+    m = np.tile(np.arange(8), 16)
+    v = np.where(e == 0, np.ldexp(m / 8.0, 1 - bias), np.ldexp(1.0 + m / 8.0, e - bias))
+    return np.concatenate([v, -v]).astype(np.float32)
+
+
+def _matmul_raw(A, B, bA, bB, bR, table, flags):
+    """fp8a_matmul through ctypes with a caller-owned workspace: returns (C, flag word)."""
+    from fp8_quantization_amd import _lib
+    L = _lib.load()
+    A = torch.from_numpy(np.ascontiguousarray(A)).to(DEV)
+    B = torch.from_numpy(np.ascontiguousarray(B)).to(DEV)
+    Mr, K = A.shape
+    N = B.shape[1]
+    C = torch.empty((Mr, N), dtype=torch.float32, device=DEV)
+    ws = torch.zeros(max(int(L.fp8a_matmul_workspace_size_mnk(Mr, N, K)), 256), dtype=torch.uint8, device=DEV)
+    tA = torch.tensor([bA], dtype=torch.int32, device=DEV)
+    tB = torch.as_tensor(np.asarray(bB, np.int32).reshape(-1)).to(DEV)
+    tR = torch.tensor([bR], dtype=torch.int32, device=DEV)
+    tab = torch.as_tensor(np.ascontiguousarray(table, np.int32)) if table is not None else None
+    rc = L.fp8a_matmul(_lib.dev_ptr(A), K, _lib.dev_ptr(B), N, 1, _lib.dev_ptr(C), N, Mr, N, K, 4, 3,
+                       _lib.dev_ptr(tA), _lib.dev_ptr(tB), 0 if tB.numel() == 1 else 1, _lib.dev_ptr(tR),
+                       _lib.host_ptr(tab) if tab is not None else None, flags, _lib.dev_ptr(ws), ws.numel(),
+                       _lib.stream_ptr(DEV))
+    _lib.check(rc, "fp8a_matmul")
+    torch.cuda.synchronize()
+    flag = int(ws[:4].view(torch.int32).item())
+    return C.cpu().numpy(), flag
+
+
+def _terms_equal(got, ref):
+    same = (got.view(np.uint32) == ref.view(np.uint32)) | ((got == 0) & (ref == 0))
+    if not same.all():
+        i = tuple(np.argwhere(~same)[0])
+        raise AssertionError(f"{np.count_nonzero(~same)} terms differ; first at {i}: got {got[i]!r} ref {ref[i]!r}")
+
+
+@pytest.mark.parametrize("table", ["nocomp", "comp", "none"])
+@pytest.mark.parametrize("biases", [(12, 12, 8), (10, 13, 7), (9, 9, 2), (12, 14, 0), (8, 8, -14), (20, 18, 22)])
+def test_every_code_pair_bitexact(biases, table):
+    bA, bB, bR = biases
+    A = _all_codes(bA).reshape(-1, 1)
+    B = _all_codes(bB).reshape(1, -1)
+    tab = gio.load("g2_matmul.npz")["E4M3_table_comp" if table == "comp" else "E4M3_table_nocomp"]
+    fl = orc.flags_of(approx=table != "none", s2n=True, qbma=True)
+    C, flag = _matmul_raw(A, B, bA, bB, bR, tab, fl)
+    ref = orc.terms(A, B, 4, 3, bA, bB, bR, tab, fl)[:, 0, :]
+    _terms_equal(C, ref)
+    # every term fits the e4m3 range of these biases: the fast form ran, nothing fell back
+    assert flag == 0, "fallback flag raised: the fast form did not produce these terms"
+
+
+def test_terms_beyond_e4m3_range_fall_back():
+    bA, bB, bR = 12, 12, 14  # products up to ~2^7 * 3.5 exceed the result grid's top binade
+    A = _all_codes(bA).reshape(-1, 1)
+    B = _all_codes(bB).reshape(1, -1)
+    tab = gio.load("g2_matmul.npz")["E4M3_table_nocomp"]
+    fl = orc.flags_of(approx=True, s2n=True, qbma=True)
+    C, flag = _matmul_raw(A, B, bA, bB, bR, tab, fl)
+    assert flag != 0
+    _terms_equal(C, orc.terms(A, B, 4, 3, bA, bB, bR, tab, fl)[:, 0, :])
+
+
+@pytest.mark.parametrize("shape", [(256, 576, 64), (130, 300, 129), (1, 4608, 7), (512, 1152, 256)])
+def test_sums_within_bar(shape):
+    Mr, K, N = shape
+    rng = np.random.default_rng(Mr + K + N)
+    bA, bR = 9, 3  # no product reaches the result grid's top binade (bR <= bA + min bB - 16)
+    bB = rng.integers(11, 15, size=N).astype(np.int32)
+    e = rng.integers(3, 16, size=(Mr, K))
+    m = rng.integers(0, 8, size=(Mr, K))
+    A = np.ldexp(1.0 + m / 8.0, e - bA) * rng.choice([-1.0, 1.0], size=(Mr, K))
+    A[rng.random((Mr, K)) < 0.4] = 0.0
+    e = rng.integers(5, 16, size=(K, N))
+    m = rng.integers(0, 8, size=(K, N))
+    B = np.ldexp(1.0 + m / 8.0, e - bB[None, :]) * rng.choice([-1.0, 1.0], size=(K, N))
+    A, B = A.astype(np.float32), B.astype(np.float32)
+    tab = gio.load("g2_matmul.npz")["E4M3_table_nocomp"]
+    fl = orc.flags_of(approx=True, s2n=True, qbma=True)
+    C, flag = _matmul_raw(A, B, bA, bB, bR, tab, fl)
+    Cref, S = orc.matmul(A, B, 4, 3, bA, bB, bR, tab, fl, with_abs=True)
+    assert flag == 0
+    assert np.all(np.abs(C.astype(np.float64) - Cref) <= gio.sum_tolerance(S.astype(np.float64)))
