@@ -189,6 +189,63 @@ __device__ __forceinline__ bool stage_decode(float x, int M, uint32_t emn, bool 
     return grid && win;
 }
 
+// Writes one thread's TM x TN outputs (rows m0 + ty*TM + i, columns n0 + tx*TN + j) to the
+// output mapping, or to its split-K partial slice (same layout); applies the fused BN/activation
+// epilogue when unsplit.
+__device__ __forceinline__ void store_tile(const GemmArgs &p, int64_t split, int64_t m0, int64_t n0, int ty, int tx,
+                                           float (&acc)[TM][TN]) {
+    const bool partial = p.splits > 1;
+    float *const C = partial ? p.part + split * p.M * p.N : p.C;
+    const int64_t ldc = partial ? p.N : p.ldc, ctot = partial ? p.N : p.ctot, coff = partial ? 0 : p.coff;
+    const int64_t nb = n0 + tx * TN;
+    if (!partial && p.ep != nullptr) {  // fused BN + activation (split-K applies it in the reduction)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int64_t ch = p.coff + min<int64_t>(nb + j, p.N - 1);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) acc[i][j] = epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, ch, acc[i][j]);
+        }
+    }
+    if (!p.nchw) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int64_t m = m0 + ty * TM + i;
+            if (m >= p.M) continue;
+            if (nb + TN <= p.N && ((ldc & 3) == 0) && ((((uintptr_t)C) & 15) == 0)) {
+                *reinterpret_cast<float4 *>(&C[m * ldc + nb]) = make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    if (nb + j < p.N) C[m * ldc + nb + j] = acc[i][j];
+            }
+        }
+    } else {
+        // NCHW: the thread's 4 rows are 4 consecutive pixels; when they lie in one image and
+        // start 16-B aligned, each output channel gets one float4 store.
+        const int64_t mb = m0 + ty * TM;
+        const int64_t img = mb / p.hw, pix = mb - img * p.hw;
+        const bool vec = (pix + TM <= p.hw) && (mb + TM <= p.M) && ((p.hw & 3) == 0) &&
+                         ((((uintptr_t)C) & 15) == 0);
+        if (vec) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                if (nb + j < p.N)
+                    *reinterpret_cast<float4 *>(&C[(img * ctot + coff + nb + j) * p.hw + pix]) =
+                        make_float4(acc[0][j], acc[1][j], acc[2][j], acc[3][j]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int64_t m = mb + i;
+                if (m >= p.M) continue;
+                const int64_t im = m / p.hw, px = m - im * p.hw;
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    if (nb + j < p.N) C[(im * ctot + coff + nb + j) * p.hw + px] = acc[i][j];
+            }
+        }
+    }
+}
+
 template <bool S2N, bool QBMA, bool GCLIP, int TMODE>
 __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
     constexpr bool QAMAA = TMODE == TM_QAMAA;
@@ -551,58 +608,11 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
             for (int j = 0; j < TN; ++j) nan |= __builtin_isnan(acc[i][j]);
         if (__syncthreads_or(nan ? 1 : 0) && tid == 0) atomicOr(p.flag, 1u);
     }
-    // ---- epilogue (a split-K partial goes to its slice of the workspace, same layout)
-    const bool partial = p.splits > 1;
-    float *const C = partial ? p.part + split * p.M * p.N : p.C;
-    const int64_t ldc = partial ? p.N : p.ldc, ctot = partial ? p.N : p.ctot, coff = partial ? 0 : p.coff;
-    const int64_t nb = n0 + tx * TN;
-    if (!partial && p.ep != nullptr) {  // fused BN + activation (split-K applies it in the reduction)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int64_t ch = p.coff + min<int64_t>(nb + j, p.N - 1);
-#pragma unroll
-            for (int i = 0; i < TM; ++i) acc[i][j] = epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, ch, acc[i][j]);
-        }
-    }
-    if (!p.nchw) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            const int64_t m = m0 + ty * TM + i;
-            if (m >= p.M) continue;
-            if (nb + TN <= p.N && ((ldc & 3) == 0) && ((((uintptr_t)C) & 15) == 0)) {
-                *reinterpret_cast<float4 *>(&C[m * ldc + nb]) = make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
-            } else {
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-                    if (nb + j < p.N) C[m * ldc + nb + j] = acc[i][j];
-            }
-        }
-    } else {
-        // NCHW: the thread's 4 rows are 4 consecutive pixels; when they lie in one image and
-        // start 16-B aligned, each output channel gets one float4 store.
-        const int64_t mb = m0 + ty * TM;
-        const int64_t img = mb / p.hw, pix = mb - img * p.hw;
-        const bool vec = (pix + TM <= p.hw) && (mb + TM <= p.M) && ((p.hw & 3) == 0) &&
-                         ((((uintptr_t)C) & 15) == 0);
-        if (vec) {
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-                if (nb + j < p.N)
-                    *reinterpret_cast<float4 *>(&C[(img * ctot + coff + nb + j) * p.hw + pix]) =
-                        make_float4(acc[0][j], acc[1][j], acc[2][j], acc[3][j]);
-        } else {
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                const int64_t m = mb + i;
-                if (m >= p.M) continue;
-                const int64_t im = m / p.hw, px = m - im * p.hw;
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-                    if (nb + j < p.N) C[(im * ctot + coff + nb + j) * p.hw + px] = acc[i][j];
-            }
-        }
-    }
+    // ---- epilogue
+    store_tile(p, split, m0, n0, ty, tx, acc);
 }
+
+#include "gemm_f8mx.h"
 
 // Sums the split-K partials in split order (deterministic) and writes the output mapping.
 // Partial layout: row-major [M][N] (rowmajor output) or [img][N][hw] (NCHW output).
@@ -924,7 +934,12 @@ static void launch_fast(int mode, const GemmArgs &a, hipStream_t s) {
         return;
     }
     if (mode == TM_F8) {  // s2n + qbma, no golden clip (selected in run_gemm)
-        gemm_fast_kernel<true, true, false, TM_F8><<<grid, NT, 0, s>>>(a);
+        // matrix-core accumulation (gemm_f8mx.h); FP8A_NO_MX=1 keeps the VALU-accumulating form
+        static const bool no_mx = getenv("FP8A_NO_MX") != nullptr;
+        if (no_mx)
+            gemm_fast_kernel<true, true, false, TM_F8><<<grid, NT, 0, s>>>(a);
+        else
+            gemm_f8mx_kernel<<<grid, NT, 0, s>>>(a);
         return;
     }
     const bool s2n = a.flags & F_S2N, q = a.flags & F_QBMA, gc = a.flags & F_GCLIP;

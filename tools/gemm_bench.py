@@ -51,22 +51,27 @@ def main():
     E, M, wc = MODES[args.mode]
     tab = get_error_table_NN(E, M, wc, 3)
     fl = fa.make_flags(with_approx=True, with_s2nn2s_opt=True, quant_btw_mult_accu=True)
+    bA, bB = 2 ** (E - 1) + 3, 2 ** (E - 1) + 8
+    # E4M3: a result bias that keeps every term inside the scaled-e4m3 range (bA + bB - bR >= 16, as
+    # the calibrated ResNet-18 layers have: ~14 + 19 - 15), else the launch falls back to the exact
+    # kernel and this measures the fallback
+    bR = bA + bB - 17 if E == 4 else 2 ** (E - 1) + 6
     rng = np.random.default_rng(0)
     tot_t, tot_mac = 0.0, 0
     for (name, cin, cout, k, s, p, h) in RESNET18:
         if args.layers and name not in args.layers.split(","):
             continue
-        x = grid(rng, E, M, (args.batch, cin, h, h), 2 ** (E - 1) + 3, 0.5).to(dev)
-        w = grid(rng, E, M, (cout, cin, k, k), 2 ** (E - 1) + 8, 0.0).to(dev)
-        bW = torch.full((cout,), 2 ** (E - 1) + 8, dtype=torch.int32, device=dev)
+        x = grid(rng, E, M, (args.batch, cin, h, h), bA, 0.5).to(dev)
+        w = grid(rng, E, M, (cout, cin, k, k), bB, 0.0).to(dev)
+        bW = torch.full((cout,), bB, dtype=torch.int32, device=dev)
         args_ = dict(flags=fl, stride=(s, s), padding=(p, p))
-        y = fa.approx_conv2d(x, w, E, M, 2 ** (E - 1) + 3, bW, 2 ** (E - 1) + 6, tab, **args_)
+        y = fa.approx_conv2d(x, w, E, M, bA, bW, bR, tab, **args_)
         torch.cuda.synchronize()
         ts = []
         for _ in range(args.reps):
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
-            fa.approx_conv2d(x, w, E, M, 2 ** (E - 1) + 3, bW, 2 ** (E - 1) + 6, tab, **args_)
+            fa.approx_conv2d(x, w, E, M, bA, bW, bR, tab, **args_)
             b.record()
             b.synchronize()
             ts.append(a.elapsed_time(b) / 1e3)
