@@ -133,6 +133,14 @@ struct GemmArgs {
     const float2 *ep;
     int ep_act;
     float ep_lo, ep_hi;
+    // pre-decoded operands of the matrix-core E4M3 kernel (gemm_f8mx.h): A words (conv: the
+    // group's [Bn][aw_c][H][W] slice; matrix: [M][awld]), B as c_b [Kpad][npad] + pair offsets
+    // [Kpad][npad / 2]
+    const uint32_t *aw;
+    int64_t awld, aw_c;
+    const float *bcw;
+    const uint32_t *bpw;
+    int64_t npad;
     TablePack tab;
 };
 
@@ -934,12 +942,12 @@ static void launch_fast(int mode, const GemmArgs &a, hipStream_t s) {
         return;
     }
     if (mode == TM_F8) {  // s2n + qbma, no golden clip (selected in run_gemm)
-        // matrix-core accumulation (gemm_f8mx.h); FP8A_NO_MX=1 keeps the VALU-accumulating form
-        static const bool no_mx = getenv("FP8A_NO_MX") != nullptr;
-        if (no_mx)
-            gemm_fast_kernel<true, true, false, TM_F8><<<grid, NT, 0, s>>>(a);
-        else
+        // matrix-core accumulation on pre-decoded operands (gemm_f8mx.h) when run_gemm staged
+        // them, else the VALU-accumulating form
+        if (a.aw)
             gemm_f8mx_kernel<<<grid, NT, 0, s>>>(a);
+        else
+            gemm_fast_kernel<true, true, false, TM_F8><<<grid, NT, 0, s>>>(a);
         return;
     }
     const bool s2n = a.flags & F_S2N, q = a.flags & F_QBMA, gc = a.flags & F_GCLIP;
@@ -1014,9 +1022,24 @@ static int choose_splits(int64_t M, int64_t N, int64_t K) {
     return bs;
 }
 
-static size_t gemm_workspace_bytes(int64_t M, int64_t N, int64_t K) {
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Bytes of the pre-decoded operands of the matrix-core E4M3 kernel (gemm_f8mx.h): A words
+// (a_words of them) + c_b [Kpad][Npad] + pair offsets [Kpad][Npad / 2].
+static size_t xm_operand_bytes(int64_t N, int64_t K, int64_t a_words) {
+    const int64_t kpad = (K + BK - 1) / BK * BK, npad = (N + BN - 1) / BN * BN;
+    return align256((size_t)a_words * 4) + align256((size_t)(kpad * npad) * 4) + align256((size_t)(kpad * npad / 2) * 4);
+}
+
+static size_t splitk_bytes(int64_t M, int64_t N, int64_t K) {
     const int S = choose_splits(M, N, K);
-    return FLAG_BYTES + (S > 1 ? (size_t)S * (size_t)M * (size_t)N * sizeof(float) : 0);
+    return S > 1 ? align256((size_t)S * (size_t)M * (size_t)N * sizeof(float)) : 0;
+}
+
+// flag word + split-K partials + the pre-decoded operands (a_words: the A operand's element
+// count as the matrix-core E4M3 path stores it; 0 = no room for that path)
+static size_t gemm_workspace_bytes(int64_t M, int64_t N, int64_t K, int64_t a_words) {
+    return FLAG_BYTES + splitk_bytes(M, N, K) + (a_words > 0 ? xm_operand_bytes(N, K, a_words) : 0);
 }
 
 // Fast tiled kernel + gated exact kernel (int-bias path), or the exact kernel alone (tb path).
@@ -1059,11 +1082,36 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     a.flag = (uint32_t *)ws;
     // split-K when the caller's workspace holds the partials (else one split)
     a.splits = choose_splits(a.M, a.N, a.K);
-    if (a.splits > 1 && ws_bytes < FLAG_BYTES + (size_t)a.splits * a.M * a.N * sizeof(float)) a.splits = 1;
+    if (a.splits > 1 && ws_bytes < FLAG_BYTES + splitk_bytes(a.M, a.N, a.K)) a.splits = 1;
     const int64_t kt = (a.K + BK - 1) / BK;
     a.kchunk = ((kt + a.splits - 1) / a.splits) * BK;
     a.part = a.splits > 1 ? (float *)((char *)ws + FLAG_BYTES) : nullptr;
     if (hipMemsetAsync(ws, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a flag reset");
+    // the matrix-core E4M3 kernel needs its pre-decoded operands in the workspace (else the
+    // VALU-accumulating form runs); FP8A_NO_MX=1 forces the latter
+    static const bool no_mx = getenv("FP8A_NO_MX") != nullptr;
+    a.aw = nullptr;
+    if (mode == TM_F8 && !no_mx) {
+        const int64_t kpad = kt * BK, npad = (a.N + BN - 1) / BN * BN;
+        const int64_t a_words = a.conv ? (a.M / (a.Ho * a.Wo)) * a.aw_c * a.H * a.W : a.M * kpad;
+        const size_t off = FLAG_BYTES + (a.splits > 1 ? splitk_bytes(a.M, a.N, a.K) : 0);
+        const bool fits32 = !a.conv || a_words < (1ll << 31);
+        if (fits32 && ws_bytes >= off + xm_operand_bytes(a.N, a.K, a_words)) {
+            char *base = (char *)ws + off;
+            a.aw = (const uint32_t *)base;
+            a.awld = kpad;
+            a.bcw = (const float *)(base + align256((size_t)a_words * 4));
+            a.bpw = (const uint32_t *)(base + align256((size_t)a_words * 4) + align256((size_t)(kpad * npad) * 4));
+            a.npad = npad;
+            const int64_t rows = a.conv ? a.M / (a.Ho * a.Wo) : a.M, cols = a_words / std::max<int64_t>(rows, 1);
+            const dim3 ga((unsigned)std::min<int64_t>((cols + 255) / 256, 64), (unsigned)std::min<int64_t>(rows, 1024));
+            xm_decode_a<<<ga, 256, 0, s>>>(a);
+            const unsigned gb = (unsigned)std::min<int64_t>((kpad * npad / 2 + 255) / 256, 4096);
+            xm_decode_b<<<gb, 256, 0, s>>>(a, kpad);
+            rc = hip_check("fp8a operand pre-decode launch");
+            if (rc) return rc;
+        }
+    }
     launch_fast(mode, a, s);
     rc = hip_check("fp8a fast gemm launch");
     if (rc) return rc;
@@ -1144,7 +1192,7 @@ size_t fp8a_matmul_workspace_size(void) { return FLAG_BYTES; }
 
 size_t fp8a_matmul_workspace_size_mnk(int64_t M, int64_t N, int64_t K) {
     if (M <= 0 || N <= 0 || K <= 0) return FLAG_BYTES;
-    return gemm_workspace_bytes(M, N, K);
+    return gemm_workspace_bytes(M, N, K, M * ((K + BK - 1) / BK * BK));
 }
 
 int fp8a_matmul(const float *A, int64_t lda, const float *B, int64_t sbk, int64_t sbn, float *C, int64_t ldc,
@@ -1193,7 +1241,7 @@ size_t fp8a_conv2d_workspace_size(int64_t Bn, int64_t Cin, int64_t H, int64_t W,
     // implicit GEMM (no im2col image): the off-grid flag word + split-K partials of one group
     const int64_t Mrows = Bn * Ho * Wo, cog = Cout / groups, Kg = (Cin / groups) * kh * kw;
     if (Mrows <= 0 || Kg <= 0) return FLAG_BYTES;
-    return gemm_workspace_bytes(Mrows, cog, Kg);
+    return gemm_workspace_bytes(Mrows, cog, Kg, Bn * (Cin / groups) * H * W);
 }
 
 int fp8a_conv2d(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
@@ -1266,7 +1314,7 @@ int fp8a_conv2d_bn_act(const float *x, const float *w, float *y, int64_t Bn, int
         a.coff = g * cog;
         a.conv = 1;
         a.X = x;
-        a.Cin = Cin; a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo; a.cbase = g * cig;
+        a.Cin = Cin; a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo; a.cbase = g * cig; a.aw_c = cig;
         a.kh = kh; a.kw = kw; a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw; a.dh = dh; a.dw = dw;
         fastdiv_params((uint32_t)(kh * kw), a.kk_mul, a.kk_shift);
         fastdiv_params((uint32_t)kw, a.kw_mul, a.kw_shift);

@@ -17,6 +17,13 @@
 // issues: half an LDS address add, one multiply and half a scaled conversion (the f32 decode and
 // the add are gone), and the table read is one ds_read_b64 per two products.
 //
+// Operands are decoded ONCE per launch by two pre-pass kernels (xm_decode_a / xm_decode_b):
+// an A element becomes one 32-bit word (cvt scale bits | table row offset), a B element its c_b
+// plus, per column pair, the pair block offset.  The GEMM's staging is then a gather and two
+// bit-field ops, instead of a full decode for every element of every tile (a 3x3 conv gathers
+// each input element 9 times).  The pre-passes also carry the fallback checks (off-grid operand,
+// exactness window, e4m3 scale range, bias window) into the launch's flag word.
+//
 // LDS table layout [pair][copy][row][2 floats]: pair = (m_b of column 2q) + 8 (m_b of column
 // 2q+1), row = 8 s_a + m_a (zero A operands take scale 2^127, so the conversion returns 0 for
 // them and they need no row of their own), copy = parity of the consuming thread's column
@@ -31,6 +38,7 @@ typedef short xm_s2 __attribute__((ext_vector_type(2)));
 
 constexpr int XM_LUT_FLOATS = 64 * 2 * 16 * 2;  // 16 KiB
 constexpr int XM_BQ = BN / 2 + 2;                // pair slots per staged K row (padded)
+constexpr uint32_t XM_ZERO_WORD = 254u << 23;    // A = 0: cvt scale 2^127 (the code is 0), row 0
 struct XmSmem {
     float lut[XM_LUT_FLOATS];
     float as[BK][AP];        // cvt scale of A(m, k): 2^(7-bR)/|c_a|, 2^127 for zeros (as bits)
@@ -41,10 +49,83 @@ struct XmSmem {
 constexpr int XM_CP = BN + 1;  // epilogue transpose tile [BM][BN + 1] floats, aliased on XmSmem
 static_assert(sizeof(float) * BM * XM_CP <= sizeof(XmSmem), "epilogue tile must fit the staging LDS");
 
+// Exactness / range window shared by the pre-passes (as bias_ok in gemm_fast_kernel)
+__device__ __forceinline__ bool xm_bias_ok(int b) { return b >= -100 && b <= 120; }
+
+// A element -> word: bits 23-30 the cvt scale exponent se (scale 2^(se-127) = 2^(7-bR-e_a)),
+// bits 3-6 the table row (8 s_a + m_a); zeros XM_ZERO_WORD.  ok = on the (3, bA) grid, inside the
+// exactness window and the scale range.
+__device__ __forceinline__ uint32_t xm_word_a(float x, uint32_t emnA, int bR, bool &ok) {
+    float c;
+    uint32_t mc;
+    ok = stage_decode(x, 3, emnA, true, c, mc);
+    const uint32_t cb = __float_as_uint(c);
+    const int se = 261 - bR - (int)((cb >> 23) & 0xFFu);
+    if ((cb & 0x7FFFFFFFu) == 0u) return XM_ZERO_WORD;
+    ok = ok && se >= 1 && se <= 254;
+    return ((uint32_t)min(max(se, 1), 254) << 23) | (((cb >> 31) * 8u + mc) << 3);
+}
+
+// A pre-pass, one (image | row) per blockIdx.y step.  conv: the group's channel slice of x
+// [Bn][Cin][H][W] (channels cbase..cbase+aw_c) -> words [Bn][aw_c][H][W]; matrix: A [M][lda] ->
+// words [M][awld] (columns >= K zero words).
+__global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
+    const int bA = *p.bA, bR = *p.bR;
+    const uint32_t emnA = (uint32_t)(128 - bA) << 23;
+    bool bad = !(xm_bias_ok(bA) && xm_bias_ok(bR));
+    uint32_t *const out = const_cast<uint32_t *>(p.aw);
+    const int64_t hw = p.H * p.W;
+    const int64_t rows = p.conv ? p.M / (p.Ho * p.Wo) : p.M, cols = p.conv ? p.aw_c * hw : p.awld;
+    for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) {
+        const float *in = p.conv ? p.X + (r * p.Cin + p.cbase) * hw : p.A + r * p.lda;
+        const int64_t lim = p.conv ? cols : p.K;
+        uint32_t *o = out + r * cols;
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cols; i += (int64_t)gridDim.x * blockDim.x) {
+            bool ok = true;
+            o[i] = (i < lim) ? xm_word_a(in[i], emnA, bR, ok) : XM_ZERO_WORD;
+            bad |= !ok;
+        }
+    }
+    if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, 1u);
+}
+
+// B pre-pass: per (k, pair Q) of the padded [Kpad][npad] extent, c_b of both columns and the
+// pair block offset ((m_b0 + 8 m_b1) * 256 + copy * 128 bytes, copy = parity of the consuming
+// thread's 4-column group = (Q >> 1) & 1); out-of-range elements are zeros.
+__global__ __launch_bounds__(256) void xm_decode_b(const GemmArgs p, int64_t kpad) {
+    const int bA = *p.bA, bR = *p.bR;
+    bool bad = !(xm_bias_ok(bA) && xm_bias_ok(bR));
+    const int64_t hq = p.npad / 2, n = kpad * hq;
+    float *const bc = const_cast<float *>(p.bcw);
+    uint32_t *const bp = const_cast<uint32_t *>(p.bpw);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int64_t k = i / hq, q = i - k * hq;
+        float c[2];
+        uint32_t mc[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int64_t col = 2 * q + h;
+            c[h] = 0.0f;
+            mc[h] = 0;
+            if (k < p.K && col < p.N) {
+                const int bb = p.bB[col * p.bBs];
+                const bool ok = stage_decode(p.B[k * p.sbk + col * p.sbn], 3, (uint32_t)(128 - bb) << 23, true,
+                                             c[h], mc[h]);
+                bad |= !ok || !xm_bias_ok(bb);
+            }
+        }
+        *reinterpret_cast<float2 *>(&bc[k * p.npad + 2 * q]) = make_float2(c[0], c[1]);
+        bp[i] = (mc[0] + 8u * mc[1]) * 256u + (uint32_t)((q >> 1) & 1) * 128u;
+    }
+    if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, 1u);
+}
+
 __global__ __launch_bounds__(NT) void gemm_f8mx_kernel(const GemmArgs p) {
     __shared__ __attribute__((aligned(16))) XmSmem sm;
 
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wvu = __builtin_amdgcn_readfirstlane(wv);
     const int ty = lane & 15, tx = 4 * wv + (lane >> 4);  // half-wave = 16 row groups x 2 column groups
     const int64_t num_mt = (p.M + BM - 1) / BM;
     const int64_t tiles = num_mt * ((p.N + BN - 1) / BN);
@@ -52,9 +133,7 @@ __global__ __launch_bounds__(NT) void gemm_f8mx_kernel(const GemmArgs p) {
     const int64_t m0 = (bid % num_mt) * BM;
     const int64_t n0 = (bid / num_mt) * BN;
     const int64_t kbeg = split * p.kchunk, kend = min(p.K, kbeg + p.kchunk);
-    constexpr int M = 3;
-    const int bA = *p.bA, bR = *p.bR;
-    const uint32_t emnA = (uint32_t)(128 - bA) << 23;
+    const int bR = *p.bR;
 
     // table: V'(s_a, m_a, m_b) for both columns of a pair, both copies
     for (int e = tid; e < XM_LUT_FLOATS / 2; e += NT) {
@@ -74,71 +153,73 @@ __global__ __launch_bounds__(NT) void gemm_f8mx_kernel(const GemmArgs p) {
         *reinterpret_cast<float2 *>(&sm.lut[2 * e]) = make_float2(v2[0], v2[1]);
     }
 
-    // B staging slots: (pair q, k row kk), two per thread; lanes along k for k-contiguous weights
-    const bool b_ncontig = (p.sbn == 1);
+    // B staging slots: pair q = e & 31 (lanes along n: coalesced), k row kk = e >> 5
+    const int64_t hq = p.npad / 2;
+    const float *bcg[2];
+    const uint32_t *bpg[2];
     int bq[2], bkk[2];
-    uint32_t emnB[2][2];
-    bool bias_ok = bR >= -100 && bR <= 120 && bA >= -100 && bA <= 120;
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
         const int e = tid + NT * r;
-        bq[r] = b_ncontig ? (e & 31) : (e >> 4);
-        bkk[r] = b_ncontig ? (e >> 5) : (e & 15);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int64_t n = n0 + 2 * bq[r] + h;
-            const int bb = (n < p.N) ? p.bB[n * p.bBs] : 0;
-            bias_ok = bias_ok && bb >= -100 && bb <= 120;
-            emnB[r][h] = (uint32_t)(128 - bb) << 23;
-        }
+        bq[r] = e & 31;
+        bkk[r] = e >> 5;
+        bcg[r] = p.bcw + (kbeg + bkk[r]) * p.npad + n0 + 2 * bq[r];
+        bpg[r] = p.bpw + (kbeg + bkk[r]) * hq + n0 / 2 + bq[r];
     }
 
-    // implicit-conv row of this thread (fixed across k tiles)
+    // A staging.  conv: lanes along m (consecutive pixels), k row = wave + 4 r (wave-uniform: the
+    // k -> (c, ky, kx) split runs on the scalar unit); matrix: lanes along k.
     bool crow_ok = false;
-    int64_t cxoff = 0, chi0 = 0, cwi0 = 0;
+    int64_t cbase_w = 0;
+    int chi0 = 0, cwi0 = 0;
     if (p.conv) {
-        const int64_t m = m0 + (tid & 63);
+        const int64_t m = m0 + lane;
         crow_ok = m < p.M;
         const int64_t hw = p.Ho * p.Wo;
         const int64_t img = crow_ok ? m / hw : 0, pix = crow_ok ? m - img * hw : 0;
         const int64_t ho = pix / p.Wo, wo = pix - ho * p.Wo;
-        cxoff = (img * p.Cin + p.cbase) * p.H * p.W;
-        chi0 = ho * p.sh - p.ph;
-        cwi0 = wo * p.sw - p.pw;
+        chi0 = (int)(ho * p.sh - p.ph);
+        cwi0 = (int)(wo * p.sw - p.pw);
+        cbase_w = img * p.aw_c * p.H * p.W + (int64_t)chi0 * p.W + cwi0;
     }
     int arow[(BM * BK) / NT], akk[(BM * BK) / NT];
 #pragma unroll
     for (int r = 0; r < (BM * BK) / NT; ++r) {
         const int e = tid + NT * r;
-        arow[r] = p.conv ? (tid & 63) : (e >> 4);
-        akk[r] = p.conv ? ((tid >> 6) + 4 * r) : (e & 15);
+        arow[r] = p.conv ? lane : (e >> 4);
+        akk[r] = p.conv ? (wvu + 4 * r) : (e & 15);
     }
-    float xa[(BM * BK) / NT], xb[2][2];
+    uint32_t wa[(BM * BK) / NT];
+    float2 wbc[2];
+    uint32_t wbp[2];
     auto load_tile = [&](int64_t k0) {
 #pragma unroll
         for (int r = 0; r < (BM * BK) / NT; ++r) {
-            float x = 0.0f;
-            const int64_t k = k0 + akk[r];
+            uint32_t w = XM_ZERO_WORD;
             if (!p.conv) {
                 const int64_t m = m0 + arow[r];
-                if (m < p.M && k < kend) x = p.A[m * p.lda + k];
-            } else if (crow_ok && k < kend) {  // implicit im2col (approx_calculation.py:724-747)
-                const uint32_t c = fastdiv((uint32_t)k, p.kk_mul, p.kk_shift);
-                const uint32_t t = (uint32_t)k - c * (uint32_t)(p.kh * p.kw);
-                const uint32_t ky = fastdiv(t, p.kw_mul, p.kw_shift);
-                const uint32_t kx = t - ky * (uint32_t)p.kw;
-                const int64_t hi = chi0 + (int64_t)ky * p.dh, wi = cwi0 + (int64_t)kx * p.dw;
-                if (hi >= 0 && hi < p.H && wi >= 0 && wi < p.W) x = p.X[cxoff + ((int64_t)c * p.H + hi) * p.W + wi];
+                if (m < p.M) w = p.aw[m * p.awld + k0 + akk[r]];
+            } else {
+                const int64_t k = k0 + akk[r];  // wave-uniform
+                if (k < kend) {
+                    const uint32_t c = fastdiv((uint32_t)k, p.kk_mul, p.kk_shift);
+                    const uint32_t t = (uint32_t)k - c * (uint32_t)(p.kh * p.kw);
+                    const uint32_t ky = fastdiv(t, p.kw_mul, p.kw_shift);
+                    const uint32_t kx = t - ky * (uint32_t)p.kw;
+                    const int dy = (int)ky * p.dh, dx = (int)kx * p.dw;
+                    const int64_t koff = (int64_t)c * p.H * p.W + (int64_t)dy * p.W + dx;
+                    if (crow_ok && (uint32_t)(chi0 + dy) < (uint32_t)p.H && (uint32_t)(cwi0 + dx) < (uint32_t)p.W)
+                        w = p.aw[cbase_w + koff];
+                }
             }
-            xa[r] = x;
+            wa[r] = w;
         }
 #pragma unroll
-        for (int r = 0; r < 2; ++r)
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int64_t n = n0 + 2 * bq[r] + h, k = k0 + bkk[r];
-                xb[r][h] = (n < p.N && k < kend) ? p.B[k * p.sbk + n * p.sbn] : 0.0f;
-            }
+        for (int r = 0; r < 2; ++r) {
+            const int64_t o = k0 - kbeg;
+            wbc[r] = *reinterpret_cast<const float2 *>(bcg[r] + o * p.npad);
+            wbp[r] = bpg[r][o * hq];
+        }
     };
     load_tile(kbeg);
 
@@ -161,38 +242,25 @@ __global__ __launch_bounds__(NT) void gemm_f8mx_kernel(const GemmArgs p) {
     xm_v16f dacc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) dacc[r] = 0.0f;
+    xm_v8i av = {0, 0, 0, 0, 0, 0, 0, 0};
     const char *lut = reinterpret_cast<const char *>(sm.lut);
 
     for (int64_t k0 = kbeg; k0 < kend; k0 += BK) {
-        bool bad = !bias_ok;
 #pragma unroll
         for (int r = 0; r < (BM * BK) / NT; ++r) {
-            float c;
-            uint32_t mc;
-            bad |= !stage_decode(xa[r], M, emnA, true, c, mc);
-            const uint32_t cb = __float_as_uint(c);
-            const int se = 261 - bR - (int)((cb >> 23) & 0xFFu);
-            const bool zero = (cb & 0x7FFFFFFFu) == 0u;
-            bad |= !zero && (se < 1 || se > 254);
-            sm.as[akk[r]][arow[r]] = __uint_as_float((uint32_t)(zero ? 254 : min(max(se, 1), 254)) << 23);
-            sm.ar[akk[r]][arow[r]] = zero ? 0u : ((cb >> 31) * 8u + mc) * 8u;
+            sm.as[akk[r]][arow[r]] = __uint_as_float(wa[r] & 0xFF800000u);
+            sm.ar[akk[r]][arow[r]] = wa[r] & 0x78u;
         }
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
-            float c0, c1;
-            uint32_t m0c, m1c;
-            bad |= !stage_decode(xb[r][0], M, emnB[r][0], true, c0, m0c);
-            bad |= !stage_decode(xb[r][1], M, emnB[r][1], true, c1, m1c);
-            *reinterpret_cast<float2 *>(&sm.bc[bkk[r]][2 * bq[r]]) = make_float2(c0, c1);
-            sm.bp[bkk[r]][bq[r]] = (m0c + 8u * m1c) * 256u + (uint32_t)((bq[r] >> 1) & 1) * 128u;
+            *reinterpret_cast<float2 *>(&sm.bc[bkk[r]][2 * bq[r]]) = wbc[r];
+            sm.bp[bkk[r]][bq[r]] = wbp[r];
         }
-        const int anybad = __syncthreads_or(bad ? 1 : 0);
-        if (anybad && tid == 0) atomicOr(p.flag, 1u);
-        if (k0 + BK < kend) load_tile(k0 + BK);
+        __syncthreads();
+        if (k0 + BK < kend) load_tile(k0 + BK);  // next tile's loads fly during this tile's math
 
 #pragma unroll
         for (int kp = 0; kp < BK; kp += 2) {
-            uint32_t code[8];
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
                 const int kk = kp + s;
@@ -206,14 +274,14 @@ __global__ __launch_bounds__(NT) void gemm_f8mx_kernel(const GemmArgs p) {
                 for (int i = 0; i < TM; ++i) {
                     const float2 v01 = *reinterpret_cast<const float2 *>(lut + (ar[i] + bp2.x));
                     const float2 v23 = *reinterpret_cast<const float2 *>(lut + (ar[i] + bp2.y));
-                    xm_s2 cv = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32((xm_s2){0, 0}, v01.x * bc4.x, v01.y * bc4.y,
-                                                                        as[i], false);
+                    // the low-word conversion's other half is overwritten by the high-word one, so
+                    // the register's previous contents serve as its input (no zeroing move)
+                    xm_s2 cv = __builtin_bit_cast(xm_s2, av[4 * s + i]);
+                    cv = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(cv, v01.x * bc4.x, v01.y * bc4.y, as[i], false);
                     cv = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(cv, v23.x * bc4.z, v23.y * bc4.w, as[i], true);
-                    code[4 * s + i] = __builtin_bit_cast(uint32_t, cv);
+                    av[4 * s + i] = __builtin_bit_cast(int, cv);
                 }
             }
-            const xm_v8i av = {(int)code[0], (int)code[1], (int)code[2], (int)code[3],
-                               (int)code[4], (int)code[5], (int)code[6], (int)code[7]};
             dacc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av, sel, dacc, 0, 0, 0, 127, 0, 127);
         }
         __syncthreads();
@@ -249,4 +317,3 @@ __global__ __launch_bounds__(NT) void gemm_f8mx_kernel(const GemmArgs p) {
         for (int j = 0; j < TN; ++j) acc[i][j] = ct[(ety * TM + i) * XM_CP + etx * TN + j];
     store_tile(p, split, m0, n0, ety, etx, acc);
 }
-
