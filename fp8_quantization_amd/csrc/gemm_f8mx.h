@@ -270,14 +270,23 @@ __global__ __launch_bounds__(NT) void gemm_f8mx_kernel(const GemmArgs p) {
                 const uint2 bp2 = *reinterpret_cast<const uint2 *>(&sm.bp[kk][tx * 2]);
                 const float as[TM] = {as4.x, as4.y, as4.z, as4.w};
                 const uint32_t ar[TM] = {ar4.x, ar4.y, ar4.z, ar4.w};
+                // all table reads of the K-step first, then the math (+5 % over reading each row's
+                // pair just before its use: the reads' latency overlaps)
+                float2 v01s[TM], v23s[TM];
 #pragma unroll
                 for (int i = 0; i < TM; ++i) {
-                    const float2 v01 = *reinterpret_cast<const float2 *>(lut + (ar[i] + bp2.x));
-                    const float2 v23 = *reinterpret_cast<const float2 *>(lut + (ar[i] + bp2.y));
-                    // the low-word conversion's other half is overwritten by the high-word one, so
-                    // the register's previous contents serve as its input (no zeroing move)
-                    xm_s2 cv = __builtin_bit_cast(xm_s2, av[4 * s + i]);
-                    cv = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(cv, v01.x * bc4.x, v01.y * bc4.y, as[i], false);
+                    v01s[i] = *reinterpret_cast<const float2 *>(lut + (ar[i] + bp2.x));
+                    v23s[i] = *reinterpret_cast<const float2 *>(lut + (ar[i] + bp2.y));
+                }
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const float2 v01 = v01s[i], v23 = v23s[i];
+                    // the low-word conversion's high half is overwritten by the high-word one, so it
+                    // needs no input register (the builtin ties one, and the compiler zeroes it)
+                    xm_s2 cv;
+                    asm("v_cvt_scalef32_pk_fp8_f32 %0, %1, %2, %3"
+                        : "=v"(cv)
+                        : "v"(v01.x * bc4.x), "v"(v01.y * bc4.y), "v"(as[i]));
                     cv = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(cv, v23.x * bc4.z, v23.y * bc4.w, as[i], true);
                     av[4 * s + i] = __builtin_bit_cast(int, cv);
                 }

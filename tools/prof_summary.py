@@ -1,12 +1,15 @@
 #!/usr/bin/env python
-"""Summarise rocprofv3 CSV output for the approx GEMM kernel (profiles/ evidence).
+"""Summarise rocprofv3 CSV output for the approx GEMM op (profiles/ evidence).
 
     python tools/prof_summary.py --trace DIR/..._kernel_trace.csv --stats DIR/..._kernel_stats.csv \
         [--pmc DIR/..._counter_collection.csv ...] --timed-launches N --out profiles/rocprof_r01
 
 Writes <out>.json (machine-readable) and <out>.txt (human-readable).  The timed-region
-average takes the LAST N dispatches of gemm_fast_kernel (bench.py's timed steps come last).
-PMC counters are averaged per dispatch of gemm_fast_kernel; HBM traffic per launch =
+average takes the LAST N dispatches of --kernel (the dominant kernel, gemm_f8mx_kernel; bench.py's
+timed steps come last); op_avg_ns adds every kernel of one approx op (--op-kernels: operand
+pre-decodes, the GEMM, the split-K reduce, the gated exact kernel) over the same window -- the
+quantity bench.py times with HIP events.  PMC counters are averaged per dispatch of --kernel;
+HBM traffic per launch =
 (FETCH_SIZE + WRITE_SIZE) * 1024 bytes -- rocprofv3's KB units; on gfx950 FETCH_SIZE is
 calibrated only for 16-B-per-lane streaming reads (MI355X_MICROARCH.md §HBM), these loads
 are 4 B per lane, so the read side is reported raw and marked uncalibrated.
@@ -16,7 +19,7 @@ import collections
 import csv
 import json
 
-KERNEL = "gemm_fast_kernel"
+OP_KERNELS = "xm_decode_a,xm_decode_b,gemm_f8mx_kernel,gemm_fast_kernel,splitk_reduce_kernel,gemm_exact_kernel"
 
 
 def read_csv(path):
@@ -33,14 +36,26 @@ def main():
     ap.add_argument("--out", required=True)
     ap.add_argument("--note", default="")
     ap.add_argument("--pmc-json", default="", help="also write the per-launch PMC summary bench.py reads")
+    ap.add_argument("--kernel", default="gemm_f8mx_kernel")
+    ap.add_argument("--op-kernels", default=OP_KERNELS)
     a = ap.parse_args()
+    KERNEL = a.kernel
 
-    rows = [r for r in read_csv(a.trace) if KERNEL in r["Kernel_Name"]]
+    trace = read_csv(a.trace)
+    rows = [r for r in trace if KERNEL in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     timed = rows[-a.timed_launches:]
     durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in timed]
+    # the op window: from the first timed dispatch's preceding pre-decode (if any) to the end
+    t0 = int(timed[0]["Start_Timestamp"]) if timed else 0
+    pre = [int(r["Start_Timestamp"]) for r in trace if "xm_decode_a" in r["Kernel_Name"] and int(r["Start_Timestamp"]) < t0]
+    w0 = max(pre) if pre else t0
+    opk = [k for k in a.op_kernels.split(",") if k]
+    op_rows = [r for r in trace if int(r["Start_Timestamp"]) >= w0 and any(k in r["Kernel_Name"] for k in opk)]
+    op_ns = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in op_rows)
     res = dict(kernel=KERNEL, all_dispatches=len(rows), timed_dispatches=len(timed),
                timed_avg_ns=sum(durs) / max(1, len(durs)), timed_total_ns=sum(durs),
+               op_avg_ns=op_ns / max(1, len(timed)), op_kernels=opk,
                vgpr=timed[-1]["VGPR_Count"] if timed else None, lds=timed[-1]["LDS_Block_Size"] if timed else None,
                note=a.note)
     if a.stats:
@@ -55,18 +70,18 @@ def main():
         res["pmc_avg_per_dispatch"] = {k: sum(v) / len(v) for k, v in counters.items()}
         pm = res["pmc_avg_per_dispatch"]
         if "FETCH_SIZE" in pm and "WRITE_SIZE" in pm:
-            res["gemm_fast_bytes_per_launch"] = (pm["FETCH_SIZE"] + pm["WRITE_SIZE"]) * 1024.0
+            res["bytes_per_launch"] = (pm["FETCH_SIZE"] + pm["WRITE_SIZE"]) * 1024.0
             res["traffic_note"] = "FETCH_SIZE uncalibrated for 4-byte-per-lane loads (raw KB x 1024)"
         if "SQ_INSTS_VALU" in pm and "SQ_WAVES" in pm:
             res["valu_instr_per_wave"] = pm["SQ_INSTS_VALU"] / pm["SQ_WAVES"]
     if counters and a.pmc_json:
         pm = res["pmc_avg_per_dispatch"]
         pj = dict(source="rocprofv3 --kernel-trace --pmc (separate passes per counter group, "
-                         "--kernel-include-regex gemm_fast) on bench.py --steps 2 --warmup 1",
-                  note="per gemm_fast_kernel dispatch, averaged; FETCH_SIZE/WRITE_SIZE in KB (x1024 = bytes); "
+                         f"--kernel-include-regex {KERNEL}) on bench.py --steps 2 --warmup 1",
+                  note=f"per {KERNEL} dispatch, averaged; FETCH_SIZE/WRITE_SIZE in KB (x1024 = bytes); "
                        "FETCH_SIZE uncalibrated for 4-byte-per-lane loads (MI355X_MICROARCH.md HBM section)")
         if "FETCH_SIZE" in pm and "WRITE_SIZE" in pm:
-            pj.update(gemm_fast_bytes_per_launch=(pm["FETCH_SIZE"] + pm["WRITE_SIZE"]) * 1024.0,
+            pj.update(kernel=KERNEL, bytes_per_launch=(pm["FETCH_SIZE"] + pm["WRITE_SIZE"]) * 1024.0,
                       fetch_kb=pm["FETCH_SIZE"], write_kb=pm["WRITE_SIZE"])
         if "SQ_INSTS_VALU" in pm and "GRBM_GUI_ACTIVE" in pm:
             # GRBM_GUI_ACTIVE is summed over the 8 XCDs; 1024 SIMDs; a wave64 VALU op issues in 2 cycles
