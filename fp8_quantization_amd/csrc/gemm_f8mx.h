@@ -35,6 +35,7 @@
 typedef int xm_v8i __attribute__((ext_vector_type(8)));
 typedef float xm_v16f __attribute__((ext_vector_type(16)));
 typedef short xm_s2 __attribute__((ext_vector_type(2)));
+typedef float xm_f2 __attribute__((ext_vector_type(2)));
 
 constexpr int XM_LUT_FLOATS = 64 * 2 * 16 * 2;  // 16 KiB
 constexpr int XM_BQ = BN / 2 + 2;                // pair slots per staged K row (padded)
@@ -121,7 +122,10 @@ __global__ __launch_bounds__(256) void xm_decode_b(const GemmArgs p, int64_t kpa
     if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, 1u);
 }
 
-__global__ __launch_bounds__(NT) void gemm_f8mx_kernel(const GemmArgs p) {
+#ifndef XM_WAVES
+#define XM_WAVES 1
+#endif
+__global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs p) {
     __shared__ __attribute__((aligned(16))) XmSmem sm;
 
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -283,11 +287,16 @@ __global__ __launch_bounds__(NT) void gemm_f8mx_kernel(const GemmArgs p) {
                     const float2 v01 = v01s[i], v23 = v23s[i];
                     // the low-word conversion's high half is overwritten by the high-word one, so it
                     // needs no input register (the builtin ties one, and the compiler zeroes it)
+#ifdef XM_PK
+                    const xm_f2 x01 = xm_f2{v01.x, v01.y} * xm_f2{bc4.x, bc4.y};
+                    const xm_f2 x23 = xm_f2{v23.x, v23.y} * xm_f2{bc4.z, bc4.w};
+#else
+                    const xm_f2 x01 = {v01.x * bc4.x, v01.y * bc4.y};
+                    const xm_f2 x23 = {v23.x * bc4.z, v23.y * bc4.w};
+#endif
                     xm_s2 cv;
-                    asm("v_cvt_scalef32_pk_fp8_f32 %0, %1, %2, %3"
-                        : "=v"(cv)
-                        : "v"(v01.x * bc4.x), "v"(v01.y * bc4.y), "v"(as[i]));
-                    cv = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(cv, v23.x * bc4.z, v23.y * bc4.w, as[i], true);
+                    asm("v_cvt_scalef32_pk_fp8_f32 %0, %1, %2, %3" : "=v"(cv) : "v"(x01.x), "v"(x01.y), "v"(as[i]));
+                    cv = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(cv, x23.x, x23.y, as[i], true);
                     av[4 * s + i] = __builtin_bit_cast(int, cv);
                 }
             }
