@@ -35,15 +35,14 @@
 typedef int xm_v8i __attribute__((ext_vector_type(8)));
 typedef float xm_v16f __attribute__((ext_vector_type(16)));
 typedef short xm_s2 __attribute__((ext_vector_type(2)));
-typedef float xm_f2 __attribute__((ext_vector_type(2)));
+typedef float xm_f2 __attribute__((ext_vector_type(2)));  // (a plain pair: v_pk_mul_f32 lost in A/B)
 
 constexpr int XM_LUT_FLOATS = 64 * 2 * 16 * 2;  // 16 KiB
 constexpr int XM_BQ = BN / 2 + 2;                // pair slots per staged K row (padded)
 constexpr uint32_t XM_ZERO_WORD = 254u << 23;    // A = 0: cvt scale 2^127 (the code is 0), row 0
 struct XmSmem {
     float lut[XM_LUT_FLOATS];
-    float as[BK][AP];        // cvt scale of A(m, k): 2^(7-bR)/|c_a|, 2^127 for zeros (as bits)
-    uint32_t ar[BK][AP];     // byte offset of A(m, k)'s table row
+    uint32_t aw[BK][AP];     // A(m, k)'s word: cvt scale exponent << 23 | table row << 3
     float bc[BK][BP];        // c_b = sign(b) 2^floor(log2|b|), 0 for b = 0
     uint32_t bp[BK][XM_BQ];  // byte offset of the (column 2q, 2q+1) pair block incl. the copy
 };
@@ -122,6 +121,9 @@ __global__ __launch_bounds__(256) void xm_decode_b(const GemmArgs p, int64_t kpa
     if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, 1u);
 }
 
+#ifndef XM_PIPE
+#define XM_PIPE 0
+#endif
 #ifndef XM_WAVES
 #define XM_WAVES 1
 #endif
@@ -252,8 +254,7 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
     for (int64_t k0 = kbeg; k0 < kend; k0 += BK) {
 #pragma unroll
         for (int r = 0; r < (BM * BK) / NT; ++r) {
-            sm.as[akk[r]][arow[r]] = __uint_as_float(wa[r] & 0xFF800000u);
-            sm.ar[akk[r]][arow[r]] = wa[r] & 0x78u;
+            sm.aw[akk[r]][arow[r]] = wa[r];
         }
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
@@ -263,44 +264,58 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
         __syncthreads();
         if (k0 + BK < kend) load_tile(k0 + BK);  // next tile's loads fly during this tile's math
 
+        // per K-step: one word per A element (the conversion reads only the scale's exponent
+        // field; the table row offset is bits 3-6), c_b and the pair offsets of the thread's
+        // columns, then all 8 table reads of the step, then the math.  XM_PIPE issues the next
+        // step's reads before this step's math.
+        uint4 aw4 = *reinterpret_cast<const uint4 *>(&sm.aw[0][ty * TM]);
+        float4 bc4 = *reinterpret_cast<const float4 *>(&sm.bc[0][tx * TN]);
+        uint2 bp2 = *reinterpret_cast<const uint2 *>(&sm.bp[0][tx * 2]);
+        float2 v01s[TM], v23s[TM];
+        auto lut_reads = [&](const uint4 &w4, const uint2 &p2, float2 (&a01)[TM], float2 (&a23)[TM]) {
+            const uint32_t ar[TM] = {w4.x & 0x78u, w4.y & 0x78u, w4.z & 0x78u, w4.w & 0x78u};
 #pragma unroll
-        for (int kp = 0; kp < BK; kp += 2) {
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const int kk = kp + s;
-                const float4 as4 = *reinterpret_cast<const float4 *>(&sm.as[kk][ty * TM]);
-                const uint4 ar4 = *reinterpret_cast<const uint4 *>(&sm.ar[kk][ty * TM]);
-                const float4 bc4 = *reinterpret_cast<const float4 *>(&sm.bc[kk][tx * TN]);
-                const uint2 bp2 = *reinterpret_cast<const uint2 *>(&sm.bp[kk][tx * 2]);
-                const float as[TM] = {as4.x, as4.y, as4.z, as4.w};
-                const uint32_t ar[TM] = {ar4.x, ar4.y, ar4.z, ar4.w};
-                // all table reads of the K-step first, then the math (+5 % over reading each row's
-                // pair just before its use: the reads' latency overlaps)
-                float2 v01s[TM], v23s[TM];
-#pragma unroll
-                for (int i = 0; i < TM; ++i) {
-                    v01s[i] = *reinterpret_cast<const float2 *>(lut + (ar[i] + bp2.x));
-                    v23s[i] = *reinterpret_cast<const float2 *>(lut + (ar[i] + bp2.y));
-                }
-#pragma unroll
-                for (int i = 0; i < TM; ++i) {
-                    const float2 v01 = v01s[i], v23 = v23s[i];
-                    // the low-word conversion's high half is overwritten by the high-word one, so it
-                    // needs no input register (the builtin ties one, and the compiler zeroes it)
-#ifdef XM_PK
-                    const xm_f2 x01 = xm_f2{v01.x, v01.y} * xm_f2{bc4.x, bc4.y};
-                    const xm_f2 x23 = xm_f2{v23.x, v23.y} * xm_f2{bc4.z, bc4.w};
-#else
-                    const xm_f2 x01 = {v01.x * bc4.x, v01.y * bc4.y};
-                    const xm_f2 x23 = {v23.x * bc4.z, v23.y * bc4.w};
-#endif
-                    xm_s2 cv;
-                    asm("v_cvt_scalef32_pk_fp8_f32 %0, %1, %2, %3" : "=v"(cv) : "v"(x01.x), "v"(x01.y), "v"(as[i]));
-                    cv = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(cv, x23.x, x23.y, as[i], true);
-                    av[4 * s + i] = __builtin_bit_cast(int, cv);
-                }
+            for (int i = 0; i < TM; ++i) {
+                a01[i] = *reinterpret_cast<const float2 *>(lut + (ar[i] + p2.x));
+                a23[i] = *reinterpret_cast<const float2 *>(lut + (ar[i] + p2.y));
             }
-            dacc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av, sel, dacc, 0, 0, 0, 127, 0, 127);
+        };
+        lut_reads(aw4, bp2, v01s, v23s);
+#pragma unroll
+        for (int kk = 0; kk < BK; ++kk) {
+            const float as[TM] = {__uint_as_float(aw4.x), __uint_as_float(aw4.y), __uint_as_float(aw4.z),
+                                  __uint_as_float(aw4.w)};
+            const float4 bcc = bc4;
+            float2 c01[TM], c23[TM];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                c01[i] = v01s[i];
+                c23[i] = v23s[i];
+            }
+            if (XM_PIPE && kk + 1 < BK) {
+                aw4 = *reinterpret_cast<const uint4 *>(&sm.aw[kk + 1][ty * TM]);
+                bc4 = *reinterpret_cast<const float4 *>(&sm.bc[kk + 1][tx * TN]);
+                bp2 = *reinterpret_cast<const uint2 *>(&sm.bp[kk + 1][tx * 2]);
+                lut_reads(aw4, bp2, v01s, v23s);
+            }
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const xm_f2 x01 = {c01[i].x * bcc.x, c01[i].y * bcc.y};
+                const xm_f2 x23 = {c23[i].x * bcc.z, c23[i].y * bcc.w};
+                // the low-word conversion's high half is overwritten by the high-word one, so it
+                // needs no input register (the builtin ties one, and the compiler zeroes it)
+                xm_s2 cv;
+                asm("v_cvt_scalef32_pk_fp8_f32 %0, %1, %2, %3" : "=v"(cv) : "v"(x01.x), "v"(x01.y), "v"(as[i]));
+                cv = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(cv, x23.x, x23.y, as[i], true);
+                av[4 * (kk & 1) + i] = __builtin_bit_cast(int, cv);
+            }
+            if (!XM_PIPE && kk + 1 < BK) {
+                aw4 = *reinterpret_cast<const uint4 *>(&sm.aw[kk + 1][ty * TM]);
+                bc4 = *reinterpret_cast<const float4 *>(&sm.bc[kk + 1][tx * TN]);
+                bp2 = *reinterpret_cast<const uint2 *>(&sm.bp[kk + 1][tx * 2]);
+                lut_reads(aw4, bp2, v01s, v23s);
+            }
+            if (kk & 1) dacc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av, sel, dacc, 0, 0, 0, 127, 0, 127);
         }
         __syncthreads();
     }
