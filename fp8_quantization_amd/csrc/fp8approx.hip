@@ -134,12 +134,10 @@ struct GemmArgs {
     int ep_act;
     float ep_lo, ep_hi;
     // pre-decoded operands of the matrix-core E4M3 kernel (gemm_f8mx.h): A words (conv: the
-    // group's [Bn][aw_c][H][W] slice; matrix: [M][awld]), B as c_b [Kpad][npad] + pair offsets
-    // [Kpad][npad / 2]
+    // group's [Bn][aw_c][H][W] slice; matrix: [M][awld]), B column pairs [Kpad][npad / 2]
     const uint32_t *aw;
     int64_t awld, aw_c;
-    const float *bcw;
-    const uint32_t *bpw;
+    const uint2 *bqw;
     int64_t npad;
     TablePack tab;
 };
@@ -1025,10 +1023,10 @@ static int choose_splits(int64_t M, int64_t N, int64_t K) {
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // Bytes of the pre-decoded operands of the matrix-core E4M3 kernel (gemm_f8mx.h): A words
-// (a_words of them) + c_b [Kpad][Npad] + pair offsets [Kpad][Npad / 2].
+// (a_words of them) + B column pairs [Kpad][Npad / 2] of 8 bytes.
 static size_t xm_operand_bytes(int64_t N, int64_t K, int64_t a_words) {
     const int64_t kpad = (K + BK - 1) / BK * BK, npad = (N + BN - 1) / BN * BN;
-    return align256((size_t)a_words * 4) + align256((size_t)(kpad * npad) * 4) + align256((size_t)(kpad * npad / 2) * 4);
+    return align256((size_t)a_words * 4) + align256((size_t)(kpad * npad / 2) * 8);
 }
 
 static size_t splitk_bytes(int64_t M, int64_t N, int64_t K) {
@@ -1100,8 +1098,7 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
             char *base = (char *)ws + off;
             a.aw = (const uint32_t *)base;
             a.awld = kpad;
-            a.bcw = (const float *)(base + align256((size_t)a_words * 4));
-            a.bpw = (const uint32_t *)(base + align256((size_t)a_words * 4) + align256((size_t)(kpad * npad) * 4));
+            a.bqw = (const uint2 *)(base + align256((size_t)a_words * 4));
             a.npad = npad;
             const int64_t rows = a.conv ? a.M / (a.Ho * a.Wo) : a.M, cols = a_words / std::max<int64_t>(rows, 1);
             const dim3 ga((unsigned)std::min<int64_t>((cols + 255) / 256, 64), (unsigned)std::min<int64_t>(rows, 1024));

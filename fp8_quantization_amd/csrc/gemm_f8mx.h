@@ -1,50 +1,59 @@
-// gemm_f8mx.h -- the E4M3 fast path with matrix-core accumulation (included by fp8approx.hip).
+// gemm_f8mx.h -- the E4M3 fast path with matrix-core accumulation (included by fp8approx.hip,
+// inside namespace fp8a, after GemmArgs / stage_decode / store_tile).  DESIGN.md §3a.
 //
 // Same arithmetic as gemm_fast_kernel<.., TM_F8>: for on-grid E4M3 operands with
 // s2n and per-product quantization (v9:51-113), each term is
 //     Q_R(V'(s_a, m_a, m_b) * c_b * |c_a|)  =  2^(7-bR) * e4m3(V' * c_b / scale_a),
-// scale_a = 2^(7-bR) / |c_a|, where V' = min(sig_a sig_b - T[m_a][m_b] 2^-M, top of its binade)
-// is an LDS table value and e4m3() is gfx950's scaled fp8 conversion (RNE; the bR grid is the
-// OCP e4m3 grid scaled by 2^(7-bR), subnormal band included).
+// scale_a = 2^(7-bR) / |c_a|, where V' = min(sig_a sig_b - T[m_a][m_b] 2^-M, pre-clamp bound of
+// its binade) is an LDS table value and e4m3() is gfx950's scaled fp8 conversion (RNE; the bR
+// grid is the OCP e4m3 grid scaled by 2^(7-bR), subnormal band included).
 //
-// What is new: the fp8 codes the conversion produces are NOT decoded and added on the VALU.
-// They are summed by the matrix core: one v_mfma_scale_f32_32x32x64_f8f6f4 per two K-steps
-// multiplies the wave's 2048 codes by a constant 0/1 selection matrix S, so that
-//     D[m][n] += sum over the two K-steps of the code of output (n mod 16) of lane m + 32 (n / 16).
-// Products with 1.0 and 0 are exact, the accumulator is fp32 (D is in units of 2^(7-bR)), so the
-// sum differs from an in-order fp32 sum only by accumulation order -- inside the reference's own
-// order freedom (v9:113, torch's sum) and the 1e-5 * sum|term| bar.  Per product the VALU now
-// issues: half an LDS address add, one multiply and half a scaled conversion (the f32 decode and
-// the add are gone), and the table read is one ds_read_b64 per two products.
+// Summation on the matrix core: the fp8 codes are not decoded and added on the VALU; one
+// v_mfma_scale_f32_32x32x64_f8f6f4 per two K-steps multiplies the wave's 2048 codes by a
+// constant 0/1 selection operand S, so that
+//     D[m][n] += the two K-steps' codes of output (n mod 16) of lane m + 32 (n / 16).
+// Products with 1.0 and 0 are exact and D is fp32 in units of 2^(7-bR): the sum differs from an
+// in-order fp32 sum only by accumulation order, inside the reference's own order freedom
+// (v9:113, torch's sum) and the 1e-5 * sum|term| bar.
+//
+// The table holds bf16 PAIRS V'(row, code0), V'(row, code1): V' has at most 8 significant bits
+// and the pre-clamp bound 1.8671875 x binade is bf16-exact (any bound in (1.8125, 1.875) x
+// binade rounds like the reference's saturating mantissa, F6, and its subnormal top tie).  B
+// codes are 0-7 = m_b and 8 = a zero B (entry +0).  c_b = s_b 2^e_b is applied as one packed
+// 16-bit integer add on the pair (v_pk_add_u16 of (s_b << 15) + (e_b << 7) per half: exponent
+// add and sign flip, no carry between the halves), and the pair goes straight into the bf16
+// form of the scaled conversion.  Per product pair the VALU issues one LDS address add, one
+// packed add and one conversion; the table read is one ds_read_b32.  (A/B on the ResNet-18
+// layer set: +15 % over the f32 form, which paid two multiplies per pair and a ds_read_b64.)
 //
 // Operands are decoded ONCE per launch by two pre-pass kernels (xm_decode_a / xm_decode_b):
-// an A element becomes one 32-bit word (cvt scale bits | table row offset), a B element its c_b
-// plus, per column pair, the pair block offset.  The GEMM's staging is then a gather and two
-// bit-field ops, instead of a full decode for every element of every tile (a 3x3 conv gathers
-// each input element 9 times).  The pre-passes also carry the fallback checks (off-grid operand,
-// exactness window, e4m3 scale range, bias window) into the launch's flag word.
+// an A element becomes one 32-bit word (cvt scale exponent << 23 | table row offset; the
+// conversion reads only the scale's exponent field), a B column pair one (addend pair, pair
+// block offset) uint2.  The GEMM's staging is then a gather and stores (a 3x3 conv gathers
+// each input element 9 times).  The pre-passes also carry the fallback checks (off-grid
+// operand, exactness window, e4m3 scale range, bias window) into the launch's flag word.
 //
-// LDS table layout [pair][copy][row][2 floats]: pair = (m_b of column 2q) + 8 (m_b of column
-// 2q+1), row = 8 s_a + m_a (zero A operands take scale 2^127, so the conversion returns 0 for
-// them and they need no row of their own), copy = parity of the consuming thread's column
-// group.  Threads are mapped so that each 32-lane half-wave holds 16 row groups x 2 column
-// groups: per read it touches at most 16 rows of one copy per column group, each on its own
-// bank pair -- conflict-free (MI355X_MICROARCH.md §LDS: ds_read_b64 banks (a/4) mod 64).
-// (included inside namespace fp8a, after GemmArgs / stage_decode / store_tile)
+// LDS table layout [pair (code0 + 9 code1)][copy][row (8 s_a + m_a)] u32: zero A operands take
+// scale 2^127 (the conversion returns 0), so they need no row; copy = parity of the consuming
+// thread's column group.  Threads are mapped so that each 32-lane half-wave holds 16 row groups
+// x 2 column groups: a read touches at most 16 rows of one copy per column group, each on its
+// own bank -- conflict-free (MI355X_MICROARCH.md §LDS: ds_read_b32 banks (a/4) mod 32).
 
 typedef int xm_v8i __attribute__((ext_vector_type(8)));
 typedef float xm_v16f __attribute__((ext_vector_type(16)));
 typedef short xm_s2 __attribute__((ext_vector_type(2)));
-typedef float xm_f2 __attribute__((ext_vector_type(2)));  // (a plain pair: v_pk_mul_f32 lost in A/B)
+typedef unsigned short xm_u2 __attribute__((ext_vector_type(2)));
+typedef __bf16 xm_b2 __attribute__((ext_vector_type(2)));
 
-constexpr int XM_LUT_FLOATS = 64 * 2 * 16 * 2;  // 16 KiB
-constexpr int XM_BQ = BN / 2 + 2;                // pair slots per staged K row (padded)
-constexpr uint32_t XM_ZERO_WORD = 254u << 23;    // A = 0: cvt scale 2^127 (the code is 0), row 0
+constexpr int XM_NPAIR = 81;
+constexpr int XM_LUT_WORDS = XM_NPAIR * 2 * 16;  // [pair][copy][row] u32, 10.1 KiB
+constexpr uint32_t XM_ROW_SHIFT = 2, XM_ROW_MASK = 0x3Cu;
+constexpr int XM_BQ = BN / 2 + 2;              // pair slots per staged K row (padded)
+constexpr uint32_t XM_ZERO_WORD = 254u << 23;  // A = 0: cvt scale 2^127 (the code is 0), row 0
 struct XmSmem {
-    float lut[XM_LUT_FLOATS];
-    uint32_t aw[BK][AP];     // A(m, k)'s word: cvt scale exponent << 23 | table row << 3
-    float bc[BK][BP];        // c_b = sign(b) 2^floor(log2|b|), 0 for b = 0
-    uint32_t bp[BK][XM_BQ];  // byte offset of the (column 2q, 2q+1) pair block incl. the copy
+    uint32_t lut[XM_LUT_WORDS];
+    uint32_t aw[BK][AP];     // A(m, k)'s word: cvt scale exponent << 23 | table row offset
+    uint2 bq[BK][XM_BQ];     // per column pair: (c_b addend pair, byte offset of the pair block)
 };
 constexpr int XM_CP = BN + 1;  // epilogue transpose tile [BM][BN + 1] floats, aliased on XmSmem
 static_assert(sizeof(float) * BM * XM_CP <= sizeof(XmSmem), "epilogue tile must fit the staging LDS");
@@ -63,7 +72,7 @@ __device__ __forceinline__ uint32_t xm_word_a(float x, uint32_t emnA, int bR, bo
     const int se = 261 - bR - (int)((cb >> 23) & 0xFFu);
     if ((cb & 0x7FFFFFFFu) == 0u) return XM_ZERO_WORD;
     ok = ok && se >= 1 && se <= 254;
-    return ((uint32_t)min(max(se, 1), 254) << 23) | (((cb >> 31) * 8u + mc) << 3);
+    return ((uint32_t)min(max(se, 1), 254) << 23) | (((cb >> 31) * 8u + mc) << XM_ROW_SHIFT);
 }
 
 // A pre-pass, one (image | row) per blockIdx.y step.  conv: the group's channel slice of x
@@ -89,15 +98,15 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
     if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, 1u);
 }
 
-// B pre-pass: per (k, pair Q) of the padded [Kpad][npad] extent, c_b of both columns and the
-// pair block offset ((m_b0 + 8 m_b1) * 256 + copy * 128 bytes, copy = parity of the consuming
-// thread's 4-column group = (Q >> 1) & 1); out-of-range elements are zeros.
+// B pre-pass: per (k, pair Q) of the padded [Kpad][npad / 2] pair grid, the addend pair
+// ((s_b << 15) + (e_b << 7) per bf16 half, 0 for a zero B) and the pair block's byte offset
+// ((code0 + 9 code1) * 128 + copy * 64, copy = parity of the consuming thread's 4-column group
+// = (Q >> 1) & 1); out-of-range elements are zeros.
 __global__ __launch_bounds__(256) void xm_decode_b(const GemmArgs p, int64_t kpad) {
     const int bA = *p.bA, bR = *p.bR;
     bool bad = !(xm_bias_ok(bA) && xm_bias_ok(bR));
     const int64_t hq = p.npad / 2, n = kpad * hq;
-    float *const bc = const_cast<float *>(p.bcw);
-    uint32_t *const bp = const_cast<uint32_t *>(p.bpw);
+    uint2 *const bq = const_cast<uint2 *>(p.bqw);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const int64_t k = i / hq, q = i - k * hq;
@@ -115,15 +124,23 @@ __global__ __launch_bounds__(256) void xm_decode_b(const GemmArgs p, int64_t kpa
                 bad |= !ok || !xm_bias_ok(bb);
             }
         }
-        *reinterpret_cast<float2 *>(&bc[k * p.npad + 2 * q]) = make_float2(c[0], c[1]);
-        bp[i] = (mc[0] + 8u * mc[1]) * 256u + (uint32_t)((q >> 1) & 1) * 128u;
+        uint32_t add = 0, code[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t cb = __float_as_uint(c[h]);
+            if ((cb & 0x7FFFFFFFu) == 0u) {
+                code[h] = 8u;
+            } else {
+                code[h] = mc[h];
+                const uint32_t eb = ((cb >> 23) & 0xFFu) - 127u;  // mod 2^9 in the field below
+                add |= ((((cb >> 31) << 15) + (eb << 7)) & 0xFFFFu) << (16 * h);
+            }
+        }
+        bq[i] = make_uint2(add, ((code[0] + 9u * code[1]) * 2u + (uint32_t)((q >> 1) & 1)) * 64u);
     }
     if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, 1u);
 }
 
-#ifndef XM_PIPE
-#define XM_PIPE 0
-#endif
 #ifndef XM_WAVES
 #define XM_WAVES 1
 #endif
@@ -142,35 +159,35 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
     const int bR = *p.bR;
 
     // table: V'(s_a, m_a, m_b) for both columns of a pair, both copies
-    for (int e = tid; e < XM_LUT_FLOATS / 2; e += NT) {
+    for (int e = tid; e < XM_LUT_WORDS; e += NT) {
         const int pr = e >> 5, row = e & 15;
         const int ma = row & 7;
-        float v2[2];
+        uint32_t w = 0;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            const int mb = h ? (pr >> 3) : (pr & 7);
-            const float t = (float)p.tab.raw[ma * 8 + mb];
-            float v = __fmaf_rn(1.0f + 0.125f * ma, 1.0f + 0.125f * mb, -t * 0.125f);  // exact
-            // Q_R's pre-clamp (QC::kb): the mantissa saturates instead of carrying, and on the
-            // subnormal grid the top tie rounds down
-            v = fminf(v, __uint_as_float(__float_as_uint(v) & 0x7F800000u) * (1.875f - p2(-22)));
-            v2[h] = (row >= 8) ? -v : v;
+            const int cd = h ? (pr / 9) : (pr % 9);
+            if (cd == 8) continue;  // zero B: +0
+            const float t = (float)p.tab.raw[ma * 8 + cd];
+            float v = __fmaf_rn(1.0f + 0.125f * ma, 1.0f + 0.125f * cd, -t * 0.125f);  // exact, <= 8 bits
+            // Q_R's pre-clamp in bf16: any bound in (1.8125, 1.875) x binade rounds like the
+            // reference's saturating mantissa (and the subnormal top tie rounding down)
+            v = fminf(v, __uint_as_float(__float_as_uint(v) & 0x7F800000u) * 1.8671875f);
+            if (row >= 8) v = -v;
+            w |= (__float_as_uint(v) >> 16) << (16 * h);
         }
-        *reinterpret_cast<float2 *>(&sm.lut[2 * e]) = make_float2(v2[0], v2[1]);
+        sm.lut[e] = w;
     }
 
     // B staging slots: pair q = e & 31 (lanes along n: coalesced), k row kk = e >> 5
     const int64_t hq = p.npad / 2;
-    const float *bcg[2];
-    const uint32_t *bpg[2];
     int bq[2], bkk[2];
+    int64_t boff[2];
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
         const int e = tid + NT * r;
         bq[r] = e & 31;
         bkk[r] = e >> 5;
-        bcg[r] = p.bcw + (kbeg + bkk[r]) * p.npad + n0 + 2 * bq[r];
-        bpg[r] = p.bpw + (kbeg + bkk[r]) * hq + n0 / 2 + bq[r];
+        boff[r] = (kbeg + bkk[r]) * hq + n0 / 2 + bq[r];  // pair index
     }
 
     // A staging.  conv: lanes along m (consecutive pixels), k row = wave + 4 r (wave-uniform: the
@@ -196,8 +213,7 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
         akk[r] = p.conv ? (wvu + 4 * r) : (e & 15);
     }
     uint32_t wa[(BM * BK) / NT];
-    float2 wbc[2];
-    uint32_t wbp[2];
+    uint2 wbq[2];
     auto load_tile = [&](int64_t k0) {
 #pragma unroll
         for (int r = 0; r < (BM * BK) / NT; ++r) {
@@ -222,9 +238,8 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
         }
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
-            const int64_t o = k0 - kbeg;
-            wbc[r] = *reinterpret_cast<const float2 *>(bcg[r] + o * p.npad);
-            wbp[r] = bpg[r][o * hq];
+            const int64_t o = boff[r] + (k0 - kbeg) * hq;
+            wbq[r] = p.bqw[o];
         }
     };
     load_tile(kbeg);
@@ -258,62 +273,35 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
         }
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
-            *reinterpret_cast<float2 *>(&sm.bc[bkk[r]][2 * bq[r]]) = wbc[r];
-            sm.bp[bkk[r]][bq[r]] = wbp[r];
+            sm.bq[bkk[r]][bq[r]] = wbq[r];
         }
         __syncthreads();
         if (k0 + BK < kend) load_tile(k0 + BK);  // next tile's loads fly during this tile's math
 
         // per K-step: one word per A element (the conversion reads only the scale's exponent
-        // field; the table row offset is bits 3-6), c_b and the pair offsets of the thread's
-        // columns, then all 8 table reads of the step, then the math.  XM_PIPE issues the next
-        // step's reads before this step's math.
-        uint4 aw4 = *reinterpret_cast<const uint4 *>(&sm.aw[0][ty * TM]);
-        float4 bc4 = *reinterpret_cast<const float4 *>(&sm.bc[0][tx * TN]);
-        uint2 bp2 = *reinterpret_cast<const uint2 *>(&sm.bp[0][tx * 2]);
-        float2 v01s[TM], v23s[TM];
-        auto lut_reads = [&](const uint4 &w4, const uint2 &p2, float2 (&a01)[TM], float2 (&a23)[TM]) {
-            const uint32_t ar[TM] = {w4.x & 0x78u, w4.y & 0x78u, w4.z & 0x78u, w4.w & 0x78u};
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                a01[i] = *reinterpret_cast<const float2 *>(lut + (ar[i] + p2.x));
-                a23[i] = *reinterpret_cast<const float2 *>(lut + (ar[i] + p2.y));
-            }
-        };
-        lut_reads(aw4, bp2, v01s, v23s);
+        // field; the table row offset is a bit field of it), the thread's two column pairs, all 8
+        // table reads of the step, then the math; the next step's reads follow the math
 #pragma unroll
         for (int kk = 0; kk < BK; ++kk) {
-            const float as[TM] = {__uint_as_float(aw4.x), __uint_as_float(aw4.y), __uint_as_float(aw4.z),
-                                  __uint_as_float(aw4.w)};
-            const float4 bcc = bc4;
-            float2 c01[TM], c23[TM];
+            const uint4 aw4 = *reinterpret_cast<const uint4 *>(&sm.aw[kk][ty * TM]);
+            const uint32_t awv[TM] = {aw4.x, aw4.y, aw4.z, aw4.w};
+            const uint4 bq4 = *reinterpret_cast<const uint4 *>(&sm.bq[kk][tx * 2]);  // add0, off0, add1, off1
+            uint32_t v0[TM], v1[TM];
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
-                c01[i] = v01s[i];
-                c23[i] = v23s[i];
-            }
-            if (XM_PIPE && kk + 1 < BK) {
-                aw4 = *reinterpret_cast<const uint4 *>(&sm.aw[kk + 1][ty * TM]);
-                bc4 = *reinterpret_cast<const float4 *>(&sm.bc[kk + 1][tx * TN]);
-                bp2 = *reinterpret_cast<const uint2 *>(&sm.bp[kk + 1][tx * 2]);
-                lut_reads(aw4, bp2, v01s, v23s);
+                v0[i] = *reinterpret_cast<const uint32_t *>(lut + ((awv[i] & XM_ROW_MASK) + bq4.y));
+                v1[i] = *reinterpret_cast<const uint32_t *>(lut + ((awv[i] & XM_ROW_MASK) + bq4.w));
             }
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
-                const xm_f2 x01 = {c01[i].x * bcc.x, c01[i].y * bcc.y};
-                const xm_f2 x23 = {c23[i].x * bcc.z, c23[i].y * bcc.w};
-                // the low-word conversion's high half is overwritten by the high-word one, so it
-                // needs no input register (the builtin ties one, and the compiler zeroes it)
-                xm_s2 cv;
-                asm("v_cvt_scalef32_pk_fp8_f32 %0, %1, %2, %3" : "=v"(cv) : "v"(x01.x), "v"(x01.y), "v"(as[i]));
-                cv = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(cv, x23.x, x23.y, as[i], true);
+                const uint32_t x0 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(xm_u2, v0[i]) +
+                                                                     __builtin_bit_cast(xm_u2, bq4.x));
+                const xm_u2 x1 = __builtin_bit_cast(xm_u2, v1[i]) + __builtin_bit_cast(xm_u2, bq4.z);
+                const float sc = __uint_as_float(awv[i]);
+                xm_s2 cv;  // low word: no input register needed (see the f32 form)
+                asm("v_cvt_scalef32_pk_fp8_bf16 %0, %1, %2" : "=v"(cv) : "v"(x0), "v"(sc));
+                cv = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(cv, __builtin_bit_cast(xm_b2, x1), sc, true);
                 av[4 * (kk & 1) + i] = __builtin_bit_cast(int, cv);
-            }
-            if (!XM_PIPE && kk + 1 < BK) {
-                aw4 = *reinterpret_cast<const uint4 *>(&sm.aw[kk + 1][ty * TM]);
-                bc4 = *reinterpret_cast<const float4 *>(&sm.bc[kk + 1][tx * TN]);
-                bp2 = *reinterpret_cast<const uint2 *>(&sm.bp[kk + 1][tx * 2]);
-                lut_reads(aw4, bp2, v01s, v23s);
             }
             if (kk & 1) dacc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av, sel, dacc, 0, 0, 0, 127, 0, 127);
         }
