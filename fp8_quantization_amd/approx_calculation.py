@@ -63,13 +63,13 @@ class ApproxOpMixin:
         res_bias = self._default_bias(res_bias, E, x.device)
         if y.shape[1] != 1:
             if self.approx_flag:
-                return approx_matmul(x, y, E, M, x_bias, y_bias.reshape(-1), res_bias, table, flags=flags)
+                return approx_matmul(x, y, E, M, x_bias, y_bias, res_bias, table, flags=flags)
             if self.quantize_after_mult_and_add:  # approx_calculation.py:787-795
                 return qamaa_matmul(x, y, *self._qamaa_params())
             return x @ y
         if self.approx_flag:  # single column: biases stay tensors -> tensor-bias semantics (F5)
             tb = 0 if flags & _lib.V5 else _lib.TB  # (v5 never had tensor-bias semantics)
-            return approx_matmul(x, y, E, M, x_bias, y_bias.reshape(-1), res_bias, table, flags=flags | tb)
+            return approx_matmul(x, y, E, M, x_bias, y_bias, res_bias, table, flags=flags | tb)
         return x @ y
 
     def multiply(self, x, y):
@@ -106,7 +106,7 @@ class ApproxConv2dMixin(ApproxOpMixin):
             if w_bias is None:  # the reference indexes weight_fp_bias[...] (approx_calculation.py:868)
                 raise TypeError("'NoneType' object is not subscriptable")
             out = approx_conv2d(x.detach(), weight.detach(), E, M, self._default_bias(a_bias, E, x.device),
-                                w_bias.reshape(-1), self._default_bias(r_bias, E, x.device), table, flags=flags,
+                                w_bias, self._default_bias(r_bias, E, x.device), table, flags=flags,
                                 stride=self.stride, padding=self.padding, dilation=self.dilation, groups=self.groups,
                                 epilogue=epilogue)
         elif self.quantize_after_mult_and_add and self.out_channels // self.groups != 1:

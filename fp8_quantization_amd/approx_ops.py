@@ -67,6 +67,9 @@ def _prof_end(start, macs):
 def _bias_dev(b, device, n=None):
     """Device int32 bias vector from an int or a (float/int) tensor; no host sync for tensors."""
     if isinstance(b, torch.Tensor):
+        i32 = getattr(b, "_fp8a_i32", None)  # set by fp8_fake_quantize: no conversion launch
+        if i32 is not None and i32.device == device:
+            return i32
         t = b.detach().reshape(-1)
         if t.device != device:
             t = t.to(device)
@@ -346,12 +349,15 @@ def fp8_fake_quantize(x, maxval, n_bits, mantissa_bits, sign_bits=1, per_row=Fal
     rows = mx.numel() if per_row else 1
     out = torch.empty_like(x)
     bias = torch.empty(rows, dtype=torch.float32, device=x.device)
+    ibias = torch.empty(rows, dtype=torch.int32, device=x.device)
     rc = L.fp8a_fp8_quantize(_lib.dev_ptr(x), rows, x.numel() // rows, _lib.dev_ptr(mx), int(per_row), int(n_bits),
-                             int(mantissa_bits), int(sign_bits), _lib.dev_ptr(out), _lib.dev_ptr(bias), None,
-                             _lib.stream_ptr(x.device))
+                             int(mantissa_bits), int(sign_bits), _lib.dev_ptr(out), _lib.dev_ptr(bias),
+                             _lib.dev_ptr(ibias), _lib.stream_ptr(x.device))
     _lib.check(rc, "fp8a_fp8_quantize")
     if per_row and rows > 1:
         bias = bias.view([-1] + [1] * (x.dim() - 1))
+    # the same bias as int32, written by the same kernel: the approx ops take it as is (_bias_dev)
+    bias._fp8a_i32 = ibias
     return out, bias
 
 

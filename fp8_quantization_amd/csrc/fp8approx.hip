@@ -1237,7 +1237,7 @@ size_t fp8a_conv2d_workspace_size(int64_t Bn, int64_t Cin, int64_t H, int64_t W,
     if (Ho <= 0 || Wo <= 0) return 0;
     // implicit GEMM (no im2col image): the off-grid flag word + split-K partials of one group
     const int64_t Mrows = Bn * Ho * Wo, cog = Cout / groups, Kg = (Cin / groups) * kh * kw;
-    if (Mrows <= 0 || Kg <= 0) return FLAG_BYTES;
+    if (Mrows <= 0 || Kg <= 0 || cog == 1) return FLAG_BYTES;  // cog == 1: tensor-bias kernels
     return gemm_workspace_bytes(Mrows, cog, Kg, Bn * (Cin / groups) * H * W);
 }
 

@@ -31,20 +31,29 @@ def test_version_string():
     assert _lib.version().startswith("fp8approx gfx950")
 
 
+def _a256(x):
+    return (x + 255) // 256 * 256
+
+
 def test_workspace_queries_are_host_only():
     L = _lib.load()
     assert L.fp8a_matmul_workspace_size() >= 4
-    # split-K sizing is host logic (no device: 256 CUs assumed): a fraction-of-a-wave shape
-    # gets room for partial sums, a many-wave shape does not
     flag = L.fp8a_matmul_workspace_size()
-    assert L.fp8a_matmul_workspace_size_mnk(12544, 512, 4608) > flag
-    assert L.fp8a_matmul_workspace_size_mnk(3211264, 64, 147) == flag
-    # depthwise (single output channel per group): no im2col image; the flag word only (the
-    # v9 tensor-bias kernel needs none, the v5 mode takes the GEMM path)
+    # split-K sizing is host logic (no device: 256 CUs assumed): a fraction-of-a-wave shape
+    # gets room for partial sums, a many-wave shape does not; every GEMM-shaped query also
+    # holds the matrix-core E4M3 path's pre-decoded operands (A words + B column pairs)
+    Mr, N, K = 3211264, 64, 147
+    kpad, npad = (K + 15) // 16 * 16, (N + 63) // 64 * 64
+    assert L.fp8a_matmul_workspace_size_mnk(Mr, N, K) == flag + _a256(Mr * kpad * 4) + _a256(kpad * npad // 2 * 8)
+    Mr, N, K = 12544, 512, 4608
+    assert L.fp8a_matmul_workspace_size_mnk(Mr, N, K) > flag + _a256(Mr * K * 4) + _a256(K * N // 2 * 8)  # split
+    # depthwise (single output channel per group): the tensor-bias kernels need the flag word only
+    # (the v5 mode takes the GEMM path and runs unsplit without a pre-decode in that workspace)
     assert L.fp8a_conv2d_workspace_size(2, 8, 6, 6, 8, 3, 3, 1, 1, 1, 1, 1, 1, 8) == flag
-    # implicit-GEMM conv: only the off-grid flag word, independent of the batch
-    n = L.fp8a_conv2d_workspace_size(2, 3, 8, 8, 4, 3, 3, 1, 1, 1, 1, 1, 1, 1)
-    assert n == L.fp8a_conv2d_workspace_size(256, 3, 224, 224, 4, 3, 3, 1, 1, 1, 1, 1, 1, 1) >= 4
+    # implicit-GEMM conv: no im2col image; the A words of one group's input slice
+    n2 = L.fp8a_conv2d_workspace_size(2, 3, 8, 8, 4, 3, 3, 1, 1, 1, 1, 1, 1, 1)
+    assert n2 >= flag + 2 * 3 * 8 * 8 * 4
+    assert L.fp8a_conv2d_workspace_size(256, 3, 224, 224, 4, 3, 3, 1, 1, 1, 1, 1, 1, 1) >= flag + 256 * 3 * 224 * 224 * 4
 
 
 def test_bad_format_maps_to_value_error():
