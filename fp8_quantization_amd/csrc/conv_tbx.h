@@ -1,0 +1,119 @@
+// conv_tbx.h -- E4M3 depthwise (single-output-channel groups) with the tensor-bias semantics,
+// table form (included by fp8approx.hip inside namespace fp8a, after conv_tb_fast_kernel).
+//
+// The reference takes single-column products down its tensor-bias path (approx_calculation.py:
+// 800-809): with int32-tensor biases >= 2, param_prepare's integer powers make
+// min_norm 0, so every nonzero value decodes at its own binade and Q_R rounds at the value's own
+// binade (no subnormal floor).  Rounding is then scale-invariant, so for on-grid E4M3 operands
+// with s2n, per-product quantization, no golden clip and a {0,1} (or zero) error table the term
+// is a TABLE value times the operands' binades:
+//     r = L(m_a, m_b) * c_a * c_b,   L = Q3c(sig_a sig_b - T[m_a][m_b] / 8)
+// (Q3c: round to 3 mantissa bits at V's own binade with Q_R's saturating clamp, F6), followed by
+// the two quirks the general kernel (conv_tb_fast_kernel) applies per term:
+//   * the binade [2^-bR, 2^(1-bR)) has expo field 0 and decodes as 2^(1-bR) m / 8, i.e.
+//     r -> 2 r - sign 2^(1-bR) there;
+//   * F7: the sign comes from Q_R(g), g = a b, which is 0 only for |g| in [2^-bR, 2^-bR 17/16];
+//     a negative such g gives |r|.  |g| = u |c_a c_b| with u = sig_a sig_b, so F7 fires only for
+//     c_a c_b = -2^-bR with u <= 17/16 or c_a c_b = -2^(-1-bR) with u in [2, 17/8]: the table
+//     carries that trigger value per (m_a, m_b) beside L.
+// Per term that is an LDS read, two multiplies and two compare-selects (~13 VALU ops against
+// ~30 for the general form).  A is pre-decoded once per launch into words (sign/exponent bits of
+// a | m_a << 6, so the table byte offset is one v_and_or with m_b << 3); each thread computes 4
+// consecutive outputs of one row and gathers the input words they share once.  Off-grid inputs,
+// the exactness window and the bias window raise the gate word and conv_tb_direct_kernel
+// recomputes the launch exactly (as behind conv_tb_fast_kernel).
+constexpr int TBX_TW = 4;  // outputs per thread along wo
+
+struct TbxArgs {
+    int64_t Cin, H, W, Cout, Ho, Wo;
+    int kh, ph, pw, dh, cpg;
+    uint32_t nwg, items;  // column groups per row, Bn * Cout * Ho * nwg
+};
+
+// x (NCHW floats) -> words: (bits(x) & 0xFF800000) | (m << 6); 0 for zeros; gate on off-grid
+// values / the exactness window (tensor-bias decode: every value at its own binade).
+__global__ __launch_bounds__(256) void tbx_decode_a(const float *x, int64_t n, uint32_t *out, uint32_t *gate) {
+    bool bad = false;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t u = __float_as_uint(x[i]), ua = u & 0x7FFFFFFFu;
+        bad |= (ua != 0u) && ((ua & 0xFFFFFu) != 0u || ua < 0x20800000u || ua > 0x58800000u);
+        out[i] = ua == 0u ? 0u : ((u & 0xFF800000u) | (((ua >> 20) & 7u) << 6));
+    }
+    if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(gate, 1u);
+}
+
+template <int SW>
+__global__ __launch_bounds__(256) void conv_tbx_kernel(const uint32_t *aw, const float *w, float *y, TbxArgs t,
+                                                       const int32_t *bA, const int32_t *bW, const int32_t *bR,
+                                                       TablePack tab, uint32_t *gate, const float2 *ep, int ep_act,
+                                                       float ep_lo, float ep_hi) {
+    constexpr int KW = 3, NCOL = (TBX_TW - 1) * SW + KW;
+    __shared__ float2 sL[64];
+    const int a_b = *bA, r_b = *bR;
+    bool bad = !(a_b >= 2 && a_b <= 120 && r_b >= 2 && r_b <= 120);
+    if (threadIdx.x < 64) {
+        const int ma = threadIdx.x >> 3, mb = threadIdx.x & 7;
+        const float u = (1.0f + 0.125f * ma) * (1.0f + 0.125f * mb);  // exact
+        const float v = __fmaf_rn(1.0f + 0.125f * ma, 1.0f + 0.125f * mb, -0.125f * (float)tab.raw[ma * 8 + mb]);
+        const float pe = __uint_as_float(__float_as_uint(v) & 0x7F800000u);
+        const float xs = fminf(v, pe * (1.875f - p2(-22))), cc = pe * 1048576.0f * 1.5f;
+        const float L = (xs + cc) - cc;  // Q3c(V'): RNE at V's binade after the saturating clamp
+        uint32_t f7 = 0xFFFFFFFFu;       // never equal to a product of binades
+        if (u <= 1.0625f) f7 = 0x80000000u | ((uint32_t)(127 - r_b) << 23);
+        else if (u >= 2.0f && u <= 2.125f) f7 = 0x80000000u | ((uint32_t)(126 - r_b) << 23);
+        sL[threadIdx.x] = make_float2(L, __uint_as_float(f7));
+    }
+    __syncthreads();
+    const uint32_t q0exp = (uint32_t)(127 - r_b) << 23;
+    const float twoq = __uint_as_float((uint32_t)(128 - r_b) << 23);
+    const char *lut = reinterpret_cast<const char *>(sL);
+    const int64_t HW = t.H * t.W;
+
+    for (uint32_t item = blockIdx.x * blockDim.x + threadIdx.x; item < t.items; item += gridDim.x * blockDim.x) {
+        const uint32_t wg = item % t.nwg, r1 = item / t.nwg;
+        const uint32_t ho = r1 % (uint32_t)t.Ho, r2 = r1 / (uint32_t)t.Ho;
+        const uint32_t co = r2 % (uint32_t)t.Cout, img = r2 / (uint32_t)t.Cout;
+        const int wb = bW[co];
+        bad |= !(wb >= 2 && wb <= 120);
+        const int wo0 = (int)wg * TBX_TW, wi0 = wo0 * SW - t.pw;
+        float acc[TBX_TW] = {0.0f, 0.0f, 0.0f, 0.0f};
+        for (int c = 0; c < t.cpg; ++c) {
+            const uint32_t *plane = aw + ((int64_t)img * t.Cin + (int64_t)co * t.cpg + c) * HW;
+            const float *wk = w + ((int64_t)co * t.cpg + c) * t.kh * KW;
+            for (int ky = 0; ky < t.kh; ++ky) {
+                const int hi = (int)ho * (int)(SW == 1 ? 1 : 2) - t.ph + ky * t.dh;
+                const bool rowok = (uint32_t)hi < (uint32_t)t.H;
+                const uint32_t *row = plane + (int64_t)hi * t.W;
+                uint32_t col[NCOL];
+#pragma unroll
+                for (int j = 0; j < NCOL; ++j) {
+                    const int wi = wi0 + j;
+                    col[j] = (rowok && (uint32_t)wi < (uint32_t)t.W) ? row[wi] : 0u;
+                }
+#pragma unroll
+                for (int kx = 0; kx < KW; ++kx) {
+                    const uint32_t bw = __float_as_uint(wk[ky * KW + kx]), bwa = bw & 0x7FFFFFFFu;
+                    bad |= (bwa != 0u) && ((bwa & 0xFFFFFu) != 0u || bwa < 0x20800000u || bwa > 0x58800000u);
+                    const float cB = __uint_as_float(bw & 0xFF800000u);
+                    const uint32_t mb8 = ((bwa >> 20) & 7u) << 3;
+#pragma unroll
+                    for (int q = 0; q < TBX_TW; ++q) {
+                        const uint32_t wa = col[q * SW + kx];
+                        const float2 e = *reinterpret_cast<const float2 *>(lut + ((wa & 0x1C0u) | mb8));
+                        const float cab = __uint_as_float(wa & 0xFF800000u) * cB;  // exact
+                        float r = e.x * cab;                                         // exact
+                        const float rs = __fmaf_rn(2.0f, r, -copysignf(twoq, r));    // expo field 0
+                        r = ((__float_as_uint(r) & 0x7F800000u) == q0exp) ? rs : r;
+                        r = (__float_as_uint(cab) == __float_as_uint(e.y)) ? fabsf(r) : r;  // F7
+                        acc[q] += r;
+                    }
+                }
+            }
+        }
+        float *yr = y + (((int64_t)img * t.Cout + co) * t.Ho + ho) * t.Wo;
+#pragma unroll
+        for (int q = 0; q < TBX_TW; ++q)
+            if (wo0 + q < t.Wo) yr[wo0 + q] = epi(ep, ep_act, ep_lo, ep_hi, co, acc[q]);
+    }
+    if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(gate, 1u);
+}

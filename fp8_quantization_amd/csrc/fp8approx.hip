@@ -891,6 +891,8 @@ __global__ __launch_bounds__(256) void conv_tb_fast_kernel(const float *x, const
     if (live) y[((img * Cout + co) * Ho + ho) * Wo + wo] = epi(ep, ep_act, ep_lo, ep_hi, co, acc);
 }
 
+#include "conv_tbx.h"
+
 // FP8 fake quantizer (fp8_quantizer.py:97-173), one sign bit.
 __global__ __launch_bounds__(256) void fp8_quantize_kernel(const float *x, int64_t rows, int64_t inner,
                                                            const float *maxval, int per_row, int E, int M,
@@ -1237,7 +1239,8 @@ size_t fp8a_conv2d_workspace_size(int64_t Bn, int64_t Cin, int64_t H, int64_t W,
     if (Ho <= 0 || Wo <= 0) return 0;
     // implicit GEMM (no im2col image): the off-grid flag word + split-K partials of one group
     const int64_t Mrows = Bn * Ho * Wo, cog = Cout / groups, Kg = (Cin / groups) * kh * kw;
-    if (Mrows <= 0 || Kg <= 0 || cog == 1) return FLAG_BYTES;  // cog == 1: tensor-bias kernels
+    if (Mrows <= 0 || Kg <= 0) return FLAG_BYTES;
+    if (cog == 1) return FLAG_BYTES + (size_t)(Bn * Cin * H * W) * 4;  // tensor-bias kernels: A words
     return gemm_workspace_bytes(Mrows, cog, Kg, Bn * (Cin / groups) * H * W);
 }
 
@@ -1276,7 +1279,32 @@ int fp8a_conv2d_bn_act(const float *x, const float *w, float *y, int64_t Bn, int
         // fast form: needs s2n on and golden_clip_OF off (else every launch would fall back)
         const bool fast_ok = (flags & F_S2N) && !(flags & F_GCLIP) && workspace != nullptr &&
                              workspace_bytes >= FLAG_BYTES && Cout <= 65535 && Bn <= 65535;
-        if (fast_ok) {
+        // E4M3 table form (conv_tbx.h): {0,1} / zero table, qbma, 3-wide kernel rows, stride 1 or 2
+        const int64_t nwg = (Wo + TBX_TW - 1) / TBX_TW, items = Bn * Cout * Ho * nwg;
+        static const bool no_tbx = getenv("FP8A_NO_TBX") != nullptr;
+        const bool tbx_ok = fast_ok && !no_tbx && E == 4 && Mw == 3 && (mode == TM_NONE || mode == TM_W1U) &&
+                            (flags & F_QBMA) && kw == 3 && dw == 1 && sh == sw && (sw == 1 || sw == 2) &&
+                            items < (1ll << 31) && Ho * Wo < (1ll << 31) &&
+                            workspace_bytes >= FLAG_BYTES + (size_t)(Bn * Cin * H * W) * 4;
+        if (tbx_ok) {
+            gate = (uint32_t *)workspace;
+            uint32_t *aw = (uint32_t *)((char *)workspace + FLAG_BYTES);
+            if (hipMemsetAsync(gate, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a gate reset");
+            const int64_t nx = Bn * Cin * H * W;
+            tbx_decode_a<<<(unsigned)std::min<int64_t>((nx + 255) / 256, 8192), 256, 0, s>>>(x, nx, aw, gate);
+            TbxArgs ta;
+            ta.Cin = Cin; ta.H = H; ta.W = W; ta.Cout = Cout; ta.Ho = Ho; ta.Wo = Wo;
+            ta.kh = kh; ta.ph = ph; ta.pw = pw; ta.dh = dh; ta.cpg = (int)cig;
+            ta.nwg = (uint32_t)nwg;
+            ta.items = (uint32_t)items;
+            const unsigned gb = (unsigned)std::min<int64_t>((items + 255) / 256, 8 * 1024);
+            if (sw == 1)
+                conv_tbx_kernel<1><<<gb, 256, 0, s>>>(aw, w, y, ta, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi);
+            else
+                conv_tbx_kernel<2><<<gb, 256, 0, s>>>(aw, w, y, ta, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi);
+            rc = hip_check("fp8a_conv2d (tensor-bias groups, E4M3 table form)");
+            if (rc) return rc;
+        } else if (fast_ok) {
             gate = (uint32_t *)workspace;
             if (hipMemsetAsync(gate, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a gate reset");
             dim3 grid((unsigned)((Ho * Wo + 255) / 256), (unsigned)Cout, (unsigned)Bn);

@@ -47,9 +47,9 @@ def test_workspace_queries_are_host_only():
     assert L.fp8a_matmul_workspace_size_mnk(Mr, N, K) == flag + _a256(Mr * kpad * 4) + _a256(kpad * npad // 2 * 8)
     Mr, N, K = 12544, 512, 4608
     assert L.fp8a_matmul_workspace_size_mnk(Mr, N, K) > flag + _a256(Mr * K * 4) + _a256(K * N // 2 * 8)  # split
-    # depthwise (single output channel per group): the tensor-bias kernels need the flag word only
-    # (the v5 mode takes the GEMM path and runs unsplit without a pre-decode in that workspace)
-    assert L.fp8a_conv2d_workspace_size(2, 8, 6, 6, 8, 3, 3, 1, 1, 1, 1, 1, 1, 8) == flag
+    # depthwise (single output channel per group): the tensor-bias kernels need the flag word and
+    # the E4M3 table form's input words (the v5 mode takes the GEMM path, unsplit, no pre-decode)
+    assert L.fp8a_conv2d_workspace_size(2, 8, 6, 6, 8, 3, 3, 1, 1, 1, 1, 1, 1, 8) == flag + 2 * 8 * 6 * 6 * 4
     # implicit-GEMM conv: no im2col image; the A words of one group's input slice
     n2 = L.fp8a_conv2d_workspace_size(2, 3, 8, 8, 4, 3, 3, 1, 1, 1, 1, 1, 1, 1)
     assert n2 >= flag + 2 * 3 * 8 * 8 * 4

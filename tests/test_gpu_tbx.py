@@ -1,0 +1,147 @@
+"""The E4M3 tensor-bias (depthwise) table kernel conv_tbx_kernel (csrc/conv_tbx.h).
+
+Single-output-channel groups take the reference's tensor-bias semantics.  For E4M3,
+s2n, qbma, a {0,1} or zero table, 3-wide kernel rows and stride 1 / 2 the term is a table value
+times the operands' binades plus the expo-0-binade and F7 fix-ups.  Checked here:
+  * every one of the 256 x 256 E4M3 code pairs as a term, bit-exact against the oracle's
+    tensor-bias terms: a 3x3 depthwise conv whose weights are zero except one tap makes every
+    output exactly one term (several bias triples, both tables, the expo-0 binade and the F7
+    band included: biases put products near 2^-bR);
+  * sums of realistic MobileNetV2-like depthwise layers (stride 1 and 2, 3x3) within the bar;
+  * an off-grid input raises the gate and the exact kernel's result is returned.
+The launch's gate word is read back: 0 proves the table form produced the result.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as orc
+from tests import golden_io as gio
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+E, M = 4, 3
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device")
+    from fp8_quantization_amd import _lib
+    _lib.load()
+
+
+def _codes(bias):
+    e = np.repeat(np.arange(16), 8)
+    m = np.tile(np.arange(8), 16)
+    v = np.where(e == 0, np.ldexp(m / 8.0, 1 - bias), np.ldexp(1.0 + m / 8.0, e - bias))
+    return np.concatenate([v, -v]).astype(np.float32)
+
+
+def _dw_raw(x, w, bA, bW, bR, table, flags, stride, pad):
+    """fp8a_conv2d on a depthwise layer with a caller-owned workspace: (y, gate word)."""
+    from fp8_quantization_amd import _lib
+    L = _lib.load()
+    Bn, C, H, W = x.shape
+    kh, kw = w.shape[2], w.shape[3]
+    Ho = (H + 2 * pad - kh) // stride + 1
+    Wo = (W + 2 * pad - kw) // stride + 1
+    xt = torch.as_tensor(np.ascontiguousarray(x)).to(DEV)
+    wt = torch.as_tensor(np.ascontiguousarray(w)).to(DEV)
+    y = torch.empty((Bn, C, Ho, Wo), dtype=torch.float32, device=DEV)
+    n = int(L.fp8a_conv2d_workspace_size(Bn, C, H, W, C, kh, kw, stride, stride, pad, pad, 1, 1, C))
+    ws = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    tA = torch.tensor([bA], dtype=torch.int32, device=DEV)
+    tW = torch.as_tensor(np.asarray(bW, np.int32)).to(DEV)
+    tR = torch.tensor([bR], dtype=torch.int32, device=DEV)
+    tab = torch.as_tensor(np.ascontiguousarray(table, np.int32))
+    rc = L.fp8a_conv2d(_lib.dev_ptr(xt), _lib.dev_ptr(wt), _lib.dev_ptr(y), Bn, C, H, W, C, kh, kw, stride, stride,
+                       pad, pad, 1, 1, C, E, M, _lib.dev_ptr(tA), _lib.dev_ptr(tW), _lib.dev_ptr(tR),
+                       _lib.host_ptr(tab), flags, _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(DEV))
+    _lib.check(rc, "fp8a_conv2d")
+    torch.cuda.synchronize()
+    return y.cpu().numpy(), int(ws[:4].view(torch.int32).item())
+
+
+def _terms_equal(got, ref, what):
+    same = (got.view(np.uint32) == ref.view(np.uint32)) | ((got == 0) & (ref == 0))
+    if not same.all():
+        i = tuple(np.argwhere(~same)[0])
+        raise AssertionError(f"{what}: {np.count_nonzero(~same)} terms differ; first at {i}: "
+                             f"got {got[i]!r} ref {ref[i]!r}")
+
+
+FL = orc.flags_of(approx=True, s2n=True, qbma=True)
+
+
+@pytest.mark.parametrize("table", ["nocomp", "comp"])
+@pytest.mark.parametrize("biases", [(12, 12, 8), (10, 13, 7), (9, 9, 2), (14, 14, 20), (8, 8, 3)])
+@pytest.mark.parametrize("stride", [1, 2])
+def test_every_code_pair_bitexact(biases, table, stride):
+    bA, bW_, bR = biases
+    a = _codes(bA)          # 256 input values: one image of 16 x 16 pixels, same in every channel
+    b = _codes(bW_)         # 256 channels, channel c's weight = b[c] at the center tap
+    C = 256
+    if stride == 1:
+        x = np.broadcast_to(a.reshape(1, 1, 16, 16), (1, C, 16, 16)).copy()
+        pad = 1
+    else:  # stride 2 with padding 1: output (i, j) centres on input (2i, 2j)
+        x = np.zeros((1, C, 32, 32), np.float32)
+        x[:, :, 0::2, 0::2] = a.reshape(1, 1, 16, 16)
+        pad = 1
+    w = np.zeros((C, 1, 3, 3), np.float32)
+    w[:, 0, 1, 1] = b
+    bW = np.full(C, bW_, np.int32)
+    tab = gio.load("g2_matmul.npz")["E4M3_table_comp" if table == "comp" else "E4M3_table_nocomp"]
+    y, gate = _dw_raw(x, w, bA, bW, bR, tab, FL, stride, pad)
+    assert gate == 0, "gate raised: the table form did not produce these terms"
+    ref = orc.terms(a.reshape(-1, 1), b.reshape(1, -1), E, M, bA, bW, bR, tab, FL | orc.TB)[:, 0, :]  # [256 a, 256 b]
+    got = y[0].reshape(C, 256).T  # [pixel = a index, channel = b index]
+    _terms_equal(got, ref, f"biases {biases} {table} stride {stride}")
+
+
+def _grid(rng, shape, bias, zero_frac=0.0, lo=3):
+    expo = rng.integers(lo, 16, size=shape)
+    mant = rng.integers(0, 8, size=shape)
+    v = np.ldexp(1.0 + mant / 8.0, expo - bias) * rng.choice([-1.0, 1.0], size=shape)
+    v[rng.random(shape) < zero_frac] = 0.0
+    return v.astype(np.float32)
+
+
+@pytest.mark.parametrize("cfg", [dict(C=32, hw=28, s=1), dict(C=24, hw=29, s=2), dict(C=48, hw=7, s=1),
+                                 dict(C=16, hw=14, s=2)])
+def test_depthwise_layer_sums(cfg):
+    rng = np.random.default_rng(cfg["C"] * 100 + cfg["hw"])
+    bA, bR = 10, 9
+    C, hw, s = cfg["C"], cfg["hw"], cfg["s"]
+    x = _grid(rng, (3, C, hw, hw), bA, zero_frac=0.4)
+    bW = rng.integers(12, 16, size=C).astype(np.int32)
+    w = _grid(rng, (C, 1, 3, 3), bW[:, None, None, None])
+    tab = gio.load("g2_matmul.npz")["E4M3_table_nocomp"]
+    y, gate = _dw_raw(x, w, bA, bW, bR, tab, FL, s, 1)
+    assert gate == 0
+    cols = torch.nn.functional.unfold(torch.from_numpy(x), (3, 3), padding=1, stride=s)
+    cols = cols.transpose(1, 2).reshape(-1, C * 9).numpy()
+    for c in range(C):
+        ref, S = orc.matmul(cols[:, c * 9:(c + 1) * 9], w[c].reshape(9, 1), E, M, bA, bW[c:c + 1], bR, tab,
+                            FL | orc.TB, with_abs=True)
+        got = y[:, c].reshape(-1, 1).astype(np.float64)
+        assert np.all(np.abs(got - ref) <= gio.sum_tolerance(S.astype(np.float64))), f"channel {c}"
+
+
+def test_off_grid_input_falls_back():
+    rng = np.random.default_rng(4)
+    bA, bR = 10, 9
+    x = _grid(rng, (2, 8, 9, 9), bA, zero_frac=0.3)
+    x[1, 2, 4, 4] = 0.3
+    bW = np.full(8, 13, np.int32)
+    w = _grid(rng, (8, 1, 3, 3), 13)
+    tab = gio.load("g2_matmul.npz")["E4M3_table_nocomp"]
+    y, gate = _dw_raw(x, w, bA, bW, bR, tab, FL, 1, 1)
+    assert gate != 0
+    cols = torch.nn.functional.unfold(torch.from_numpy(x), (3, 3), padding=1).transpose(1, 2).reshape(-1, 72).numpy()
+    for c in range(8):
+        ref, S = orc.matmul(cols[:, c * 9:(c + 1) * 9], w[c].reshape(9, 1), E, M, bA, bW[c:c + 1], bR, tab,
+                            FL | orc.TB, with_abs=True)
+        got = y[:, c].reshape(-1, 1).astype(np.float64)
+        assert np.all(np.abs(got - ref) <= gio.sum_tolerance(S.astype(np.float64))), f"channel {c}"
