@@ -92,12 +92,17 @@ class ApproxConv2dMixin(ApproxOpMixin):
         return out
 
     supports_bn_act_epilogue = True
+    supports_input_quant_fusion = True
 
-    def run_forward(self, x, weight, bias, offsets=None, epilogue=None):
+    def run_forward(self, x, weight, bias, offsets=None, epilogue=None, qin=None):
+        """qin: the layer's input FPQuantizer when the hijacker fused it (x unquantized; the op
+        applies it and its custom_bias is set as its own forward would)."""
         x = x.contiguous()
         weight = weight.contiguous()
         if epilogue is not None and (bias is not None or not self.approx_flag):
             raise AssertionError("the fused BN epilogue needs the approx product without a conv bias")
+        if qin is not None and not self.approx_flag:
+            raise AssertionError("the fused input quantizer needs the approx product")
         w_bias = self.get_weights_fp_bias()
         a_bias = self.get_acts_fp_bias()
         r_bias = self.get_res_fp_bias()
@@ -105,10 +110,15 @@ class ApproxConv2dMixin(ApproxOpMixin):
         if self.approx_flag:
             if w_bias is None:  # the reference indexes weight_fp_bias[...] (approx_calculation.py:868)
                 raise TypeError("'NoneType' object is not subscriptable")
-            out = approx_conv2d(x.detach(), weight.detach(), E, M, self._default_bias(a_bias, E, x.device),
-                                w_bias, self._default_bias(r_bias, E, x.device), table, flags=flags,
-                                stride=self.stride, padding=self.padding, dilation=self.dilation, groups=self.groups,
-                                epilogue=epilogue)
+            args = dict(flags=flags, stride=self.stride, padding=self.padding, dilation=self.dilation,
+                        groups=self.groups, epilogue=epilogue)
+            if qin is not None:
+                out, qin.custom_bias = approx_conv2d(
+                    x.detach(), weight.detach(), E, M, None, w_bias, self._default_bias(r_bias, E, x.device), table,
+                    qin=(qin.maxval, qin.n_bits, qin._mbits_int, qin.sign_bits), **args)
+            else:
+                out = approx_conv2d(x.detach(), weight.detach(), E, M, self._default_bias(a_bias, E, x.device),
+                                    w_bias, self._default_bias(r_bias, E, x.device), table, **args)
         elif self.quantize_after_mult_and_add and self.out_channels // self.groups != 1:
             out = qamaa_conv2d(x.detach(), weight.detach(), *self._qamaa_params(), stride=self.stride,
                                padding=self.padding, dilation=self.dilation, groups=self.groups)

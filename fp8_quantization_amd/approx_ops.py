@@ -285,15 +285,62 @@ def _(x, w, bA, bW, bR, table, E, M, flags, stride, padding, dilation, groups, b
     return x.new_empty((Bn, Cout, Ho, Wo))
 
 
+@torch.library.custom_op("fp8approx::conv2d_qin", mutates_args=())
+def _conv2d_qin_op(x: torch.Tensor, w: torch.Tensor, maxval: torch.Tensor, bW: torch.Tensor, bR: torch.Tensor,
+                   table: torch.Tensor, E: int, M: int, flags: int, stride: list[int], padding: list[int],
+                   dilation: list[int], groups: int, n_bits: int, mbits: int, sign_bits: int,
+                   bn: Optional[torch.Tensor] = None, act: int = 0, act_lo: float = 0.0,
+                   act_hi: float = 0.0) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    L = _lib.load()
+    x = x.contiguous()
+    w = w.contiguous()
+    Bn, Cin, H, W = x.shape
+    Cout, _, kh, kw = w.shape
+    sh, sw = stride
+    ph, pw = padding
+    dh, dw = dilation
+    Ho = (H + 2 * ph - dh * (kh - 1) - 1) // sh + 1
+    Wo = (W + 2 * pw - dw * (kw - 1) - 1) // sw + 1
+    y = torch.empty((Bn, Cout, Ho, Wo), dtype=torch.float32, device=x.device)
+    bias = torch.empty(1, dtype=torch.float32, device=x.device)
+    ibias = torch.empty(1, dtype=torch.int32, device=x.device)
+    ws = _workspace(x.device, L.fp8a_conv2d_qin_workspace_size(Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw,
+                                                               groups))
+    if bn is not None and (bn.shape != (Cout, 2) or bn.dtype != torch.float32 or not bn.is_contiguous()):
+        raise AssertionError(f"approx_conv2d: epilogue parameters must be contiguous float32 [{Cout}, 2]")
+    rc = L.fp8a_conv2d_qin(_lib.dev_ptr(x), _lib.dev_ptr(w), _lib.dev_ptr(y), Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph,
+                           pw, dh, dw, groups, E, M, _lib.dev_ptr(bW), _lib.dev_ptr(bR), _lib.host_ptr(table), flags,
+                           _lib.dev_ptr(bn) if bn is not None else None, int(act), float(act_lo), float(act_hi),
+                           _lib.dev_ptr(maxval), int(n_bits), int(mbits), int(sign_bits), _lib.dev_ptr(bias),
+                           _lib.dev_ptr(ibias), _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(x.device))
+    _lib.check(rc, "fp8a_conv2d_qin")
+    return y, bias, ibias
+
+
+@_conv2d_qin_op.register_fake
+def _(x, w, maxval, bW, bR, table, E, M, flags, stride, padding, dilation, groups, n_bits, mbits, sign_bits, bn=None,
+      act=0, act_lo=0.0, act_hi=0.0):
+    Bn, _, H, W = x.shape
+    Cout, _, kh, kw = w.shape
+    Ho = (H + 2 * padding[0] - dilation[0] * (kh - 1) - 1) // stride[0] + 1
+    Wo = (W + 2 * padding[1] - dilation[1] * (kw - 1) - 1) // stride[1] + 1
+    return x.new_empty((Bn, Cout, Ho, Wo)), x.new_empty((1,)), x.new_empty((1,), dtype=torch.int32)
+
+
 def approx_conv2d(x, w, E, M, bA, bW, bR, table=None, flags=None, stride=(1, 1), padding=(0, 0), dilation=(1, 1),
-                  groups=1, epilogue=None, **flag_kwargs):
+                  groups=1, epilogue=None, qin=None, **flag_kwargs):
     """approx_v9 convolution, NCHW in / NCHW out (pre-BN), K ordered (c, ky, kx) like the
     reference im2col (approx_calculation.py:724-747); single-output-channel groups get the
     tensor-bias semantics (approx_calculation.py:800-809).  bW: per output channel.
 
     epilogue: optional ``(scale_shift [Cout, 2] float32 device tensor, act, lo, hi)`` fusing
     the layer's eval-mode BatchNorm (y * scale + shift) and a clamp activation into the
-    kernel's store (fp8a_conv2d_bn_act, include/fp8approx.h); see ``bn_act_epilogue``."""
+    kernel's store (fp8a_conv2d_bn_act, include/fp8approx.h); see ``bn_act_epilogue``.
+
+    qin: optional ``(maxval [1] device tensor, n_bits, mantissa_bits, sign_bits)`` of the layer's
+    per-tensor input activation quantizer: x is then UNQUANTIZED, the op applies
+    quantize_to_fp8_ste_MM itself (fp8a_conv2d_qin: inside the E4M3 operand pre-decode where that
+    path runs) and returns ``(y, float bias [1])`` -- the quantizer's custom_bias (bA is unused)."""
     if flags is None:
         flags = make_flags(**flag_kwargs)
     flags &= ~_lib.TB
@@ -305,6 +352,18 @@ def approx_conv2d(x, w, E, M, bA, bW, bR, table=None, flags=None, stride=(1, 1),
     if bW_.numel() != w.shape[0]:
         raise AssertionError(f"approx_conv2d: {bW_.numel()} weight biases for {w.shape[0]} output channels")
     ev = _prof_start()
+    if qin is not None:
+        mx, nb, mb, sb = qin
+        mx = _as_f32(mx).reshape(-1).contiguous()
+        if mx.numel() != 1:
+            raise AssertionError("approx_conv2d: the fused input quantizer must be per tensor")
+        y, bias, ibias = _conv2d_qin_op(_as_f32(x), _as_f32(w), mx.to(dev), bW_, _bias_dev(bR, dev), tab, int(E),
+                                        int(M), int(flags), [int(s) for s in stride], [int(p) for p in padding],
+                                        [int(d) for d in dilation], int(groups), int(nb), int(mb), int(sb),
+                                        *(epilogue or ()))
+        bias._fp8a_i32 = ibias
+        _prof_end(ev, y.shape[0] * y.shape[2] * y.shape[3] * w.shape[0] * w.shape[1] * w.shape[2] * w.shape[3])
+        return y, bias
     y = _conv2d_op(_as_f32(x), _as_f32(w), _bias_dev(bA, dev), bW_, _bias_dev(bR, dev), tab,
                    int(E), int(M), int(flags), [int(s) for s in stride], [int(p) for p in padding],
                    [int(d) for d in dilation], int(groups), *(epilogue or ()))

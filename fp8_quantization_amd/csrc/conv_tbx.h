@@ -32,10 +32,19 @@ struct TbxArgs {
 
 // x (NCHW floats) -> words: (bits(x) & 0xFF800000) | (m << 6); 0 for zeros; gate on off-grid
 // values / the exactness window (tensor-bias decode: every value at its own binade).
-__global__ __launch_bounds__(256) void tbx_decode_a(const float *x, int64_t n, uint32_t *out, uint32_t *gate) {
+// With fused input quantization (fq.mx set) the values are fq(x) and the quantizer's bias is
+// written to fq_bias / fq_ibias (the kernels' bA).
+__global__ __launch_bounds__(256) void tbx_decode_a(const float *x, int64_t n, uint32_t *out, uint32_t *gate,
+                                                    FqIn fq, float *fq_bias_out, int32_t *fq_ibias_out) {
     bool bad = false;
+    const float fmx = fq.mx ? *fq.mx : 0.0f, fbias = fq.mx ? fq_bias(fmx, fq.E, fq.M) : 0.0f;
+    if (fq.mx && blockIdx.x == 0 && threadIdx.x == 0) {
+        *fq_bias_out = fbias;
+        *fq_ibias_out = (int32_t)fbias;
+    }
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t u = __float_as_uint(x[i]), ua = u & 0x7FFFFFFFu;
+        const float v = fq.mx ? fq_apply(x[i], fmx, fbias, fq.M, fq.S) : x[i];
+        const uint32_t u = __float_as_uint(v), ua = u & 0x7FFFFFFFu;
         bad |= (ua != 0u) && ((ua & 0xFFFFFu) != 0u || ua < 0x20800000u || ua > 0x58800000u);
         out[i] = ua == 0u ? 0u : ((u & 0xFF800000u) | (((ua >> 20) & 7u) << 6));
     }

@@ -92,6 +92,27 @@ static int pack_table(const int32_t *table, int M, bool approx, TablePack &tp, i
 }
 
 // ------------------------------------------------------------------------- GEMM arguments
+// FP8 fake quantizer of the activations (quantize_to_fp8_ste_MM, fp8_quantizer.py:97-173),
+// per tensor: the bias from maxval, then clamp / binade step / round.  fp8_quantize_kernel and the
+// fused input quantization of the approx ops (fp8a_conv2d_qin) share these, bit for bit.
+struct FqIn {
+    const float *mx;  // device maxval [1]; nullptr = the input is already quantized
+    int E, M, S;      // exponent / mantissa / sign bits of the quantizer
+};
+
+__device__ __forceinline__ float fq_bias(float mx, int E, int M) {
+    return rintf((float)(1 << E) - log2f(mx) + log2f(2.0f - p2(-M)) - 1.0f);
+}
+
+__device__ __forceinline__ float fq_apply(float v, float mx, float bias, int M, int sign_bits) {
+    const float xc = fminf(fmaxf(v, sign_bits ? -mx : 0.0f), mx);
+    int e;
+    frexpf(xc, &e);
+    const float ls = (xc == 0.0f) ? 1.0f : fmaxf((float)(e - 1) + bias, 1.0f);
+    const float sc = p2((int)(ls - (float)M - bias));
+    return rintf(xc / sc) * sc;
+}
+
 struct GemmArgs {
     const float *A;
     int64_t lda;
@@ -139,6 +160,11 @@ struct GemmArgs {
     int64_t awld, aw_c;
     const uint2 *bqw;
     int64_t npad;
+    // fused input quantization (fp8a_conv2d_qin): A = fq(X); the quantizer's bias is written to
+    // fq_bias / fq_ibias by the A pre-decode, and bA points at fq_ibias
+    FqIn fqin;
+    float *fq_bias;
+    int32_t *fq_ibias;
     TablePack tab;
 };
 
@@ -686,7 +712,10 @@ __device__ __forceinline__ float load_A(const GemmArgs &p, int64_t m, int64_t k)
     const int64_t taps = (int64_t)p.kh * p.kw, c = k / taps, t = k - c * taps, ky = t / p.kw, kx = t - ky * p.kw;
     const int64_t hi = ho * p.sh - p.ph + ky * p.dh, wi = wo * p.sw - p.pw + kx * p.dw;
     if (hi < 0 || hi >= p.H || wi < 0 || wi >= p.W) return 0.0f;
-    return p.X[((img * p.Cin + p.cbase + c) * p.H + hi) * p.W + wi];
+    const float v = p.X[((img * p.Cin + p.cbase + c) * p.H + hi) * p.W + wi];
+    if (p.fqin.mx == nullptr) return v;
+    const float mx = *p.fqin.mx;
+    return fq_apply(v, mx, fq_bias(mx, p.fqin.E, p.fqin.M), p.fqin.M, p.fqin.S);
 }
 
 __global__ __launch_bounds__(256) void gemm_exact_kernel(const GemmArgs p) {
@@ -769,12 +798,13 @@ __global__ __launch_bounds__(256) void conv_tb_direct_kernel(const float *x, con
                                                              int Mw, const int32_t *bA, const int32_t *bW,
                                                              const int32_t *bR, TablePack tab, uint32_t flags,
                                                              const uint32_t *gate, const float2 *ep, int ep_act,
-                                                             float ep_lo, float ep_hi) {
+                                                             float ep_lo, float ep_hi, FqIn fq) {
     // after conv_tb_fast_kernel: run only if it flagged inputs outside its exactness window
     if (gate != nullptr && __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
     const int64_t total = Bn * Cout * Ho * Wo;
     const int64_t cpg = Cin / groups;   // input channels per group
     const DFmt fA = dfmt(E, Mw, *bA, true), fR = dfmt(E, Mw, *bR, true);
+    const float fmx = fq.mx ? *fq.mx : 0.0f, fbias = fq.mx ? fq_bias(fmx, fq.E, fq.M) : 0.0f;
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
          idx += (int64_t)gridDim.x * blockDim.x) {
         const int64_t wo = idx % Wo, ho = (idx / Wo) % Ho, co = (idx / (Wo * Ho)) % Cout, b = idx / (Wo * Ho * Cout);
@@ -786,8 +816,9 @@ __global__ __launch_bounds__(256) void conv_tb_direct_kernel(const float *x, con
             for (int ky = 0; ky < kh; ++ky)
                 for (int kx = 0; kx < kw; ++kx) {
                     const int64_t hi = ho * sh - ph + ky * dh, wi = wo * sw - pw + kx * dw;
-                    const float a = (hi >= 0 && hi < H && wi >= 0 && wi < W)
-                                        ? x[((b * Cin + g * cpg + c) * H + hi) * W + wi] : 0.0f;
+                    float a = (hi >= 0 && hi < H && wi >= 0 && wi < W)
+                                  ? x[((b * Cin + g * cpg + c) * H + hi) * W + wi] : 0.0f;
+                    if (fq.mx) a = fq_apply(a, fmx, fbias, fq.M, fq.S);
                     const float bv = w[((co * cpg + c) * kh + ky) * kw + kx];
                     part += exact_term(a, bv, fA, fB, fR, tab.raw, flags | F_TB);
                     if (++cnt == 16) {
@@ -899,19 +930,12 @@ __global__ __launch_bounds__(256) void fp8_quantize_kernel(const float *x, int64
                                                            int sign_bits, float *out, float *bias_out,
                                                            int32_t *ibias_out) {
     const int64_t total = rows * inner;
-    const float cM = log2f(2.0f - p2(-M));
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
          idx += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = per_row ? idx / inner : 0;
         const float mx = maxval[r];
-        const float bias = rintf((float)(1 << E) - log2f(mx) + cM - 1.0f);
-        const float v = x[idx];
-        const float xc = fminf(fmaxf(v, sign_bits ? -mx : 0.0f), mx);
-        int e;
-        frexpf(xc, &e);
-        const float ls = (xc == 0.0f) ? 1.0f : fmaxf((float)(e - 1) + bias, 1.0f);
-        const float sc = p2((int)(ls - (float)M - bias));
-        out[idx] = rintf(xc / sc) * sc;
+        const float bias = fq_bias(mx, E, M);
+        out[idx] = fq_apply(x[idx], mx, bias, M, sign_bits);
         if ((idx % inner) == 0) {
             if (bias_out) bias_out[r] = bias;
             if (ibias_out) ibias_out[r] = (int32_t)bias;
@@ -1042,6 +1066,20 @@ static size_t gemm_workspace_bytes(int64_t M, int64_t N, int64_t K, int64_t a_wo
     return FLAG_BYTES + splitk_bytes(M, N, K) + (a_words > 0 ? xm_operand_bytes(N, K, a_words) : 0);
 }
 
+// The E4M3 table + hardware-fp8 form applies (TM_F8; run_gemm then takes the matrix-core kernel
+// when the workspace holds its pre-decoded operands): E4M3, a {0,1} or zero table, s2n + qbma, no
+// golden clip, int-bias semantics, not v5.
+static bool f8_form(int E, int Mw, uint32_t flags, int table_mode) {
+    static const bool no_f8 = getenv("FP8A_NO_F8") != nullptr;
+    return !no_f8 && !(flags & F_V5) && E == 4 && Mw == 3 && (table_mode == TM_NONE || table_mode == TM_W1U) &&
+           (flags & F_S2N) && (flags & F_QBMA) && !(flags & F_GCLIP) && !(flags & F_TB);
+}
+
+static bool no_mx() {
+    static const bool v = getenv("FP8A_NO_MX") != nullptr;
+    return v;
+}
+
 // Fast tiled kernel + gated exact kernel (int-bias path), or the exact kernel alone (tb path).
 static int run_qamaa(GemmArgs &a, hipStream_t s);
 
@@ -1067,10 +1105,7 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     if (v5) mode = TM_V5;
     // E4M3 with a {0,1} (or no) table, s2n and per-product quantization: the LUT + hardware-fp8
     // form (FP8A_NO_F8=1 keeps the arithmetic form, for comparison)
-    static const bool no_f8 = getenv("FP8A_NO_F8") != nullptr;
-    if (!v5 && !no_f8 && a.E == 4 && a.Mw == 3 && (mode == TM_NONE || mode == TM_W1U) && (a.flags & F_S2N) &&
-        (a.flags & F_QBMA) && !(a.flags & F_GCLIP) && !(a.flags & F_TB))
-        mode = TM_F8;
+    if (f8_form(a.E, a.Mw, a.flags, mode)) mode = TM_F8;
     const int64_t total = a.M * a.N;
     const unsigned eblocks = (unsigned)std::min<int64_t>((total + 255) / 256, 4096);
     if (a.flags & F_TB) {
@@ -1089,9 +1124,8 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     if (hipMemsetAsync(ws, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a flag reset");
     // the matrix-core E4M3 kernel needs its pre-decoded operands in the workspace (else the
     // VALU-accumulating form runs); FP8A_NO_MX=1 forces the latter
-    static const bool no_mx = getenv("FP8A_NO_MX") != nullptr;
     a.aw = nullptr;
-    if (mode == TM_F8 && !no_mx) {
+    if (mode == TM_F8 && !no_mx()) {
         const int64_t kpad = kt * BK, npad = (a.N + BN - 1) / BN * BN;
         const int64_t a_words = a.conv ? (a.M / (a.Ho * a.Wo)) * a.aw_c * a.H * a.W : a.M * kpad;
         const size_t off = FLAG_BYTES + (a.splits > 1 ? splitk_bytes(a.M, a.N, a.K) : 0);
@@ -1111,6 +1145,8 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
             if (rc) return rc;
         }
     }
+    if (a.fqin.mx && !a.aw)  // the caller (conv2d_impl) only fuses where the pre-decode runs
+        return fail(FP8A_EINVAL, "internal: fused input quantization without the matrix-core path");
     launch_fast(mode, a, s);
     rc = hip_check("fp8a fast gemm launch");
     if (rc) return rc;
@@ -1252,14 +1288,17 @@ int fp8a_conv2d(const float *x, const float *w, float *y, int64_t Bn, int64_t Ci
                               table, flags, nullptr, 0, 0.0f, 0.0f, workspace, workspace_bytes, stream);
 }
 
-int fp8a_conv2d_bn_act(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
+// The convolution entry points.  fq.mx set: x is NOT yet quantized; the activation quantizer
+// (fp8_quantizer.py:97-173, per tensor) is applied inside the matrix-core / tensor-bias-table
+// pre-decodes (its bias written to fqb / fqi, which serve as bA), or -- for every other path --
+// into xq (numel(x) floats) by one fake-quant pass first.
+static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
                        int64_t Cout, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw, int groups,
                        int E, int Mw, const int32_t *bA, const int32_t *bW, const int32_t *bR, const int32_t *table,
                        uint32_t flags, const float *bn, int act, float act_lo, float act_hi, void *workspace,
-                       size_t workspace_bytes, fp8a_stream_t stream) {
+                       size_t workspace_bytes, hipStream_t s, FqIn fq, float *fqb, int32_t *fqi, float *xq) {
     const float2 *ep = reinterpret_cast<const float2 *>(bn);
     if (ep && (((uintptr_t)bn) & 7) != 0) return fail(FP8A_EINVAL, "bn parameters must be 8-byte aligned");
-    hipStream_t s = (hipStream_t)stream;
     int rc = check_format(E, Mw);
     if (rc) return rc;
     if (groups <= 0 || Cout % groups != 0 || Cin % groups != 0) return fail(FP8A_EINVAL, "bad groups");
@@ -1269,6 +1308,16 @@ int fp8a_conv2d_bn_act(const float *x, const float *w, float *y, int64_t Bn, int
     const int64_t cog = Cout / groups, cig = Cin / groups;
     const int64_t Mrows = Bn * Ho * Wo, Ktot = Cin * kh * kw, Kg = cig * kh * kw;
     if (Mrows == 0) return FP8A_OK;
+    // non-fused input quantization: one fake-quant pass into xq, then the plain path on it
+    auto materialize = [&]() -> int {
+        const int64_t nx = Bn * Cin * H * W;
+        fp8_quantize_kernel<<<(unsigned)std::max<int64_t>(1, std::min<int64_t>((nx + 255) / 256, 65536)), 256, 0, s>>>(
+            x, 1, nx, fq.mx, 0, fq.E, fq.M, fq.S, xq, fqb, fqi);
+        x = xq;
+        bA = fqi;
+        fq.mx = nullptr;
+        return hip_check("fp8a input fake-quant");
+    };
     if (cog == 1 && !(flags & F_V5)) {  // v5 never had tensor-bias semantics: it takes the GEMM path
         TablePack tp;
         int mode;
@@ -1286,12 +1335,18 @@ int fp8a_conv2d_bn_act(const float *x, const float *w, float *y, int64_t Bn, int
                             (flags & F_QBMA) && kw == 3 && dw == 1 && sh == sw && (sw == 1 || sw == 2) &&
                             items < (1ll << 31) && Ho * Wo < (1ll << 31) &&
                             workspace_bytes >= FLAG_BYTES + (size_t)(Bn * Cin * H * W) * 4;
+        if (fq.mx && !tbx_ok) {
+            rc = materialize();
+            if (rc) return rc;
+        }
         if (tbx_ok) {
             gate = (uint32_t *)workspace;
             uint32_t *aw = (uint32_t *)((char *)workspace + FLAG_BYTES);
             if (hipMemsetAsync(gate, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a gate reset");
             const int64_t nx = Bn * Cin * H * W;
-            tbx_decode_a<<<(unsigned)std::min<int64_t>((nx + 255) / 256, 8192), 256, 0, s>>>(x, nx, aw, gate);
+            tbx_decode_a<<<(unsigned)std::min<int64_t>((nx + 255) / 256, 8192), 256, 0, s>>>(x, nx, aw, gate, fq, fqb,
+                                                                                                fqi);
+            if (fq.mx) bA = fqi;
             TbxArgs ta;
             ta.Cin = Cin; ta.H = H; ta.W = W; ta.Cout = Cout; ta.Ho = Ho; ta.Wo = Wo;
             ta.kh = kh; ta.ph = ph; ta.pw = pw; ta.dh = dh; ta.cpg = (int)cig;
@@ -1318,11 +1373,11 @@ int fp8a_conv2d_bn_act(const float *x, const float *w, float *y, int64_t Bn, int
         if (fast_ok) {  // gated, grid-capped: a no-op launch unless the fast kernel flagged
             conv_tb_direct_kernel<<<eb, 256, 0, s>>>(x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw,
                                                     groups, Ho, Wo, E, Mw, bA, bW, bR, tp, flags | F_TB, gate, ep,
-                                                    act, act_lo, act_hi);
+                                                    act, act_lo, act_hi, fq);
         } else {
             conv_tb_direct_kernel<<<eb, 256, 0, s>>>(x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw,
                                                      groups, Ho, Wo, E, Mw, bA, bW, bR, tp, flags | F_TB, nullptr, ep,
-                                                     act, act_lo, act_hi);
+                                                     act, act_lo, act_hi, FqIn{});
         }
         return hip_check("fp8a_conv2d (tensor-bias groups)");
     }
@@ -1330,6 +1385,18 @@ int fp8a_conv2d_bn_act(const float *x, const float *w, float *y, int64_t Bn, int
     if (workspace == nullptr || workspace_bytes < FLAG_BYTES) return fail(FP8A_EINVAL, "conv2d workspace too small");
     if (Kg >= (1ll << 31)) return fail(FP8A_EINVAL, "conv2d window too large");
     (void)Ktot;
+    if (fq.mx) {  // fuse into the matrix-core pre-decode only where run_gemm will take that path
+        TablePack tp;
+        int mode;
+        rc = pack_table(table, Mw, (flags & (F_APPROX | F_V5)) != 0, tp, mode);
+        if (rc) return rc;
+        const bool fused = f8_form(E, Mw, flags & ~F_TB, mode) && !no_mx() && Bn * cig * H * W < (1ll << 31) &&
+                           workspace_bytes >= gemm_workspace_bytes(Mrows, cog, Kg, Bn * cig * H * W);
+        if (!fused) {
+            rc = materialize();
+            if (rc) return rc;
+        }
+    }
     for (int g = 0; g < groups; ++g) {
         GemmArgs a = make_args(nullptr, 0, w + g * cog * Kg, 1, Kg, y, 0, Mrows, cog, Kg, E, Mw, bA, bW + g * cog, 1,
                                bR, flags & ~F_TB);
@@ -1344,10 +1411,52 @@ int fp8a_conv2d_bn_act(const float *x, const float *w, float *y, int64_t Bn, int
         fastdiv_params((uint32_t)(kh * kw), a.kk_mul, a.kk_shift);
         fastdiv_params((uint32_t)kw, a.kw_mul, a.kw_shift);
         a.ep = ep; a.ep_act = act; a.ep_lo = act_lo; a.ep_hi = act_hi;
+        if (fq.mx) {
+            a.fqin = fq;
+            a.fq_bias = fqb;
+            a.fq_ibias = fqi;
+            a.bA = fqi;  // written by the A pre-decode before any kernel reads it
+        }
         rc = run_gemm(a, table, workspace, workspace_bytes, s);
         if (rc) return rc;
     }
     return FP8A_OK;
+}
+
+int fp8a_conv2d_bn_act(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
+                       int64_t Cout, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw, int groups,
+                       int E, int Mw, const int32_t *bA, const int32_t *bW, const int32_t *bR, const int32_t *table,
+                       uint32_t flags, const float *bn, int act, float act_lo, float act_hi, void *workspace,
+                       size_t workspace_bytes, fp8a_stream_t stream) {
+    return conv2d_impl(x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups, E, Mw, bA, bW, bR, table,
+                       flags, bn, act, act_lo, act_hi, workspace, workspace_bytes, (hipStream_t)stream, FqIn{}, nullptr,
+                       nullptr, nullptr);
+}
+
+size_t fp8a_conv2d_qin_workspace_size(int64_t Bn, int64_t Cin, int64_t H, int64_t W, int64_t Cout, int kh, int kw,
+                                      int sh, int sw, int ph, int pw, int dh, int dw, int groups) {
+    const size_t n = fp8a_conv2d_workspace_size(Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups);
+    return n == 0 ? 0 : align256(n) + align256((size_t)(Bn * Cin * H * W) * sizeof(float));
+}
+
+int fp8a_conv2d_qin(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
+                    int64_t Cout, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw, int groups, int E,
+                    int Mw, const int32_t *bW, const int32_t *bR, const int32_t *table, uint32_t flags,
+                    const float *bn, int act, float act_lo, float act_hi, const float *in_maxval, int in_nbits,
+                    int in_mbits, int in_sign_bits, float *in_bias_out, int32_t *in_ibias_out, void *workspace,
+                    size_t workspace_bytes, fp8a_stream_t stream) {
+    if (!in_maxval || !in_bias_out || !in_ibias_out) return fail(FP8A_EINVAL, "null pointer");
+    const int qE = in_nbits - in_sign_bits - in_mbits;
+    if (in_mbits < 1 || qE < 1) return fail(FP8A_EFORMAT, "bad FP8 quantizer format");
+    const size_t xq_bytes = align256((size_t)(Bn * Cin * H * W) * sizeof(float));
+    if (workspace == nullptr || workspace_bytes < FLAG_BYTES + xq_bytes)
+        return fail(FP8A_EINVAL, "conv2d_qin workspace too small");
+    // the fake-quant buffer of the non-fused paths sits at the workspace's end
+    const size_t rest = (workspace_bytes - xq_bytes) & ~(size_t)255;
+    float *xq = (float *)((char *)workspace + rest);
+    return conv2d_impl(x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups, E, Mw, nullptr, bW, bR,
+                       table, flags, bn, act, act_lo, act_hi, workspace, rest, (hipStream_t)stream,
+                       FqIn{in_maxval, qE, in_mbits, in_sign_bits}, in_bias_out, in_ibias_out, xq);
 }
 
 int fp8a_matmul_qamaa(const float *A, int64_t lda, const float *B, int64_t sbk, int64_t sbn, float *C, int64_t M,

@@ -79,7 +79,14 @@ __device__ __forceinline__ uint32_t xm_word_a(float x, uint32_t emnA, int bR, bo
 // [Bn][Cin][H][W] (channels cbase..cbase+aw_c) -> words [Bn][aw_c][H][W]; matrix: A [M][lda] ->
 // words [M][awld] (columns >= K zero words).
 __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
-    const int bA = *p.bA, bR = *p.bR;
+    // fused input quantization: A = fq(X) with the quantizer's own bias, which becomes bA
+    const float fmx = p.fqin.mx ? *p.fqin.mx : 0.0f;
+    const float fbias = p.fqin.mx ? fq_bias(fmx, p.fqin.E, p.fqin.M) : 0.0f;
+    const int bA = p.fqin.mx ? (int)fbias : *p.bA, bR = *p.bR;
+    if (p.fqin.mx && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+        *p.fq_bias = fbias;
+        *p.fq_ibias = bA;
+    }
     const uint32_t emnA = (uint32_t)(128 - bA) << 23;
     bool bad = !(xm_bias_ok(bA) && xm_bias_ok(bR));
     uint32_t *const out = const_cast<uint32_t *>(p.aw);
@@ -91,7 +98,9 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
         uint32_t *o = out + r * cols;
         for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cols; i += (int64_t)gridDim.x * blockDim.x) {
             bool ok = true;
-            o[i] = (i < lim) ? xm_word_a(in[i], emnA, bR, ok) : XM_ZERO_WORD;
+            float v = (i < lim) ? in[i] : 0.0f;
+            if (p.fqin.mx) v = fq_apply(v, fmx, fbias, p.fqin.M, p.fqin.S);
+            o[i] = (i < lim) ? xm_word_a(v, emnA, bR, ok) : XM_ZERO_WORD;
             bad |= !ok;
         }
     }

@@ -6,11 +6,13 @@ forward() keeps the reference's ordering exactly (hijacker.py:77-115):
   [output act-quant].  The ValueError for approx/qamaa without res_quantizer_flag is kept.
 """
 import copy
+import os
 
 from torch import nn
 
 from .base_quantized_classes import QuantizedModule
-from .quantization_manager import QuantizationManager
+from .fp8_quantizer import FPQuantizer
+from .quantization_manager import QuantizationManager, Qstates
 from .range_estimators import CurrentMinMaxEstimator
 
 activations_set = [nn.ReLU, nn.ReLU6, nn.Hardtanh, nn.Sigmoid, nn.Tanh, nn.GELU, nn.PReLU, nn.SiLU, nn.Hardswish,
@@ -18,6 +20,11 @@ activations_set = [nn.ReLU, nn.ReLU6, nn.Hardtanh, nn.Sigmoid, nn.Tanh, nn.GELU,
 
 
 class QuantizationHijacker(QuantizedModule):
+    # fused input quantization (MI355X-side, same result bit for bit): in the fixed-range approx
+    # forward the input fake-quant runs inside the approx op (fp8a_conv2d_qin) instead of as its
+    # own pass; FP8A_FUSE_QIN=0 or ``fuse_input_quant = False`` keeps the separate pass
+    fuse_input_quant = os.environ.get("FP8A_FUSE_QIN", "1") != "0"
+
     def __init__(self, *args, activation: nn.Module = None, **kwargs):
         super().__init__(*args, **kwargs)
         if activation:
@@ -41,12 +48,26 @@ class QuantizationHijacker(QuantizedModule):
                              "you need to set res_quantizer_flag to True if you want to use "
                              "quantize_after_mult_and_add or approx_flag")
 
+    def _fused_input_quantizer(self, qa):
+        """The input FPQuantizer when its forward can run inside the approx op: the quantized
+        input then feeds nothing but the one approx product of a fixed-range eval forward."""
+        if not (self.fuse_input_quant and qa and self.quantize_input and self.fix_ranges_flag
+                and not self.original_quantize_res and self.approx_flag and self.res_quantizer_flag
+                and not self.quantize_after_mult_and_add and getattr(self, "supports_input_quant_fusion", False)):
+            return None
+        mgr = self.activation_quantizer
+        q = getattr(mgr, "quantizer", None)
+        if getattr(mgr, "state", None) != Qstates.fix_ranges or not isinstance(q, FPQuantizer) or q.maxval.numel() != 1:
+            return None
+        return q
+
     def _core(self, x, offsets=None, epilogue=None):
         """Shared part of QuantizationHijacker.forward and BNFusedHijacker.forward.  epilogue
         (BNFusedHijacker's fused BN + activation) goes to the approx product only; the caller
         guarantees that product is the only one this forward runs."""
         qa = self._qa()
-        if self.quantize_input and qa:
+        fq = self._fused_input_quantizer(qa)
+        if self.quantize_input and qa and fq is None:
             x = self.activation_quantizer(x)
         weight, bias = self.get_params()
         res = None
@@ -57,10 +78,12 @@ class QuantizationHijacker(QuantizedModule):
         if self.res_quantizer_flag and self.quantize_after_mult_and_add:
             res = self.run_forward(x, weight, bias)
         if self.res_quantizer_flag and self.approx_flag:
+            kw = {}
             if epilogue is not None:
-                res = self.run_forward(x, weight, bias, offsets=offsets, epilogue=epilogue)
-            else:
-                res = self.run_forward(x, weight, bias, offsets=offsets)
+                kw["epilogue"] = epilogue
+            if fq is not None:
+                kw["qin"] = fq  # x is unquantized; the op quantizes it and sets fq.custom_bias
+            res = self.run_forward(x, weight, bias, offsets=offsets, **kw)
         self._check_res_flag()
         return res, qa
 

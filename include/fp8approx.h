@@ -133,6 +133,28 @@ int fp8a_conv2d_bn_act(const float *x, const float *w, float *y, int64_t Bn, int
                        size_t workspace_bytes, fp8a_stream_t stream);
 
 /*
+ * fp8a_conv2d_bn_act with the layer's input activation quantizer fused in (the hijacker's
+ * `x = activation_quantizer(x)` before run_forward, hijacker.py:81-83, in the fixed-range eval
+ * state): x is the UNQUANTIZED input; the op applies quantize_to_fp8_ste_MM
+ * (fp8_quantizer.py:97-173) with the per-tensor in_maxval (device float [1]) and format, writes
+ * the quantizer's bias to in_bias_out (float [1]) / in_ibias_out (int32 [1], what it returns as
+ * custom_bias) and uses it as bA.  Same result as fp8a_fp8_quantize followed by
+ * fp8a_conv2d_bn_act; where the E4M3 matrix-core or tensor-bias table kernels run, the
+ * quantization happens inside their operand pre-decode (no quantized copy of x is written).
+ * workspace: fp8a_conv2d_qin_workspace_size() bytes.
+ */
+size_t fp8a_conv2d_qin_workspace_size(int64_t Bn, int64_t Cin, int64_t H, int64_t W, int64_t Cout,
+                                      int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw,
+                                      int groups);
+int fp8a_conv2d_qin(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H,
+                    int64_t W, int64_t Cout, int kh, int kw, int sh, int sw, int ph, int pw, int dh,
+                    int dw, int groups, int E, int Mw, const int32_t *bW, const int32_t *bR,
+                    const int32_t *table, uint32_t flags, const float *bn, int act, float act_lo,
+                    float act_hi, const float *in_maxval, int in_nbits, int in_mbits,
+                    int in_sign_bits, float *in_bias_out, int32_t *in_ibias_out, void *workspace,
+                    size_t workspace_bytes, fp8a_stream_t stream);
+
+/*
  * quantize_after_mult_and_add (qamaa) path of approx_multiply (approx_calculation.py:787-795):
  *   C = fq(sum_k fq(A[m,k] * B(k,n))),  fq = quantize_to_fp8_ste_MM with the res quantizer's
  *   n_bits / mantissa bits / sign bits and per-tensor maxval (device float [1]).

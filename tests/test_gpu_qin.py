@@ -1,0 +1,103 @@
+"""Fused input quantization (fp8a_conv2d_qin; hijacker.py `_fused_input_quantizer`).
+
+In the fixed-range approx forward the layer's input fake-quant (quantize_to_fp8_ste_MM,
+fp8_quantizer.py:97-173) runs inside the approx op: inside the operand pre-decode of the E4M3
+matrix-core and tensor-bias table kernels, or as one fake-quant pass into the workspace for every
+other path.  Checked here, bit for bit, against the unfused sequence (fp8a_fp8_quantize, then the
+plain convolution): outputs, the quantizer's float / int32 bias, every path (E4M3 GEMM and
+depthwise, E3M4 GEMM and depthwise, with and without the BN epilogue); and at model level,
+logits with the fusion on and off.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as orc
+from tests import golden_io as gio
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device")
+    from fp8_quantization_amd import _lib
+    _lib.load()
+
+
+@pytest.mark.parametrize("fmt", [(4, 3, "E4M3", "nocomp"), (3, 4, "E3M4", "comp3")])
+@pytest.mark.parametrize("layer", ["gemm", "depthwise", "depthwise_s2", "conv1x1"])
+@pytest.mark.parametrize("bn", [False, True])
+def test_fused_equals_quantize_then_conv(fmt, layer, bn):
+    from fp8_quantization_amd.approx_ops import approx_conv2d, bn_act_epilogue, fp8_fake_quantize
+    E, M, fname, tname = fmt
+    rng = np.random.default_rng(E * 1000 + sum(map(ord, layer)) * 2 + int(bn))
+    C = 24
+    if layer == "gemm":
+        x = rng.standard_normal((2, C, 13, 13)).astype(np.float32)
+        w_shape, groups, stride, pad = (40, C, 3, 3), 1, 1, 1
+    elif layer == "conv1x1":
+        x = rng.standard_normal((2, C, 9, 9)).astype(np.float32)
+        w_shape, groups, stride, pad = (32, C, 1, 1), 1, 2, 0
+    else:
+        x = rng.standard_normal((2, C, 15, 15)).astype(np.float32)
+        w_shape, groups, stride, pad = (C, 1, 3, 3), C, (2 if layer.endswith("s2") else 1), 1
+    x = np.maximum(x, 0) * 0.7
+    xt = torch.from_numpy(x).to(DEV)
+    maxval = torch.tensor([float(x.max()) * 0.9], device=DEV)  # some values clip
+    # per-channel quantized weights, as the weight quantizer gives them
+    wf = torch.from_numpy((rng.standard_normal(w_shape) * 0.1).astype(np.float32)).to(DEV)
+    wmax = wf.abs().reshape(w_shape[0], -1).amax(1)
+    wq, wb = fp8_fake_quantize(wf, wmax, 8, M, per_row=True)
+    bR = torch.tensor([2 ** (E - 1) + 6], dtype=torch.int32, device=DEV)
+    tab = gio.load("g2_matmul.npz")[f"{fname}_table_{tname}"]
+    fl = orc.flags_of(approx=True, s2n=True, qbma=True)
+    ep = None
+    if bn:
+        cout = w_shape[0]
+        g = torch.Generator().manual_seed(1)
+        ep = bn_act_epilogue(torch.randn(cout, generator=g).to(DEV) * 0.1, torch.rand(cout, generator=g).to(DEV) + 0.5,
+                             torch.randn(cout, generator=g).to(DEV), torch.randn(cout, generator=g).to(DEV) * 0.1,
+                             1e-5, torch.nn.ReLU())
+    args = dict(flags=fl, stride=(stride, stride), padding=(pad, pad), groups=groups, epilogue=ep)
+    xq, xb = fp8_fake_quantize(xt, maxval, 8, M)
+    y_ref = approx_conv2d(xq, wq, E, M, xb, wb, bR, torch.as_tensor(tab), **args)
+    y, b = approx_conv2d(xt, wq, E, M, None, wb, bR, torch.as_tensor(tab), qin=(maxval, 8, M, 1), **args)
+    torch.cuda.synchronize()
+    assert torch.equal(b, xb), "quantizer bias differs"
+    assert torch.equal(b._fp8a_i32, xb._fp8a_i32), "int32 quantizer bias differs"
+    assert torch.equal(y.view(torch.int32), y_ref.view(torch.int32)), f"{layer} {fname}: fused result differs"
+
+
+@pytest.mark.parametrize("arch", ["resnet18", "mobilenet_v2"])
+def test_model_logits_identical_with_and_without_fusion(arch):
+    from fp8_quantization_amd.mobilenet_workload import mobilenet_v2_approx
+    from fp8_quantization_amd.quantization.hijacker import QuantizationHijacker
+    from fp8_quantization_amd.resnet_workload import resnet18_approx
+    torch.manual_seed(0)
+    if arch == "resnet18":
+        model = resnet18_approx(bn_stats_batches=1, device=DEV)
+        shape = (3, 64, 64)
+    else:
+        model = mobilenet_v2_approx(input_size=64, bn_stats_batches=1, device=DEV)
+        shape = (3, 64, 64)
+    model = model.to(DEV).eval()
+    g = torch.Generator().manual_seed(3)
+    cal = torch.randn((4,) + shape, generator=g).to(DEV)
+    x = torch.randn((6,) + shape, generator=g).to(DEV)
+    with torch.no_grad():
+        model.quantized()
+        model.estimate_ranges()
+        model(cal)
+        model.fix_ranges()
+        try:
+            QuantizationHijacker.fuse_input_quant = False
+            ref = model(x)
+            QuantizationHijacker.fuse_input_quant = True
+            got = model(x)
+        finally:
+            QuantizationHijacker.fuse_input_quant = True
+    torch.cuda.synchronize()
+    assert torch.equal(got.view(torch.int32), ref.view(torch.int32)), "logits differ with the fusion on"
