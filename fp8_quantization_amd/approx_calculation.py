@@ -94,9 +94,11 @@ class ApproxConv2dMixin(ApproxOpMixin):
     supports_bn_act_epilogue = True
     supports_input_quant_fusion = True
 
-    def run_forward(self, x, weight, bias, offsets=None, epilogue=None, qin=None):
+    def run_forward(self, x, weight, bias, offsets=None, epilogue=None, qin=None, post=None):
         """qin: the layer's input FPQuantizer when the hijacker fused it (x unquantized; the op
-        applies it and its custom_bias is set as its own forward would)."""
+        applies it and its custom_bias is set as its own forward would).  post: ``(residual,
+        clamp, lo, hi, output FPQuantizer or None)`` of a residual block's tail (quantized_folded_bn
+        .BNFusedHijacker.forward); the output quantizer's custom_bias is set likewise."""
         x = x.contiguous()
         weight = weight.contiguous()
         if epilogue is not None and (bias is not None or not self.approx_flag):
@@ -112,10 +114,20 @@ class ApproxConv2dMixin(ApproxOpMixin):
                 raise TypeError("'NoneType' object is not subscriptable")
             args = dict(flags=flags, stride=self.stride, padding=self.padding, dilation=self.dilation,
                         groups=self.groups, epilogue=epilogue)
-            if qin is not None:
-                out, qin.custom_bias = approx_conv2d(
-                    x.detach(), weight.detach(), E, M, None, w_bias, self._default_bias(r_bias, E, x.device), table,
-                    qin=(qin.maxval, qin.n_bits, qin._mbits_int, qin.sign_bits), **args)
+            if qin is not None or post is not None:
+                qt = lambda q: (q.maxval, q.n_bits, q._mbits_int, q.sign_bits)  # noqa: E731
+                pq = None
+                if post is not None:
+                    pq = post[4]
+                    args["post"] = tuple(post[:4]) + ((qt(pq) if pq is not None else None),)
+                a_b = None if qin is not None else self._default_bias(a_bias, E, x.device)
+                out, ib, ob = approx_conv2d(x.detach(), weight.detach(), E, M, a_b, w_bias,
+                                            self._default_bias(r_bias, E, x.device), table,
+                                            qin=qt(qin) if qin is not None else None, **args)
+                if qin is not None:
+                    qin.custom_bias = ib
+                if pq is not None:
+                    pq.custom_bias = ob
             else:
                 out = approx_conv2d(x.detach(), weight.detach(), E, M, self._default_bias(a_bias, E, x.device),
                                     w_bias, self._default_bias(r_bias, E, x.device), table, **args)

@@ -285,12 +285,17 @@ def _(x, w, bA, bW, bR, table, E, M, flags, stride, padding, dilation, groups, b
     return x.new_empty((Bn, Cout, Ho, Wo))
 
 
-@torch.library.custom_op("fp8approx::conv2d_qin", mutates_args=())
-def _conv2d_qin_op(x: torch.Tensor, w: torch.Tensor, maxval: torch.Tensor, bW: torch.Tensor, bR: torch.Tensor,
-                   table: torch.Tensor, E: int, M: int, flags: int, stride: list[int], padding: list[int],
-                   dilation: list[int], groups: int, n_bits: int, mbits: int, sign_bits: int,
-                   bn: Optional[torch.Tensor] = None, act: int = 0, act_lo: float = 0.0,
-                   act_hi: float = 0.0) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+@torch.library.custom_op("fp8approx::conv2d_block", mutates_args=())
+def _conv2d_block_op(x: torch.Tensor, w: torch.Tensor, bA: Optional[torch.Tensor], bW: torch.Tensor,
+                     bR: torch.Tensor, table: torch.Tensor, E: int, M: int, flags: int, stride: list[int],
+                     padding: list[int], dilation: list[int], groups: int, in_maxval: Optional[torch.Tensor],
+                     in_nbits: int, in_mbits: int, in_sign_bits: int, res: Optional[torch.Tensor], post_act: int,
+                     post_lo: float, post_hi: float, out_maxval: Optional[torch.Tensor], out_nbits: int,
+                     out_mbits: int, out_sign_bits: int, bn: Optional[torch.Tensor] = None, act: int = 0,
+                     act_lo: float = 0.0, act_hi: float = 0.0
+                     ) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
+    """fp8a_conv2d_block: y = fq_out(clamp(bn_act(conv(fq_in(x))) + res)); returns y and the input /
+    output quantizers' float and int32 biases (1-element tensors, unset when unused)."""
     L = _lib.load()
     x = x.contiguous()
     w = w.contiguous()
@@ -302,33 +307,52 @@ def _conv2d_qin_op(x: torch.Tensor, w: torch.Tensor, maxval: torch.Tensor, bW: t
     Ho = (H + 2 * ph - dh * (kh - 1) - 1) // sh + 1
     Wo = (W + 2 * pw - dw * (kw - 1) - 1) // sw + 1
     y = torch.empty((Bn, Cout, Ho, Wo), dtype=torch.float32, device=x.device)
-    bias = torch.empty(1, dtype=torch.float32, device=x.device)
-    ibias = torch.empty(1, dtype=torch.int32, device=x.device)
-    ws = _workspace(x.device, L.fp8a_conv2d_qin_workspace_size(Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw,
-                                                               groups))
+    ib, iib = torch.empty(1, device=x.device), torch.empty(1, dtype=torch.int32, device=x.device)
+    ob, oib = torch.empty(1, device=x.device), torch.empty(1, dtype=torch.int32, device=x.device)
+    if res is not None:
+        res = res.contiguous()
+        if res.shape != y.shape or res.dtype != torch.float32 or res.device != x.device:
+            raise AssertionError(f"approx_conv2d: residual must be float32 {tuple(y.shape)} on {x.device}")
     if bn is not None and (bn.shape != (Cout, 2) or bn.dtype != torch.float32 or not bn.is_contiguous()):
         raise AssertionError(f"approx_conv2d: epilogue parameters must be contiguous float32 [{Cout}, 2]")
-    rc = L.fp8a_conv2d_qin(_lib.dev_ptr(x), _lib.dev_ptr(w), _lib.dev_ptr(y), Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph,
-                           pw, dh, dw, groups, E, M, _lib.dev_ptr(bW), _lib.dev_ptr(bR), _lib.host_ptr(table), flags,
-                           _lib.dev_ptr(bn) if bn is not None else None, int(act), float(act_lo), float(act_hi),
-                           _lib.dev_ptr(maxval), int(n_bits), int(mbits), int(sign_bits), _lib.dev_ptr(bias),
-                           _lib.dev_ptr(ibias), _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(x.device))
-    _lib.check(rc, "fp8a_conv2d_qin")
-    return y, bias, ibias
+    ws = _workspace(x.device, L.fp8a_conv2d_block_workspace_size(Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh,
+                                                                 dw, groups))
+    opt = lambda t: _lib.dev_ptr(t) if t is not None else None  # noqa: E731
+    rc = L.fp8a_conv2d_block(_lib.dev_ptr(x), _lib.dev_ptr(w), _lib.dev_ptr(y), Bn, Cin, H, W, Cout, kh, kw, sh, sw,
+                             ph, pw, dh, dw, groups, E, M, opt(bA), _lib.dev_ptr(bW), _lib.dev_ptr(bR),
+                             _lib.host_ptr(table), flags, opt(bn), int(act), float(act_lo), float(act_hi),
+                             opt(in_maxval), int(in_nbits), int(in_mbits), int(in_sign_bits), _lib.dev_ptr(ib),
+                             _lib.dev_ptr(iib), opt(res), int(post_act), float(post_lo), float(post_hi),
+                             opt(out_maxval), int(out_nbits), int(out_mbits), int(out_sign_bits), _lib.dev_ptr(ob),
+                             _lib.dev_ptr(oib), _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(x.device))
+    _lib.check(rc, "fp8a_conv2d_block")
+    return y, ib, iib, ob, oib
 
 
-@_conv2d_qin_op.register_fake
-def _(x, w, maxval, bW, bR, table, E, M, flags, stride, padding, dilation, groups, n_bits, mbits, sign_bits, bn=None,
-      act=0, act_lo=0.0, act_hi=0.0):
+@_conv2d_block_op.register_fake
+def _(x, w, bA, bW, bR, table, E, M, flags, stride, padding, dilation, groups, in_maxval, in_nbits, in_mbits,
+      in_sign_bits, res, post_act, post_lo, post_hi, out_maxval, out_nbits, out_mbits, out_sign_bits, bn=None, act=0,
+      act_lo=0.0, act_hi=0.0):
     Bn, _, H, W = x.shape
     Cout, _, kh, kw = w.shape
     Ho = (H + 2 * padding[0] - dilation[0] * (kh - 1) - 1) // stride[0] + 1
     Wo = (W + 2 * padding[1] - dilation[1] * (kw - 1) - 1) // stride[1] + 1
-    return x.new_empty((Bn, Cout, Ho, Wo)), x.new_empty((1,)), x.new_empty((1,), dtype=torch.int32)
+    one = x.new_empty((1,))
+    onei = x.new_empty((1,), dtype=torch.int32)
+    return x.new_empty((Bn, Cout, Ho, Wo)), one, onei, one.clone(), onei.clone()
+
+
+def _quantizer_args(q):
+    """(maxval [1] device tensor, n_bits, mantissa bits, sign bits) of a per-tensor quantizer tuple."""
+    mx, nb, mb, sb = q
+    mx = _as_f32(mx).reshape(-1).contiguous()
+    if mx.numel() != 1:
+        raise AssertionError("approx_conv2d: fused quantizers must be per tensor")
+    return mx, int(nb), int(mb), int(sb)
 
 
 def approx_conv2d(x, w, E, M, bA, bW, bR, table=None, flags=None, stride=(1, 1), padding=(0, 0), dilation=(1, 1),
-                  groups=1, epilogue=None, qin=None, **flag_kwargs):
+                  groups=1, epilogue=None, qin=None, post=None, **flag_kwargs):
     """approx_v9 convolution, NCHW in / NCHW out (pre-BN), K ordered (c, ky, kx) like the
     reference im2col (approx_calculation.py:724-747); single-output-channel groups get the
     tensor-bias semantics (approx_calculation.py:800-809).  bW: per output channel.
@@ -340,7 +364,14 @@ def approx_conv2d(x, w, E, M, bA, bW, bR, table=None, flags=None, stride=(1, 1),
     qin: optional ``(maxval [1] device tensor, n_bits, mantissa_bits, sign_bits)`` of the layer's
     per-tensor input activation quantizer: x is then UNQUANTIZED, the op applies
     quantize_to_fp8_ste_MM itself (fp8a_conv2d_qin: inside the E4M3 operand pre-decode where that
-    path runs) and returns ``(y, float bias [1])`` -- the quantizer's custom_bias (bA is unused)."""
+    path runs); bA is unused.
+
+    post: optional ``(residual tensor or None, clamp (0/1), lo, hi, output quantizer tuple or
+    None)``: a residual block's tail in the store, y = fq_out(clamp(y + residual))
+    (fp8a_conv2d_block).
+
+    With qin or post the result is ``(y, input quantizer bias or None, output quantizer bias or
+    None)`` -- the float biases the quantizers would have set as their custom_bias."""
     if flags is None:
         flags = make_flags(**flag_kwargs)
     flags &= ~_lib.TB
@@ -352,18 +383,20 @@ def approx_conv2d(x, w, E, M, bA, bW, bR, table=None, flags=None, stride=(1, 1),
     if bW_.numel() != w.shape[0]:
         raise AssertionError(f"approx_conv2d: {bW_.numel()} weight biases for {w.shape[0]} output channels")
     ev = _prof_start()
-    if qin is not None:
-        mx, nb, mb, sb = qin
-        mx = _as_f32(mx).reshape(-1).contiguous()
-        if mx.numel() != 1:
-            raise AssertionError("approx_conv2d: the fused input quantizer must be per tensor")
-        y, bias, ibias = _conv2d_qin_op(_as_f32(x), _as_f32(w), mx.to(dev), bW_, _bias_dev(bR, dev), tab, int(E),
-                                        int(M), int(flags), [int(s) for s in stride], [int(p) for p in padding],
-                                        [int(d) for d in dilation], int(groups), int(nb), int(mb), int(sb),
-                                        *(epilogue or ()))
-        bias._fp8a_i32 = ibias
+    if qin is not None or post is not None:
+        iq = _quantizer_args(qin) if qin is not None else (None, 0, 0, 0)
+        res, pact, plo, phi, oq = post if post is not None else (None, 0, 0.0, 0.0, None)
+        oq = _quantizer_args(oq) if oq is not None else (None, 0, 0, 0)
+        y, ib, iib, ob, oib = _conv2d_block_op(
+            _as_f32(x), _as_f32(w), None if qin is not None else _bias_dev(bA, dev), bW_, _bias_dev(bR, dev), tab,
+            int(E), int(M), int(flags), [int(s) for s in stride], [int(p) for p in padding],
+            [int(d) for d in dilation], int(groups), iq[0].to(dev) if iq[0] is not None else None, iq[1], iq[2],
+            iq[3], res, int(pact), float(plo), float(phi), oq[0].to(dev) if oq[0] is not None else None, oq[1],
+            oq[2], oq[3], *(epilogue or ()))
+        ib._fp8a_i32 = iib
+        ob._fp8a_i32 = oib
         _prof_end(ev, y.shape[0] * y.shape[2] * y.shape[3] * w.shape[0] * w.shape[1] * w.shape[2] * w.shape[3])
-        return y, bias
+        return y, (ib if qin is not None else None), (ob if oq[0] is not None else None)
     y = _conv2d_op(_as_f32(x), _as_f32(w), _bias_dev(bA, dev), bW_, _bias_dev(bR, dev), tab,
                    int(E), int(M), int(flags), [int(s) for s in stride], [int(p) for p in padding],
                    [int(d) for d in dilation], int(groups), *(epilogue or ()))

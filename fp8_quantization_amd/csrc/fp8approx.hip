@@ -165,8 +165,39 @@ struct GemmArgs {
     FqIn fqin;
     float *fq_bias;
     int32_t *fq_ibias;
+    // block-output epilogue (fp8a_conv2d_block): after BN / activation, y += res (same index as
+    // y), then the post clamp (post_act), then the block's output quantizer (post_fq)
+    const float *res;
+    int post_act;
+    float post_lo, post_hi;
+    FqIn post_fq;
     TablePack tab;
 };
+
+// The block-output epilogue on one value / four values of the output at index o; pb = the post
+// quantizer's bias (post_bias()).
+__device__ __forceinline__ float post_bias(const GemmArgs &p) {
+    return p.post_fq.mx ? fq_bias(*p.post_fq.mx, p.post_fq.E, p.post_fq.M) : 0.0f;
+}
+
+__device__ __forceinline__ float post_tail(const GemmArgs &p, float v, float pb) {
+    if (p.post_act) v = fminf(fmaxf(v, p.post_lo), p.post_hi);
+    if (p.post_fq.mx) v = fq_apply(v, *p.post_fq.mx, pb, p.post_fq.M, p.post_fq.S);
+    return v;
+}
+
+__device__ __forceinline__ float post1(const GemmArgs &p, int64_t o, float v, float pb) {
+    if (p.res) v += p.res[o];
+    return post_tail(p, v, pb);
+}
+
+__device__ __forceinline__ float4 post4(const GemmArgs &p, int64_t o, float4 v, float pb) {
+    if (p.res) {
+        const float4 r = *reinterpret_cast<const float4 *>(p.res + o);
+        v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+    }
+    return make_float4(post_tail(p, v.x, pb), post_tail(p, v.y, pb), post_tail(p, v.z, pb), post_tail(p, v.w, pb));
+}
 
 // y = x * scale + shift with scale = gamma * invstd, shift = beta - mean * scale (ATen's eval
 // batch-norm transform), then the activation clamp; c = output channel
@@ -238,17 +269,22 @@ __device__ __forceinline__ void store_tile(const GemmArgs &p, int64_t split, int
             for (int i = 0; i < TM; ++i) acc[i][j] = epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, ch, acc[i][j]);
         }
     }
+    const float pb = partial ? 0.0f : post_bias(p);
+    const GemmArgs &q = p;
+    auto fin1 = [&](int64_t o, float v) { return partial ? v : post1(q, o, v, pb); };
+    auto fin4 = [&](int64_t o, float4 v) { return partial ? v : post4(q, o, v, pb); };
     if (!p.nchw) {
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
             const int64_t m = m0 + ty * TM + i;
             if (m >= p.M) continue;
             if (nb + TN <= p.N && ((ldc & 3) == 0) && ((((uintptr_t)C) & 15) == 0)) {
-                *reinterpret_cast<float4 *>(&C[m * ldc + nb]) = make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+                *reinterpret_cast<float4 *>(&C[m * ldc + nb]) =
+                    fin4(m * ldc + nb, make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]));
             } else {
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
-                    if (nb + j < p.N) C[m * ldc + nb + j] = acc[i][j];
+                    if (nb + j < p.N) C[m * ldc + nb + j] = fin1(m * ldc + nb + j, acc[i][j]);
             }
         }
     } else {
@@ -261,9 +297,10 @@ __device__ __forceinline__ void store_tile(const GemmArgs &p, int64_t split, int
         if (vec) {
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-                if (nb + j < p.N)
-                    *reinterpret_cast<float4 *>(&C[(img * ctot + coff + nb + j) * p.hw + pix]) =
-                        make_float4(acc[0][j], acc[1][j], acc[2][j], acc[3][j]);
+                if (nb + j < p.N) {
+                    const int64_t o = (img * ctot + coff + nb + j) * p.hw + pix;
+                    *reinterpret_cast<float4 *>(&C[o]) = fin4(o, make_float4(acc[0][j], acc[1][j], acc[2][j], acc[3][j]));
+                }
         } else {
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
@@ -272,7 +309,10 @@ __device__ __forceinline__ void store_tile(const GemmArgs &p, int64_t split, int
                 const int64_t im = m / p.hw, px = m - im * p.hw;
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
-                    if (nb + j < p.N) C[(im * ctot + coff + nb + j) * p.hw + px] = acc[i][j];
+                    if (nb + j < p.N) {
+                        const int64_t o = (im * ctot + coff + nb + j) * p.hw + px;
+                        C[o] = fin1(o, acc[i][j]);
+                    }
             }
         }
     }
@@ -650,9 +690,11 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
 // Partial layout: row-major [M][N] (rowmajor output) or [img][N][hw] (NCHW output).
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs p) {
     const int64_t MN = p.M * p.N;
+    const float pb = post_bias(p);
     const int S = p.splits;
     const bool vec = p.nchw ? ((p.hw & 3) == 0) : ((p.N & 3) == 0 && (p.ldc & 3) == 0);
-    const bool aligned = ((((uintptr_t)p.C) & 15) == 0) && ((((uintptr_t)p.part) & 15) == 0) && ((MN & 3) == 0);
+    const bool aligned = ((((uintptr_t)p.C) & 15) == 0) && ((((uintptr_t)p.part) & 15) == 0) && ((MN & 3) == 0) &&
+                         ((((uintptr_t)p.res) & 15) == 0);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     if (vec && aligned) {
         for (int64_t q4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q4 < MN / 4; q4 += stride) {
@@ -683,7 +725,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs p) {
                     acc.w = epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, p.coff + n + 3, acc.w);
                 }
             }
-            *reinterpret_cast<float4 *>(p.C + o) = acc;
+            *reinterpret_cast<float4 *>(p.C + o) = post4(p, o, acc, pb);
         }
         return;
     }
@@ -700,7 +742,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs p) {
             o = m * p.ldc + n;
             ch = p.coff + n;
         }
-        p.C[o] = epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, ch, acc);
+        p.C[o] = post1(p, o, epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, ch, acc), pb);
     }
 }
 
@@ -737,7 +779,8 @@ __global__ __launch_bounds__(256) void gemm_exact_kernel(const GemmArgs p) {
             }
         }
         s += part;
-        p.C[out_index(p, m, n)] = epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, p.coff + n, s);
+        const int64_t o = out_index(p, m, n);
+        p.C[o] = post1(p, o, epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, p.coff + n, s), post_bias(p));
     }
 }
 
@@ -1296,7 +1339,9 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
                        int64_t Cout, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw, int groups,
                        int E, int Mw, const int32_t *bA, const int32_t *bW, const int32_t *bR, const int32_t *table,
                        uint32_t flags, const float *bn, int act, float act_lo, float act_hi, void *workspace,
-                       size_t workspace_bytes, hipStream_t s, FqIn fq, float *fqb, int32_t *fqi, float *xq) {
+                       size_t workspace_bytes, hipStream_t s, FqIn fq, float *fqb, int32_t *fqi, float *xq,
+                       const float *res = nullptr, int post_act = 0, float post_lo = 0.0f, float post_hi = 0.0f,
+                       FqIn post_fq = FqIn{}) {
     const float2 *ep = reinterpret_cast<const float2 *>(bn);
     if (ep && (((uintptr_t)bn) & 7) != 0) return fail(FP8A_EINVAL, "bn parameters must be 8-byte aligned");
     int rc = check_format(E, Mw);
@@ -1318,7 +1363,11 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
         fq.mx = nullptr;
         return hip_check("fp8a input fake-quant");
     };
+    const bool post = res || post_act || post_fq.mx;
+    if (res && (res == y || (((uintptr_t)res) & 15) != 0))
+        return fail(FP8A_EINVAL, "the residual must be a 16-byte aligned tensor other than the output");
     if (cog == 1 && !(flags & F_V5)) {  // v5 never had tensor-bias semantics: it takes the GEMM path
+        if (post) return fail(FP8A_EINVAL, "no block-output epilogue for single-output-channel groups");
         TablePack tp;
         int mode;
         rc = pack_table(table, Mw, flags & F_APPROX, tp, mode);
@@ -1417,6 +1466,7 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
             a.fq_ibias = fqi;
             a.bA = fqi;  // written by the A pre-decode before any kernel reads it
         }
+        a.res = res; a.post_act = post_act; a.post_lo = post_lo; a.post_hi = post_hi; a.post_fq = post_fq;
         rc = run_gemm(a, table, workspace, workspace_bytes, s);
         if (rc) return rc;
     }
@@ -1457,6 +1507,55 @@ int fp8a_conv2d_qin(const float *x, const float *w, float *y, int64_t Bn, int64_
     return conv2d_impl(x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups, E, Mw, nullptr, bW, bR,
                        table, flags, bn, act, act_lo, act_hi, workspace, rest, (hipStream_t)stream,
                        FqIn{in_maxval, qE, in_mbits, in_sign_bits}, in_bias_out, in_ibias_out, xq);
+}
+
+// The output quantizer's bias (quantize_to_fp8_ste_MM's custom_bias) from its maxval.
+__global__ void fq_bias_kernel(FqIn fq, float *bias_out, int32_t *ibias_out) {
+    const float b = fq_bias(*fq.mx, fq.E, fq.M);
+    *bias_out = b;
+    *ibias_out = (int32_t)b;
+}
+
+size_t fp8a_conv2d_block_workspace_size(int64_t Bn, int64_t Cin, int64_t H, int64_t W, int64_t Cout, int kh,
+                                        int kw, int sh, int sw, int ph, int pw, int dh, int dw, int groups) {
+    return fp8a_conv2d_qin_workspace_size(Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups);
+}
+
+int fp8a_conv2d_block(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
+                      int64_t Cout, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw, int groups, int E,
+                      int Mw, const int32_t *bA, const int32_t *bW, const int32_t *bR, const int32_t *table,
+                      uint32_t flags, const float *bn, int act, float act_lo, float act_hi, const float *in_maxval,
+                      int in_nbits, int in_mbits, int in_sign_bits, float *in_bias_out, int32_t *in_ibias_out,
+                      const float *res, int post_act, float post_lo, float post_hi, const float *out_maxval,
+                      int out_nbits, int out_mbits, int out_sign_bits, float *out_bias_out, int32_t *out_ibias_out,
+                      void *workspace, size_t workspace_bytes, fp8a_stream_t stream) {
+    hipStream_t s = (hipStream_t)stream;
+    FqIn fin{}, fout{};
+    if (in_maxval) {
+        const int qE = in_nbits - in_sign_bits - in_mbits;
+        if (in_mbits < 1 || qE < 1) return fail(FP8A_EFORMAT, "bad FP8 quantizer format");
+        if (!in_bias_out || !in_ibias_out) return fail(FP8A_EINVAL, "null pointer");
+        fin = FqIn{in_maxval, qE, in_mbits, in_sign_bits};
+    } else if (!bA) {
+        return fail(FP8A_EINVAL, "null pointer");
+    }
+    if (out_maxval) {
+        const int qE = out_nbits - out_sign_bits - out_mbits;
+        if (out_mbits < 1 || qE < 1) return fail(FP8A_EFORMAT, "bad FP8 quantizer format");
+        if (!out_bias_out || !out_ibias_out) return fail(FP8A_EINVAL, "null pointer");
+        fout = FqIn{out_maxval, qE, out_mbits, out_sign_bits};
+        fq_bias_kernel<<<1, 1, 0, s>>>(fout, out_bias_out, out_ibias_out);
+        int rc = hip_check("fp8a output-quantizer bias");
+        if (rc) return rc;
+    }
+    const size_t xq_bytes = fin.mx ? align256((size_t)(Bn * Cin * H * W) * sizeof(float)) : 0;
+    if (workspace == nullptr || workspace_bytes < FLAG_BYTES + xq_bytes)
+        return fail(FP8A_EINVAL, "conv2d_block workspace too small");
+    const size_t rest = (workspace_bytes - xq_bytes) & ~(size_t)255;
+    float *xq = fin.mx ? (float *)((char *)workspace + rest) : nullptr;
+    return conv2d_impl(x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups, E, Mw,
+                       fin.mx ? nullptr : bA, bW, bR, table, flags, bn, act, act_lo, act_hi, workspace, rest, s, fin,
+                       in_bias_out, in_ibias_out, xq, res, post_act, post_lo, post_hi, fout);
 }
 
 int fp8a_matmul_qamaa(const float *A, int64_t lda, const float *B, int64_t sbk, int64_t sbn, float *C, int64_t M,

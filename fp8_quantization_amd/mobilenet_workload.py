@@ -13,7 +13,7 @@ import math
 
 from torch import nn
 
-from .model_wrap import Flattener, QuantizedModel, quantize_model, quantize_sequential
+from .model_wrap import Flattener, QuantizedModel, fused_block_tail, quantize_model, quantize_sequential
 from .quantization.base_quantized_classes import FP32Acts, QuantizedActivation
 
 # t (expansion), c (channels), n (repeats), s (first stride) -- the MobileNetV2 table
@@ -90,6 +90,9 @@ class QuantizedInvertedResidual(QuantizedActivation):
 
     def forward(self, x):
         if self.use_res_connect:
+            fused = fused_block_tail(self, self.conv, x, lambda t: t, None)
+            if fused is not None:
+                return fused
             return self.quantize_activations(x + self.conv(x))
         return self.conv(x)
 

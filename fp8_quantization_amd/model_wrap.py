@@ -13,6 +13,7 @@ QCustomConv2dTorch (exact product, as in the reference), Linear -> QCustomLinear
 reference's non-approx quantized layers (Conv1d, ConvTranspose, LayerNorm, Linear + BN) are
 outside the hot path and raise NotImplementedError here.
 """
+import os
 import copy
 import warnings
 
@@ -244,3 +245,35 @@ def quantize_model(model, specials=None, tie_activation_quantizers=False, **quan
             if new is not None:
                 setattr(q, name, new)
     return q
+
+
+# ----------------------------------------------------------------------------------- block tails
+FUSE_BLOCK = os.environ.get("FP8A_FUSE_BLOCK", "1") != "0"
+
+
+def fused_block_tail(block, features, x, residual_fn, clamp):
+    """A residual block's tail fused into its last conv's store (fp8a_conv2d_block):
+    quantize_activations(clamp(features(x) + residual)) as one launch for the last conv, when that
+    conv runs the fused BN store (BNFusedHijacker.block_epilogue_ok) and the block's activation
+    quantizer is a per-tensor FPQuantizer in the fixed-range state (or off).  Returns None when the
+    block must run unfused.  residual_fn(x) gives the residual (identity or downsample); clamp is
+    (lo, hi) or None.  Same result bit for bit as the reference's order (add, clamp, quantize)."""
+    from .quantization.fp8_quantizer import FPQuantizer
+    from .quantization.quantization_manager import Qstates
+    from .quantization.quantized_folded_bn import BNFusedHijacker
+    if not FUSE_BLOCK or len(features) == 0:
+        return None
+    last = features[-1]
+    if not isinstance(last, BNFusedHijacker) or not last.block_epilogue_ok():
+        return None
+    q = None
+    if block._qa():
+        mgr = block.activation_quantizer
+        q = getattr(mgr, "quantizer", None)
+        if getattr(mgr, "state", None) != Qstates.fix_ranges or not isinstance(q, FPQuantizer) \
+                or q.maxval.numel() != 1:
+            return None
+    residual = residual_fn(x)
+    h = features[:-1](x) if len(features) > 1 else x
+    lo, hi = clamp if clamp is not None else (0.0, 0.0)
+    return last(h, post=(residual, int(clamp is not None), lo, hi, q))

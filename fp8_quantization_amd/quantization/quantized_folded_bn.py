@@ -51,10 +51,21 @@ class BNFusedHijacker(QuantizationHijacker):
             self._bn_act_cache = cached
         return cached[1]
 
-    def forward(self, x):
+    def block_epilogue_ok(self):
+        """Whether forward(x, post=...) can fuse a residual block's tail: the fused BN / activation
+        store runs, the product is not a tensor-bias (single-output-channel) one, and nothing
+        follows the product inside this layer (no output quantizer of its own)."""
+        return (self._fused_epilogue() is not None and self.out_channels // self.groups != 1
+                and (self.quantize_input or not self._qa()))
+
+    def forward(self, x, post=None):
+        """post: ``(residual, clamp, lo, hi, output FPQuantizer or None)`` -- the caller's block
+        tail y = q(clamp(y + residual)) fused into the store (only when block_epilogue_ok())."""
         ep = self._fused_epilogue()
+        if post is not None and not self.block_epilogue_ok():
+            raise AssertionError("block epilogue requested where the fused store does not run")
         if ep is not None:
-            res, qa = self._core(x, epilogue=ep)
+            res, qa = self._core(x, epilogue=ep, post=post)
             return self._epilogue(res, qa, activation_done=True)
         res, qa = self._core(x)
         res = F.batch_norm(res, self.running_mean, self.running_var, self.gamma, self.beta, self.training,

@@ -14,7 +14,7 @@ import torch
 from torch import nn
 
 from .approx_calculation import QCustomBNConv2dTorch, QCustomLinearTorch
-from .model_wrap import Flattener, QuantizedActivationWrapper, QuantizedModel, quantize_model
+from .model_wrap import Flattener, QuantizedActivationWrapper, QuantizedModel, fused_block_tail, quantize_model
 from .quantization import FPQuantizer, RangeEstimators
 from .quantization.base_quantized_classes import FP32Acts, QuantizedActivation
 
@@ -172,6 +172,10 @@ class QuantizedBlock(QuantizedActivation):
         self.relu = block.relu
 
     def forward(self, x):
+        fused = fused_block_tail(self, self.features, x,
+                                 lambda t: t if self.downsample is None else self.downsample(t), (0.0, float("inf")))
+        if fused is not None:
+            return fused
         residual = x if self.downsample is None else self.downsample(x)
         out = self.features(x)
         out += residual

@@ -155,6 +155,30 @@ int fp8a_conv2d_qin(const float *x, const float *w, float *y, int64_t Bn, int64_
                     size_t workspace_bytes, fp8a_stream_t stream);
 
 /*
+ * A residual block's last convolution with the block's tail fused into its store
+ * (resnet_quantized_approx.py:11-41 QuantizedBlock: out = relu(features(x) + residual), then the
+ * block's activation quantizer; mobilenet_v2_quantized_approx.py:11-23: quantize(x + conv(x))):
+ *   y = fq_out(clamp(bn_act(conv(fq_in(x))) + res, post_lo, post_hi))
+ * in_maxval NULL: x is already quantized and bA is used (else as fp8a_conv2d_qin).  res: NULL or
+ * a 16-byte aligned tensor of y's shape (not y itself).  post_act 0: no clamp.  out_maxval NULL:
+ * no output quantizer; else its bias is written to out_bias_out / out_ibias_out.  Not for
+ * single-output-channel groups (EINVAL).  workspace: fp8a_conv2d_block_workspace_size() bytes.
+ */
+size_t fp8a_conv2d_block_workspace_size(int64_t Bn, int64_t Cin, int64_t H, int64_t W, int64_t Cout,
+                                        int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw,
+                                        int groups);
+int fp8a_conv2d_block(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H,
+                      int64_t W, int64_t Cout, int kh, int kw, int sh, int sw, int ph, int pw, int dh,
+                      int dw, int groups, int E, int Mw, const int32_t *bA, const int32_t *bW,
+                      const int32_t *bR, const int32_t *table, uint32_t flags, const float *bn,
+                      int act, float act_lo, float act_hi, const float *in_maxval, int in_nbits,
+                      int in_mbits, int in_sign_bits, float *in_bias_out, int32_t *in_ibias_out,
+                      const float *res, int post_act, float post_lo, float post_hi,
+                      const float *out_maxval, int out_nbits, int out_mbits, int out_sign_bits,
+                      float *out_bias_out, int32_t *out_ibias_out, void *workspace,
+                      size_t workspace_bytes, fp8a_stream_t stream);
+
+/*
  * quantize_after_mult_and_add (qamaa) path of approx_multiply (approx_calculation.py:787-795):
  *   C = fq(sum_k fq(A[m,k] * B(k,n))),  fq = quantize_to_fp8_ste_MM with the res quantizer's
  *   n_bits / mantissa bits / sign bits and per-tensor maxval (device float [1]).
