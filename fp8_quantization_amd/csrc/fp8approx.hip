@@ -159,6 +159,7 @@ struct GemmArgs {
     const uint32_t *aw;
     int64_t awld, aw_c;
     const uint2 *bqw;
+    const uint32_t *lutw;  // the LDS table image (XM_LUT_WORDS words), written by xm_decode_b
     int64_t npad;
     // fused input quantization (fp8a_conv2d_qin): A = fq(X); the quantizer's bias is written to
     // fq_bias / fq_ibias by the A pre-decode, and bA points at fq_ibias
@@ -1095,7 +1096,7 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // (a_words of them) + B column pairs [Kpad][Npad / 2] of 8 bytes.
 static size_t xm_operand_bytes(int64_t N, int64_t K, int64_t a_words) {
     const int64_t kpad = (K + BK - 1) / BK * BK, npad = (N + BN - 1) / BN * BN;
-    return align256((size_t)a_words * 4) + align256((size_t)(kpad * npad / 2) * 8);
+    return align256((size_t)a_words * 4) + align256((size_t)(kpad * npad / 2) * 8) + 16384;  // + table image
 }
 
 static size_t splitk_bytes(int64_t M, int64_t N, int64_t K) {
@@ -1178,6 +1179,7 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
             a.aw = (const uint32_t *)base;
             a.awld = kpad;
             a.bqw = (const uint2 *)(base + align256((size_t)a_words * 4));
+            a.lutw = (const uint32_t *)(base + align256((size_t)a_words * 4) + align256((size_t)(kpad * npad / 2) * 8));
             a.npad = npad;
             const int64_t rows = a.conv ? a.M / (a.Ho * a.Wo) : a.M, cols = a_words / std::max<int64_t>(rows, 1);
             const dim3 ga((unsigned)std::min<int64_t>((cols + 255) / 256, 64), (unsigned)std::min<int64_t>(rows, 1024));

@@ -62,6 +62,26 @@ static_assert(sizeof(float) * BM * XM_CP <= sizeof(XmSmem), "epilogue tile must 
 // Exactness / range window shared by the pre-passes (as bias_ok in gemm_fast_kernel)
 __device__ __forceinline__ bool xm_bias_ok(int b) { return b >= -100 && b <= 120; }
 
+// Table word e of layout [pair][copy][row]: the bf16 pair V'(row, code0), V'(row, code1).
+__device__ __forceinline__ uint32_t xm_lut_word(const TablePack &tab, int e) {
+    const int pr = e >> 5, row = e & 15;
+    const int ma = row & 7;
+    uint32_t w = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int cd = h ? (pr / 9) : (pr % 9);
+        if (cd == 8) continue;  // zero B: +0
+        const float t = (float)tab.raw[ma * 8 + cd];
+        float v = __fmaf_rn(1.0f + 0.125f * ma, 1.0f + 0.125f * cd, -t * 0.125f);  // exact, <= 8 bits
+        // Q_R's pre-clamp in bf16: any bound in (1.8125, 1.875) x binade rounds like the
+        // reference's saturating mantissa (and the subnormal top tie rounding down)
+        v = fminf(v, __uint_as_float(__float_as_uint(v) & 0x7F800000u) * 1.8671875f);
+        if (row >= 8) v = -v;
+        w |= (__float_as_uint(v) >> 16) << (16 * h);
+    }
+    return w;
+}
+
 // A element -> word: bits 23-30 the cvt scale exponent se (scale 2^(se-127) = 2^(7-bR-e_a)),
 // bits 3-6 the table row (8 s_a + m_a); zeros XM_ZERO_WORD.  ok = on the (3, bA) grid, inside the
 // exactness window and the scale range.
@@ -117,6 +137,8 @@ __global__ __launch_bounds__(256) void xm_decode_b(const GemmArgs p, int64_t kpa
     bool bad = !(xm_bias_ok(bA) && xm_bias_ok(bR));
     const int64_t hq = p.npad / 2, n = kpad * hq;
     uint2 *const bq = const_cast<uint2 *>(p.bqw);
+    if (blockIdx.x == 0)  // the table image every GEMM workgroup copies into LDS
+        for (int e = threadIdx.x; e < XM_LUT_WORDS; e += blockDim.x) const_cast<uint32_t *>(p.lutw)[e] = xm_lut_word(p.tab, e);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const int64_t k = i / hq, q = i - k * hq;
@@ -168,25 +190,9 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
     const int64_t kbeg = split * p.kchunk, kend = min(p.K, kbeg + p.kchunk);
     const int bR = *p.bR;
 
-    // table: V'(s_a, m_a, m_b) for both columns of a pair, both copies
-    for (int e = tid; e < XM_LUT_WORDS; e += NT) {
-        const int pr = e >> 5, row = e & 15;
-        const int ma = row & 7;
-        uint32_t w = 0;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int cd = h ? (pr / 9) : (pr % 9);
-            if (cd == 8) continue;  // zero B: +0
-            const float t = (float)p.tab.raw[ma * 8 + cd];
-            float v = __fmaf_rn(1.0f + 0.125f * ma, 1.0f + 0.125f * cd, -t * 0.125f);  // exact, <= 8 bits
-            // Q_R's pre-clamp in bf16: any bound in (1.8125, 1.875) x binade rounds like the
-            // reference's saturating mantissa (and the subnormal top tie rounding down)
-            v = fminf(v, __uint_as_float(__float_as_uint(v) & 0x7F800000u) * 1.8671875f);
-            if (row >= 8) v = -v;
-            w |= (__float_as_uint(v) >> 16) << (16 * h);
-        }
-        sm.lut[e] = w;
-    }
+    // table: copied from the launch's pre-computed image (xm_decode_b), 16-B per thread and step
+    for (int e = 4 * tid; e < XM_LUT_WORDS; e += 4 * NT)
+        *reinterpret_cast<uint4 *>(&sm.lut[e]) = *reinterpret_cast<const uint4 *>(&p.lutw[e]);
 
     // B staging slots: pair q = e & 31 (lanes along n: coalesced), k row kk = e >> 5
     const int64_t hq = p.npad / 2;
