@@ -503,3 +503,52 @@ def qamaa_conv2d(x, w, maxval, n_bits, mantissa_bits, sign_bits=1, stride=(1, 1)
                              _lib.stream_ptr(x.device))
     _lib.check(rc, "fp8a_conv2d_qamaa")
     return y
+
+
+# ----------------------------------------------------------------------------------- max pool
+@torch.library.custom_op("fp8approx::max_pool2d", mutates_args=())
+def _max_pool2d_op(x: torch.Tensor, kernel: list[int], stride: list[int], padding: list[int]) -> torch.Tensor:
+    L = _lib.load()
+    x = x.contiguous()
+    Bn, C, H, W = x.shape
+    Ho = (H + 2 * padding[0] - kernel[0]) // stride[0] + 1
+    Wo = (W + 2 * padding[1] - kernel[1]) // stride[1] + 1
+    y = torch.empty((Bn, C, Ho, Wo), dtype=x.dtype, device=x.device)
+    rc = L.fp8a_max_pool2d(_lib.dev_ptr(x), _lib.dev_ptr(y), Bn, C, H, W, kernel[0], kernel[1], stride[0], stride[1],
+                           padding[0], padding[1], _lib.stream_ptr(x.device))
+    _lib.check(rc, "fp8a_max_pool2d")
+    return y
+
+
+@_max_pool2d_op.register_fake
+def _(x, kernel, stride, padding):
+    Bn, C, H, W = x.shape
+    return x.new_empty((Bn, C, (H + 2 * padding[0] - kernel[0]) // stride[0] + 1,
+                        (W + 2 * padding[1] - kernel[1]) // stride[1] + 1))
+
+
+class MaxPool2d(nn.Module):
+    """nn.MaxPool2d (dilation 1, floor mode) on the HIP kernel fp8a_max_pool2d; same values
+    (max is exact, NaN propagates).  ``from_module`` keeps other configurations on torch."""
+
+    def __init__(self, kernel_size, stride, padding):
+        super().__init__()
+        pair = lambda v: [int(v), int(v)] if isinstance(v, int) else [int(t) for t in v]  # noqa: E731
+        self.kernel_size, self.stride, self.padding = pair(kernel_size), pair(stride), pair(padding)
+
+    @staticmethod
+    def from_module(m):
+        if (type(m) is nn.MaxPool2d and m.dilation in (1, (1, 1)) and not m.ceil_mode and not m.return_indices
+                and m.stride is not None):
+            mp = MaxPool2d(m.kernel_size, m.stride, m.padding)
+            if all(2 * p <= k for p, k in zip(mp.padding, mp.kernel_size)):
+                return mp
+        return m
+
+    def forward(self, x):
+        if x.dtype != torch.float32 or x.dim() != 4 or not x.is_cuda:
+            return nn.functional.max_pool2d(x, self.kernel_size, self.stride, self.padding)
+        return _max_pool2d_op(x, self.kernel_size, self.stride, self.padding)
+
+    def extra_repr(self):
+        return f"kernel_size={self.kernel_size}, stride={self.stride}, padding={self.padding} (HIP)"

@@ -987,6 +987,37 @@ __global__ __launch_bounds__(256) void fp8_quantize_kernel(const float *x, int64
     }
 }
 
+// nn.MaxPool2d (dilation 1, floor mode) on NCHW fp32: the stem pooling between the first conv
+// and layer1 of the ResNets (torchvision layout), one thread per output, NaN-propagating like
+// ATen's max_pool2d.  Not an approx op: it sits on the benchmarked step (torch's kernel took
+// 0.59 ms of a 38 ms ResNet-18 batch-256 step).
+__global__ __launch_bounds__(256) void max_pool2d_kernel(const float *x, float *y, int64_t planes, int H, int W,
+                                                         int Ho, int Wo, int kh, int kw, int sh, int sw, int ph,
+                                                         int pw) {
+    const int64_t total = planes * Ho * Wo;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int wo = (int)(idx % Wo);
+        const int64_t t = idx / Wo;
+        const int ho = (int)(t % Ho);
+        const int64_t pl = t / Ho;
+        const float *xp = x + pl * H * W;
+        float m = -INFINITY;
+        const int h0 = ho * sh - ph, w0 = wo * sw - pw;
+        for (int ky = 0; ky < kh; ++ky) {
+            const int hi = h0 + ky;
+            if ((unsigned)hi >= (unsigned)H) continue;
+            for (int kx = 0; kx < kw; ++kx) {
+                const int wi = w0 + kx;
+                if ((unsigned)wi >= (unsigned)W) continue;
+                const float v = xp[(int64_t)hi * W + wi];
+                m = (v > m || v != v) ? v : m;
+            }
+        }
+        y[idx] = m;
+    }
+}
+
 // ------------------------------------------------------------------------- host dispatch
 template <bool S2N, bool QBMA, bool GCLIP>
 static void launch_fast_t(int mode, const GemmArgs &a, dim3 grid, hipStream_t s) {
@@ -1558,6 +1589,20 @@ int fp8a_conv2d_block(const float *x, const float *w, float *y, int64_t Bn, int6
     return conv2d_impl(x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups, E, Mw,
                        fin.mx ? nullptr : bA, bW, bR, table, flags, bn, act, act_lo, act_hi, workspace, rest, s, fin,
                        in_bias_out, in_ibias_out, xq, res, post_act, post_lo, post_hi, fout);
+}
+
+int fp8a_max_pool2d(const float *x, float *y, int64_t Bn, int64_t C, int64_t H, int64_t W, int kh, int kw, int sh,
+                    int sw, int ph, int pw, fp8a_stream_t stream) {
+    if (!x || !y) return fail(FP8A_EINVAL, "null pointer");
+    if (kh < 1 || kw < 1 || sh < 1 || sw < 1 || ph < 0 || pw < 0 || 2 * ph > kh || 2 * pw > kw)
+        return fail(FP8A_EINVAL, "bad pooling window");
+    const int64_t Ho = (H + 2 * ph - kh) / sh + 1, Wo = (W + 2 * pw - kw) / sw + 1;
+    if (Ho <= 0 || Wo <= 0) return fail(FP8A_EINVAL, "empty pooling output");
+    const int64_t total = Bn * C * Ho * Wo;
+    if (total == 0) return FP8A_OK;
+    max_pool2d_kernel<<<(unsigned)std::min<int64_t>((total + 255) / 256, 65536), 256, 0, (hipStream_t)stream>>>(
+        x, y, Bn * C, (int)H, (int)W, (int)Ho, (int)Wo, kh, kw, sh, sw, ph, pw);
+    return hip_check("fp8a_max_pool2d");
 }
 
 int fp8a_matmul_qamaa(const float *A, int64_t lda, const float *B, int64_t sbk, int64_t sbn, float *C, int64_t M,

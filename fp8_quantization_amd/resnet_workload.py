@@ -14,6 +14,7 @@ import torch
 from torch import nn
 
 from .approx_calculation import QCustomBNConv2dTorch, QCustomLinearTorch
+from .approx_ops import MaxPool2d
 from .model_wrap import Flattener, QuantizedActivationWrapper, QuantizedModel, fused_block_tail, quantize_model
 from .quantization import FPQuantizer, RangeEstimators
 from .quantization.base_quantized_classes import FP32Acts, QuantizedActivation
@@ -188,8 +189,8 @@ class QuantizedResNet(QuantizedModel):
     def __init__(self, resnet, input_size=(1, 3, 224, 224), quant_setup=None, **quant_params):
         super().__init__(input_size)
         specials = {BasicBlock: QuantizedBlock, Bottleneck: QuantizedBlock}
-        feats = nn.Sequential(resnet.conv1, resnet.bn1, resnet.relu, resnet.maxpool, resnet.layer1, resnet.layer2,
-                              resnet.layer3, resnet.layer4)
+        feats = nn.Sequential(resnet.conv1, resnet.bn1, resnet.relu, MaxPool2d.from_module(resnet.maxpool),
+                              resnet.layer1, resnet.layer2, resnet.layer3, resnet.layer4)
         self.features = quantize_model(feats, specials=specials, **quant_params)
         self.avgpool = QuantizedActivationWrapper(resnet.avgpool, tie_activation_quantizers=True,
                                                   input_quantizer=self.features[-1][-1].activation_quantizer,

@@ -179,6 +179,13 @@ int fp8a_conv2d_block(const float *x, const float *w, float *y, int64_t Bn, int6
                       size_t workspace_bytes, fp8a_stream_t stream);
 
 /*
+ * nn.MaxPool2d (dilation 1, floor mode, padding <= half the window) on NCHW fp32 y[Bn][C][Ho][Wo]:
+ * the ResNet stem pooling on the benchmarked step (not an approx op).
+ */
+int fp8a_max_pool2d(const float *x, float *y, int64_t Bn, int64_t C, int64_t H, int64_t W, int kh,
+                    int kw, int sh, int sw, int ph, int pw, fp8a_stream_t stream);
+
+/*
  * quantize_after_mult_and_add (qamaa) path of approx_multiply (approx_calculation.py:787-795):
  *   C = fq(sum_k fq(A[m,k] * B(k,n))),  fq = quantize_to_fp8_ste_MM with the res quantizer's
  *   n_bits / mantissa bits / sign bits and per-tensor maxval (device float [1]).

@@ -158,3 +158,23 @@ def test_block_tail_equals_unfused(case, tail):
         assert torch.equal(ob, ob_ref) and torch.equal(ob._fp8a_i32, ob_ref._fp8a_i32)
     ok = (y.view(torch.int32) == ref.view(torch.int32)) | ((y == 0) & (ref == 0))
     assert bool(ok.all()), f"{case} {tail}: {int((~ok).sum())} outputs differ"
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 112, 112), (2, 3, 7, 9), (1, 5, 1, 1)])
+@pytest.mark.parametrize("cfg", [(3, 2, 1), (2, 2, 0), (3, 1, 1)])
+def test_max_pool2d_matches_torch(shape, cfg):
+    """fp8a_max_pool2d (the ResNet stem pooling) against torch's max_pool2d, bit for bit, NaN included."""
+    from fp8_quantization_amd.approx_ops import MaxPool2d
+    k, s, p = cfg
+    if shape[2] + 2 * p < k or shape[3] + 2 * p < k:
+        pytest.skip("window larger than the padded input")
+    g = torch.Generator().manual_seed(sum(shape) + k)
+    x = torch.randn(shape, generator=g).to(DEV)
+    x.view(-1)[min(7, x.numel() - 1)] = float("nan")
+    mp = MaxPool2d.from_module(torch.nn.MaxPool2d(k, s, p))
+    assert isinstance(mp, MaxPool2d)
+    y = mp(x)
+    ref = torch.nn.functional.max_pool2d(x, k, s, p)
+    assert y.shape == ref.shape
+    assert torch.equal(torch.isnan(y), torch.isnan(ref))
+    assert torch.equal(torch.nan_to_num(y, nan=0.0), torch.nan_to_num(ref, nan=0.0))
