@@ -22,9 +22,16 @@
 // codes are 0-7 = m_b and 8 = a zero B (entry +0).  c_b = s_b 2^e_b is applied as one packed
 // 16-bit integer add on the pair (v_pk_add_u16 of (s_b << 15) + (e_b << 7) per half: exponent
 // add and sign flip, no carry between the halves), and the pair goes straight into the bf16
-// form of the scaled conversion.  Per product pair the VALU issues one LDS address add, one
-// packed add and one conversion; the table read is one ds_read_b32.  (A/B on the ResNet-18
-// layer set: +15 % over the f32 form, which paid two multiplies per pair and a ds_read_b64.)
+// form of the scaled conversion.
+//
+// Tile table.  c_b depends only on the column, so the packed add is done ONCE per staged K-step
+// and column pair for all 16 rows (8 s_a + m_a), not once per product: each staged tile builds
+// tt[kk][tx][row][j] = V'(row, pair 2 tx + j) (+) c_b (2 KiB per K-step) from the static table,
+// and the math loop reads, per A element, the thread's 4 columns with ONE ds_read_b64 at
+// (row offset | column block) + kk * stride: one v_and_or per A element, one conversion per
+// product pair, no packed add.  The build's stores are conflict-free because odd K-steps sit
+// 16 banks over (stride 528 words); the math loop's reads are conflict-free because each
+// 32-lane group holds one even and one odd column block (64-bank ds_read_b64 banking).
 //
 // Operands are decoded ONCE per launch by two pre-pass kernels (xm_decode_a / xm_decode_b):
 // an A element becomes one 32-bit word (cvt scale exponent << 23 | table row offset; the
@@ -33,11 +40,9 @@
 // each input element 9 times).  The pre-passes also carry the fallback checks (off-grid
 // operand, exactness window, e4m3 scale range, bias window) into the launch's flag word.
 //
-// LDS table layout [pair (code0 + 9 code1)][copy][row (8 s_a + m_a)] u32: zero A operands take
-// scale 2^127 (the conversion returns 0), so they need no row; copy = parity of the consuming
-// thread's column group.  Threads are mapped so that each 32-lane half-wave holds 16 row groups
-// x 2 column groups: a read touches at most 16 rows of one copy per column group, each on its
-// own bank -- conflict-free (MI355X_MICROARCH.md §LDS: ds_read_b32 banks (a/4) mod 32).
+// Static table layout [pair (code0 + 9 code1)][m_a] u32 for s_a = + (a negative A row is the same
+// pair with the sign bits flipped, folded into the build's addend); zero A operands take scale
+// 2^127 (the conversion returns 0), so their row is irrelevant.
 
 typedef int xm_v8i __attribute__((ext_vector_type(8)));
 typedef float xm_v16f __attribute__((ext_vector_type(16)));
@@ -46,15 +51,15 @@ typedef unsigned short xm_u2 __attribute__((ext_vector_type(2)));
 typedef __bf16 xm_b2 __attribute__((ext_vector_type(2)));
 
 constexpr int XM_NPAIR = 81;
-constexpr int XM_LUT_WORDS = XM_NPAIR * 2 * 16;  // [pair][copy][row] u32, 10.1 KiB
-constexpr uint32_t XM_ROW_SHIFT = 2, XM_ROW_MASK = 0x3Cu;
-constexpr int XM_BQ = BN / 2 + 2;              // pair slots per staged K row (padded)
+constexpr int XM_LUT_WORDS = XM_NPAIR * 8;  // [pair][m_a] u32 (s_a = +), 2.5 KiB
+constexpr uint32_t XM_ROW_SHIFT = 3, XM_ROW_MASK = 0x78u;  // A word bits 3-6: row * 8 = byte offset in a column block
+constexpr int XBK = 8;                         // K-steps per staged tile
+constexpr int XM_TTK = 16 * 32 + 16;           // tile-table words per K-step: [tx 16][row 16][j 2] + bank shift
 constexpr uint32_t XM_ZERO_WORD = 254u << 23;  // A = 0: cvt scale 2^127 (the code is 0), row 0
 struct XmSmem {
+    uint32_t tt[XBK][XM_TTK];  // c_b-applied pairs [kk][tx][row][j] (first: its byte offsets are the reads' immediates)
     uint32_t lut[XM_LUT_WORDS];
-    uint32_t aw[BK][AP];     // A(m, k)'s word: cvt scale exponent << 23 | table row offset
-
-    uint2 bq[BK][XM_BQ];     // per column pair: (c_b addend pair, byte offset of the pair block)
+    uint32_t aw[XBK][AP];      // A(m, k)'s word: cvt scale exponent << 23 | row << 3
 };
 constexpr int XM_CP = BN + 1;  // epilogue transpose tile [BM][BN + 1] floats, aliased on XmSmem
 static_assert(sizeof(float) * BM * XM_CP <= sizeof(XmSmem), "epilogue tile must fit the staging LDS");
@@ -62,10 +67,9 @@ static_assert(sizeof(float) * BM * XM_CP <= sizeof(XmSmem), "epilogue tile must 
 // Exactness / range window shared by the pre-passes (as bias_ok in gemm_fast_kernel)
 __device__ __forceinline__ bool xm_bias_ok(int b) { return b >= -100 && b <= 120; }
 
-// Table word e of layout [pair][copy][row]: the bf16 pair V'(row, code0), V'(row, code1).
+// Table word e of layout [pair][m_a]: the bf16 pair V'(m_a, code0), V'(m_a, code1), s_a = +.
 __device__ __forceinline__ uint32_t xm_lut_word(const TablePack &tab, int e) {
-    const int pr = e >> 5, row = e & 15;
-    const int ma = row & 7;
+    const int pr = e >> 3, ma = e & 7;
     uint32_t w = 0;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -76,14 +80,13 @@ __device__ __forceinline__ uint32_t xm_lut_word(const TablePack &tab, int e) {
         // Q_R's pre-clamp in bf16: any bound in (1.8125, 1.875) x binade rounds like the
         // reference's saturating mantissa (and the subnormal top tie rounding down)
         v = fminf(v, __uint_as_float(__float_as_uint(v) & 0x7F800000u) * 1.8671875f);
-        if (row >= 8) v = -v;
         w |= (__float_as_uint(v) >> 16) << (16 * h);
     }
     return w;
 }
 
 // A element -> word: bits 23-30 the cvt scale exponent se (scale 2^(se-127) = 2^(7-bR-e_a)),
-// bits 3-6 the table row (8 s_a + m_a); zeros XM_ZERO_WORD.  ok = on the (3, bA) grid, inside the
+// bits 3-6 the tile-table row (8 s_a + m_a); zeros XM_ZERO_WORD.  ok = on the (3, bA) grid, inside the
 // exactness window and the scale range.
 __device__ __forceinline__ uint32_t xm_word_a(float x, uint32_t emnA, int bR, bool &ok) {
     float c;
@@ -129,9 +132,8 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
 }
 
 // B pre-pass: per (k, pair Q) of the padded [Kpad][npad / 2] pair grid, the addend pair
-// ((s_b << 15) + (e_b << 7) per bf16 half, 0 for a zero B) and the pair block's byte offset
-// ((code0 + 9 code1) * 128 + copy * 64, copy = parity of the consuming thread's 4-column group
-// = (Q >> 1) & 1); out-of-range elements are zeros.
+// ((s_b << 15) + (e_b << 7) per bf16 half, 0 for a zero B) and the pair's byte offset in the
+// static table ((code0 + 9 code1) * 32); out-of-range elements are zeros.
 __global__ __launch_bounds__(256) void xm_decode_b(const GemmArgs p, int64_t kpad) {
     const int bA = *p.bA, bR = *p.bR;
     bool bad = !(xm_bias_ok(bA) && xm_bias_ok(bR));
@@ -168,7 +170,7 @@ __global__ __launch_bounds__(256) void xm_decode_b(const GemmArgs p, int64_t kpa
                 add |= ((((cb >> 31) << 15) + (eb << 7)) & 0xFFFFu) << (16 * h);
             }
         }
-        bq[i] = make_uint2(add, ((code[0] + 9u * code[1]) * 2u + (uint32_t)((q >> 1) & 1)) * 64u);
+        bq[i] = make_uint2(add, (code[0] + 9u * code[1]) * 32u);
     }
     if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, 1u);
 }
@@ -194,16 +196,16 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
     for (int e = 4 * tid; e < XM_LUT_WORDS; e += 4 * NT)
         *reinterpret_cast<uint4 *>(&sm.lut[e]) = *reinterpret_cast<const uint4 *>(&p.lutw[e]);
 
-    // B staging slots: pair q = e & 31 (lanes along n: coalesced), k row kk = e >> 5
+    // tile-table build units: thread = (m_a pair q4, column block btx, two K-steps bkk[u]); the
+    // 8 lanes of a ds_write_b128 group are 4 q4 x an even and an odd K-step (16 banks apart)
     const int64_t hq = p.npad / 2;
-    int bq[2], bkk[2];
+    const int q4 = tid & 3, btx = (tid >> 3) & 15;
+    int bkk[2];
     int64_t boff[2];
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
-        const int e = tid + NT * r;
-        bq[r] = e & 31;
-        bkk[r] = e >> 5;
-        boff[r] = (kbeg + bkk[r]) * hq + n0 / 2 + bq[r];  // pair index
+    for (int u = 0; u < 2; ++u) {
+        bkk[u] = 4 * u + 2 * (tid >> 7) + ((tid >> 2) & 1);
+        boff[u] = (kbeg + bkk[u]) * hq + n0 / 2 + 2 * btx;  // pair index of pair 2 btx (even: 16-B aligned)
     }
 
     // A staging.  conv: lanes along m (consecutive pixels), k row = wave + 4 r (wave-uniform: the
@@ -221,18 +223,19 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
         cwi0 = (int)(wo * p.sw - p.pw);
         cbase_w = img * p.aw_c * p.H * p.W + (int64_t)chi0 * p.W + cwi0;
     }
-    int arow[(BM * BK) / NT], akk[(BM * BK) / NT];
+    constexpr int AR = (BM * XBK) / NT;
+    int arow[AR], akk[AR];
 #pragma unroll
-    for (int r = 0; r < (BM * BK) / NT; ++r) {
+    for (int r = 0; r < AR; ++r) {
         const int e = tid + NT * r;
-        arow[r] = p.conv ? lane : (e >> 4);
-        akk[r] = p.conv ? (wvu + 4 * r) : (e & 15);
+        arow[r] = p.conv ? lane : (e / XBK);
+        akk[r] = p.conv ? (wvu + 4 * r) : (e % XBK);
     }
-    uint32_t wa[(BM * BK) / NT];
-    uint2 wbq[2];
+    uint32_t wa[AR];
+    uint4 wbq[2];
     auto load_tile = [&](int64_t k0) {
 #pragma unroll
-        for (int r = 0; r < (BM * BK) / NT; ++r) {
+        for (int r = 0; r < AR; ++r) {
             uint32_t w = XM_ZERO_WORD;
             if (!p.conv) {
                 const int64_t m = m0 + arow[r];
@@ -253,10 +256,8 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
             wa[r] = w;
         }
 #pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            const int64_t o = boff[r] + (k0 - kbeg) * hq;
-            wbq[r] = p.bqw[o];
-        }
+        for (int u = 0; u < 2; ++u)  // (add0, off0, add1, off1) of pairs 2 btx, 2 btx + 1
+            wbq[u] = *reinterpret_cast<const uint4 *>(p.bqw + boff[u] + (k0 - kbeg) * hq);
     };
     load_tile(kbeg);
 
@@ -281,43 +282,54 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
     for (int r = 0; r < 16; ++r) dacc[r] = 0.0f;
     xm_v8i av = {0, 0, 0, 0, 0, 0, 0, 0};
     const char *lut = reinterpret_cast<const char *>(sm.lut);
+    const uint32_t txo = (uint32_t)tx * 128u;  // the thread's column block in a K-step of the tile table
+    __syncthreads();  // the static table is in LDS before the first build reads it
 
-    for (int64_t k0 = kbeg; k0 < kend; k0 += BK) {
+    for (int64_t k0 = kbeg; k0 < kend; k0 += XBK) {
 #pragma unroll
-        for (int r = 0; r < (BM * BK) / NT; ++r) {
-            sm.aw[akk[r]][arow[r]] = wa[r];
-        }
+        for (int r = 0; r < AR; ++r) sm.aw[akk[r]][arow[r]] = wa[r];
+        // build: rows 2 q4, 2 q4 + 1 of both signs for the unit's two column pairs
 #pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            sm.bq[bkk[r]][bq[r]] = wbq[r];
+        for (int u = 0; u < 2; ++u) {
+            const uint4 b = wbq[u];
+            const uint2 s0 = *reinterpret_cast<const uint2 *>(lut + b.y + 8 * q4);
+            const uint2 s1 = *reinterpret_cast<const uint2 *>(lut + b.w + 8 * q4);
+            const xm_u2 a0 = __builtin_bit_cast(xm_u2, b.x), a1 = __builtin_bit_cast(xm_u2, b.z);
+            const xm_u2 n0 = __builtin_bit_cast(xm_u2, b.x ^ 0x80008000u), n1 = __builtin_bit_cast(xm_u2, b.z ^ 0x80008000u);
+            auto pk = [](uint32_t v, xm_u2 ad) { return __builtin_bit_cast(uint32_t, __builtin_bit_cast(xm_u2, v) + ad); };
+            uint32_t *d = &sm.tt[bkk[u]][btx * 32 + q4 * 4];
+            *reinterpret_cast<uint4 *>(d) = make_uint4(pk(s0.x, a0), pk(s1.x, a1), pk(s0.y, a0), pk(s1.y, a1));
+            *reinterpret_cast<uint4 *>(d + 16) = make_uint4(pk(s0.x, n0), pk(s1.x, n1), pk(s0.y, n0), pk(s1.y, n1));
         }
         __syncthreads();
-        if (k0 + BK < kend) load_tile(k0 + BK);  // next tile's loads fly during this tile's math
+        if (k0 + XBK < kend) load_tile(k0 + XBK);  // next tile's loads fly during this tile's math
 
         // per K-step: one word per A element (the conversion reads only the scale's exponent
-        // field; the table row offset is a bit field of it), the thread's two column pairs, all 8
-        // table reads of the step, then the math; the next step's reads follow the math
+        // field; the row offset is a bit field of it), one ds_read_b64 per A element for the
+        // thread's 4 columns, one conversion per product pair
 #pragma unroll
-        for (int kk = 0; kk < BK; ++kk) {
+        for (int kk = 0; kk < XBK; ++kk) {
             const uint4 aw4 = *reinterpret_cast<const uint4 *>(&sm.aw[kk][ty * TM]);
             const uint32_t awv[TM] = {aw4.x, aw4.y, aw4.z, aw4.w};
-            const uint4 bq4 = *reinterpret_cast<const uint4 *>(&sm.bq[kk][tx * 2]);  // add0, off0, add1, off1
-            uint32_t v0[TM], v1[TM];
+            // (volatile: otherwise the two halves, used as different types, are split into two loads
+            // and re-merged into a ds_read2_b32 -- half the LDS rate of ds_read_b64)
+            typedef const volatile __attribute__((address_space(3))) uint64_t xm_lds_u64;
+            xm_lds_u64 *ttk = (xm_lds_u64 *)(&sm.tt[kk][0]);
+            uint2 v[TM];
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
-                // (one word per A element; two LDS arrays without the mask: -2.6 % in A/B)
-                v0[i] = *reinterpret_cast<const uint32_t *>(lut + ((awv[i] & XM_ROW_MASK) + bq4.y));
-                v1[i] = *reinterpret_cast<const uint32_t *>(lut + ((awv[i] & XM_ROW_MASK) + bq4.w));
+                uint32_t a;  // (row offset | column block) in one v_and_or_b32 (the compiler splits it)
+                asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(a) : "v"(awv[i]), "s"(XM_ROW_MASK), "v"(txo));
+                __builtin_assume((a & 7u) == 0u);
+                const uint64_t w = ttk[a >> 3];
+                v[i] = make_uint2((uint32_t)w, (uint32_t)(w >> 32));
             }
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
-                const uint32_t x0 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(xm_u2, v0[i]) +
-                                                                     __builtin_bit_cast(xm_u2, bq4.x));
-                const xm_u2 x1 = __builtin_bit_cast(xm_u2, v1[i]) + __builtin_bit_cast(xm_u2, bq4.z);
                 const float sc = __uint_as_float(awv[i]);
                 xm_s2 cv;  // low word: no input register needed (see the f32 form)
-                asm("v_cvt_scalef32_pk_fp8_bf16 %0, %1, %2" : "=v"(cv) : "v"(x0), "v"(sc));
-                cv = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(cv, __builtin_bit_cast(xm_b2, x1), sc, true);
+                asm("v_cvt_scalef32_pk_fp8_bf16 %0, %1, %2" : "=v"(cv) : "v"(v[i].x), "v"(sc));
+                cv = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(cv, __builtin_bit_cast(xm_b2, v[i].y), sc, true);
                 av[4 * (kk & 1) + i] = __builtin_bit_cast(int, cv);
             }
             if (kk & 1) dacc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av, sel, dacc, 0, 0, 0, 127, 0, 127);
