@@ -1104,7 +1104,12 @@ static int choose_splits(int64_t M, int64_t N, int64_t K) {
     if (forced > 0) return (int)std::max<int64_t>(1, std::min<int64_t>(forced, kt));
     const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
     const double slots = 4.0 * device_cus();
-    const double t_round = (double)BM * BN * K / 4.4e9;                     // s
+    static double rate = 0.0;  // approx-MAC/s of one 64x64 workgroup at 4 per CU (FP8A_SPLITK_RATE overrides)
+    if (rate == 0.0) {
+        const char *e = getenv("FP8A_SPLITK_RATE");
+        rate = e ? std::max(1e8, atof(e)) : 4.4e9;
+    }
+    const double t_round = (double)BM * BN * K / rate;                      // s
     const double t_split = 2.0 * (double)M * N * sizeof(float) / 2.0e12;   // s per split
     double best = 1e300;
     int bs = 1;
