@@ -1018,6 +1018,43 @@ __global__ __launch_bounds__(256) void max_pool2d_kernel(const float *x, float *
     }
 }
 
+// The ResNet stem configuration (3x3 window, stride 2, padding 1) on rows of W % 8 == 0: each
+// thread makes 4 consecutive outputs of one row from two aligned float4 loads + one scalar per
+// input row (27 scalar loads before), one float4 store.  Same scan order (window row, then
+// column) and NaN rule as max_pool2d_kernel, so the same bits.
+__global__ __launch_bounds__(256) void max_pool2d_s2k3_kernel(const float *x, float *y, int64_t planes, int H, int W,
+                                                             int Ho) {
+    const int Wq = W / 8;  // 4-output groups per output row (Wo = W / 2)
+    const int64_t total = planes * Ho * Wq;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int q = (int)(idx % Wq);
+        const int64_t t = idx / Wq;
+        const int ho = (int)(t % Ho);
+        const int64_t pl = t / Ho;
+        const float *xp = x + pl * H * W;
+        float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        const int c0 = 8 * q;  // input columns c0 - 1 .. c0 + 7
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+            const int hi = 2 * ho - 1 + ky;
+            if ((unsigned)hi >= (unsigned)H) continue;
+            const float *r = xp + (int64_t)hi * W + c0;
+            const float4 a = *reinterpret_cast<const float4 *>(r), b = *reinterpret_cast<const float4 *>(r + 4);
+            const float v[9] = {c0 > 0 ? r[-1] : -INFINITY, a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+            for (int o = 0; o < 4; ++o)
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx) {
+                    if (o == 0 && kx == 0 && c0 == 0) continue;  // left padding
+                    const float u = v[2 * o + kx];
+                    m[o] = (u > m[o] || u != u) ? u : m[o];
+                }
+        }
+        *reinterpret_cast<float4 *>(y + (pl * Ho + ho) * (int64_t)(W / 2) + 4 * q) = make_float4(m[0], m[1], m[2], m[3]);
+    }
+}
+
 // ------------------------------------------------------------------------- host dispatch
 template <bool S2N, bool QBMA, bool GCLIP>
 static void launch_fast_t(int mode, const GemmArgs &a, dim3 grid, hipStream_t s) {
@@ -1605,6 +1642,13 @@ int fp8a_max_pool2d(const float *x, float *y, int64_t Bn, int64_t C, int64_t H, 
     if (Ho <= 0 || Wo <= 0) return fail(FP8A_EINVAL, "empty pooling output");
     const int64_t total = Bn * C * Ho * Wo;
     if (total == 0) return FP8A_OK;
+    if (kh == 3 && kw == 3 && sh == 2 && sw == 2 && ph == 1 && pw == 1 && W % 8 == 0 && H * W < (1ll << 31) &&
+        ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0) {
+        const int64_t groups = Bn * C * Ho * (W / 8);
+        max_pool2d_s2k3_kernel<<<(unsigned)std::min<int64_t>((groups + 255) / 256, 65536), 256, 0, (hipStream_t)stream>>>(
+            x, y, Bn * C, (int)H, (int)W, (int)Ho);
+        return hip_check("fp8a_max_pool2d");
+    }
     max_pool2d_kernel<<<(unsigned)std::min<int64_t>((total + 255) / 256, 65536), 256, 0, (hipStream_t)stream>>>(
         x, y, Bn * C, (int)H, (int)W, (int)Ho, (int)Wo, kh, kw, sh, sw, ph, pw);
     return hip_check("fp8a_max_pool2d");

@@ -160,7 +160,7 @@ def test_block_tail_equals_unfused(case, tail):
     assert bool(ok.all()), f"{case} {tail}: {int((~ok).sum())} outputs differ"
 
 
-@pytest.mark.parametrize("shape", [(4, 64, 112, 112), (2, 3, 7, 9), (1, 5, 1, 1)])
+@pytest.mark.parametrize("shape", [(4, 64, 112, 112), (2, 5, 9, 16), (2, 3, 7, 9), (1, 5, 1, 1)])
 @pytest.mark.parametrize("cfg", [(3, 2, 1), (2, 2, 0), (3, 1, 1)])
 def test_max_pool2d_matches_torch(shape, cfg):
     """fp8a_max_pool2d (the ResNet stem pooling) against torch's max_pool2d, bit for bit, NaN included."""
@@ -171,6 +171,10 @@ def test_max_pool2d_matches_torch(shape, cfg):
     g = torch.Generator().manual_seed(sum(shape) + k)
     x = torch.randn(shape, generator=g).to(DEV)
     x.view(-1)[min(7, x.numel() - 1)] = float("nan")
+    if x.shape[3] >= 10 and x.shape[2] >= 3:
+        x[-1, -1, 1, 0] = float("nan")  # a left-edge window
+        x[0, 0, 2, 8] = -0.0  # signed-zero ties keep the first in scan order
+        x[0, 0, 2, 9] = 0.0
     mp = MaxPool2d.from_module(torch.nn.MaxPool2d(k, s, p))
     assert isinstance(mp, MaxPool2d)
     y = mp(x)
