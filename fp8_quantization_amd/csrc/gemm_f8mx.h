@@ -116,15 +116,37 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
     uint32_t *const out = const_cast<uint32_t *>(p.aw);
     const int64_t hw = p.H * p.W;
     const int64_t rows = p.conv ? p.M / (p.Ho * p.Wo) : p.M, cols = p.conv ? p.aw_c * hw : p.awld;
+    auto word = [&](float v, bool &ok) {
+        if (p.fqin.mx) v = fq_apply(v, fmx, fbias, p.fqin.M, p.fqin.S);
+        return xm_word_a(v, emnA, bR, ok);
+    };
+    // 16-B form: every row start 16-B aligned and the valid columns a multiple of 4 (all the
+    // conv images here; matrix rows when lda and K are)
+    const int64_t lim0 = p.conv ? cols : p.K, istride = p.conv ? p.Cin * hw : p.lda;
+    const float *in0 = p.conv ? p.X + p.cbase * hw : p.A;
+    const bool vec = (lim0 % 4 == 0) && (cols % 4 == 0) && (istride % 4 == 0) && (((uintptr_t)in0 & 15) == 0) &&
+                     (((uintptr_t)out & 15) == 0);
     for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) {
         const float *in = p.conv ? p.X + (r * p.Cin + p.cbase) * hw : p.A + r * p.lda;
         const int64_t lim = p.conv ? cols : p.K;
         uint32_t *o = out + r * cols;
+        if (vec) {
+            for (int64_t i = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x); i < cols;
+                 i += 4 * (int64_t)gridDim.x * blockDim.x) {
+                uint4 w = make_uint4(XM_ZERO_WORD, XM_ZERO_WORD, XM_ZERO_WORD, XM_ZERO_WORD);
+                if (i < lim) {
+                    const float4 v = *reinterpret_cast<const float4 *>(in + i);
+                    bool ok0 = true, ok1 = true, ok2 = true, ok3 = true;
+                    w = make_uint4(word(v.x, ok0), word(v.y, ok1), word(v.z, ok2), word(v.w, ok3));
+                    bad |= !(ok0 && ok1 && ok2 && ok3);
+                }
+                *reinterpret_cast<uint4 *>(o + i) = w;
+            }
+            continue;
+        }
         for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cols; i += (int64_t)gridDim.x * blockDim.x) {
             bool ok = true;
-            float v = (i < lim) ? in[i] : 0.0f;
-            if (p.fqin.mx) v = fq_apply(v, fmx, fbias, p.fqin.M, p.fqin.S);
-            o[i] = (i < lim) ? xm_word_a(v, emnA, bR, ok) : XM_ZERO_WORD;
+            o[i] = (i < lim) ? word(in[i], ok) : XM_ZERO_WORD;
             bad |= !ok;
         }
     }
