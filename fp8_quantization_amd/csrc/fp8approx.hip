@@ -109,8 +109,11 @@ __device__ __forceinline__ float fq_apply(float v, float mx, float bias, int M, 
     int e;
     frexpf(xc, &e);
     const float ls = (xc == 0.0f) ? 1.0f : fmaxf((float)(e - 1) + bias, 1.0f);
-    const float sc = p2((int)(ls - (float)M - bias));
-    return rintf(xc / sc) * sc;
+    const int k = (int)(ls - (float)M - bias);
+    const float sc = p2(k);
+    // sc is a power of two: x / sc == x * 2^-k exactly (same exact quotient, one rounding) while
+    // 2^-k is finite -- a multiply instead of the IEEE division sequence
+    return (k >= -126) ? rintf(xc * p2(-k)) * sc : rintf(xc / sc) * sc;
 }
 
 struct GemmArgs {

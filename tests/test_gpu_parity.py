@@ -361,6 +361,21 @@ def test_fp8_fake_quantize_matches_oracle(M):
     np.testing.assert_array_equal(y1.cpu().numpy().view(np.uint32), yr1.view(np.uint32))
 
 
+@pytest.mark.parametrize("scale", [1e-38, 1e-33, 1e-25, 1e25, 1e33])
+def test_fp8_fake_quantize_extreme_ranges(scale):
+    """Ranges where the quantization step 2^k leaves the reciprocal's range (k < -126: the
+    kernel divides) or sits next to it (it multiplies by 2^-k): same bits as the oracle."""
+    rng = np.random.default_rng(int(np.log10(scale)) + 60)
+    x = (rng.standard_normal((4, 300)) * scale).astype(np.float32)
+    x[:, :5] = [0.0, -0.0, scale, -scale, scale * 1e-3]
+    mx = (np.abs(x).max(axis=1) * np.array([1.0, 0.5, 2.0, 1e-3])).astype(np.float32)
+    for M in (3, 4):
+        y, b = fa().fp8_fake_quantize(t(x), t(mx), 8, M, per_row=True)
+        yr, br = orc.fp8_fake_quant(x, mx, 7 - M, M, per_row=True)
+        np.testing.assert_array_equal(b.cpu().numpy().reshape(-1), br)
+        np.testing.assert_array_equal(y.cpu().numpy().view(np.uint32), yr.view(np.uint32))
+
+
 # ------------------------------------------------------------------------------ qamaa
 @pytest.mark.parametrize("case", META["g6"], ids=lambda c: c["key"])
 def test_qamaa_matmul(case):
