@@ -42,12 +42,22 @@ __global__ __launch_bounds__(256) void tbx_decode_a(const float *x, int64_t n, u
         *fq_bias_out = fbias;
         *fq_ibias_out = (int32_t)fbias;
     }
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const float v = fq.mx ? fq_apply(x[i], fmx, fbias, fq.M, fq.S) : x[i];
+    auto word = [&](float v) {
+        if (fq.mx) v = fq_apply(v, fmx, fbias, fq.M, fq.S);
         const uint32_t u = __float_as_uint(v), ua = u & 0x7FFFFFFFu;
         bad |= (ua != 0u) && ((ua & 0xFFFFFu) != 0u || ua < 0x20800000u || ua > 0x58800000u);
-        out[i] = ua == 0u ? 0u : ((u & 0xFF800000u) | (((ua >> 20) & 7u) << 6));
+        return ua == 0u ? 0u : ((u & 0xFF800000u) | (((ua >> 20) & 7u) << 6));
+    };
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t i0 = 0;
+    if ((((uintptr_t)x | (uintptr_t)out) & 15) == 0) {  // 16-byte form over the n / 4 quads
+        for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n / 4; q += stride) {
+            const float4 v = reinterpret_cast<const float4 *>(x)[q];
+            reinterpret_cast<uint4 *>(out)[q] = make_uint4(word(v.x), word(v.y), word(v.z), word(v.w));
+        }
+        i0 = n / 4 * 4;
     }
+    for (int64_t i = i0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = word(x[i]);
     if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(gate, 1u);
 }
 
