@@ -125,9 +125,10 @@ FL = orc.flags_of(approx=True, s2n=True, qbma=True)
     dict(B=2, cin=32, cout=48, k=1, s=2, p=0, d=1, g=1, hw=15),    # 1x1 downsample class
     dict(B=2, cin=16, cout=32, k=3, s=1, p=1, d=1, g=2, hw=9),     # groups
     dict(B=1, cin=256, cout=128, k=3, s=1, p=1, d=1, g=1, hw=7),   # split-K (K = 2304)
-    dict(B=2, cin=16, cout=24, k=3, s=2, p=1, d=1, g=1, hw=28),    # stride 2, phase planes, W % 4 == 0 (16-B pre-decode)
-    dict(B=2, cin=24, cout=16, k=1, s=2, p=0, d=1, g=1, hw=16),    # 1x1 stride-2 downsample on phase planes
-    dict(B=2, cin=8, cout=20, k=3, s=2, p=2, d=2, g=2, hw=14),     # phase planes with dilation, groups, W % 4 != 0
+    dict(B=2, cin=16, cout=24, k=3, s=2, p=1, d=1, g=1, hw=28),    # stride 2, H*W % 4 == 0 (16-B A pre-decode)
+    dict(B=2, cin=24, cout=16, k=1, s=2, p=0, d=1, g=1, hw=16),    # 1x1 stride-2 downsample
+    dict(B=2, cin=8, cout=20, k=3, s=2, p=2, d=2, g=2, hw=14),     # stride 2 + dilation + groups, 16-B pre-decode
+    dict(B=2, cin=8, cout=20, k=3, s=2, p=2, d=2, g=2, hw=15),     # the same with H*W % 4 != 0: scalar A pre-decode
 ])
 def test_conv_fast_path_matches_oracle(cfg):
     rng = np.random.default_rng(cfg["cin"] * 31 + cfg["cout"])
