@@ -163,7 +163,6 @@ struct GemmArgs {
     int64_t awld, aw_c;
     int64_t awH, awW;  // conv: the word image's height / width (H + 2 ph, W + 2 pw when zero-padded)
     int awph, awpw;    // conv: x's offset inside the word image (the zero border's width)
-    int xw;            // the wave-independent kernel (gemm_f8w_kernel) runs on these operands
     const uint2 *bqw;
     const uint32_t *lutw;  // the LDS table image (XM_LUT_WORDS words), written by xm_decode_b
     int64_t npad;
@@ -1086,9 +1085,7 @@ static void launch_fast(int mode, const GemmArgs &a, hipStream_t s) {
     if (mode == TM_F8) {  // s2n + qbma, no golden clip (selected in run_gemm)
         // matrix-core accumulation on pre-decoded operands (gemm_f8mx.h) when run_gemm staged
         // them, else the VALU-accumulating form
-        if (a.aw && a.xw)
-            gemm_f8w_kernel<<<grid, NT, 0, s>>>(a);
-        else if (a.aw)
+        if (a.aw)
             gemm_f8mx_kernel<<<grid, NT, 0, s>>>(a);
         else
             gemm_fast_kernel<true, true, false, TM_F8><<<grid, NT, 0, s>>>(a);
@@ -1205,19 +1202,12 @@ static bool no_mx() {
     return v;
 }
 
-// The wave-independent matrix-core kernel (gemm_f8w_kernel) unless FP8A_NO_F8W is set.
-static bool no_f8w() {
-    static const bool v = getenv("FP8A_NO_F8W") != nullptr;
-    return v;
-}
-
-// Words of the pre-decoded A operand: conv, the group's word image [Bn][aw_c][H + 2 ph][W + 2 pw]
-// (zero border: gemm_f8w_kernel) or [Bn][aw_c][H][W] (gemm_f8mx_kernel); matrix, [M][Kpad].
-static int64_t xm_a_words(const GemmArgs &a, bool padded) {
+// Words of the pre-decoded A operand: conv, the group's zero-bordered word image
+// [Bn][aw_c][H + 2 ph][W + 2 pw]; matrix, [M][Kpad].
+static int64_t xm_a_words(const GemmArgs &a) {
     const int64_t kpad = (a.K + BK - 1) / BK * BK;
     if (!a.conv) return a.M * kpad;
-    const int64_t hp = padded ? a.H + 2 * a.ph : a.H, wp = padded ? a.W + 2 * a.pw : a.W;
-    return (a.M / (a.Ho * a.Wo)) * a.aw_c * hp * wp;
+    return (a.M / (a.Ho * a.Wo)) * a.aw_c * (a.H + 2 * a.ph) * (a.W + 2 * a.pw);
 }
 
 // Fast tiled kernel + gated exact kernel (int-bias path), or the exact kernel alone (tb path).
@@ -1268,14 +1258,10 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     if (mode == TM_F8 && !no_mx()) {
         const int64_t kpad = kt * BK, npad = (a.N + BN - 1) / BN * BN;
         const size_t off = FLAG_BYTES + (a.splits > 1 ? splitk_bytes(a.M, a.N, a.K) : 0);
-        // gemm_f8w_kernel addresses the A words with 32-bit byte offsets: < 2^30 words; else
-        // gemm_f8mx_kernel on the unpadded image (< 2^31 words, conv)
-        int64_t a_words = xm_a_words(a, true);
-        a.xw = !no_f8w() && a_words < (1ll << 30) && ws_bytes >= off + xm_operand_bytes(a.N, a.K, a_words);
-        if (!a.xw) a_words = xm_a_words(a, false);
-        a.awH = a.H; a.awW = a.W; a.awph = 0; a.awpw = 0;
-        if (a.xw && a.conv) { a.awH = a.H + 2 * a.ph; a.awW = a.W + 2 * a.pw; a.awph = a.ph; a.awpw = a.pw; }
-        const bool fits32 = !a.conv || a_words < (1ll << 31);
+        // gemm_f8mx_kernel reads its operands with 32-bit byte offsets
+        const int64_t a_words = xm_a_words(a);
+        a.awH = a.H + 2 * a.ph; a.awW = a.W + 2 * a.pw; a.awph = a.ph; a.awpw = a.pw;
+        const bool fits32 = a_words < (1ll << 30) && kpad * npad * 4 < (1ll << 32);
         if (fits32 && ws_bytes >= off + xm_operand_bytes(a.N, a.K, a_words)) {
             char *base = (char *)ws + off;
             a.aw = (const uint32_t *)base;
@@ -1424,7 +1410,7 @@ size_t fp8a_conv2d_workspace_size(int64_t Bn, int64_t Cin, int64_t H, int64_t W,
     const int64_t Mrows = Bn * Ho * Wo, cog = Cout / groups, Kg = (Cin / groups) * kh * kw;
     if (Mrows <= 0 || Kg <= 0) return FLAG_BYTES;
     if (cog == 1) return FLAG_BYTES + (size_t)(Bn * Cin * H * W) * 4;  // tensor-bias kernels: A words
-    // A words: the zero-bordered word image of gemm_f8w_kernel (xm_a_words)
+    // A words: the zero-bordered word image of gemm_f8mx_kernel (xm_a_words)
     return gemm_workspace_bytes(Mrows, cog, Kg, Bn * (Cin / groups) * (H + 2 * ph) * (W + 2 * pw));
 }
 
@@ -1544,8 +1530,11 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
         int mode;
         rc = pack_table(table, Mw, (flags & (F_APPROX | F_V5)) != 0, tp, mode);
         if (rc) return rc;
-        const bool fused = f8_form(E, Mw, flags & ~F_TB, mode) && !no_mx() && Bn * cig * H * W < (1ll << 31) &&
-                           workspace_bytes >= gemm_workspace_bytes(Mrows, cog, Kg, Bn * cig * H * W);
+        const int64_t a_words = Bn * cig * (H + 2 * ph) * (W + 2 * pw);  // as xm_a_words / run_gemm
+        const int64_t kpad = (Kg + BK - 1) / BK * BK, npad = (cog + BN - 1) / BN * BN;
+        const bool fused = f8_form(E, Mw, flags & ~F_TB, mode) && !no_mx() && a_words < (1ll << 30) &&
+                           kpad * npad * 4 < (1ll << 32) &&
+                           workspace_bytes >= gemm_workspace_bytes(Mrows, cog, Kg, a_words);
         if (!fused) {
             rc = materialize();
             if (rc) return rc;

@@ -56,20 +56,12 @@ constexpr uint32_t XM_ROW_SHIFT = 3, XM_ROW_MASK = 0x78u;  // A word bits 3-6: r
 constexpr int XBK = 8;                         // K-steps per staged tile
 constexpr int XM_TTK = 16 * 32 + 16;           // tile-table words per K-step: [tx 16][row 16][j 2] + bank shift
 constexpr uint32_t XM_ZERO_WORD = 254u << 23;  // A = 0: cvt scale 2^127 (the code is 0), row 0
-#ifndef XM_ROWLANE
-#define XM_ROWLANE 1
-#endif
-// A words in LDS.  Row-per-lane math (XM_ROWLANE): [kk / 4][row][kk % 4], one ds_read_b128 per
-// lane gives a row's words for four K-steps; otherwise [kk][row].
+// A words in LDS: [kk / 4][row][kk % 4] -- one ds_read_b128 gives a row's words of four K-steps
 constexpr int XM_AWQ = 4 * BM + 4;
 struct XmSmem {
     uint32_t tt[XBK][XM_TTK];  // c_b-applied pairs [kk][tx][row][j] (first: its byte offsets are the reads' immediates)
     uint32_t lut[XM_LUT_WORDS];
-#if XM_ROWLANE
-    uint32_t aw[XBK / 4][XM_AWQ];
-#else
-    uint32_t aw[XBK][AP];      // A(m, k)'s word: cvt scale exponent << 23 | row << 3
-#endif
+    uint32_t aw[XBK / 4][XM_AWQ];  // A(m, k)'s word: cvt scale exponent << 23 | row << 3
 };
 constexpr int XM_CP = BN + 1;  // epilogue transpose tile [BM][BN + 1] floats, aliased on XmSmem
 static_assert(sizeof(float) * BM * XM_CP <= sizeof(XmSmem), "epilogue tile must fit the staging LDS");
@@ -231,18 +223,24 @@ __global__ __launch_bounds__(256) void xm_decode_b(const GemmArgs p, int64_t kpa
 #ifndef XM_WAVES
 #define XM_WAVES 1
 #endif
+// The GEMM.  Tile 64 x 64, 4 waves.  Math mapping: lane = tile row, wave wv = the 16 columns
+// 16 wv .. 16 wv + 15 (column blocks tx = 4 wv + c of the tile table).  Per K-step and lane: the
+// row's A word (four K-steps per ds_read_b128), ONE v_and_or_b32 (row offset | the wave's column
+// base; block c and the K-step are the reads' immediates), four ds_read_b64 (16 columns), eight
+// conversions; one MFMA per two K-steps.  Operands are read through buffer descriptors: uniform
+// K-step offsets in SGPRs, 32-bit lane offsets (run_gemm keeps the word images below 2^32 bytes);
+// the conv word image carries the zero padding (xm_decode_a), so the gather has no bounds checks.
 __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs p) {
     __shared__ __attribute__((aligned(16))) XmSmem sm;
 
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wvu = __builtin_amdgcn_readfirstlane(wv);
-    const int ty = lane & 15, tx = 4 * wv + (lane >> 4);  // half-wave = 16 row groups x 2 column groups
     const int64_t num_mt = (p.M + BM - 1) / BM;
     const int64_t tiles = num_mt * ((p.N + BN - 1) / BN);
     const int64_t bid = (int64_t)blockIdx.x % tiles, split = (int64_t)blockIdx.x / tiles;
     const int64_t m0 = (bid % num_mt) * BM;
     const int64_t n0 = (bid / num_mt) * BN;
-    const int64_t kbeg = split * p.kchunk, kend = min(p.K, kbeg + p.kchunk);
+    const int kbeg = (int)(split * p.kchunk), kend = (int)min(p.K, (int64_t)kbeg + p.kchunk), K32 = (int)p.K;
     const int bR = *p.bR;
 
     // table: copied from the launch's pre-computed image (xm_decode_b), 16-B per thread and step
@@ -251,66 +249,65 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
 
     // tile-table build units: thread = (m_a pair q4, column block btx, two K-steps bkk[u]); the
     // 8 lanes of a ds_write_b128 group are 4 q4 x an even and an odd K-step (16 banks apart)
-    const int64_t hq = p.npad / 2;
+    const uint32_t hq8 = (uint32_t)(p.npad / 2) * 8u;  // bytes per K-step of the B pair grid
     const int q4 = tid & 3, btx = (tid >> 3) & 15;
     int bkk[2];
-    int64_t boff[2];
+    uint32_t boff[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
         bkk[u] = 4 * u + 2 * (tid >> 7) + ((tid >> 2) & 1);
-        boff[u] = (kbeg + bkk[u]) * hq + n0 / 2 + 2 * btx;  // pair index of pair 2 btx (even: 16-B aligned)
+        boff[u] = (uint32_t)(kbeg + bkk[u]) * hq8 + (uint32_t)(n0 / 2 + 2 * btx) * 8u;  // pair 2 btx: 16-B aligned
     }
+    const __amdgpu_buffer_rsrc_t brsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint2 *>(p.bqw), (short)0, -1, 0x00020000);
 
-    // A staging.  conv: lanes along m (consecutive pixels), k row = wave + 4 r (wave-uniform: the
-    // k -> (c, ky, kx) split runs on the scalar unit); matrix: lanes along k.
-    bool crow_ok = false;
-    int64_t cbase_w = 0;
-    int chi0 = 0, cwi0 = 0;
-    if (p.conv) {
-        const int64_t m = m0 + lane;
-        crow_ok = m < p.M;
-        const int64_t hw = p.Ho * p.Wo;
-        const int64_t img = crow_ok ? m / hw : 0, pix = crow_ok ? m - img * hw : 0;
-        const int64_t ho = pix / p.Wo, wo = pix - ho * p.Wo;
-        chi0 = (int)(ho * p.sh - p.ph);
-        cwi0 = (int)(wo * p.sw - p.pw);
-        cbase_w = img * p.aw_c * p.H * p.W + (int64_t)chi0 * p.W + cwi0;
-    }
+    // A staging.  conv: lane = row (consecutive pixels), k row = wave + 4 r (wave-uniform: the
+    // k -> (c, ky, kx) split and the word offset run on the scalar unit); matrix: lanes along k.
+    // Rows past M re-read row M - 1 (store_tile drops them).
     constexpr int AR = (BM * XBK) / NT;
     int arow[AR], akk[AR];
+    uint32_t aoff[AR];
+    const uint32_t phw = (uint32_t)(p.awH * p.awW), uW = (uint32_t)p.awW;
 #pragma unroll
     for (int r = 0; r < AR; ++r) {
         const int e = tid + NT * r;
         arow[r] = p.conv ? lane : (e / XBK);
         akk[r] = p.conv ? (wvu + 4 * r) : (e % XBK);
+        const int64_t m = min(m0 + arow[r], p.M - 1);
+        if (p.conv) {
+            const int64_t hw = p.Ho * p.Wo, img = m / hw, pix = m - img * hw, ho = pix / p.Wo, wo = pix - ho * p.Wo;
+            aoff[r] = (uint32_t)(4 * (img * p.aw_c * (int64_t)phw + ho * p.sh * p.awW + wo * p.sw));
+        } else {
+            aoff[r] = (uint32_t)(4 * (m * p.awld + akk[r]));
+        }
     }
+    const __amdgpu_buffer_rsrc_t arsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(p.aw), (short)0, -1, 0x00020000);
+    const int khw = p.kh * p.kw;
     uint32_t wa[AR];
     uint4 wbq[2];
-    auto load_tile = [&](int64_t k0) {
+    auto load_tile = [&](int k0) {
 #pragma unroll
         for (int r = 0; r < AR; ++r) {
-            uint32_t w = XM_ZERO_WORD;
-            if (!p.conv) {
-                const int64_t m = m0 + arow[r];
-                if (m < p.M) w = p.aw[m * p.awld + k0 + akk[r]];
+            uint32_t ko;
+            if (p.conv) {
+                const int k = k0 + akk[r];  // wave-uniform
+                const uint32_t c = fastdiv((uint32_t)k, p.kk_mul, p.kk_shift);
+                const uint32_t t = (uint32_t)k - c * (uint32_t)khw;
+                const uint32_t ky = fastdiv(t, p.kw_mul, p.kw_shift);
+                const uint32_t kx = t - ky * (uint32_t)p.kw;
+                ko = 4u * (c * phw + ky * (uint32_t)p.dh * uW + kx * (uint32_t)p.dw);
             } else {
-                const int64_t k = k0 + akk[r];  // wave-uniform
-                if (k < kend) {
-                    const uint32_t c = fastdiv((uint32_t)k, p.kk_mul, p.kk_shift);
-                    const uint32_t t = (uint32_t)k - c * (uint32_t)(p.kh * p.kw);
-                    const uint32_t ky = fastdiv(t, p.kw_mul, p.kw_shift);
-                    const uint32_t kx = t - ky * (uint32_t)p.kw;
-                    const int dy = (int)ky * p.dh, dx = (int)kx * p.dw;
-                    const int64_t koff = (int64_t)c * p.H * p.W + (int64_t)dy * p.W + dx;
-                    if (crow_ok && (uint32_t)(chi0 + dy) < (uint32_t)p.H && (uint32_t)(cwi0 + dx) < (uint32_t)p.W)
-                        w = p.aw[cbase_w + koff];
-                }
+                ko = 4u * (uint32_t)k0;  // the matrix words are zero-padded to Kpad
             }
-            wa[r] = w;
+            ko = __builtin_amdgcn_readfirstlane(ko);
+            wa[r] = __builtin_amdgcn_raw_buffer_load_b32(arsrc, (int)aoff[r], (int)ko, 0);
+            if (p.conv && k0 + akk[r] >= K32) wa[r] = XM_ZERO_WORD;  // past the group's last channel (uniform)
         }
+        const uint32_t kb = __builtin_amdgcn_readfirstlane((uint32_t)(k0 - kbeg) * hq8);
 #pragma unroll
         for (int u = 0; u < 2; ++u)  // (add0, off0, add1, off1) of pairs 2 btx, 2 btx + 1
-            wbq[u] = *reinterpret_cast<const uint4 *>(p.bqw + boff[u] + (k0 - kbeg) * hq);
+            wbq[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(brsrc, (int)boff[u], (int)kb, 0));
     };
     load_tile(kbeg);
 
@@ -335,18 +332,13 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
     for (int r = 0; r < 16; ++r) dacc[r] = 0.0f;
     xm_v8i av = {0, 0, 0, 0, 0, 0, 0, 0};
     const char *lut = reinterpret_cast<const char *>(sm.lut);
-    const uint32_t txo = (uint32_t)tx * 128u;  // the thread's column block in a K-step of the tile table
+    const uint32_t wvo = (uint32_t)wvu * 512u;  // the wave's first column block (4 wv) in a K-step of the table
+    typedef const volatile __attribute__((address_space(3))) uint64_t xm_lds_u64;
     __syncthreads();  // the static table is in LDS before the first build reads it
 
-    for (int64_t k0 = kbeg; k0 < kend; k0 += XBK) {
+    for (int k0 = kbeg; k0 < kend; k0 += XBK) {
 #pragma unroll
-        for (int r = 0; r < AR; ++r) {
-#if XM_ROWLANE
-            sm.aw[akk[r] >> 2][arow[r] * 4 + (akk[r] & 3)] = wa[r];
-#else
-            sm.aw[akk[r]][arow[r]] = wa[r];
-#endif
-        }
+        for (int r = 0; r < AR; ++r) sm.aw[akk[r] >> 2][arow[r] * 4 + (akk[r] & 3)] = wa[r];
         // build: rows 2 q4, 2 q4 + 1 of both signs for the unit's two column pairs
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
@@ -363,13 +355,6 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
         __syncthreads();
         if (k0 + XBK < kend) load_tile(k0 + XBK);  // next tile's loads fly during this tile's math
 
-#if XM_ROWLANE
-        // Row-per-lane: lane = tile row, wave wv = the 16 columns 16 wv .. 16 wv + 15 (column
-        // blocks 4 wv + c).  Per K-step: the row's A word (read four K-steps at a time), ONE
-        // v_and_or_b32 (row offset | the wave's column base; the block c and the K-step are
-        // the reads' immediates), four ds_read_b64 (16 columns), eight conversions.
-        typedef const volatile __attribute__((address_space(3))) uint64_t xm_lds_u64r;
-        const uint32_t wvo = (uint32_t)wvu * 512u;
 #pragma unroll
         for (int q = 0; q < XBK / 4; ++q) {
             const uint4 aq = *reinterpret_cast<const uint4 *>(&sm.aw[q][lane * 4]);
@@ -377,20 +362,22 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
 #pragma unroll
             for (int k4 = 0; k4 < 4; ++k4) {
                 const int kk = 4 * q + k4;
-                uint32_t a;
+                uint32_t a;  // (row offset | the wave's column base) in one v_and_or_b32
                 asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(a) : "v"(awq[k4]), "s"(XM_ROW_MASK), "v"(wvo));
                 __builtin_assume((a & 7u) == 0u);
-                xm_lds_u64r *ttk = (xm_lds_u64r *)(&sm.tt[kk][0]);
+                // (volatile: otherwise the two halves, used as different types, are split into two
+                // loads and re-merged into a ds_read2_b32 -- half the LDS rate of ds_read_b64)
+                xm_lds_u64 *ttk = (xm_lds_u64 *)(&sm.tt[kk][0]);
                 uint2 v[4];
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
                     const uint64_t w = ttk[(a >> 3) + 16 * c];
                     v[c] = make_uint2((uint32_t)w, (uint32_t)(w >> 32));
                 }
-                const float sc = __uint_as_float(awq[k4]);
+                const float sc = __uint_as_float(awq[k4]);  // the conversion reads only its exponent field
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
-                    xm_s2 cv;
+                    xm_s2 cv;  // low word: no input register needed (see the f32 form)
                     asm("v_cvt_scalef32_pk_fp8_bf16 %0, %1, %2" : "=v"(cv) : "v"(v[c].x), "v"(sc));
                     cv = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(cv, __builtin_bit_cast(xm_b2, v[c].y), sc, true);
                     av[4 * (kk & 1) + c] = __builtin_bit_cast(int, cv);
@@ -398,38 +385,6 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
                 if (kk & 1) dacc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av, sel, dacc, 0, 0, 0, 127, 0, 127);
             }
         }
-#else
-        // per K-step: one word per A element (the conversion reads only the scale's exponent
-        // field; the row offset is a bit field of it), one ds_read_b64 per A element for the
-        // thread's 4 columns, one conversion per product pair
-#pragma unroll
-        for (int kk = 0; kk < XBK; ++kk) {
-            const uint4 aw4 = *reinterpret_cast<const uint4 *>(&sm.aw[kk][ty * TM]);
-            const uint32_t awv[TM] = {aw4.x, aw4.y, aw4.z, aw4.w};
-            // (volatile: otherwise the two halves, used as different types, are split into two loads
-            // and re-merged into a ds_read2_b32 -- half the LDS rate of ds_read_b64)
-            typedef const volatile __attribute__((address_space(3))) uint64_t xm_lds_u64;
-            xm_lds_u64 *ttk = (xm_lds_u64 *)(&sm.tt[kk][0]);
-            uint2 v[TM];
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                uint32_t a;  // (row offset | column block) in one v_and_or_b32 (the compiler splits it)
-                asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(a) : "v"(awv[i]), "s"(XM_ROW_MASK), "v"(txo));
-                __builtin_assume((a & 7u) == 0u);
-                const uint64_t w = ttk[a >> 3];
-                v[i] = make_uint2((uint32_t)w, (uint32_t)(w >> 32));
-            }
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                const float sc = __uint_as_float(awv[i]);
-                xm_s2 cv;  // low word: no input register needed (see the f32 form)
-                asm("v_cvt_scalef32_pk_fp8_bf16 %0, %1, %2" : "=v"(cv) : "v"(v[i].x), "v"(sc));
-                cv = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(cv, __builtin_bit_cast(xm_b2, v[i].y), sc, true);
-                av[4 * (kk & 1) + i] = __builtin_bit_cast(int, cv);
-            }
-            if (kk & 1) dacc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av, sel, dacc, 0, 0, 0, 127, 0, 127);
-        }
-#endif
         __syncthreads();
     }
 
@@ -440,194 +395,9 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
     for (int r = 0; r < 16; ++r) nan |= __builtin_isnan(dacc[r]);
     if (__syncthreads_or(nan ? 1 : 0) && tid == 0) atomicOr(p.flag, 1u);
 
-    // D (units of 2^(7-bR)) -> [BM][BN] tile in LDS -> each thread's 4x4 block, epilogue mapping
-    // with consecutive lanes on consecutive pixels (coalesced NCHW stores)
-    const float f8S = __uint_as_float((uint32_t)min(max(134 - bR, 1), 254) << 23);
-    float *ct = reinterpret_cast<float *>(&sm);
-    {
-        const int n = lane & 31, src = 32 * (n >> 4), o = n & 15;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int m = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            const int L = m + src;  // the lane whose output o this is
-#if XM_ROWLANE
-            const int row = L, col = 16 * wv + o;
-#else
-            const int row = (L & 15) * TM + (o >> 2), col = (4 * wv + (L >> 4)) * TN + (o & 3);
-#endif
-            ct[row * XM_CP + col] = dacc[r] * f8S;
-        }
-    }
-    __syncthreads();
-    const int ety = tid & 15, etx = tid >> 4;
-    float acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = ct[(ety * TM + i) * XM_CP + etx * TN + j];
-    store_tile(p, split, m0, n0, ety, etx, acc);
-}
-
-// ------------------------------------------------------------------ wave-independent form
-// gemm_f8w_kernel: the same terms, tile table and matrix-core summation as gemm_f8mx_kernel,
-// with no workgroup barrier in the K loop.  Lane = tile row, wave = the tile's 16 columns
-// 16 wv .. 16 wv + 15, and every wave stages only what it reads itself:
-//   * A: the lane's own row, gathered straight into registers one chunk ahead -- one
-//     global_load_dword per K-step with the K-step's offset (c, ky, kx -> word offset, on the
-//     scalar unit) as the uniform base and the row's offset as the 32-bit lane offset; the
-//     conv word image carries the zero padding (xm_decode_a), so there are no bounds checks;
-//   * the tile table of the wave's 4 column blocks, built by the wave into its own LDS slice
-//     (lane = K-step x block x sign half: two static-table rows, eight packed adds, four
-//     ds_write_b128) and read back by the same wave: LDS operations of one wave complete in
-//     order, so neither the build -> read nor the next build's overwrite needs a barrier.
-// Per K-step and lane: one v_and_or_b32 (row offset | the wave's slice), four ds_read_b64 (block
-// and K-step in the immediate), eight scaled conversions; one MFMA per two K-steps.
-constexpr int XW_TXS = 36;         // words per (K-step, column block): 16 rows x 2 + 4 (build bank shift)
-constexpr int XW_KS = 4 * XW_TXS;  // words per K-step of one wave's slice
-struct XwSmem {
-    uint32_t tt[4][XBK][XW_KS];  // per wave [kk][block][row][j]
-    uint32_t lut[XM_LUT_WORDS];
-};
-static_assert(sizeof(float) * BM * XM_CP <= sizeof(XwSmem), "epilogue tile must fit the wave slices");
-
-__global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8w_kernel(const GemmArgs p) {
-    __shared__ __attribute__((aligned(16))) XwSmem sm;
-
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int wvu = __builtin_amdgcn_readfirstlane(wv);
-    const int64_t num_mt = (p.M + BM - 1) / BM;
-    const int64_t tiles = num_mt * ((p.N + BN - 1) / BN);
-    const int64_t bid = (int64_t)blockIdx.x % tiles, split = (int64_t)blockIdx.x / tiles;
-    const int64_t m0 = (bid % num_mt) * BM;
-    const int64_t n0 = (bid / num_mt) * BN;
-    const int64_t kbeg = split * p.kchunk, kend = min(p.K, kbeg + p.kchunk);
-    const int bR = *p.bR;
-
-    for (int e = 4 * tid; e < XM_LUT_WORDS; e += 4 * NT)
-        *reinterpret_cast<uint4 *>(&sm.lut[e]) = *reinterpret_cast<const uint4 *>(&p.lutw[e]);
-
-    // the lane's row (rows past M re-read row M - 1; store_tile drops them): byte offset of its
-    // word A(m, k = 0) in the word image, read through a buffer descriptor (32-bit lane offset
-    // + the K-step's uniform offset; run_gemm keeps the image below 2^32 bytes)
-    const int64_t m = min(m0 + lane, p.M - 1);
-    const uint32_t phw = (uint32_t)(p.awH * p.awW), uW = (uint32_t)p.awW;
-    uint32_t aoff;
-    if (p.conv) {
-        const int64_t hw = p.Ho * p.Wo, img = m / hw, pix = m - img * hw, ho = pix / p.Wo, wo = pix - ho * p.Wo;
-        aoff = (uint32_t)(4 * (img * p.aw_c * (int64_t)phw + ho * p.sh * p.awW + wo * p.sw));
-    } else {
-        aoff = (uint32_t)(4 * m * p.awld);
-    }
-    const __amdgpu_buffer_rsrc_t arsrc =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(p.aw), (short)0, -1, 0x00020000);
-    const int K32 = (int)p.K, khw = p.kh * p.kw;
-    uint32_t wa[XBK];
-    auto load_a = [&](int k0) {
-#pragma unroll
-        for (int kk = 0; kk < XBK; ++kk) {
-            const int k = k0 + kk;  // uniform
-            uint32_t ko;
-            if (p.conv) {
-                const uint32_t c = fastdiv((uint32_t)k, p.kk_mul, p.kk_shift);
-                const uint32_t t = (uint32_t)k - c * (uint32_t)khw;
-                const uint32_t ky = fastdiv(t, p.kw_mul, p.kw_shift);
-                const uint32_t kx = t - ky * (uint32_t)p.kw;
-                ko = 4u * (c * phw + ky * (uint32_t)p.dh * uW + kx * (uint32_t)p.dw);
-            } else {
-                ko = 4u * (uint32_t)k;  // the matrix words are zero-padded to Kpad
-            }
-            ko = __builtin_amdgcn_readfirstlane(ko);
-            wa[kk] = __builtin_amdgcn_raw_buffer_load_b32(arsrc, (int)aoff, (int)ko, 0);
-        }
-        if (p.conv && k0 + XBK > K32) {  // last chunk: past the group's last channel (uniform)
-#pragma unroll
-            for (int kk = 0; kk < XBK; ++kk)
-                if (k0 + kk >= K32) wa[kk] = XM_ZERO_WORD;
-        }
-    };
-    // B: lane = (K-step bkk, column block bc, sign half bh); its two column pairs 2 bc, 2 bc + 1
-    // of the wave's eight
-    const int64_t hq = p.npad / 2;
-    const int bkk = lane >> 3, bc = (lane >> 1) & 3, bh = lane & 1;
-    const uint2 *const bq0 = p.bqw + (kbeg + bkk) * hq + n0 / 2 + 8 * wvu + 2 * bc;
-    uint4 wb;
-    auto load_b = [&](int64_t k0) { wb = *reinterpret_cast<const uint4 *>(bq0 + (k0 - kbeg) * hq); };
-    load_a((int)kbeg);
-    load_b(kbeg);
-
-    xm_v8i sel;
-    {
-        const int n = lane & 31, h = lane >> 5;
-#pragma unroll
-        for (int v = 0; v < 8; ++v) {
-            uint32_t w = 0;
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int pb = 4 * v + b;
-                if ((n >> 4) == h && (pb & 15) == (n & 15)) w |= 0x38u << (8 * b);
-            }
-            sel[v] = (int)w;
-        }
-    }
-    xm_v16f dacc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dacc[r] = 0.0f;
-    xm_v8i av = {0, 0, 0, 0, 0, 0, 0, 0};
-    const char *lut = reinterpret_cast<const char *>(sm.lut);
-    uint32_t *const bdst = &sm.tt[wvu][bkk][bc * XW_TXS + 16 * bh];
-    const uint32_t wvo = (uint32_t)wvu * (uint32_t)(XBK * XW_KS * 4);  // the wave's slice, bytes
-    typedef const volatile __attribute__((address_space(3))) uint64_t xw_lds_u64;
-    __syncthreads();  // the static table is in LDS
-
-    for (int64_t k0 = kbeg; k0 < kend; k0 += XBK) {
-        {  // build rows 8 bh .. 8 bh + 7 (sign bh) of block bc at K-step bkk
-            const uint4 b = wb;
-            const uint32_t fl = bh ? 0x80008000u : 0u;
-            const xm_u2 a0 = __builtin_bit_cast(xm_u2, b.x ^ fl), a1 = __builtin_bit_cast(xm_u2, b.z ^ fl);
-            const uint4 s0l = *reinterpret_cast<const uint4 *>(lut + b.y), s0h = *reinterpret_cast<const uint4 *>(lut + b.y + 16);
-            const uint4 s1l = *reinterpret_cast<const uint4 *>(lut + b.w), s1h = *reinterpret_cast<const uint4 *>(lut + b.w + 16);
-            auto pk = [](uint32_t v, xm_u2 ad) { return __builtin_bit_cast(uint32_t, __builtin_bit_cast(xm_u2, v) + ad); };
-            *reinterpret_cast<uint4 *>(bdst) = make_uint4(pk(s0l.x, a0), pk(s1l.x, a1), pk(s0l.y, a0), pk(s1l.y, a1));
-            *reinterpret_cast<uint4 *>(bdst + 4) = make_uint4(pk(s0l.z, a0), pk(s1l.z, a1), pk(s0l.w, a0), pk(s1l.w, a1));
-            *reinterpret_cast<uint4 *>(bdst + 8) = make_uint4(pk(s0h.x, a0), pk(s1h.x, a1), pk(s0h.y, a0), pk(s1h.y, a1));
-            *reinterpret_cast<uint4 *>(bdst + 12) = make_uint4(pk(s0h.z, a0), pk(s1h.z, a1), pk(s0h.w, a0), pk(s1h.w, a1));
-        }
-        uint32_t awc[XBK];
-#pragma unroll
-        for (int kk = 0; kk < XBK; ++kk) awc[kk] = wa[kk];
-        if (k0 + XBK < kend) {  // the next chunk's operands fly during this chunk's math
-            load_b(k0 + XBK);
-            load_a((int)(k0 + XBK));
-        }
-#pragma unroll
-        for (int kk = 0; kk < XBK; ++kk) {
-            uint32_t a;
-            asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(a) : "v"(awc[kk]), "s"(XM_ROW_MASK), "v"(wvo));
-            __builtin_assume((a & 7u) == 0u);
-            xw_lds_u64 *ttk = (xw_lds_u64 *)(&sm.tt[0][kk][0]);
-            uint2 v[4];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const uint64_t w = ttk[(a >> 3) + c * (XW_TXS / 2)];
-                v[c] = make_uint2((uint32_t)w, (uint32_t)(w >> 32));
-            }
-            const float sc = __uint_as_float(awc[kk]);
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                xm_s2 cv;
-                asm("v_cvt_scalef32_pk_fp8_bf16 %0, %1, %2" : "=v"(cv) : "v"(v[c].x), "v"(sc));
-                cv = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(cv, __builtin_bit_cast(xm_b2, v[c].y), sc, true);
-                av[4 * (kk & 1) + c] = __builtin_bit_cast(int, cv);
-            }
-            if (kk & 1) dacc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av, sel, dacc, 0, 0, 0, 127, 0, 127);
-        }
-    }
-
-    bool nan = false;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) nan |= __builtin_isnan(dacc[r]);
-    if (__syncthreads_or(nan ? 1 : 0) && tid == 0) atomicOr(p.flag, 1u);  // also: every slice read
-
+    // D (units of 2^(7-bR)): D[m][n] is output n mod 16 of lane m + 32 (n / 16), i.e. tile row
+    // m + 32 (n / 16), column 16 wv + n mod 16 -> [BM][BN] tile in LDS -> each thread's 4x4
+    // block, epilogue mapping with consecutive lanes on consecutive pixels (coalesced NCHW stores)
     const float f8S = __uint_as_float((uint32_t)min(max(134 - bR, 1), 254) << 23);
     float *ct = reinterpret_cast<float *>(&sm);
     {

@@ -50,10 +50,11 @@ def test_workspace_queries_are_host_only():
     # depthwise (single output channel per group): the tensor-bias kernels need the flag word and
     # the E4M3 table form's input words (the v5 mode takes the GEMM path, unsplit, no pre-decode)
     assert L.fp8a_conv2d_workspace_size(2, 8, 6, 6, 8, 3, 3, 1, 1, 1, 1, 1, 1, 8) == flag + 2 * 8 * 6 * 6 * 4
-    # implicit-GEMM conv: no im2col image; the A words of one group's input slice
+    # implicit-GEMM conv: no im2col image; the A words of one group's input slice, zero-bordered
+    # by the padding (H + 2 ph) x (W + 2 pw), + B column pairs + the table image (unsplit here)
     n2 = L.fp8a_conv2d_workspace_size(2, 3, 8, 8, 4, 3, 3, 1, 1, 1, 1, 1, 1, 1)
-    assert n2 >= flag + 2 * 3 * 8 * 8 * 4
-    assert L.fp8a_conv2d_workspace_size(256, 3, 224, 224, 4, 3, 3, 1, 1, 1, 1, 1, 1, 1) >= flag + 256 * 3 * 224 * 224 * 4
+    assert n2 == flag + _a256(2 * 3 * 10 * 10 * 4) + _a256(32 * 64 // 2 * 8) + 16384
+    assert L.fp8a_conv2d_workspace_size(256, 3, 224, 224, 4, 7, 7, 2, 2, 3, 3, 1, 1, 1) >= flag + 256 * 3 * 230 * 230 * 4
 
 
 def test_bad_format_maps_to_value_error():
