@@ -124,20 +124,36 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
         if (p.fqin.mx) v = fq_apply(v, fmx, fbias, p.fqin.M, p.fqin.S);
         return xm_word_a(v, emnA, bR, ok);
     };
-    if (p.conv && (p.awph | p.awpw)) {  // zero-bordered image (< 2^31 words, run_gemm): 32-bit index math
+    if (p.conv && (p.awph | p.awpw)) {  // zero-bordered image (< 2^30 words, run_gemm): 32-bit index math
+        // four consecutive words per thread step (one 16-B store when the image is a multiple of
+        // four words), their (c, hp, wp) stepped from the first one's
         const uint32_t ucols = (uint32_t)cols, phw = (uint32_t)(p.awH * p.awW), uW = (uint32_t)p.awW;
+        const bool v4 = (ucols % 4 == 0) && (((uintptr_t)out & 15) == 0);
+        const uint32_t per = v4 ? 4u : 1u;
         for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) {
             const float *in = p.X + (r * p.Cin + p.cbase) * hw;
             uint32_t *o = out + r * cols;
-            for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < ucols; i += gridDim.x * blockDim.x) {
-                const uint32_t c = i / phw, t = i - c * phw, hp = t / uW, wp = t - hp * uW;
-                const int hy = (int)hp - p.awph, wx = (int)wp - p.awpw;
-                bool ok = true;
-                uint32_t w = XM_ZERO_WORD;
-                if ((uint32_t)hy < (uint32_t)p.H && (uint32_t)wx < (uint32_t)p.W)
-                    w = word(in[((int64_t)c * p.H + hy) * p.W + wx], ok);
-                o[i] = w;
-                bad |= !ok;
+            for (uint32_t i = per * (blockIdx.x * blockDim.x + threadIdx.x); i < ucols; i += per * gridDim.x * blockDim.x) {
+                uint32_t c = i / phw, t = i - c * phw, hp = t / uW, wp = t - hp * uW;
+                uint32_t w[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (j >= (int)per) break;
+                    const int hy = (int)hp - p.awph, wx = (int)wp - p.awpw;
+                    bool ok = true;
+                    w[j] = XM_ZERO_WORD;
+                    if ((uint32_t)hy < (uint32_t)p.H && (uint32_t)wx < (uint32_t)p.W)
+                        w[j] = word(in[((int64_t)c * p.H + hy) * p.W + wx], ok);
+                    bad |= !ok;
+                    if (++wp == uW) {  // next line (and channel)
+                        wp = 0;
+                        if (++hp == (uint32_t)p.awH) { hp = 0; ++c; }
+                    }
+                }
+                if (v4)
+                    *reinterpret_cast<uint4 *>(o + i) = make_uint4(w[0], w[1], w[2], w[3]);
+                else
+                    o[i] = w[0];
             }
         }
         if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, 1u);

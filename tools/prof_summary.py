@@ -37,6 +37,9 @@ def main():
     ap.add_argument("--note", default="")
     ap.add_argument("--pmc-json", default="", help="also write the per-launch PMC summary bench.py reads")
     ap.add_argument("--kernel", default="gemm_f8mx_kernel")
+    ap.add_argument("--arch", default="resnet18", help="bench workload the PMC passes ran (bench.py keys on it)")
+    ap.add_argument("--E", type=int, default=4)
+    ap.add_argument("--M", type=int, default=3)
     ap.add_argument("--op-kernels", default=OP_KERNELS)
     a = ap.parse_args()
     KERNEL = a.kernel
@@ -79,7 +82,8 @@ def main():
         pj = dict(source="rocprofv3 --kernel-trace --pmc (separate passes per counter group, "
                          f"--kernel-include-regex {KERNEL}) on bench.py --steps 2 --warmup 1",
                   note=f"per {KERNEL} dispatch, averaged; FETCH_SIZE/WRITE_SIZE in KB (x1024 = bytes); "
-                       "FETCH_SIZE uncalibrated for 4-byte-per-lane loads (MI355X_MICROARCH.md HBM section)")
+                       "FETCH_SIZE uncalibrated for 4-byte-per-lane loads (MI355X_MICROARCH.md HBM section)",
+                  arch=a.arch, E=a.E, M=a.M)
         if "FETCH_SIZE" in pm and "WRITE_SIZE" in pm:
             pj.update(kernel=KERNEL, bytes_per_launch=(pm["FETCH_SIZE"] + pm["WRITE_SIZE"]) * 1024.0,
                       fetch_kb=pm["FETCH_SIZE"], write_kb=pm["WRITE_SIZE"])
