@@ -239,6 +239,9 @@ __global__ __launch_bounds__(256) void xm_decode_b(const GemmArgs p, int64_t kpa
 #ifndef XM_WAVES
 #define XM_WAVES 1
 #endif
+#ifndef XM_ABL
+#define XM_ABL 0  // timing-only ablations (wrong results): 1 no table reads, 2 no conversions, 4 no table build
+#endif
 // The GEMM.  Tile 64 x 64, 4 waves.  Math mapping: lane = tile row, wave wv = the 16 columns
 // 16 wv .. 16 wv + 15 (column blocks tx = 4 wv + c of the tile table).  Per K-step and lane: the
 // row's A word (four K-steps per ds_read_b128), ONE v_and_or_b32 (row offset | the wave's column
@@ -365,8 +368,12 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
             const xm_u2 n0 = __builtin_bit_cast(xm_u2, b.x ^ 0x80008000u), n1 = __builtin_bit_cast(xm_u2, b.z ^ 0x80008000u);
             auto pk = [](uint32_t v, xm_u2 ad) { return __builtin_bit_cast(uint32_t, __builtin_bit_cast(xm_u2, v) + ad); };
             uint32_t *d = &sm.tt[bkk[u]][btx * 32 + q4 * 4];
+#if !(XM_ABL & 4)
             *reinterpret_cast<uint4 *>(d) = make_uint4(pk(s0.x, a0), pk(s1.x, a1), pk(s0.y, a0), pk(s1.y, a1));
             *reinterpret_cast<uint4 *>(d + 16) = make_uint4(pk(s0.x, n0), pk(s1.x, n1), pk(s0.y, n0), pk(s1.y, n1));
+#else
+            if (b.x == 0x12345u) *d = pk(s0.x, a0) ^ pk(s1.y, n1);
+#endif
         }
         __syncthreads();
         if (k0 + XBK < kend) load_tile(k0 + XBK);  // next tile's loads fly during this tile's math
@@ -387,16 +394,24 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
                 uint2 v[4];
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
+#if !(XM_ABL & 1)
                     const uint64_t w = ttk[(a >> 3) + 16 * c];
                     v[c] = make_uint2((uint32_t)w, (uint32_t)(w >> 32));
+#else
+                    v[c] = make_uint2(a + c, a ^ c);
+#endif
                 }
                 const float sc = __uint_as_float(awq[k4]);  // the conversion reads only its exponent field
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
+#if !(XM_ABL & 2)
                     xm_s2 cv;  // low word: no input register needed (see the f32 form)
                     asm("v_cvt_scalef32_pk_fp8_bf16 %0, %1, %2" : "=v"(cv) : "v"(v[c].x), "v"(sc));
                     cv = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(cv, __builtin_bit_cast(xm_b2, v[c].y), sc, true);
                     av[4 * (kk & 1) + c] = __builtin_bit_cast(int, cv);
+#else
+                    av[4 * (kk & 1) + c] = (int)(v[c].x ^ v[c].y);
+#endif
                 }
                 if (kk & 1) dacc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av, sel, dacc, 0, 0, 0, 127, 0, 127);
             }
@@ -409,7 +424,7 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
     bool nan = false;
 #pragma unroll
     for (int r = 0; r < 16; ++r) nan |= __builtin_isnan(dacc[r]);
-    if (__syncthreads_or(nan ? 1 : 0) && tid == 0) atomicOr(p.flag, 1u);
+    if (__syncthreads_or(nan ? 1 : 0) && tid == 0 && !XM_ABL) atomicOr(p.flag, 1u);
 
     // D (units of 2^(7-bR)): D[m][n] is output n mod 16 of lane m + 32 (n / 16), i.e. tile row
     // m + 32 (n / 16), column 16 wv + n mod 16 -> [BM][BN] tile in LDS -> each thread's 4x4
