@@ -44,12 +44,16 @@ def metric_name(arch, E, M):
 
 
 def dominant_kernel(E, M):
-    """(kernel name, description) of the approx GEMM kernel the format runs on (run_gemm in
-    csrc/fp8approx.hip): the E4M3 matrix-core form for E4M3 (s2n + qbma, {0,1} / zero table),
-    the VALU tiled kernel with the format's compensation table otherwise."""
+    """(kernel name, description) of the approx GEMM kernel the bench's format runs on (run_gemm
+    in csrc/fp8approx.hip; the bench uses s2n + qbma and the withComp=False tables): the E4M3
+    matrix-core form for E4M3, the tile-table kernel for E3M4 / E2M5 (their tables have no
+    negative entries), the VALU tiled kernel otherwise."""
     if (E, M) == (4, 3):
         return "gemm_f8mx_kernel", ("implicit-GEMM approx conv / linear, E4M3 terms by the hardware fp8 "
                                     "conversion, codes summed on the matrix core")
+    if M in (4, 5):
+        return "gemm_tt_kernel", (f"implicit-GEMM approx conv / linear on the VALU, E{E}M{M} terms from a "
+                                  "per-tile c_b-applied table, one multiply + magic-constant Q_R + add per product")
     return "gemm_fast_kernel", (f"implicit-GEMM approx conv / linear on the VALU, E{E}M{M} error-table "
                                 "term, arithmetic Q_R")
 

@@ -163,6 +163,8 @@ struct GemmArgs {
     int64_t awld, aw_c;
     int64_t awH, awW;  // conv: the word image's height / width (H + 2 ph, W + 2 pw when zero-padded)
     int awph, awpw;    // conv: x's offset inside the word image (the zero border's width)
+    int wfmt;          // pre-decoded operand format: 0 = gemm_f8mx_kernel's, 1 = gemm_tt_kernel's
+    int ttf7;          // gemm_tt_kernel: the table has negative entries (the F7 sign rule)
     const uint2 *bqw;
     const uint32_t *lutw;  // the LDS table image (XM_LUT_WORDS words), written by xm_decode_b
     int64_t npad;
@@ -691,6 +693,7 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
 }
 
 #include "gemm_f8mx.h"
+#include "gemm_tt.h"
 
 // Sums the split-K partials in split order (deterministic) and writes the output mapping.
 // Partial layout: row-major [M][N] (rowmajor output) or [img][N][hw] (NCHW output).
@@ -1082,6 +1085,13 @@ static void launch_fast(int mode, const GemmArgs &a, hipStream_t s) {
         gemm_fast_kernel<false, false, false, TM_V5><<<grid, NT, 0, s>>>(a);
         return;
     }
+    if (a.aw && a.wfmt == 1) {  // the tile-table kernel on pre-decoded operands (run_gemm)
+        if (a.Mw == 4)
+            a.ttf7 ? gemm_tt_kernel<4, true><<<grid, NT, 0, s>>>(a) : gemm_tt_kernel<4, false><<<grid, NT, 0, s>>>(a);
+        else
+            gemm_tt_kernel<5, false><<<grid, NT, 0, s>>>(a);
+        return;
+    }
     if (mode == TM_F8) {  // s2n + qbma, no golden clip (selected in run_gemm)
         // matrix-core accumulation on pre-decoded operands (gemm_f8mx.h) when run_gemm staged
         // them, else the VALU-accumulating form
@@ -1197,6 +1207,20 @@ static bool f8_form(int E, int Mw, uint32_t flags, int table_mode) {
            (flags & F_S2N) && (flags & F_QBMA) && !(flags & F_GCLIP) && !(flags & F_TB);
 }
 
+// The tile-table kernel (gemm_tt_kernel) applies: E3M4 / E2M5 (mantissa 4 or 5), any table mode
+// of the int-bias path, s2n + qbma, no golden clip, not v5 (FP8A_NO_TT=1 keeps gemm_fast_kernel);
+// not E2M5 with a signed table: its F7 form (two 32-row tables, one K-step per staged tile) was
+// measured slower than gemm_fast_kernel.
+static bool tt_form(int Mw, uint32_t flags, const TablePack &tab) {
+    static const bool no_tt = getenv("FP8A_NO_TT") != nullptr;
+    if (no_tt || (flags & F_V5) || !(Mw == 4 || Mw == 5) || !(flags & F_S2N) || !(flags & F_QBMA) ||
+        (flags & F_GCLIP) || (flags & F_TB))
+        return false;
+    bool neg = false;
+    for (int i = 0; i < (1 << (2 * Mw)); ++i) neg |= tab.raw[i] < 0;
+    return Mw == 4 || !neg;
+}
+
 static bool no_mx() {
     static const bool v = getenv("FP8A_NO_MX") != nullptr;
     return v;
@@ -1252,10 +1276,11 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     a.kchunk = ((kt + a.splits - 1) / a.splits) * BK;
     a.part = a.splits > 1 ? (float *)((char *)ws + FLAG_BYTES) : nullptr;
     if (hipMemsetAsync(ws, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a flag reset");
-    // the matrix-core E4M3 kernel needs its pre-decoded operands in the workspace (else the
-    // VALU-accumulating form runs); FP8A_NO_MX=1 forces the latter
+    // the matrix-core E4M3 kernel and the tile-table kernel (E3M4 / E2M5) need their pre-decoded
+    // operands in the workspace (else gemm_fast_kernel runs); FP8A_NO_MX=1 forces the latter
     a.aw = nullptr;
-    if (mode == TM_F8 && !no_mx()) {
+    const bool tt = mode != TM_F8 && tt_form(a.Mw, a.flags, a.tab);
+    if ((mode == TM_F8 || tt) && !no_mx()) {
         const int64_t kpad = kt * BK, npad = (a.N + BN - 1) / BN * BN;
         const size_t off = FLAG_BYTES + (a.splits > 1 ? splitk_bytes(a.M, a.N, a.K) : 0);
         // gemm_f8mx_kernel reads its operands with 32-bit byte offsets
@@ -1269,11 +1294,19 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
             a.bqw = (const uint2 *)(base + align256((size_t)a_words * 4));
             a.lutw = (const uint32_t *)(base + align256((size_t)a_words * 4) + align256((size_t)(kpad * npad / 2) * 8));
             a.npad = npad;
+            a.wfmt = tt ? 1 : 0;
+            a.ttf7 = 0;
+            for (int i = 0; tt && i < (1 << (2 * a.Mw)); ++i) a.ttf7 |= a.tab.raw[i] < 0;
             const int64_t rows = a.conv ? a.M / (a.Ho * a.Wo) : a.M, cols = a_words / std::max<int64_t>(rows, 1);
             const dim3 ga((unsigned)std::min<int64_t>((cols + 255) / 256, 64), (unsigned)std::min<int64_t>(rows, 1024));
             xm_decode_a<<<ga, 256, 0, s>>>(a);
-            const unsigned gb = (unsigned)std::min<int64_t>((kpad * npad / 2 + 255) / 256, 4096);
-            xm_decode_b<<<gb, 256, 0, s>>>(a, kpad);
+            if (tt) {  // B words [Kpad][Npad] (the same bytes as the E4M3 pair grid) + the static image
+                const unsigned gb = (unsigned)std::min<int64_t>((kpad * npad + 255) / 256, 4096);
+                tt_decode_b<<<gb, 256, 0, s>>>(a, kpad);
+            } else {
+                const unsigned gb = (unsigned)std::min<int64_t>((kpad * npad / 2 + 255) / 256, 4096);
+                xm_decode_b<<<gb, 256, 0, s>>>(a, kpad);
+            }
             rc = hip_check("fp8a operand pre-decode launch");
             if (rc) return rc;
         }

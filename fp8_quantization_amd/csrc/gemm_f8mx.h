@@ -101,6 +101,20 @@ __device__ __forceinline__ uint32_t xm_word_a(float x, uint32_t emnA, int bR, bo
     return ((uint32_t)min(max(se, 1), 254) << 23) | (((cb >> 31) * 8u + mc) << XM_ROW_SHIFT);
 }
 
+constexpr int TT_RS = 68;  // floats per m_a row of a K-step's table (64 columns + 4: conflict-free
+                           // ds_read_b128 of 16 rows by a lane group)
+constexpr uint32_t TT_EXP = 0xFF800000u;  // sign + exponent field of c (its mantissa is zero)
+// gemm_tt_kernel's A word (gemm_tt.h): c_a's sign and exponent bits (mantissa field zero) |
+// m_a x the table row stride; zeros 0.  ok = on the (M, bA) grid and inside the exactness window.
+__device__ __forceinline__ uint32_t tt_word_a(float x, int M, uint32_t emnA, bool &ok) {
+    float c;
+    uint32_t mc;
+    ok = stage_decode(x, M, emnA, true, c, mc);
+    const uint32_t cb = __float_as_uint(c);
+    if ((cb & 0x7FFFFFFFu) == 0u) return 0u;
+    return (cb & TT_EXP) | (mc * (uint32_t)(4 * TT_RS));
+}
+
 // A pre-pass, one (image | row) per blockIdx.y step.  conv: the group's channel slice of x
 // [Bn][Cin][H][W] (channels cbase..cbase+aw_c) -> words [Bn][aw_c][awH][awW], x at (awph, awpw)
 // inside a border of zero words (the padding the convolution reads, so the wave-independent
@@ -122,8 +136,9 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
     const int64_t rows = p.conv ? p.M / (p.Ho * p.Wo) : p.M, cols = p.conv ? p.aw_c * p.awH * p.awW : p.awld;
     auto word = [&](float v, bool &ok) {
         if (p.fqin.mx) v = fq_apply(v, fmx, fbias, p.fqin.M, p.fqin.S);
-        return xm_word_a(v, emnA, bR, ok);
+        return p.wfmt ? tt_word_a(v, p.Mw, emnA, ok) : xm_word_a(v, emnA, bR, ok);
     };
+    const uint32_t zw = p.wfmt ? 0u : XM_ZERO_WORD;  // the word of a zero (padding, columns >= K)
     if (p.conv && (p.awph | p.awpw)) {  // zero-bordered image (< 2^30 words, run_gemm): 32-bit index math
         // four consecutive words per thread step (one 16-B store when the image is a multiple of
         // four words), their (c, hp, wp) stepped from the first one's
@@ -141,7 +156,7 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
                     if (j >= (int)per) break;
                     const int hy = (int)hp - p.awph, wx = (int)wp - p.awpw;
                     bool ok = true;
-                    w[j] = XM_ZERO_WORD;
+                    w[j] = zw;
                     if ((uint32_t)hy < (uint32_t)p.H && (uint32_t)wx < (uint32_t)p.W)
                         w[j] = word(in[((int64_t)c * p.H + hy) * p.W + wx], ok);
                     bad |= !ok;
@@ -172,7 +187,7 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
         if (vec) {
             for (int64_t i = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x); i < cols;
                  i += 4 * (int64_t)gridDim.x * blockDim.x) {
-                uint4 w = make_uint4(XM_ZERO_WORD, XM_ZERO_WORD, XM_ZERO_WORD, XM_ZERO_WORD);
+                uint4 w = make_uint4(zw, zw, zw, zw);
                 if (i < lim) {
                     const float4 v = *reinterpret_cast<const float4 *>(in + i);
                     bool ok0 = true, ok1 = true, ok2 = true, ok3 = true;
@@ -185,7 +200,7 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
         }
         for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cols; i += (int64_t)gridDim.x * blockDim.x) {
             bool ok = true;
-            o[i] = (i < lim) ? word(in[i], ok) : XM_ZERO_WORD;
+            o[i] = (i < lim) ? word(in[i], ok) : zw;
             bad |= !ok;
         }
     }

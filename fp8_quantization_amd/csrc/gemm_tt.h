@@ -1,0 +1,245 @@
+// gemm_tt.h -- the tile-table kernel for the wider-mantissa formats (E3M4, E2M5), included by
+// fp8approx.hip after gemm_f8mx.h (inside namespace fp8a).  DESIGN.md §3b.
+//
+// Same term as gemm_fast_kernel's table modes (v9:51-113) for on-grid operands
+// with s2n and per-product quantization, no golden clip:
+//     term = Q_R(V(m_a, m_b) c_a c_b),   V = min(sig_a sig_b - T[m_a][m_b] 2^-M, kb x its binade)
+// with c = sign 2^floor(log2|x|) and kb = 2 - 2^-M - 2^-22, Q_R's pre-clamp (the mantissa
+// saturates instead of carrying, F6, and the subnormal top tie rounds down).  The clamp scales
+// with the value's binade, and c_a c_b is a power of two, so the clamp is applied once to the
+// table value; Q_R is then its magic-constant rounding alone: pe = x & EXP, C = max(pe 1.5
+// 2^(23-M), 2^(1-bR) 1.5 2^(23-M)), r = (x + C) - C.
+//
+// Tile table.  c_b depends only on the column, so every staged K-step builds, for the tile's 64
+// columns, tt[kk][m_a][col] = V(m_a, m_b(col)) c_b(col) (2^M rows of 64 floats); the math loop
+// (lane = tile row, wave = 16 columns, as gemm_f8mx_kernel) reads its row's 16 values with four
+// ds_read_b128 and spends per product: one multiply by c_a, the 5-op rounding, one add.
+//
+// F7 (tables with negative entries): the reference takes the product's sign from Q_R(a b),
+// which is -0 (sign +) for a b in [-2^(-bR-M), 0).  Since V > 0, the term's sign is then the
+// sign of a b + 2^(-bR-M): one fma on a second table tg = sig_a sig_b c_b, and one v_bfi_b32.
+//
+// Operands are pre-decoded once per launch: an A element becomes c_a's sign and exponent bits
+// (mantissa field zero) | m_a x the table row stride in its low bits; a B element c_b's bits | m_b.
+// The pre-passes carry the fallback checks into the flag word (gemm_exact_kernel reruns).
+
+constexpr int TT_IMG_FLOATS = 2048;       // static image: V [m_b][m_a] then sig_a sig_b [m_b][m_a]
+
+template <int MW, bool F7> struct TtCfg {
+    static constexpr int NM = 1 << MW;                     // table rows (m_a codes)
+    static constexpr int XK = (4 << (F7 ? 0 : 1)) >> (MW - 3);  // K-steps per staged tile: ~17 KB of table per tile
+    static constexpr int PARTS = NM / 16;                  // build: 16 rows per thread
+    static constexpr int UNITS = XK * 64 * PARTS;          // build units (<= 256 threads)
+};
+
+// B pre-pass for gemm_tt_kernel: words [Kpad][Npad] (c_b's bits | m_b, 0 for zeros and padding),
+// and (block 0) the static image V / sig_a sig_b.
+__global__ __launch_bounds__(256) void tt_decode_b(const GemmArgs p, int64_t kpad) {
+    const int bA = *p.bA, bR = *p.bR, M = p.Mw, nm = 1 << M;
+    bool bad = !(xm_bias_ok(bA) && xm_bias_ok(bR));
+    if (blockIdx.x == 0) {
+        float *img = const_cast<float *>(reinterpret_cast<const float *>(p.lutw));
+        const float ulp = p2(-M), kb = 2.0f - p2(-M) - p2(-22);
+        for (int e = threadIdx.x; e < nm * nm; e += blockDim.x) {
+            const int mb = e >> M, ma = e & (nm - 1);
+            const float s = (1.0f + ulp * ma) * (1.0f + ulp * mb);  // exact: 2M + 2 bits
+            float v = __fmaf_rn(-(float)p.tab.raw[ma * nm + mb], ulp, s);  // exact
+            v = fminf(v, __uint_as_float(__float_as_uint(v) & 0x7F800000u) * kb);
+            img[e] = v;
+            img[TT_IMG_FLOATS / 2 + e] = s;
+        }
+    }
+    uint32_t *const bw = reinterpret_cast<uint32_t *>(const_cast<uint2 *>(p.bqw));
+    const int64_t n = kpad * p.npad;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = i / p.npad, col = i - k * p.npad;
+        uint32_t w = 0;
+        if (k < p.K && col < p.N) {
+            const int bb = p.bB[col * p.bBs];
+            float c;
+            uint32_t mc;
+            const bool ok = stage_decode(p.B[k * p.sbk + col * p.sbn], M, (uint32_t)(128 - bb) << 23, true, c, mc);
+            bad |= !ok || !xm_bias_ok(bb);
+            const uint32_t cb = __float_as_uint(c);
+            if ((cb & 0x7FFFFFFFu) != 0u) w = (cb & TT_EXP) | mc;
+        }
+        bw[i] = w;
+    }
+    if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, 1u);
+}
+
+template <int MW, bool F7> struct TtSmem {
+    using C = TtCfg<MW, F7>;
+    union {
+        struct {
+            float tt[C::XK][C::NM][TT_RS];  // V c_b
+            float tg[F7 ? C::XK : 1][F7 ? C::NM : 1][TT_RS];  // sig_a sig_b c_b (F7)
+        } t;
+        float ct[BM * XM_CP];  // epilogue transpose tile
+    } u;
+    float img[F7 ? TT_IMG_FLOATS : TT_IMG_FLOATS / 2];
+    uint32_t aw[C::XK][BM];
+};
+
+template <int MW, bool F7>
+__global__ __launch_bounds__(NT) void gemm_tt_kernel(const GemmArgs p) {
+    using C = TtCfg<MW, F7>;
+    constexpr int NM = C::NM, XK = C::XK;
+    static_assert(C::UNITS <= NT && XK >= 1 && XK <= 4, "tile-table configuration");
+    __shared__ __attribute__((aligned(16))) TtSmem<MW, F7> sm;
+    auto &tt = sm.u.t.tt;
+    auto &tg = sm.u.t.tg;
+    auto &img = sm.img;
+    auto &aw = sm.aw;
+
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wvu = __builtin_amdgcn_readfirstlane(wv);
+    const int64_t num_mt = (p.M + BM - 1) / BM;
+    const int64_t tiles = num_mt * ((p.N + BN - 1) / BN);
+    const int64_t bid = (int64_t)blockIdx.x % tiles, split = (int64_t)blockIdx.x / tiles;
+    const int64_t m0 = (bid % num_mt) * BM;
+    const int64_t n0 = (bid / num_mt) * BN;
+    const int kbeg = (int)(split * p.kchunk), kend = (int)min(p.K, (int64_t)kbeg + p.kchunk), K32 = (int)p.K;
+    const int bR = *p.bR;
+    // Q_R constants: C = max(2^floor(log2|x|) kc15, cmin); thr = the largest |a b| Q_R flushes
+    const float kc15 = 1.5f * p2(23 - MW), cmin = 1.5f * p2(1 - bR + 23 - MW), thr = p2(-bR - MW);
+
+    // static image: V (and sig_a sig_b for F7), [m_b][m_a]
+    for (int e = tid; e < NM * NM; e += NT) {
+        img[e] = reinterpret_cast<const float *>(p.lutw)[e];
+        if (F7) img[TT_IMG_FLOATS / 2 + e] = reinterpret_cast<const float *>(p.lutw)[TT_IMG_FLOATS / 2 + e];
+    }
+
+    // build unit (threads < UNITS): K-step bkk, column bcol, rows 16 bpart .. 16 bpart + 15
+    const bool bunit = tid < C::UNITS;
+    const int bcol = tid & 63, bkk = (tid >> 6) % XK, bpart = min((tid >> 6) / XK, C::PARTS - 1);
+    const uint32_t npad4 = (uint32_t)p.npad * 4u;
+    const uint32_t boff = (uint32_t)(kbeg + bkk) * npad4 + (uint32_t)(n0 + bcol) * 4u;
+    const __amdgpu_buffer_rsrc_t brsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint2 *>(p.bqw), (short)0, -1, 0x00020000);
+
+    // A staging: one word per thread (threads < XK x 64; conv: lane = row, K-step = wave; matrix:
+    // XK threads per row).  Rows past M re-read row M - 1.
+    const bool astage = tid < XK * BM;
+    const int arow = p.conv ? lane : (tid / XK), akk = p.conv ? wvu : (tid % XK);
+    uint32_t aoff;
+    const uint32_t phw = (uint32_t)(p.awH * p.awW), uW = (uint32_t)p.awW;
+    {
+        const int64_t m = min(m0 + arow, p.M - 1);
+        if (p.conv) {
+            const int64_t hw = p.Ho * p.Wo, img_i = m / hw, pix = m - img_i * hw, ho = pix / p.Wo, wo = pix - ho * p.Wo;
+            aoff = (uint32_t)(4 * (img_i * p.aw_c * (int64_t)phw + ho * p.sh * p.awW + wo * p.sw));
+        } else {
+            aoff = (uint32_t)(4 * (m * p.awld + akk));
+        }
+    }
+    const __amdgpu_buffer_rsrc_t arsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(p.aw), (short)0, -1, 0x00020000);
+    const int khw = p.kh * p.kw;
+    uint32_t wa = 0, wb = 0;
+    auto load_tile = [&](int k0) {
+        if (astage) {
+            uint32_t ko;
+            if (p.conv) {
+                const int k = k0 + akk;  // wave-uniform
+                const uint32_t c = fastdiv((uint32_t)k, p.kk_mul, p.kk_shift);
+                const uint32_t t = (uint32_t)k - c * (uint32_t)khw;
+                const uint32_t ky = fastdiv(t, p.kw_mul, p.kw_shift);
+                const uint32_t kx = t - ky * (uint32_t)p.kw;
+                ko = 4u * (c * phw + ky * (uint32_t)p.dh * uW + kx * (uint32_t)p.dw);
+            } else {
+                ko = 4u * (uint32_t)k0;
+            }
+            ko = __builtin_amdgcn_readfirstlane(ko);
+            wa = __builtin_amdgcn_raw_buffer_load_b32(arsrc, (int)aoff, (int)ko, 0);
+            if (p.conv && k0 + akk >= K32) wa = 0u;  // past the group's last channel (uniform)
+        }
+        const uint32_t kb = __builtin_amdgcn_readfirstlane((uint32_t)(k0 - kbeg) * npad4);
+        if (bunit) wb = __builtin_amdgcn_raw_buffer_load_b32(brsrc, (int)boff, (int)kb, 0);
+    };
+    load_tile(kbeg);
+
+    float acc[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] = 0.0f;
+    const uint32_t wvo = (uint32_t)wvu * 64u;  // the wave's 16 columns, bytes into a table row
+    __syncthreads();  // the static image is in LDS
+
+    for (int k0 = kbeg; k0 < kend; k0 += XK) {
+        if (astage) aw[akk][arow] = wa;
+        if (bunit) {  // build: tt[bkk][m_a][bcol] = V(m_a, m_b) c_b for the unit's 16 rows
+            const float cb = __uint_as_float(wb & TT_EXP);
+            const int mb = (int)(wb & (uint32_t)(NM - 1));
+            const float4 *vr = reinterpret_cast<const float4 *>(&img[mb * NM + 16 * bpart]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 v = vr[q];
+                tt[bkk][16 * bpart + 4 * q + 0][bcol] = v.x * cb;
+                tt[bkk][16 * bpart + 4 * q + 1][bcol] = v.y * cb;
+                tt[bkk][16 * bpart + 4 * q + 2][bcol] = v.z * cb;
+                tt[bkk][16 * bpart + 4 * q + 3][bcol] = v.w * cb;
+            }
+            if (F7) {
+                const float4 *gr = reinterpret_cast<const float4 *>(&img[TT_IMG_FLOATS / 2 + mb * NM + 16 * bpart]);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 v = gr[q];
+                    tg[bkk][16 * bpart + 4 * q + 0][bcol] = v.x * cb;
+                    tg[bkk][16 * bpart + 4 * q + 1][bcol] = v.y * cb;
+                    tg[bkk][16 * bpart + 4 * q + 2][bcol] = v.z * cb;
+                    tg[bkk][16 * bpart + 4 * q + 3][bcol] = v.w * cb;
+                }
+            }
+        }
+        __syncthreads();
+        if (k0 + XK < kend) load_tile(k0 + XK);  // next tile's loads fly during this tile's math
+
+#pragma unroll
+        for (int kk = 0; kk < XK; ++kk) {
+            const uint32_t w = aw[kk][lane];
+            const float ca = __uint_as_float(w & TT_EXP);
+            const uint32_t off = (w & ~TT_EXP) + wvo;  // m_a row | the wave's columns
+            const char *tb = reinterpret_cast<const char *>(&tt[kk][0][0]) + off;
+            float t[16];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 v = *reinterpret_cast<const float4 *>(tb + 16 * q);
+                t[4 * q] = v.x; t[4 * q + 1] = v.y; t[4 * q + 2] = v.z; t[4 * q + 3] = v.w;
+            }
+            float g[16];
+            if (F7) {
+                const char *gb = reinterpret_cast<const char *>(&tg[kk][0][0]) + off;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 v = *reinterpret_cast<const float4 *>(gb + 16 * q);
+                    g[4 * q] = v.x; g[4 * q + 1] = v.y; g[4 * q + 2] = v.z; g[4 * q + 3] = v.w;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const float x = t[j] * ca;  // exact: V c_b c_a, already pre-clamped
+                const float pe = __uint_as_float(__float_as_uint(x) & 0x7F800000u);
+                const float cc = fmaxf(pe * kc15, cmin);
+                float r = (x + cc) - cc;
+                if (F7)  // sign of a b + 2^(-bR-M) (its rounding never crosses zero)
+                    r = __uint_as_float((__float_as_uint(r) & 0x7FFFFFFFu) |
+                                        (__float_as_uint(__fmaf_rn(g[j], ca, thr)) & 0x80000000u));
+                acc[j] += r;
+            }
+        }
+        __syncthreads();
+    }
+
+    // lane = row, 16 columns -> [BM][BN] tile in LDS -> each thread's 4x4 block (store_tile)
+    float *ct = sm.u.ct;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) ct[lane * XM_CP + 16 * wv + j] = acc[j];
+    __syncthreads();
+    const int ety = tid & 15, etx = tid >> 4;
+    float o[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) o[i][j] = ct[(ety * TM + i) * XM_CP + etx * TN + j];
+    store_tile(p, split, m0, n0, ety, etx, o);
+}

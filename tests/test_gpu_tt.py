@@ -1,0 +1,219 @@
+"""The tile-table kernel for E3M4 / E2M5 (gemm_tt_kernel, csrc/gemm_tt.h).
+
+Every case reads the launch's flag word back and asserts it is 0, i.e. the pre-decoded
+tile-table path produced the result (not the gated exact kernel).  Covered, for both formats and
+every error table the reference selects for them (withComp False: E3M4 entries 0..3, E2M5 0..5;
+withComp True, dnsmp 3: entries -1..1, which make the F7 sign rule observable -- E3M4 runs its
+F7 form, E2M5 with a signed table stays on gemm_fast_kernel and is checked here all the same)
+and no table:
+  * every code pair of the format (both signs, subnormals, zeros) as a K = 1 product, bit-exact
+    against the oracle's terms, at bias triples that put the result grid's floor inside the
+    products' range (flush, subnormal band and normal results all occur);
+  * implicit-GEMM convs with padding (the zero-bordered word image), stride, dilation, groups,
+    ragged M / N and split-K against the oracle on unfolded inputs, run-to-run bit-identity;
+  * the matrix form with lda > K and a column-strided B;
+  * an off-grid activation raises the flag and the exact kernel's result is returned.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as orc
+from tests import golden_io as gio
+from fp8_quantization_amd.error_tables import get_error_table_NN
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+FMTS = [(3, 4), (2, 5)]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device")
+    from fp8_quantization_amd import _lib
+    _lib.load()
+
+
+def _table(E, M, kind):
+    if kind == "none":
+        return np.zeros((1 << M, 1 << M), np.int32)
+    return get_error_table_NN(E, M, withComp=(kind == "comp"), dnsmp_factor=3).numpy().astype(np.int32)
+
+
+def _flags(kind):
+    return orc.flags_of(approx=kind != "none", s2n=True, qbma=True)
+
+
+def _all_codes(E, M, bias):
+    """Every value of the (E, M) format at the given bias, both signs (zeros included)."""
+    e = np.repeat(np.arange(1 << E), 1 << M)
+    m = np.tile(np.arange(1 << M), 1 << E)
+    v = np.where(e == 0, np.ldexp(m / 2.0 ** M, 1 - bias), np.ldexp(1.0 + m / 2.0 ** M, e - bias))
+    return np.concatenate([v, -v]).astype(np.float32)
+
+
+def _grid(rng, E, M, shape, bias, zero_frac=0.0, sub_frac=0.05):
+    emax = (1 << E) - 1
+    bias = np.broadcast_to(np.asarray(bias), shape)
+    expo = rng.integers(1, emax + 1, size=shape)
+    mant = rng.integers(0, 1 << M, size=shape)
+    v = np.ldexp(1.0 + mant / 2.0 ** M, expo - bias)
+    sub = rng.random(shape) < sub_frac
+    v[sub] = np.ldexp(rng.integers(1, 1 << M, size=shape) / 2.0 ** M, 1 - bias)[sub]
+    v = v * rng.choice([-1.0, 1.0], size=shape)
+    v[rng.random(shape) < zero_frac] = 0.0
+    return v.astype(np.float32)
+
+
+def _dev(a, dtype=torch.float32):
+    return torch.as_tensor(np.ascontiguousarray(a)).to(dtype=dtype, device=DEV)
+
+
+def _matmul_raw(A, lda, B, sbk, sbn, Mr, N, K, E, M, bA, bB, bR, table, flags):
+    from fp8_quantization_amd import _lib
+    L = _lib.load()
+    At, Bt = _dev(A), _dev(B)
+    C = torch.empty((Mr, N), dtype=torch.float32, device=DEV)
+    ws = torch.zeros(int(L.fp8a_matmul_workspace_size_mnk(Mr, N, K)), dtype=torch.uint8, device=DEV)
+    bB = np.array(np.broadcast_to(np.asarray(bB, np.int32), (N,)))
+    tA, tB, tR = _dev([bA], torch.int32), _dev(bB, torch.int32), _dev([bR], torch.int32)
+    tab = torch.as_tensor(np.ascontiguousarray(table, np.int32))
+    rc = L.fp8a_matmul(_lib.dev_ptr(At), lda, _lib.dev_ptr(Bt), sbk, sbn, _lib.dev_ptr(C), N, Mr, N, K, E, M,
+                       _lib.dev_ptr(tA), _lib.dev_ptr(tB), 1, _lib.dev_ptr(tR), _lib.host_ptr(tab), flags,
+                       _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(DEV))
+    _lib.check(rc, "fp8a_matmul")
+    torch.cuda.synchronize()
+    return C.cpu().numpy(), int(ws[:4].view(torch.int32).item())
+
+
+def _conv_raw(x, w, E, M, bA, bW, bR, table, flags, stride, pad, dil, groups):
+    from fp8_quantization_amd import _lib
+    L = _lib.load()
+    Bn, Cin, H, W = x.shape
+    Cout, _, kh, kw = w.shape
+    Ho = (H + 2 * pad - dil * (kh - 1) - 1) // stride + 1
+    Wo = (W + 2 * pad - dil * (kw - 1) - 1) // stride + 1
+    xt, wt = _dev(x), _dev(w)
+    y = torch.empty((Bn, Cout, Ho, Wo), dtype=torch.float32, device=DEV)
+    need = int(L.fp8a_conv2d_workspace_size(Bn, Cin, H, W, Cout, kh, kw, stride, stride, pad, pad, dil, dil, groups))
+    ws = torch.zeros(need, dtype=torch.uint8, device=DEV)
+    tA, tW, tR = _dev([bA], torch.int32), _dev(bW, torch.int32), _dev([bR], torch.int32)
+    tab = torch.as_tensor(np.ascontiguousarray(table, np.int32))
+    rc = L.fp8a_conv2d(_lib.dev_ptr(xt), _lib.dev_ptr(wt), _lib.dev_ptr(y), Bn, Cin, H, W, Cout, kh, kw, stride,
+                       stride, pad, pad, dil, dil, groups, E, M, _lib.dev_ptr(tA), _lib.dev_ptr(tW), _lib.dev_ptr(tR),
+                       _lib.host_ptr(tab), flags, _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(DEV))
+    _lib.check(rc, "fp8a_conv2d")
+    torch.cuda.synchronize()
+    return y.cpu().numpy(), int(ws[:4].view(torch.int32).item())
+
+
+def _conv_ref(x, w, E, M, bA, bW, bR, table, flags, stride, pad, dil, groups):
+    Cout, cig, kh, kw = w.shape
+    cols = torch.nn.functional.unfold(torch.from_numpy(x), (kh, kw), dilation=dil, padding=pad, stride=stride)
+    cols = cols.transpose(1, 2).reshape(-1, cols.shape[1]).numpy()
+    cog, Kg = Cout // groups, cig * kh * kw
+    outs, sums = [], []
+    for g in range(groups):
+        Wg = w[g * cog:(g + 1) * cog].reshape(cog, -1).T
+        C, S = orc.matmul(cols[:, g * Kg:(g + 1) * Kg], Wg, E, M, bA, bW[g * cog:(g + 1) * cog], bR, table, flags,
+                          with_abs=True)
+        outs.append(C)
+        sums.append(S)
+    return np.concatenate(outs, 1), np.concatenate(sums, 1)
+
+
+def _close(got, ref, S, what=""):
+    bad = np.abs(got.astype(np.float64) - ref) > gio.sum_tolerance(S.astype(np.float64))
+    assert not bad.any(), f"{what}: {np.count_nonzero(bad)} outputs outside the bar"
+
+
+def _terms_equal(got, ref):
+    same = (got.view(np.uint32) == ref.view(np.uint32)) | ((got == 0) & (ref == 0))
+    if not same.all():
+        i = tuple(np.argwhere(~same)[0])
+        raise AssertionError(f"{np.count_nonzero(~same)} terms differ; first at {i}: got {got[i]!r} ref {ref[i]!r}")
+
+
+@pytest.mark.parametrize("kind", ["nocomp", "comp", "none"])
+@pytest.mark.parametrize("fmt", FMTS, ids=["E3M4", "E2M5"])
+@pytest.mark.parametrize("shift", [0, 3, 6])
+def test_every_code_pair_bitexact(fmt, kind, shift):
+    """All (2 x 2^(E+M))^2 code pairs as K = 1 products.  bR = bA + bB - shift - base puts the
+    result grid's floor among the products: flushes, the subnormal band (incl. the F7 interval
+    for the signed tables) and normal results all occur."""
+    E, M = fmt
+    bA, bB = (1 << (E - 1)) + 2, (1 << (E - 1)) + 5
+    bR = bA + bB - (1 << E) - shift
+    A = _all_codes(E, M, bA).reshape(-1, 1)
+    B = _all_codes(E, M, bB).reshape(1, -1)
+    tab, fl = _table(E, M, kind), _flags(kind)
+    C, flag = _matmul_raw(A, 1, B, B.shape[1], 1, A.shape[0], B.shape[1], 1, E, M, bA, bB, bR, tab, fl)
+    assert flag == 0, "fallback flag raised: the tile-table path did not produce these terms"
+    ref = orc.terms(A, B, E, M, bA, bB, bR, tab, fl)[:, 0, :]
+    _terms_equal(C, ref)
+
+
+CONVS = [
+    dict(B=2, cin=3, cout=64, k=7, s=2, p=3, d=1, g=1, hw=30),     # conv1 class, padding 3
+    dict(B=3, cin=16, cout=40, k=3, s=1, p=1, d=1, g=1, hw=13),    # ragged M (507), N (40), padding 1
+    dict(B=2, cin=24, cout=72, k=3, s=2, p=2, d=2, g=1, hw=17),    # dilation, N > 64
+    dict(B=2, cin=32, cout=48, k=1, s=2, p=0, d=1, g=1, hw=15),    # 1x1 downsample class, no padding
+    dict(B=2, cin=16, cout=32, k=3, s=1, p=1, d=1, g=2, hw=9),     # groups
+    dict(B=1, cin=256, cout=128, k=3, s=1, p=1, d=1, g=1, hw=7),   # split-K (K = 2304)
+]
+
+
+@pytest.mark.parametrize("kind", ["nocomp", "comp"])
+@pytest.mark.parametrize("fmt", FMTS, ids=["E3M4", "E2M5"])
+@pytest.mark.parametrize("cfg", CONVS, ids=[f"c{i}" for i in range(len(CONVS))])
+def test_conv_matches_oracle(cfg, fmt, kind):
+    E, M = fmt
+    rng = np.random.default_rng(cfg["cin"] * 31 + cfg["cout"] + E)
+    bA, bR = (1 << (E - 1)) + 3, (1 << (E - 1)) + 4
+    x = _grid(rng, E, M, (cfg["B"], cfg["cin"], cfg["hw"], cfg["hw"]), bA, zero_frac=0.45)
+    cig = cfg["cin"] // cfg["g"]
+    bW = rng.integers((1 << (E - 1)) + 5, (1 << (E - 1)) + 8, size=cfg["cout"]).astype(np.int32)
+    w = _grid(rng, E, M, (cfg["cout"], cig, cfg["k"], cfg["k"]), bW[:, None, None, None])
+    args = (cfg["s"], cfg["p"], cfg["d"], cfg["g"])
+    tab, fl = _table(E, M, kind), _flags(kind)
+    y, flag = _conv_raw(x, w, E, M, bA, bW, bR, tab, fl, *args)
+    assert flag == 0, "fallback flag raised: the tile-table path did not produce this result"
+    ref, S = _conv_ref(x, w, E, M, bA, bW, bR, tab, fl, *args)
+    _close(y.transpose(0, 2, 3, 1).reshape(-1, y.shape[1]), ref, S, str(cfg))
+    y2, _ = _conv_raw(x, w, E, M, bA, bW, bR, tab, fl, *args)
+    assert np.array_equal(y.view(np.uint32), y2.view(np.uint32)), "not deterministic"
+
+
+@pytest.mark.parametrize("fmt", FMTS, ids=["E3M4", "E2M5"])
+@pytest.mark.parametrize("shape", [(130, 300, 129), (64, 4608, 64), (257, 17, 5)])
+def test_matmul_strided_operands(shape, fmt):
+    E, M = fmt
+    Mr, K, N = shape
+    rng = np.random.default_rng(Mr + K + N + E)
+    bA, bR = (1 << (E - 1)) + 3, (1 << (E - 1)) + 4
+    lda = K + 7
+    Afull = _grid(rng, E, M, (Mr, lda), bA, zero_frac=0.4)
+    bB = rng.integers((1 << (E - 1)) + 5, (1 << (E - 1)) + 8, size=N).astype(np.int32)
+    W = _grid(rng, E, M, (N, K), bB[:, None])
+    tab, fl = _table(E, M, "comp"), _flags("comp")
+    C, flag = _matmul_raw(Afull, lda, W, 1, K, Mr, N, K, E, M, bA, bB, bR, tab, fl)
+    assert flag == 0
+    ref, S = orc.matmul(Afull[:, :K], W.T, E, M, bA, bB, bR, tab, fl, with_abs=True)
+    _close(C, ref, S, str(shape))
+
+
+@pytest.mark.parametrize("fmt", FMTS, ids=["E3M4", "E2M5"])
+def test_off_grid_operand_falls_back(fmt):
+    E, M = fmt
+    rng = np.random.default_rng(3)
+    bA, bR = (1 << (E - 1)) + 3, (1 << (E - 1)) + 4
+    x = _grid(rng, E, M, (2, 16, 9, 9), bA, zero_frac=0.3)
+    bW = np.full(32, (1 << (E - 1)) + 6, np.int32)
+    w = _grid(rng, E, M, (32, 16, 3, 3), bW[0])
+    x[1, 3, 4, 4] = 0.3001  # off the (M, bA) grid
+    tab, fl = _table(E, M, "nocomp"), _flags("nocomp")
+    y, flag = _conv_raw(x, w, E, M, bA, bW, bR, tab, fl, 1, 1, 1, 1)
+    assert flag != 0, "pre-decode did not flag the launch"
+    ref, S = _conv_ref(x, w, E, M, bA, bW, bR, tab, fl, 1, 1, 1, 1)
+    _close(y.transpose(0, 2, 3, 1).reshape(-1, y.shape[1]), ref, S, "off-grid")
