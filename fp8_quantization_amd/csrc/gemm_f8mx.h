@@ -46,6 +46,7 @@
 
 typedef int xm_v8i __attribute__((ext_vector_type(8)));
 typedef float xm_v16f __attribute__((ext_vector_type(16)));
+typedef float xm_v4f __attribute__((ext_vector_type(4)));
 typedef short xm_s2 __attribute__((ext_vector_type(2)));
 typedef unsigned short xm_u2 __attribute__((ext_vector_type(2)));
 typedef __bf16 xm_b2 __attribute__((ext_vector_type(2)));
@@ -56,7 +57,7 @@ constexpr uint32_t XM_ROW_SHIFT = 3, XM_ROW_MASK = 0x78u;  // A word bits 3-6: r
 constexpr int XBK = 8;                         // K-steps per staged tile
 constexpr int XM_TTK = 16 * 32 + 16;           // tile-table words per K-step: [tx 16][row 16][j 2] + bank shift
 constexpr uint32_t XM_ZERO_WORD = 254u << 23;  // A = 0: cvt scale 2^127 (the code is 0), row 0
-// A words in LDS: [kk / 4][row][kk % 4] -- one ds_read_b128 gives a row's words of four K-steps
+// A words in LDS: [kk / 4][row][kk % 4] -- one ds_read_b64 gives a row's words of a K-step pair
 constexpr int XM_AWQ = 4 * BM + 4;
 struct XmSmem {
     uint32_t tt[XBK][XM_TTK];  // c_b-applied pairs [kk][tx][row][j] (first: its byte offsets are the reads' immediates)
@@ -254,16 +255,14 @@ __global__ __launch_bounds__(256) void xm_decode_b(const GemmArgs p, int64_t kpa
 #ifndef XM_WAVES
 #define XM_WAVES 1
 #endif
-#ifndef XM_ABL
-#define XM_ABL 0  // timing-only ablations (wrong results): 1 no table reads, 2 no conversions, 4 no table build
-#endif
-// The GEMM.  Tile 64 x 64, 4 waves.  Math mapping: lane = tile row, wave wv = the 16 columns
-// 16 wv .. 16 wv + 15 (column blocks tx = 4 wv + c of the tile table).  Per K-step and lane: the
-// row's A word (four K-steps per ds_read_b128), ONE v_and_or_b32 (row offset | the wave's column
-// base; block c and the K-step are the reads' immediates), four ds_read_b64 (16 columns), eight
-// conversions; one MFMA per two K-steps.  Operands are read through buffer descriptors: uniform
-// K-step offsets in SGPRs, 32-bit lane offsets (run_gemm keeps the word images below 2^32 bytes);
-// the conv word image carries the zero padding (xm_decode_a), so the gather has no bounds checks.
+// The GEMM.  Tile 64 x 64, 4 waves; wave wv = the 16 columns 16 wv .. 16 wv + 15 (column blocks
+// tx = 4 wv + c of the tile table).  Math mapping: lane = (row r16 of each 16-row block, K-step
+// pair g of the 8-step tile).  Per A element (row, K-step): ONE v_and_or_b32 (row offset | the
+// wave's column base + the K-step's table offset; block c in the reads' immediates), four
+// ds_read_b64 (16 columns), eight conversions; per 16-row block and tile one 16x16x128 MFMA sums
+// the 4 lane groups' 2 K-steps.  Operands are read through buffer descriptors: uniform K-step
+// offsets in SGPRs, 32-bit lane offsets (run_gemm keeps the word images below 2^32 bytes); the
+// conv word image carries the zero padding (xm_decode_a), so the gather has no bounds checks.
 __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs p) {
     __shared__ __attribute__((aligned(16))) XmSmem sm;
 
@@ -345,22 +344,24 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
     };
     load_tile(kbeg);
 
-    // the constant 0/1 selection operand: lane (n + 32 h) holds column n, k-half h; byte p of it
-    // is 1.0 (e4m3 0x38) where the same byte of A lane (m + 32 h) holds a code of output n mod 16
+    // the constant 0/1 selection operand of v_mfma_scale_f32_16x16x128_f8f6f4: lane (n + 16 g)
+    // holds column n, K-block g; byte p is 1.0 (e4m3 0x38) where (p & 15) == n, i.e. where the same
+    // byte of an A lane holds a code of output column n
     xm_v8i sel;
     {
-        const int n = lane & 31, h = lane >> 5;
+        const int n = lane & 15;
 #pragma unroll
         for (int v = 0; v < 8; ++v) {
             uint32_t w = 0;
 #pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int pb = 4 * v + b;
-                if ((n >> 4) == h && (pb & 15) == (n & 15)) w |= 0x38u << (8 * b);
-            }
+            for (int b = 0; b < 4; ++b)
+                if (((4 * v + b) & 15) == n) w |= 0x38u << (8 * b);
             sel[v] = (int)w;
         }
     }
+    xm_v4f dq[4];  // one 16x16 accumulator per 16-row block
+#pragma unroll
+    for (int b = 0; b < 4; ++b) dq[b] = (xm_v4f){0.0f, 0.0f, 0.0f, 0.0f};
     xm_v16f dacc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) dacc[r] = 0.0f;
@@ -383,75 +384,73 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
             const xm_u2 n0 = __builtin_bit_cast(xm_u2, b.x ^ 0x80008000u), n1 = __builtin_bit_cast(xm_u2, b.z ^ 0x80008000u);
             auto pk = [](uint32_t v, xm_u2 ad) { return __builtin_bit_cast(uint32_t, __builtin_bit_cast(xm_u2, v) + ad); };
             uint32_t *d = &sm.tt[bkk[u]][btx * 32 + q4 * 4];
-#if !(XM_ABL & 4)
             *reinterpret_cast<uint4 *>(d) = make_uint4(pk(s0.x, a0), pk(s1.x, a1), pk(s0.y, a0), pk(s1.y, a1));
             *reinterpret_cast<uint4 *>(d + 16) = make_uint4(pk(s0.x, n0), pk(s1.x, n1), pk(s0.y, n0), pk(s1.y, n1));
-#else
-            if (b.x == 0x12345u) *d = pk(s0.x, a0) ^ pk(s1.y, n1);
-#endif
         }
         __syncthreads();
         if (k0 + XBK < kend) load_tile(k0 + XBK);  // next tile's loads fly during this tile's math
 
+        // lane = (row r16 of each 16-row block, K-step pair g): per row block its A words of
+        // K-steps 2 g, 2 g + 1 (one ds_read_b64), 16 columns each, one 16x16x128 MFMA summing the
+        // block's 8 K-steps (4 lane groups x 2) -- half the matrix-pipe cycles of the 32x32 form
+        {
+            const int r16 = lane & 15, g = lane >> 4;
+            const uint32_t base = wvo + (uint32_t)(2 * g) * (uint32_t)(XM_TTK * 4);  // multiple of 128 B
+            const char *tt0 = reinterpret_cast<const char *>(&sm.tt[0][0]);
 #pragma unroll
-        for (int q = 0; q < XBK / 4; ++q) {
-            const uint4 aq = *reinterpret_cast<const uint4 *>(&sm.aw[q][lane * 4]);
-            const uint32_t awq[4] = {aq.x, aq.y, aq.z, aq.w};
+            for (int b = 0; b < 4; ++b) {
+                const uint2 aw2 = *reinterpret_cast<const uint2 *>(&sm.aw[g >> 1][(16 * b + r16) * 4 + 2 * (g & 1)]);
+                const uint32_t awh[2] = {aw2.x, aw2.y};
 #pragma unroll
-            for (int k4 = 0; k4 < 4; ++k4) {
-                const int kk = 4 * q + k4;
-                uint32_t a;  // (row offset | the wave's column base) in one v_and_or_b32
-                asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(a) : "v"(awq[k4]), "s"(XM_ROW_MASK), "v"(wvo));
-                __builtin_assume((a & 7u) == 0u);
-                // (volatile: otherwise the two halves, used as different types, are split into two
-                // loads and re-merged into a ds_read2_b32 -- half the LDS rate of ds_read_b64)
-                xm_lds_u64 *ttk = (xm_lds_u64 *)(&sm.tt[kk][0]);
-                uint2 v[4];
+                for (int h = 0; h < 2; ++h) {
+                    uint32_t a;
+                    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(a) : "v"(awh[h]), "s"(XM_ROW_MASK), "v"(base));
+                    __builtin_assume((a & 7u) == 0u);
+                    // (volatile: otherwise the two halves, used as different types, are split into
+                    // two loads and re-merged into a ds_read2_b32 -- half the LDS rate of ds_read_b64)
+                    xm_lds_u64 *ttk = (xm_lds_u64 *)(tt0 + h * XM_TTK * 4);
+                    uint2 v[4];
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
-#if !(XM_ABL & 1)
-                    const uint64_t w = ttk[(a >> 3) + 16 * c];
-                    v[c] = make_uint2((uint32_t)w, (uint32_t)(w >> 32));
-#else
-                    v[c] = make_uint2(a + c, a ^ c);
-#endif
+                    for (int c = 0; c < 4; ++c) {
+                        const uint64_t w = ttk[(a >> 3) + 16 * c];
+                        v[c] = make_uint2((uint32_t)w, (uint32_t)(w >> 32));
+                    }
+                    const float sc = __uint_as_float(awh[h]);
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        xm_s2 cv;
+                        asm("v_cvt_scalef32_pk_fp8_bf16 %0, %1, %2" : "=v"(cv) : "v"(v[c].x), "v"(sc));
+                        cv = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(cv, __builtin_bit_cast(xm_b2, v[c].y), sc, true);
+                        av[4 * h + c] = __builtin_bit_cast(int, cv);
+                    }
                 }
-                const float sc = __uint_as_float(awq[k4]);  // the conversion reads only its exponent field
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-#if !(XM_ABL & 2)
-                    xm_s2 cv;  // low word: no input register needed (see the f32 form)
-                    asm("v_cvt_scalef32_pk_fp8_bf16 %0, %1, %2" : "=v"(cv) : "v"(v[c].x), "v"(sc));
-                    cv = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(cv, __builtin_bit_cast(xm_b2, v[c].y), sc, true);
-                    av[4 * (kk & 1) + c] = __builtin_bit_cast(int, cv);
-#else
-                    av[4 * (kk & 1) + c] = (int)(v[c].x ^ v[c].y);
-#endif
-                }
-                if (kk & 1) dacc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av, sel, dacc, 0, 0, 0, 127, 0, 127);
+                dq[b] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, sel, dq[b], 0, 0, 0, 127, 0, 127);
             }
         }
         __syncthreads();
     }
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dacc[4 * b + i] = dq[b][i];
 
     // a term beyond the e4m3 range came back NaN (and poisons its column): the exact kernel
     // reruns the launch
     bool nan = false;
 #pragma unroll
     for (int r = 0; r < 16; ++r) nan |= __builtin_isnan(dacc[r]);
-    if (__syncthreads_or(nan ? 1 : 0) && tid == 0 && !XM_ABL) atomicOr(p.flag, 1u);
+    if (__syncthreads_or(nan ? 1 : 0) && tid == 0) atomicOr(p.flag, 1u);
 
-    // D (units of 2^(7-bR)): D[m][n] is output n mod 16 of lane m + 32 (n / 16), i.e. tile row
-    // m + 32 (n / 16), column 16 wv + n mod 16 -> [BM][BN] tile in LDS -> each thread's 4x4
-    // block, epilogue mapping with consecutive lanes on consecutive pixels (coalesced NCHW stores)
+    // D (units of 2^(7-bR)) of row block b: lane l holds rows 4 (l >> 4) .. + 3, column l & 15
+    // -> tile row 16 b + 4 (l >> 4) + i, column 16 wv + (l & 15) -> [BM][BN] tile in LDS -> each
+    // thread's 4x4 block, epilogue mapping with consecutive lanes on consecutive pixels
     const float f8S = __uint_as_float((uint32_t)min(max(134 - bR, 1), 254) << 23);
     float *ct = reinterpret_cast<float *>(&sm);
     {
-        const int n = lane & 31, o = n & 15;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5) + 32 * (n >> 4);
-            ct[row * XM_CP + 16 * wv + o] = dacc[r] * f8S;
+            const int row = 16 * (r >> 2) + 4 * (lane >> 4) + (r & 3);
+            ct[row * XM_CP + 16 * wv + (lane & 15)] = dacc[r] * f8S;
         }
     }
     __syncthreads();
