@@ -1226,12 +1226,35 @@ static bool no_mx() {
     return v;
 }
 
-// Words of the pre-decoded A operand: conv, the group's zero-bordered word image
-// [Bn][aw_c][H + 2 ph][W + 2 pw]; matrix, [M][Kpad].
+// The conv word image: every plane is the input plane inside a zero border at least as wide as
+// the convolution's padding -- ph rows above and below; pw columns on the left, widened to 4 when
+// W % 4 == 0 so that the interior rows start 16-B aligned, and the row length rounded up to a
+// multiple of 4 (the pre-decode then moves the interior with 16-B loads and stores).
+struct WordImage {
+    int64_t H, W;    // image height / width (words)
+    int ph, pw;      // top / left border
+};
+static WordImage word_image(int64_t H, int64_t W, int ph, int pw) {
+    WordImage w;
+    w.ph = ph;
+    w.H = H + 2 * ph;
+    if (pw > 0 && pw <= 4 && W % 4 == 0) {
+        w.pw = 4;
+        w.W = (W + 4 + pw + 3) / 4 * 4;
+    } else {
+        w.pw = pw;
+        w.W = W + 2 * pw;
+    }
+    return w;
+}
+
+// Words of the pre-decoded A operand: conv, the group's word image [Bn][aw_c][awH][awW]; matrix,
+// [M][Kpad].
 static int64_t xm_a_words(const GemmArgs &a) {
     const int64_t kpad = (a.K + BK - 1) / BK * BK;
     if (!a.conv) return a.M * kpad;
-    return (a.M / (a.Ho * a.Wo)) * a.aw_c * (a.H + 2 * a.ph) * (a.W + 2 * a.pw);
+    const WordImage w = word_image(a.H, a.W, a.ph, a.pw);
+    return (a.M / (a.Ho * a.Wo)) * a.aw_c * w.H * w.W;
 }
 
 // Fast tiled kernel + gated exact kernel (int-bias path), or the exact kernel alone (tb path).
@@ -1285,7 +1308,8 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
         const size_t off = FLAG_BYTES + (a.splits > 1 ? splitk_bytes(a.M, a.N, a.K) : 0);
         // gemm_f8mx_kernel reads its operands with 32-bit byte offsets
         const int64_t a_words = xm_a_words(a);
-        a.awH = a.H + 2 * a.ph; a.awW = a.W + 2 * a.pw; a.awph = a.ph; a.awpw = a.pw;
+        const WordImage wi = word_image(a.H, a.W, a.ph, a.pw);
+        a.awH = wi.H; a.awW = wi.W; a.awph = wi.ph; a.awpw = wi.pw;
         const bool fits32 = a_words < (1ll << 30) && kpad * npad * 4 < (1ll << 32);
         if (fits32 && ws_bytes >= off + xm_operand_bytes(a.N, a.K, a_words)) {
             char *base = (char *)ws + off;
@@ -1444,7 +1468,8 @@ size_t fp8a_conv2d_workspace_size(int64_t Bn, int64_t Cin, int64_t H, int64_t W,
     if (Mrows <= 0 || Kg <= 0) return FLAG_BYTES;
     if (cog == 1) return FLAG_BYTES + (size_t)(Bn * Cin * H * W) * 4;  // tensor-bias kernels: A words
     // A words: the zero-bordered word image of gemm_f8mx_kernel (xm_a_words)
-    return gemm_workspace_bytes(Mrows, cog, Kg, Bn * (Cin / groups) * (H + 2 * ph) * (W + 2 * pw));
+    const WordImage wi = word_image(H, W, ph, pw);
+    return gemm_workspace_bytes(Mrows, cog, Kg, Bn * (Cin / groups) * wi.H * wi.W);
 }
 
 int fp8a_conv2d(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
@@ -1563,7 +1588,8 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
         int mode;
         rc = pack_table(table, Mw, (flags & (F_APPROX | F_V5)) != 0, tp, mode);
         if (rc) return rc;
-        const int64_t a_words = Bn * cig * (H + 2 * ph) * (W + 2 * pw);  // as xm_a_words / run_gemm
+        const WordImage wi = word_image(H, W, ph, pw);
+        const int64_t a_words = Bn * cig * wi.H * wi.W;  // as xm_a_words / run_gemm
         const int64_t kpad = (Kg + BK - 1) / BK * BK, npad = (cog + BN - 1) / BN * BN;
         const bool fused = f8_form(E, Mw, flags & ~F_TB, mode) && !no_mx() && a_words < (1ll << 30) &&
                            kpad * npad * 4 < (1ll << 32) &&

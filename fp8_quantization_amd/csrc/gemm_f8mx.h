@@ -141,35 +141,47 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
     };
     const uint32_t zw = p.wfmt ? 0u : XM_ZERO_WORD;  // the word of a zero (padding, columns >= K)
     if (p.conv && (p.awph | p.awpw)) {  // zero-bordered image (< 2^30 words, run_gemm): 32-bit index math
-        // four consecutive words per thread step (one 16-B store when the image is a multiple of
-        // four words), their (c, hp, wp) stepped from the first one's
-        const uint32_t ucols = (uint32_t)cols, phw = (uint32_t)(p.awH * p.awW), uW = (uint32_t)p.awW;
-        const bool v4 = (ucols % 4 == 0) && (((uintptr_t)out & 15) == 0);
-        const uint32_t per = v4 ? 4u : 1u;
+        // interior: four input elements per thread step along W, one 16-B load and one 16-B store
+        // when W % 4 == 0 (run_gemm's word_image aligns the interior rows), else one element;
+        // then the border words (zero) of every plane
+        const uint32_t uW = (uint32_t)p.W, uH = (uint32_t)p.H, Wp = (uint32_t)p.awW, Hp = (uint32_t)p.awH;
+        const uint32_t hwin = uH * uW, ph = (uint32_t)p.awph, pw = (uint32_t)p.awpw, pr = Wp - uW - pw;
+        const uint32_t nin = (uint32_t)p.aw_c * hwin;
+        const bool v4 = (uW % 4 == 0) && (Wp % 4 == 0) && (pw % 4 == 0) &&
+                        (((uintptr_t)(p.X + p.cbase * hw) & 15) == 0) && ((p.Cin * hw) % 4 == 0) &&
+                        (((uintptr_t)out & 15) == 0) && (cols % 4 == 0);
+        const uint32_t per = v4 ? 4u : 1u, nb = 2 * ph * Wp + (pw + pr) * uH;  // border words per plane
+        const uint32_t tstride = gridDim.x * blockDim.x, t0 = blockIdx.x * blockDim.x + threadIdx.x;
         for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) {
             const float *in = p.X + (r * p.Cin + p.cbase) * hw;
             uint32_t *o = out + r * cols;
-            for (uint32_t i = per * (blockIdx.x * blockDim.x + threadIdx.x); i < ucols; i += per * gridDim.x * blockDim.x) {
-                uint32_t c = i / phw, t = i - c * phw, hp = t / uW, wp = t - hp * uW;
-                uint32_t w[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    if (j >= (int)per) break;
-                    const int hy = (int)hp - p.awph, wx = (int)wp - p.awpw;
+            for (uint32_t e = per * t0; e < nin; e += per * tstride) {
+                const uint32_t c = e / hwin, t = e - c * hwin, hy = t / uW, wx = t - hy * uW;
+                uint32_t *d = o + (c * Hp + hy + ph) * Wp + pw + wx;
+                if (v4) {
+                    const float4 v = *reinterpret_cast<const float4 *>(in + e);
+                    bool ok0 = true, ok1 = true, ok2 = true, ok3 = true;
+                    *reinterpret_cast<uint4 *>(d) = make_uint4(word(v.x, ok0), word(v.y, ok1), word(v.z, ok2), word(v.w, ok3));
+                    bad |= !(ok0 && ok1 && ok2 && ok3);
+                } else {
                     bool ok = true;
-                    w[j] = zw;
-                    if ((uint32_t)hy < (uint32_t)p.H && (uint32_t)wx < (uint32_t)p.W)
-                        w[j] = word(in[((int64_t)c * p.H + hy) * p.W + wx], ok);
+                    d[0] = word(in[e], ok);
                     bad |= !ok;
-                    if (++wp == uW) {  // next line (and channel)
-                        wp = 0;
-                        if (++hp == (uint32_t)p.awH) { hp = 0; ++c; }
-                    }
                 }
-                if (v4)
-                    *reinterpret_cast<uint4 *>(o + i) = make_uint4(w[0], w[1], w[2], w[3]);
-                else
-                    o[i] = w[0];
+            }
+            for (uint32_t j = t0; j < (uint32_t)p.aw_c * nb; j += tstride) {
+                const uint32_t c = j / nb, t = j - c * nb;
+                uint32_t row, col;
+                if (t < 2 * ph * Wp) {  // top / bottom rows
+                    const uint32_t rr = t / Wp;
+                    row = rr < ph ? rr : uH + rr;
+                    col = t - rr * Wp;
+                } else {  // left / right margins of the interior rows
+                    const uint32_t u = t - 2 * ph * Wp, rr = u / (pw + pr), sc = u - rr * (pw + pr);
+                    row = ph + rr;
+                    col = sc < pw ? sc : uW + sc;
+                }
+                o[(c * Hp + row) * Wp + col] = zw;
             }
         }
         if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, 1u);
@@ -309,7 +321,7 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
         const int64_t m = min(m0 + arow[r], p.M - 1);
         if (p.conv) {
             const int64_t hw = p.Ho * p.Wo, img = m / hw, pix = m - img * hw, ho = pix / p.Wo, wo = pix - ho * p.Wo;
-            aoff[r] = (uint32_t)(4 * (img * p.aw_c * (int64_t)phw + ho * p.sh * p.awW + wo * p.sw));
+            aoff[r] = (uint32_t)(4 * (img * p.aw_c * (int64_t)phw + ho * p.sh * p.awW + wo * p.sw + (p.awpw - p.pw)));
         } else {
             aoff[r] = (uint32_t)(4 * (m * p.awld + akk[r]));
         }

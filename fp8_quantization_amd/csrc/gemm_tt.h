@@ -128,7 +128,7 @@ __global__ __launch_bounds__(NT) void gemm_tt_kernel(const GemmArgs p) {
         const int64_t m = min(m0 + arow, p.M - 1);
         if (p.conv) {
             const int64_t hw = p.Ho * p.Wo, img_i = m / hw, pix = m - img_i * hw, ho = pix / p.Wo, wo = pix - ho * p.Wo;
-            aoff = (uint32_t)(4 * (img_i * p.aw_c * (int64_t)phw + ho * p.sh * p.awW + wo * p.sw));
+            aoff = (uint32_t)(4 * (img_i * p.aw_c * (int64_t)phw + ho * p.sh * p.awW + wo * p.sw + (p.awpw - p.pw)));
         } else {
             aoff = (uint32_t)(4 * (m * p.awld + akk));
         }

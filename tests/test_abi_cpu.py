@@ -50,10 +50,13 @@ def test_workspace_queries_are_host_only():
     # depthwise (single output channel per group): the tensor-bias kernels need the flag word and
     # the E4M3 table form's input words (the v5 mode takes the GEMM path, unsplit, no pre-decode)
     assert L.fp8a_conv2d_workspace_size(2, 8, 6, 6, 8, 3, 3, 1, 1, 1, 1, 1, 1, 8) == flag + 2 * 8 * 6 * 6 * 4
-    # implicit-GEMM conv: no im2col image; the A words of one group's input slice, zero-bordered
-    # by the padding (H + 2 ph) x (W + 2 pw), + B column pairs + the table image (unsplit here)
+    # implicit-GEMM conv: no im2col image; the A words of one group's input slice in a zero
+    # border (ph rows above / below; W % 4 == 0: a 4-word left margin and rows rounded up to 4
+    # words, here 8 + 4 + 1 -> 16), + B column pairs + the table image (unsplit here)
     n2 = L.fp8a_conv2d_workspace_size(2, 3, 8, 8, 4, 3, 3, 1, 1, 1, 1, 1, 1, 1)
-    assert n2 == flag + _a256(2 * 3 * 10 * 10 * 4) + _a256(32 * 64 // 2 * 8) + 16384
+    assert n2 == flag + _a256(2 * 3 * 10 * 16 * 4) + _a256(32 * 64 // 2 * 8) + 16384
+    n3 = L.fp8a_conv2d_workspace_size(2, 3, 7, 7, 4, 3, 3, 1, 1, 1, 1, 1, 1, 1)  # W % 4 != 0: 9 x 9
+    assert n3 == flag + _a256(2 * 3 * 9 * 9 * 4) + _a256(32 * 64 // 2 * 8) + 16384
     assert L.fp8a_conv2d_workspace_size(256, 3, 224, 224, 4, 7, 7, 2, 2, 3, 3, 1, 1, 1) >= flag + 256 * 3 * 230 * 230 * 4
 
 
