@@ -1095,8 +1095,10 @@ static void launch_fast(int mode, const GemmArgs &a, hipStream_t s) {
     if (mode == TM_F8) {  // s2n + qbma, no golden clip (selected in run_gemm)
         // matrix-core accumulation on pre-decoded operands (gemm_f8mx.h) when run_gemm staged
         // them, else the VALU-accumulating form
-        if (a.aw)
-            gemm_f8mx_kernel<<<grid, NT, 0, s>>>(a);
+        if (a.aw) {
+            const int64_t xt = ((a.M + XM_BM - 1) / XM_BM) * ((a.N + BN - 1) / BN);
+            gemm_f8mx_kernel<<<dim3((unsigned)(xt * a.splits)), XM_NT, 0, s>>>(a);
+        }
         else
             gemm_fast_kernel<true, true, false, TM_F8><<<grid, NT, 0, s>>>(a);
         return;

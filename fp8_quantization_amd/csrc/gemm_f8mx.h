@@ -8,10 +8,10 @@
 // its binade) is an LDS table value and e4m3() is gfx950's scaled fp8 conversion (RNE; the bR
 // grid is the OCP e4m3 grid scaled by 2^(7-bR), subnormal band included).
 //
-// Summation on the matrix core: the fp8 codes are not decoded and added on the VALU; one
-// v_mfma_scale_f32_32x32x64_f8f6f4 per two K-steps multiplies the wave's 2048 codes by a
-// constant 0/1 selection operand S, so that
-//     D[m][n] += the two K-steps' codes of output (n mod 16) of lane m + 32 (n / 16).
+// Summation on the matrix core: the fp8 codes are not decoded and added on the VALU; per 16-row
+// block and staged tile one v_mfma_scale_f32_16x16x128_f8f6f4 multiplies the wave's 2048 codes
+// (16 rows x 8 K-steps x 16 columns) by a constant 0/1 selection operand S, so that
+//     D[m][n] += the 8 K-steps' codes of output (row m of the block, column n of the wave).
 // Products with 1.0 and 0 are exact and D is fp32 in units of 2^(7-bR): the sum differs from an
 // in-order fp32 sum only by accumulation order, inside the reference's own order freedom
 // (v9:113, torch's sum) and the 1e-5 * sum|term| bar.
@@ -27,11 +27,14 @@
 // Tile table.  c_b depends only on the column, so the packed add is done ONCE per staged K-step
 // and column pair for all 16 rows (8 s_a + m_a), not once per product: each staged tile builds
 // tt[kk][tx][row][j] = V'(row, pair 2 tx + j) (+) c_b (2 KiB per K-step) from the static table,
-// and the math loop reads, per A element, the thread's 4 columns with ONE ds_read_b64 at
-// (row offset | column block) + kk * stride: one v_and_or per A element, one conversion per
-// product pair, no packed add.  The build's stores are conflict-free because odd K-steps sit
-// 16 banks over (stride 528 words); the math loop's reads are conflict-free because each
-// 32-lane group holds one even and one odd column block (64-bank ds_read_b64 banking).
+// and the math loop reads, per A element, 4 columns per ds_read_b64 at (row offset | column
+// block) + kk * stride: one v_and_or per A element (16 columns), one conversion per product
+// pair, no packed add.  The build's stores are conflict-free because odd K-steps sit 16 banks
+// over (stride 528 words); the math loop's reads are conflict-free because each 32-lane group
+// holds an even and an odd K-step (64-bank ds_read_b64 banking).  The tile is 128 rows x 64
+// columns, so each table build serves 128 rows (the VALU is the limit: per 8192 products a
+// wave spends 64 conversions at ~2.7x an add, and the build's packed adds are the largest
+// remaining share -- DESIGN.md §3a).
 //
 // Operands are decoded ONCE per launch by two pre-pass kernels (xm_decode_a / xm_decode_b):
 // an A element becomes one 32-bit word (cvt scale exponent << 23 | table row offset; the
@@ -57,15 +60,26 @@ constexpr uint32_t XM_ROW_SHIFT = 3, XM_ROW_MASK = 0x78u;  // A word bits 3-6: r
 constexpr int XBK = 8;                         // K-steps per staged tile
 constexpr int XM_TTK = 16 * 32 + 16;           // tile-table words per K-step: [tx 16][row 16][j 2] + bank shift
 constexpr uint32_t XM_ZERO_WORD = 254u << 23;  // A = 0: cvt scale 2^127 (the code is 0), row 0
-// A words in LDS: [kk / 4][row][kk % 4] -- one ds_read_b64 gives a row's words of a K-step pair
-constexpr int XM_AWQ = 4 * BM + 4;
+// A words in LDS: [kk / 2][row][kk % 2] -- one ds_write_b64 stores (and one ds_read_b64 reads) a
+// row's words of a K-step pair; the pair arrays sit 32 banks apart, so the math loop's reads
+// (lane groups of K-step pairs g, g + 1) and the staging's stores are conflict-free
+#ifndef XM_RB
+#define XM_RB 8  // 16-row blocks per wave
+#endif
+#ifndef XM_NWV
+#define XM_NWV 4  // waves per workgroup: 4 column groups x XM_NWV / 4 row groups
+#endif
+constexpr int XM_NT = 64 * XM_NWV;               // threads per workgroup
+constexpr int XM_BM = 16 * XM_RB * (XM_NWV / 4);  // tile rows
+static_assert((XM_RB == 4 || XM_RB == 8) && (XM_NWV == 4 || XM_NWV == 8), "gemm_f8mx_kernel tile shape");
+constexpr int XM_AWQ = 2 * XM_BM + 32;
 struct XmSmem {
     uint32_t tt[XBK][XM_TTK];  // c_b-applied pairs [kk][tx][row][j] (first: its byte offsets are the reads' immediates)
     uint32_t lut[XM_LUT_WORDS];
-    uint32_t aw[XBK / 4][XM_AWQ];  // A(m, k)'s word: cvt scale exponent << 23 | row << 3
+    uint32_t aw[XBK / 2][XM_AWQ];  // A(m, k)'s word: cvt scale exponent << 23 | row << 3
 };
-constexpr int XM_CP = BN + 1;  // epilogue transpose tile [BM][BN + 1] floats, aliased on XmSmem
-static_assert(sizeof(float) * BM * XM_CP <= sizeof(XmSmem), "epilogue tile must fit the staging LDS");
+constexpr int XM_CP = BN + 1;  // epilogue transpose slice [64][BN + 1] floats, aliased on XmSmem
+static_assert(sizeof(float) * 64 * XM_CP <= sizeof(XmSmem), "epilogue slice must fit the staging LDS");
 
 // Exactness / range window shared by the pre-passes (as bias_ok in gemm_fast_kernel)
 __device__ __forceinline__ bool xm_bias_ok(int b) { return b >= -100 && b <= 120; }
@@ -265,93 +279,99 @@ __global__ __launch_bounds__(256) void xm_decode_b(const GemmArgs p, int64_t kpa
 }
 
 #ifndef XM_WAVES
-#define XM_WAVES 1
+#define XM_WAVES 6  // register bound: 80 VGPRs, 6 waves / SIMD (the LDS allows 6 workgroups / CU)
 #endif
-// The GEMM.  Tile 64 x 64, 4 waves; wave wv = the 16 columns 16 wv .. 16 wv + 15 (column blocks
-// tx = 4 wv + c of the tile table).  Math mapping: lane = (row r16 of each 16-row block, K-step
-// pair g of the 8-step tile).  Per A element (row, K-step): ONE v_and_or_b32 (row offset | the
+// The GEMM.  Tile XM_BM x 64 (128 x 64), XM_NWV waves (4); wave wv = column group wc = wv & 3
+// (the 16 columns 16 wc .. 16 wc + 15, column blocks tx = 4 wc + c of the tile table) and row
+// group wr = wv >> 2 (16 XM_RB rows).  Math mapping: lane = (row r16 of each of the wave's XM_RB
+// 16-row blocks, K-step pair g of the 8-step tile).  Per A element (row, K-step): ONE v_and_or_b32 (row offset | the
 // wave's column base + the K-step's table offset; block c in the reads' immediates), four
 // ds_read_b64 (16 columns), eight conversions; per 16-row block and tile one 16x16x128 MFMA sums
 // the 4 lane groups' 2 K-steps.  Operands are read through buffer descriptors: uniform K-step
 // offsets in SGPRs, 32-bit lane offsets (run_gemm keeps the word images below 2^32 bytes); the
 // conv word image carries the zero padding (xm_decode_a), so the gather has no bounds checks.
-__global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs p) {
+__global__ __launch_bounds__(XM_NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs p) {
     __shared__ __attribute__((aligned(16))) XmSmem sm;
 
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wvu = __builtin_amdgcn_readfirstlane(wv);
-    const int64_t num_mt = (p.M + BM - 1) / BM;
+    const int wc = wvu & 3, wr = wvu >> 2;  // the wave's column group and row group
+    const int64_t num_mt = (p.M + XM_BM - 1) / XM_BM;
     const int64_t tiles = num_mt * ((p.N + BN - 1) / BN);
     const int64_t bid = (int64_t)blockIdx.x % tiles, split = (int64_t)blockIdx.x / tiles;
-    const int64_t m0 = (bid % num_mt) * BM;
+    const int64_t m0 = (bid % num_mt) * XM_BM;
     const int64_t n0 = (bid / num_mt) * BN;
     const int kbeg = (int)(split * p.kchunk), kend = (int)min(p.K, (int64_t)kbeg + p.kchunk), K32 = (int)p.K;
     const int bR = *p.bR;
 
     // table: copied from the launch's pre-computed image (xm_decode_b), 16-B per thread and step
-    for (int e = 4 * tid; e < XM_LUT_WORDS; e += 4 * NT)
+    for (int e = 4 * tid; e < XM_LUT_WORDS; e += 4 * XM_NT)
         *reinterpret_cast<uint4 *>(&sm.lut[e]) = *reinterpret_cast<const uint4 *>(&p.lutw[e]);
 
-    // tile-table build units: thread = (m_a pair q4, column block btx, two K-steps bkk[u]); the
-    // 8 lanes of a ds_write_b128 group are 4 q4 x an even and an odd K-step (16 banks apart)
+    // tile-table build units e = tid + XM_NT u (512 per tile): (m_a pair q4, column block btx,
+    // K-step bkk[u]); the 8 lanes of a ds_write_b128 group are 4 q4 x an even and an odd K-step
+    // (16 banks apart)
+    constexpr int BU = 512 / XM_NT;
     const uint32_t hq8 = (uint32_t)(p.npad / 2) * 8u;  // bytes per K-step of the B pair grid
     const int q4 = tid & 3, btx = (tid >> 3) & 15;
-    int bkk[2];
-    uint32_t boff[2];
+    int bkk[BU];
+    uint32_t boff[BU];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        bkk[u] = 4 * u + 2 * (tid >> 7) + ((tid >> 2) & 1);
+    for (int u = 0; u < BU; ++u) {
+        const int e = tid + XM_NT * u;
+        bkk[u] = 2 * (e >> 7) + ((e >> 2) & 1);
         boff[u] = (uint32_t)(kbeg + bkk[u]) * hq8 + (uint32_t)(n0 / 2 + 2 * btx) * 8u;  // pair 2 btx: 16-B aligned
     }
     const __amdgpu_buffer_rsrc_t brsrc =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint2 *>(p.bqw), (short)0, -1, 0x00020000);
 
-    // A staging.  conv: lane = row (consecutive pixels), k row = wave + 4 r (wave-uniform: the
-    // k -> (c, ky, kx) split and the word offset run on the scalar unit); matrix: lanes along k.
-    // Rows past M re-read row M - 1 (store_tile drops them).
-    constexpr int AR = (BM * XBK) / NT;
-    int arow[AR], akk[AR];
-    uint32_t aoff[AR];
+    // A staging: thread = (rows arow + XM_NT / 4 i, K-step pair kp), K-steps 2 kp + r.  conv:
+    // lane = row (consecutive pixels), kp = the wave's column group (wave-uniform: the k -> (c, ky,
+    // kx) split and the word offset run on the scalar unit); matrix: four threads per row.  Rows
+    // past M re-read row M - 1 (store_tile drops them).
+    constexpr int APR = XM_BM * 4 / XM_NT;  // rows per thread
+    const int arow = p.conv ? (lane + 64 * wr) : (tid >> 2), akp = p.conv ? wc : (tid & 3);
+    uint32_t aoff[APR];
     const uint32_t phw = (uint32_t)(p.awH * p.awW), uW = (uint32_t)p.awW;
 #pragma unroll
-    for (int r = 0; r < AR; ++r) {
-        const int e = tid + NT * r;
-        arow[r] = p.conv ? lane : (e / XBK);
-        akk[r] = p.conv ? (wvu + 4 * r) : (e % XBK);
-        const int64_t m = min(m0 + arow[r], p.M - 1);
+    for (int i = 0; i < APR; ++i) {
+        const int64_t m = min(m0 + arow + (XM_NT / 4) * i, p.M - 1);
         if (p.conv) {
             const int64_t hw = p.Ho * p.Wo, img = m / hw, pix = m - img * hw, ho = pix / p.Wo, wo = pix - ho * p.Wo;
-            aoff[r] = (uint32_t)(4 * (img * p.aw_c * (int64_t)phw + ho * p.sh * p.awW + wo * p.sw + (p.awpw - p.pw)));
+            aoff[i] = (uint32_t)(4 * (img * p.aw_c * (int64_t)phw + ho * p.sh * p.awW + wo * p.sw + (p.awpw - p.pw)));
         } else {
-            aoff[r] = (uint32_t)(4 * (m * p.awld + akk[r]));
+            aoff[i] = (uint32_t)(4 * (m * p.awld + 2 * akp));
         }
     }
     const __amdgpu_buffer_rsrc_t arsrc =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(p.aw), (short)0, -1, 0x00020000);
     const int khw = p.kh * p.kw;
-    uint32_t wa[AR];
-    uint4 wbq[2];
+    uint32_t wa[APR][2];
+    uint4 wbq[BU];
     auto load_tile = [&](int k0) {
 #pragma unroll
-        for (int r = 0; r < AR; ++r) {
+        for (int r = 0; r < 2; ++r) {
             uint32_t ko;
             if (p.conv) {
-                const int k = k0 + akk[r];  // wave-uniform
+                const int k = k0 + 2 * akp + r;  // wave-uniform
                 const uint32_t c = fastdiv((uint32_t)k, p.kk_mul, p.kk_shift);
                 const uint32_t t = (uint32_t)k - c * (uint32_t)khw;
                 const uint32_t ky = fastdiv(t, p.kw_mul, p.kw_shift);
                 const uint32_t kx = t - ky * (uint32_t)p.kw;
                 ko = 4u * (c * phw + ky * (uint32_t)p.dh * uW + kx * (uint32_t)p.dw);
             } else {
-                ko = 4u * (uint32_t)k0;  // the matrix words are zero-padded to Kpad
+                ko = 4u * (uint32_t)(k0 + r);  // the matrix words are zero-padded to Kpad
             }
             ko = __builtin_amdgcn_readfirstlane(ko);
-            wa[r] = __builtin_amdgcn_raw_buffer_load_b32(arsrc, (int)aoff[r], (int)ko, 0);
-            if (p.conv && k0 + akk[r] >= K32) wa[r] = XM_ZERO_WORD;  // past the group's last channel (uniform)
+#pragma unroll
+            for (int i = 0; i < APR; ++i) {
+                wa[i][r] = __builtin_amdgcn_raw_buffer_load_b32(arsrc, (int)aoff[i], (int)ko, 0);
+                if (p.conv && k0 + 2 * akp + r >= K32) wa[i][r] = XM_ZERO_WORD;  // past the group's last channel (uniform)
+            }
         }
         const uint32_t kb = __builtin_amdgcn_readfirstlane((uint32_t)(k0 - kbeg) * hq8);
 #pragma unroll
-        for (int u = 0; u < 2; ++u)  // (add0, off0, add1, off1) of pairs 2 btx, 2 btx + 1
+        for (int u = 0; u < BU; ++u)  // (add0, off0, add1, off1) of pairs 2 btx, 2 btx + 1
             wbq[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(brsrc, (int)boff[u], (int)kb, 0));
     };
     load_tile(kbeg);
@@ -371,24 +391,22 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
             sel[v] = (int)w;
         }
     }
-    xm_v4f dq[4];  // one 16x16 accumulator per 16-row block
+    xm_v4f dq[XM_RB];  // one 16x16 accumulator per 16-row block
 #pragma unroll
-    for (int b = 0; b < 4; ++b) dq[b] = (xm_v4f){0.0f, 0.0f, 0.0f, 0.0f};
-    xm_v16f dacc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dacc[r] = 0.0f;
+    for (int b = 0; b < XM_RB; ++b) dq[b] = (xm_v4f){0.0f, 0.0f, 0.0f, 0.0f};
     xm_v8i av = {0, 0, 0, 0, 0, 0, 0, 0};
     const char *lut = reinterpret_cast<const char *>(sm.lut);
-    const uint32_t wvo = (uint32_t)wvu * 512u;  // the wave's first column block (4 wv) in a K-step of the table
+    const uint32_t wvo = (uint32_t)wc * 512u;  // the wave's first column block (4 wc) in a K-step of the table
     typedef const volatile __attribute__((address_space(3))) uint64_t xm_lds_u64;
     __syncthreads();  // the static table is in LDS before the first build reads it
 
     for (int k0 = kbeg; k0 < kend; k0 += XBK) {
 #pragma unroll
-        for (int r = 0; r < AR; ++r) sm.aw[akk[r] >> 2][arow[r] * 4 + (akk[r] & 3)] = wa[r];
+        for (int i = 0; i < APR; ++i)
+            *reinterpret_cast<uint2 *>(&sm.aw[akp][2 * (arow + (XM_NT / 4) * i)]) = make_uint2(wa[i][0], wa[i][1]);
         // build: rows 2 q4, 2 q4 + 1 of both signs for the unit's two column pairs
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < BU; ++u) {
             const uint4 b = wbq[u];
             const uint2 s0 = *reinterpret_cast<const uint2 *>(lut + b.y + 8 * q4);
             const uint2 s1 = *reinterpret_cast<const uint2 *>(lut + b.w + 8 * q4);
@@ -410,8 +428,8 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
             const uint32_t base = wvo + (uint32_t)(2 * g) * (uint32_t)(XM_TTK * 4);  // multiple of 128 B
             const char *tt0 = reinterpret_cast<const char *>(&sm.tt[0][0]);
 #pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const uint2 aw2 = *reinterpret_cast<const uint2 *>(&sm.aw[g >> 1][(16 * b + r16) * 4 + 2 * (g & 1)]);
+            for (int b = 0; b < XM_RB; ++b) {
+                const uint2 aw2 = *reinterpret_cast<const uint2 *>(&sm.aw[g][2 * (16 * (XM_RB * wr + b) + r16)]);
                 const uint32_t awh[2] = {aw2.x, aw2.y};
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
@@ -441,36 +459,43 @@ __global__ __launch_bounds__(NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs 
         }
         __syncthreads();
     }
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dacc[4 * b + i] = dq[b][i];
 
     // a term beyond the e4m3 range came back NaN (and poisons its column): the exact kernel
     // reruns the launch
     bool nan = false;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) nan |= __builtin_isnan(dacc[r]);
+    for (int b = 0; b < XM_RB; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) nan |= __builtin_isnan(dq[b][i]);
     if (__syncthreads_or(nan ? 1 : 0) && tid == 0) atomicOr(p.flag, 1u);
 
     // D (units of 2^(7-bR)) of row block b: lane l holds rows 4 (l >> 4) .. + 3, column l & 15
-    // -> tile row 16 b + 4 (l >> 4) + i, column 16 wv + (l & 15) -> [BM][BN] tile in LDS -> each
-    // thread's 4x4 block, epilogue mapping with consecutive lanes on consecutive pixels
+    // -> tile row 16 (XM_RB wr + b) + 4 (l >> 4) + i, column 16 wc + (l & 15) -> a [64][BN] slice in
+    // LDS per 64 tile rows -> each thread's 4x4 block (threads < 256), epilogue mapping with
+    // consecutive lanes on consecutive pixels
     const float f8S = __uint_as_float((uint32_t)min(max(134 - bR, 1), 254) << 23);
     float *ct = reinterpret_cast<float *>(&sm);
-    {
+    const int ety = tid & 15, etx = (tid >> 4) & 15;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int row = 16 * (r >> 2) + 4 * (lane >> 4) + (r & 3);
-            ct[row * XM_CP + 16 * wv + (lane & 15)] = dacc[r] * f8S;
+    for (int h = 0; h < XM_BM / 64; ++h) {
+        if (h > 0) __syncthreads();  // the previous slice is read
+#pragma unroll
+        for (int b = 0; b < XM_RB; ++b) {
+            const int rb = 16 * (XM_RB * wr + b) - 64 * h;  // the block's first row in the slice (wave-uniform)
+            if (rb >= 0 && rb < 64) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    ct[(rb + 4 * (lane >> 4) + i) * XM_CP + 16 * wc + (lane & 15)] = dq[b][i] * f8S;
+            }
+        }
+        __syncthreads();
+        if (tid < NT) {
+            float acc[TM][TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j] = ct[(ety * TM + i) * XM_CP + etx * TN + j];
+            store_tile(p, split, m0 + 64 * h, n0, ety, etx, acc);
         }
     }
-    __syncthreads();
-    const int ety = tid & 15, etx = tid >> 4;
-    float acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = ct[(ety * TM + i) * XM_CP + etx * TN + j];
-    store_tile(p, split, m0, n0, ety, etx, acc);
 }
