@@ -163,7 +163,7 @@ struct GemmArgs {
     int64_t awld, aw_c;
     int64_t awH, awW;  // conv: the word image's height / width (H + 2 ph, W + 2 pw when zero-padded)
     int awph, awpw;    // conv: x's offset inside the word image (the zero border's width)
-    int wfmt;          // pre-decoded operand format: 0 = gemm_f8mx_kernel's, 1 = gemm_tt_kernel's
+    int wfmt;          // pre-decoded operand format: 0 = gemm_f8mx_kernel's, 1 = gemm_tt_kernel's, 2 = gemm_tt16_kernel's
     int ttf7;          // gemm_tt_kernel: the table has negative entries (the F7 sign rule)
     const uint2 *bqw;
     const uint32_t *lutw;  // the LDS table image (XM_LUT_WORDS words), written by xm_decode_b
@@ -694,6 +694,7 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
 
 #include "gemm_f8mx.h"
 #include "gemm_tt.h"
+#include "gemm_tt16.h"
 
 // Sums the split-K partials in split order (deterministic) and writes the output mapping.
 // Partial layout: row-major [M][N] (rowmajor output) or [img][N][hw] (NCHW output).
@@ -772,7 +773,7 @@ __device__ __forceinline__ float load_A(const GemmArgs &p, int64_t m, int64_t k)
 __global__ __launch_bounds__(256) void gemm_exact_kernel(const GemmArgs p) {
     // Gate: after a fast launch, run only if it flagged off-grid operands (uniform per grid;
     // the grid is capped, so the no-op case costs one small launch).
-    if (p.flag != nullptr && __hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
+    if (p.flag != nullptr && (__hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1u) == 0u) return;
     const bool tb = p.flags & F_TB;
     const DFmt fA = dfmt(p.E, p.Mw, *p.bA, tb), fR = dfmt(p.E, p.Mw, *p.bR, tb);
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < p.M * p.N;
@@ -1085,11 +1086,19 @@ static void launch_fast(int mode, const GemmArgs &a, hipStream_t s) {
         gemm_fast_kernel<false, false, false, TM_V5><<<grid, NT, 0, s>>>(a);
         return;
     }
+    if (a.aw && a.wfmt == 2) {  // E3M4: the packed-f16 tile-table kernel (run_gemm)
+        const int bm = a.ttf7 ? Tt16Cfg<true>::BMR : Tt16Cfg<false>::BMR;
+        const dim3 g16((unsigned)(((a.M + bm - 1) / bm) * ((a.N + BN - 1) / BN) * a.splits));
+        a.ttf7 ? gemm_tt16_kernel<true><<<g16, NT, 0, s>>>(a) : gemm_tt16_kernel<false><<<g16, NT, 0, s>>>(a);
+        // gated: reruns the launch in the f32 form when a tile left the f16 window (flag bit 1)
+        a.ttf7 ? gemm_tt_kernel<4, true, true><<<grid, NT, 0, s>>>(a) : gemm_tt_kernel<4, false, true><<<grid, NT, 0, s>>>(a);
+        return;
+    }
     if (a.aw && a.wfmt == 1) {  // the tile-table kernel on pre-decoded operands (run_gemm)
         if (a.Mw == 4)
-            a.ttf7 ? gemm_tt_kernel<4, true><<<grid, NT, 0, s>>>(a) : gemm_tt_kernel<4, false><<<grid, NT, 0, s>>>(a);
+            a.ttf7 ? gemm_tt_kernel<4, true, false><<<grid, NT, 0, s>>>(a) : gemm_tt_kernel<4, false, false><<<grid, NT, 0, s>>>(a);
         else
-            gemm_tt_kernel<5, false><<<grid, NT, 0, s>>>(a);
+            gemm_tt_kernel<5, false, false><<<grid, NT, 0, s>>>(a);
         return;
     }
     if (mode == TM_F8) {  // s2n + qbma, no golden clip (selected in run_gemm)
@@ -1223,6 +1232,15 @@ static bool tt_form(int Mw, uint32_t flags, const TablePack &tab) {
     return Mw == 4 || !neg;
 }
 
+// E3M4 on the tile-table path runs the packed-f16 form (gemm_tt16_kernel) for signed tables (F7:
+// +23 % on the ResNet-18 layer set) and for K >= 256 (+2-9 %); on short K its per-tile prologue
+// (the frame shift's bias range, two barriers) outweighs the gain (MobileNetV2 E3M4 -3 %), and
+// gemm_tt_kernel<4, F7> runs.  FP8A_NO_TT16=1 keeps gemm_tt_kernel everywhere.
+static bool tt16_form(int Mw, bool f7, int64_t K) {
+    static const bool no_tt16 = getenv("FP8A_NO_TT16") != nullptr;
+    return !no_tt16 && Mw == 4 && (f7 || K >= 256);
+}
+
 static bool no_mx() {
     static const bool v = getenv("FP8A_NO_MX") != nullptr;
     return v;
@@ -1320,15 +1338,15 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
             a.bqw = (const uint2 *)(base + align256((size_t)a_words * 4));
             a.lutw = (const uint32_t *)(base + align256((size_t)a_words * 4) + align256((size_t)(kpad * npad / 2) * 8));
             a.npad = npad;
-            a.wfmt = tt ? 1 : 0;
             a.ttf7 = 0;
             for (int i = 0; tt && i < (1 << (2 * a.Mw)); ++i) a.ttf7 |= a.tab.raw[i] < 0;
+            a.wfmt = tt ? (tt16_form(a.Mw, a.ttf7, a.K) ? 2 : 1) : 0;
             const int64_t rows = a.conv ? a.M / (a.Ho * a.Wo) : a.M, cols = a_words / std::max<int64_t>(rows, 1);
             const dim3 ga((unsigned)std::min<int64_t>((cols + 255) / 256, 64), (unsigned)std::min<int64_t>(rows, 1024));
             xm_decode_a<<<ga, 256, 0, s>>>(a);
             if (tt) {  // B words [Kpad][Npad] (the same bytes as the E4M3 pair grid) + the static image
                 const unsigned gb = (unsigned)std::min<int64_t>((kpad * npad + 255) / 256, 4096);
-                tt_decode_b<<<gb, 256, 0, s>>>(a, kpad);
+                tt_decode_b<<<gb, 256, 0, s>>>(a, kpad);  // (+ gemm_tt16_kernel's f16 image when wfmt == 2)
             } else {
                 const unsigned gb = (unsigned)std::min<int64_t>((kpad * npad / 2 + 255) / 256, 4096);
                 xm_decode_b<<<gb, 256, 0, s>>>(a, kpad);
@@ -1350,7 +1368,15 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
         if (rc) return rc;
     }
     gemm_exact_kernel<<<eblocks, 256, 0, s>>>(a);
-    return hip_check("fp8a gated exact gemm launch");
+    rc = hip_check("fp8a gated exact gemm launch");
+    static const bool dbg = getenv("FP8A_DEBUG_FLAGS") != nullptr;  // diagnostics: the flag word per launch
+    if (!rc && dbg) {
+        uint32_t f = 0;
+        if (hipStreamSynchronize(s) == hipSuccess && hipMemcpy(&f, a.flag, sizeof(f), hipMemcpyDeviceToHost) == hipSuccess)
+            fprintf(stderr, "fp8a flag M=%lld N=%lld K=%lld E=%d M=%d wfmt=%d flag=%u\n", (long long)a.M, (long long)a.N,
+                    (long long)a.K, a.E, a.Mw, a.aw ? a.wfmt : -1, f);
+    }
+    return rc;
 }
 
 // qamaa: term = fq(a*b) (no operand decode: exact for any fp32 inputs), then fq(sum) in place.

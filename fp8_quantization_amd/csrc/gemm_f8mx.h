@@ -130,6 +130,39 @@ __device__ __forceinline__ uint32_t tt_word_a(float x, int M, uint32_t emnA, boo
     return (cb & TT_EXP) | (mc * (uint32_t)(4 * TT_RS));
 }
 
+// gemm_tt16_kernel's operand formats (gemm_tt16.h)
+constexpr int TT16_XK = 4;                  // K-steps per staged tile (= the 4 lane groups)
+constexpr int TT16_RS = 34;                 // u32 per m_a row of a K-step's table: 32 column pairs + 2
+constexpr int TT16_KS = 16 * TT16_RS;       // u32 per K-step (2176 B)
+constexpr uint32_t TT16_RSH = 2 * TT16_RS;  // the A word's row offset unit: 2 bytes
+constexpr uint32_t TT16_EXP2 = 0xFC00FC00u; // sign + exponent fields of an f16 pair
+constexpr int TT16_IMG = 2048;             // u32 offset of the f16 image in the table region (after gemm_tt_kernel's)
+
+typedef _Float16 tt16_h2 __attribute__((ext_vector_type(2)));
+typedef _Float16 tt16_h8 __attribute__((ext_vector_type(8)));
+typedef float tt16_f4 __attribute__((ext_vector_type(4)));
+
+
+// f16 bits of sign * 2^e (normal range)
+__device__ __forceinline__ uint32_t tt16_pow2(int e, uint32_t sign) { return sign | ((uint32_t)(e + 15) << 10); }
+
+// A word (wfmt 2): c_a' = c_a 2^(bA-1) in the sign / exponent fields of both f16 halves, m_a x
+// TT16_RSH (the row's byte offset / 2) in the low half's mantissa field; zeros 0.  ok = on the
+// (4, bA) grid; win is cleared by c_a' > 2^7 (a value more than one binade above the format's
+// top one -- the quantizer's rint bias allows one -- is outside the f16 window).
+__device__ __forceinline__ uint32_t tt16_word_a(float x, uint32_t emnA, int bA, bool &ok, bool &win) {
+    float c;
+    uint32_t mc;
+    ok = stage_decode(x, 4, emnA, true, c, mc);
+    const uint32_t cb = __float_as_uint(c);
+    if ((cb & 0x7FFFFFFFu) == 0u) return 0u;
+    const int e = (int)((cb >> 23) & 0xFFu) - 127 + bA - 1;  // c_a' = c_a 2^(bA-1): in [-4, 7] on the grid
+    ok = ok && e >= -14 && e <= 15;
+    win = win && e <= 7;
+    const uint32_t h = tt16_pow2(min(max(e, -14), 15), (cb >> 16) & 0x8000u);
+    return (h << 16) | h | (mc * TT16_RSH);
+}
+
 // A pre-pass, one (image | row) per blockIdx.y step.  conv: the group's channel slice of x
 // [Bn][Cin][H][W] (channels cbase..cbase+aw_c) -> words [Bn][aw_c][awH][awW], x at (awph, awpw)
 // inside a border of zero words (the padding the convolution reads, so the wave-independent
@@ -145,13 +178,13 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
         *p.fq_ibias = bA;
     }
     const uint32_t emnA = (uint32_t)(128 - bA) << 23;
-    bool bad = !(xm_bias_ok(bA) && xm_bias_ok(bR));
+    bool bad = !(xm_bias_ok(bA) && xm_bias_ok(bR)), win = true;
     uint32_t *const out = const_cast<uint32_t *>(p.aw);
     const int64_t hw = p.H * p.W;
     const int64_t rows = p.conv ? p.M / (p.Ho * p.Wo) : p.M, cols = p.conv ? p.aw_c * p.awH * p.awW : p.awld;
     auto word = [&](float v, bool &ok) {
         if (p.fqin.mx) v = fq_apply(v, fmx, fbias, p.fqin.M, p.fqin.S);
-        return p.wfmt ? tt_word_a(v, p.Mw, emnA, ok) : xm_word_a(v, emnA, bR, ok);
+        return p.wfmt == 2 ? tt16_word_a(v, emnA, bA, ok, win) : p.wfmt ? tt_word_a(v, p.Mw, emnA, ok) : xm_word_a(v, emnA, bR, ok);
     };
     const uint32_t zw = p.wfmt ? 0u : XM_ZERO_WORD;  // the word of a zero (padding, columns >= K)
     if (p.conv && (p.awph | p.awpw)) {  // zero-bordered image (< 2^30 words, run_gemm): 32-bit index math
@@ -199,6 +232,7 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
             }
         }
         if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, 1u);
+        if (__syncthreads_or(win ? 0 : 1) && threadIdx.x == 0) atomicOr(p.flag, 4u);  // gemm_tt16_kernel's window (A)
         return;
     }
     // 16-B form: every row start 16-B aligned and the valid columns a multiple of 4 (all the
@@ -232,6 +266,7 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
         }
     }
     if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, 1u);
+    if (__syncthreads_or(win ? 0 : 1) && threadIdx.x == 0) atomicOr(p.flag, 4u);  // gemm_tt16_kernel's window (A)
 }
 
 // B pre-pass: per (k, pair Q) of the padded [Kpad][npad / 2] pair grid, the addend pair

@@ -36,7 +36,7 @@ template <int MW, bool F7> struct TtCfg {
 // and (block 0) the static image V / sig_a sig_b.
 __global__ __launch_bounds__(256) void tt_decode_b(const GemmArgs p, int64_t kpad) {
     const int bA = *p.bA, bR = *p.bR, M = p.Mw, nm = 1 << M;
-    bool bad = !(xm_bias_ok(bA) && xm_bias_ok(bR));
+    bool bad = !(xm_bias_ok(bA) && xm_bias_ok(bR)), win = true;  // win: gemm_tt16_kernel's f16 window
     if (blockIdx.x == 0) {
         float *img = const_cast<float *>(reinterpret_cast<const float *>(p.lutw));
         const float ulp = p2(-M), kb = 2.0f - p2(-M) - p2(-22);
@@ -47,6 +47,14 @@ __global__ __launch_bounds__(256) void tt_decode_b(const GemmArgs p, int64_t kpa
             v = fminf(v, __uint_as_float(__float_as_uint(v) & 0x7F800000u) * kb);
             img[e] = v;
             img[TT_IMG_FLOATS / 2 + e] = s;
+            if (p.wfmt == 2) {  // gemm_tt16_kernel's f16 image (E3M4): V with the pre-clamp bound
+                                // (2 - 2^-4 - 2^-10) x binade, then sig_a sig_b (gemm_tt16.h)
+                uint16_t *h = reinterpret_cast<uint16_t *>(img + TT16_IMG);
+                const float v16 = fminf(v, __uint_as_float(__float_as_uint(v) & 0x7F800000u) * (2.0f - p2(-M) - p2(-10)));
+                h[e] = __builtin_bit_cast(uint16_t, (_Float16)v16);
+                win = win && v16 < 4.0f;
+                h[256 + e] = __builtin_bit_cast(uint16_t, (_Float16)s);
+            }
         }
     }
     uint32_t *const bw = reinterpret_cast<uint32_t *>(const_cast<uint2 *>(p.bqw));
@@ -61,11 +69,13 @@ __global__ __launch_bounds__(256) void tt_decode_b(const GemmArgs p, int64_t kpa
             const bool ok = stage_decode(p.B[k * p.sbk + col * p.sbn], M, (uint32_t)(128 - bb) << 23, true, c, mc);
             bad |= !ok || !xm_bias_ok(bb);
             const uint32_t cb = __float_as_uint(c);
+            win = win && ((cb >> 23) & 0xFFu) <= (uint32_t)(127 + 8 - bb);  // c_b at most one binade above the format's top
             if ((cb & 0x7FFFFFFFu) != 0u) w = (cb & TT_EXP) | mc;
         }
         bw[i] = w;
     }
     if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, 1u);
+    if (p.wfmt == 2 && __syncthreads_or(win ? 0 : 1) && threadIdx.x == 0) atomicOr(p.flag, 8u);  // (B, image)
 }
 
 template <int MW, bool F7> struct TtSmem {
@@ -81,9 +91,12 @@ template <int MW, bool F7> struct TtSmem {
     uint32_t aw[C::XK][BM];
 };
 
-template <int MW, bool F7>
+// A16: the A words are gemm_tt16_kernel's (E3M4; c_a 2^bA as f16 in the high half, m_a x 68 in the
+// low bits), and the kernel runs only when that kernel left its f16 window (flag bit 1).
+template <int MW, bool F7, bool A16>
 __global__ __launch_bounds__(NT) void gemm_tt_kernel(const GemmArgs p) {
     using C = TtCfg<MW, F7>;
+    if (A16 && (__hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 30u) == 0u) return;
     constexpr int NM = C::NM, XK = C::XK;
     static_assert(C::UNITS <= NT && XK >= 1 && XK <= 4, "tile-table configuration");
     __shared__ __attribute__((aligned(16))) TtSmem<MW, F7> sm;
@@ -100,7 +113,7 @@ __global__ __launch_bounds__(NT) void gemm_tt_kernel(const GemmArgs p) {
     const int64_t m0 = (bid % num_mt) * BM;
     const int64_t n0 = (bid / num_mt) * BN;
     const int kbeg = (int)(split * p.kchunk), kend = (int)min(p.K, (int64_t)kbeg + p.kchunk), K32 = (int)p.K;
-    const int bR = *p.bR;
+    const int bR = *p.bR, bA16 = A16 ? *p.bA : 0;
     // Q_R constants: C = max(2^floor(log2|x|) kc15, cmin); thr = the largest |a b| Q_R flushes
     const float kc15 = 1.5f * p2(23 - MW), cmin = 1.5f * p2(1 - bR + 23 - MW), thr = p2(-bR - MW);
 
@@ -197,8 +210,16 @@ __global__ __launch_bounds__(NT) void gemm_tt_kernel(const GemmArgs p) {
 #pragma unroll
         for (int kk = 0; kk < XK; ++kk) {
             const uint32_t w = aw[kk][lane];
-            const float ca = __uint_as_float(w & TT_EXP);
-            const uint32_t off = (w & ~TT_EXP) + wvo;  // m_a row | the wave's columns
+            float ca;
+            uint32_t off;
+            if (A16) {  // c_a = the f16 high half / 2^bA; row offset in 2-byte units of the f16 table
+                const uint32_t h = w >> 16, e16 = (h >> 10) & 31u;
+                ca = e16 ? __uint_as_float(((h & 0x8000u) << 16) | ((e16 + (uint32_t)(113 - bA16)) << 23)) : 0.0f;
+                off = (w & 0x3FFu) * (uint32_t)(4 * TT_RS / TT16_RSH) + wvo;
+            } else {
+                ca = __uint_as_float(w & TT_EXP);
+                off = (w & ~TT_EXP) + wvo;  // m_a row | the wave's columns
+            }
             const char *tb = reinterpret_cast<const char *>(&tt[kk][0][0]) + off;
             float t[16];
 #pragma unroll

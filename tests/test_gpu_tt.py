@@ -6,7 +6,7 @@ every error table the reference selects for them (withComp False: E3M4 entries 0
 withComp True, dnsmp 3: entries -1..1, which make the F7 sign rule observable -- E3M4 runs its
 F7 form, E2M5 with a signed table stays on gemm_fast_kernel and is checked here all the same)
 and no table:
-  * every code pair of the format (both signs, subnormals, zeros) as a K = 1 product, bit-exact
+  * every code pair of the format (both signs, subnormals, zeros) as a single-term product, bit-exact
     against the oracle's terms, at bias triples that put the result grid's floor inside the
     products' range (flush, subnormal band and normal results all occur);
   * implicit-GEMM convs with padding (the zero-bordered word image), stride, dilation, groups,
@@ -145,12 +145,19 @@ def test_every_code_pair_bitexact(fmt, kind, shift):
     E, M = fmt
     bA, bB = (1 << (E - 1)) + 2, (1 << (E - 1)) + 5
     bR = bA + bB - (1 << E) - shift
-    A = _all_codes(E, M, bA).reshape(-1, 1)
-    B = _all_codes(E, M, bB).reshape(1, -1)
+    # K = 256 with one nonzero K-step: each output is exactly one term, and K is long enough for
+    # E3M4's packed-f16 form (run_gemm picks it for K >= 256 or a signed table)
+    a = _all_codes(E, M, bA).reshape(-1, 1)
+    b = _all_codes(E, M, bB).reshape(1, -1)
+    K = 256
+    A = np.zeros((a.shape[0], K), np.float32)
+    A[:, 0] = a[:, 0]
+    B = np.zeros((K, b.shape[1]), np.float32)
+    B[0] = b[0]
     tab, fl = _table(E, M, kind), _flags(kind)
-    C, flag = _matmul_raw(A, 1, B, B.shape[1], 1, A.shape[0], B.shape[1], 1, E, M, bA, bB, bR, tab, fl)
+    C, flag = _matmul_raw(A, K, B, B.shape[1], 1, A.shape[0], B.shape[1], K, E, M, bA, bB, bR, tab, fl)
     assert flag == 0, "fallback flag raised: the tile-table path did not produce these terms"
-    ref = orc.terms(A, B, E, M, bA, bB, bR, tab, fl)[:, 0, :]
+    ref = orc.terms(a, b, E, M, bA, bB, bR, tab, fl)[:, 0, :]
     _terms_equal(C, ref)
 
 
@@ -217,3 +224,58 @@ def test_off_grid_operand_falls_back(fmt):
     assert flag != 0, "pre-decode did not flag the launch"
     ref, S = _conv_ref(x, w, E, M, bA, bW, bR, tab, fl, 1, 1, 1, 1)
     _close(y.transpose(0, 2, 3, 1).reshape(-1, y.shape[1]), ref, S, "off-grid")
+
+
+# E3M4 runs the packed-f16 form (gemm_tt16_kernel): per 64-column tile the frame
+# shift S = min(min bB - 7, bR - bA + 9) must give Emn = bA - bR + S >= -10 and
+# max bB <= S + 13; a tile outside that window sets a flag bit (2: Emn, 16: the bB spread) and
+# the f32 form (gemm_tt_kernel on the same pre-decoded operands) reruns the launch.  bB offsets
+# are relative to min bB.
+WINDOW = [
+    ("edge_bR_high", [0] * 64, 3, 0),             # bR = bA + bB + 3: Emn = -10, inside
+    ("bR_too_high", [0] * 64, 4, 2),              # bR = bA + bB + 4: Emn = -11
+    ("bR_low", [0] * 64, -17, 0),                 # the S = bR - bA + 9 branch (Emn = 9)
+    ("spread_6", [0] * 32 + [6] * 32, 0, 0),      # max bB = S + 13
+    ("spread_7", [0] * 32 + [7] * 32, 0, 16),     # a column's smallest c_b' falls below 2^-16
+]
+
+
+@pytest.mark.parametrize("kind", ["nocomp", "comp"])
+@pytest.mark.parametrize("case", WINDOW, ids=[w[0] for w in WINDOW])
+def test_e3m4_f16_window(case, kind):
+    name, boffs, rdelta, want_flag = case
+    E, M = 3, 4
+    rng = np.random.default_rng(len(name) * 7 + (kind == "comp"))
+    bA = 7
+    bB = np.array([bA + o for o in boffs], np.int32)
+    bR = int(bA + bB.min() + rdelta)
+    Mr, K, N = 96, 256, 64  # K >= 256: the packed-f16 form for both table kinds
+    A = _grid(rng, E, M, (Mr, K), bA, zero_frac=0.2, sub_frac=0.1)
+    W = _grid(rng, E, M, (N, K), bB[:, None], zero_frac=0.1, sub_frac=0.1)
+    tab, fl = _table(E, M, kind), _flags(kind)
+    C, flag = _matmul_raw(A, K, W, 1, K, Mr, N, K, E, M, bA, bB, bR, tab, fl)
+    assert flag == want_flag, f"{name}: flag {flag}"
+    ref, S = orc.matmul(A, W.T, E, M, bA, bB, bR, tab, fl, with_abs=True)
+    _close(C, ref, S, name)
+
+
+@pytest.mark.parametrize("kind", ["nocomp", "comp"])
+def test_e3m4_above_top_binade_takes_f32_form(kind):
+    """An activation two binades above the format's largest one (the quantizer's rint bias allows
+    one: 5.0 at bA = 6 is inside) is on the mantissa grid but outside the f16 window: flag bit 2,
+    and the f32 form's result (which matches the oracle) is returned."""
+    E, M = 3, 4
+    rng = np.random.default_rng(11)
+    bA, bR = 6, 4
+    bB = np.full(64, 10, np.int32)
+    K = 256
+    A = _grid(rng, E, M, (80, K), bA, zero_frac=0.2)
+    A[3, 5] = 10.0
+    A[70, 40] = -13.0
+    A[71, 41] = 5.0
+    W = _grid(rng, E, M, (64, K), bB[:, None], zero_frac=0.1)
+    tab, fl = _table(E, M, kind), _flags(kind)
+    C, flag = _matmul_raw(A, K, W, 1, K, 80, 64, K, E, M, bA, bB, bR, tab, fl)
+    assert flag == 4, f"flag {flag}"
+    ref, S = orc.matmul(A, W.T, E, M, bA, bB, bR, tab, fl, with_abs=True)
+    _close(C, ref, S, "above top binade")

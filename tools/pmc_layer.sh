@@ -4,7 +4,7 @@
 TAG=$1; MODE=${2:-w1u}; LAYER=${3:-l2.c2}
 R=$(pwd); OUT=$R/gpurun_out/pmc_$TAG; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-run() { timeout -k 10 300 rocprofv3 --kernel-trace --pmc $2 --kernel-include-regex gemm_f8mx -f csv -d $OUT/$1 -o run -- \
+run() { timeout -k 10 300 rocprofv3 --kernel-trace --pmc $2 --kernel-include-regex ${KREGEX:-gemm_f8mx} -f csv -d $OUT/$1 -o run -- \
         python $R/tools/gemm_bench.py --mode $MODE --layers $LAYER --reps 3 > $OUT/$1.log 2>&1; }
 run sq1 "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU" && \
 run sq2 "SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_VALU_MFMA_BUSY_CYCLES SQ_INST_CYCLES_VMEM SQ_INSTS_VMEM" && \

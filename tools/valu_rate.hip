@@ -72,6 +72,13 @@ KERNEL(k_cndmask_s, "v_cndmask_b32_e64 %0, %0, %1, s[0:1]")
 KERNEL(k_fract, "v_fract_f32 %0, %0")
 KERNEL(k_rndne, "v_rndne_f32 %0, %0")
 KERNEL(k_frexp_exp, "v_frexp_exp_i32_f32 %0, %0")
+KERNEL(k_pk_add_f16, "v_pk_add_f16 %0, %0, %1")
+KERNEL(k_pk_mul_f16, "v_pk_mul_f16 %0, %0, %1")
+KERNEL(k_pk_fma_f16, "v_pk_fma_f16 %0, %0, %1, %2")
+KERNEL(k_pk_max_f16, "v_pk_max_f16 %0, %0, %1")
+KERNEL(k_pk_max_u16, "v_pk_max_u16 %0, %0, %1")
+KERNEL(k_pk_add_u16, "v_pk_add_u16 %0, %0, %1")
+KERNEL(k_pk_sub_f16, "v_pk_add_f16 %0, %0, %1 neg_lo:[0,1] neg_hi:[0,1]")
 
 #define PCHAINS8(INS)                                                                                 \
     asm volatile(INS : "+v"(r0) : "v"(s1), "v"(s2));                                                  \
@@ -104,7 +111,7 @@ int main() {
     struct {
         const char *name;
         kfn f;
-    } ks[] = {{"add_f32", k_add_f32}, {"sub_f32", k_sub_f32}, {"mul_f32", k_mul_f32}, {"fma_f32", k_fma_f32}, {"fmac_f32", k_fmac_f32}, {"med3_f32", k_med3_f32}, {"max_f32", k_max_f32}, {"min_f32", k_min_f32}, {"max3_f32", k_max3_f32}, {"and_or", k_and_or}, {"bfe_i32", k_bfe_i32}, {"bfe_u32", k_bfe_u32}, {"bfi_b32", k_bfi_b32}, {"perm_b32", k_perm_b32}, {"lshl_or", k_lshl_or}, {"lshl_add", k_lshl_add}, {"add3_u32", k_add3_u32}, {"add_u32", k_add_u32}, {"sub_u32", k_sub_u32}, {"sub_u32_clamp", k_sub_u32_clamp}, {"add_u32_clamp", k_add_u32_clamp}, {"max_u32", k_max_u32}, {"max_i32", k_max_i32}, {"min_u32", k_min_u32}, {"and_b32", k_and_b32}, {"or_b32", k_or_b32}, {"xor_b32", k_xor_b32}, {"lshlrev", k_lshlrev}, {"lshrrev", k_lshrrev}, {"ashrrev", k_ashrrev}, {"cvt_f32_i32", k_cvt_f32_i32}, {"cvt_f32_ubyte0", k_cvt_f32_ubyte0}, {"ldexp", k_ldexp}, {"mul_u24", k_mul_u24}, {"mad_u24", k_mad_u24}, {"mul_lo", k_mul_lo}, {"add_f32_e64", k_add_f32_e64}, {"mul_f32_abs", k_mul_f32_abs}, {"cmp_cnd", k_cmp_cnd}, {"cndmask_s", k_cndmask_s}, {"fract", k_fract}, {"rndne", k_rndne}, {"frexp_exp", k_frexp_exp}, {"pk_add_f32", k_pk_add_f32}, {"pk_mul_f32", k_pk_mul_f32}, {"pk_fma_f32", k_pk_fma_f32}};
+    } ks[] = {{"add_f32", k_add_f32}, {"sub_f32", k_sub_f32}, {"mul_f32", k_mul_f32}, {"fma_f32", k_fma_f32}, {"fmac_f32", k_fmac_f32}, {"med3_f32", k_med3_f32}, {"max_f32", k_max_f32}, {"min_f32", k_min_f32}, {"max3_f32", k_max3_f32}, {"and_or", k_and_or}, {"bfe_i32", k_bfe_i32}, {"bfe_u32", k_bfe_u32}, {"bfi_b32", k_bfi_b32}, {"perm_b32", k_perm_b32}, {"lshl_or", k_lshl_or}, {"lshl_add", k_lshl_add}, {"add3_u32", k_add3_u32}, {"add_u32", k_add_u32}, {"sub_u32", k_sub_u32}, {"sub_u32_clamp", k_sub_u32_clamp}, {"add_u32_clamp", k_add_u32_clamp}, {"max_u32", k_max_u32}, {"max_i32", k_max_i32}, {"min_u32", k_min_u32}, {"and_b32", k_and_b32}, {"or_b32", k_or_b32}, {"xor_b32", k_xor_b32}, {"lshlrev", k_lshlrev}, {"lshrrev", k_lshrrev}, {"ashrrev", k_ashrrev}, {"cvt_f32_i32", k_cvt_f32_i32}, {"cvt_f32_ubyte0", k_cvt_f32_ubyte0}, {"ldexp", k_ldexp}, {"mul_u24", k_mul_u24}, {"mad_u24", k_mad_u24}, {"mul_lo", k_mul_lo}, {"add_f32_e64", k_add_f32_e64}, {"mul_f32_abs", k_mul_f32_abs}, {"cmp_cnd", k_cmp_cnd}, {"cndmask_s", k_cndmask_s}, {"fract", k_fract}, {"rndne", k_rndne}, {"frexp_exp", k_frexp_exp}, {"pk_add_f16", k_pk_add_f16}, {"pk_mul_f16", k_pk_mul_f16}, {"pk_fma_f16", k_pk_fma_f16}, {"pk_max_f16", k_pk_max_f16}, {"pk_max_u16", k_pk_max_u16}, {"pk_add_u16", k_pk_add_u16}, {"pk_sub_f16", k_pk_sub_f16}, {"pk_add_f32", k_pk_add_f32}, {"pk_mul_f32", k_pk_mul_f32}, {"pk_fma_f32", k_pk_fma_f32}};
     hipDeviceProp_t prop;
     hipGetDeviceProperties(&prop, 0);
     const int cus = prop.multiProcessorCount;
