@@ -9,11 +9,13 @@ average takes the LAST N dispatches of --kernel (the dominant kernel, gemm_f8mx_
 timed steps come last); op_avg_ns adds every kernel of one approx op (--op-kernels: operand
 pre-decodes, the GEMM, the split-K reduce, the gated exact kernel) over the same window -- the
 quantity bench.py times with HIP events.  PMC counters are averaged per dispatch of --kernel;
-HBM traffic per launch =
-(FETCH_SIZE + WRITE_SIZE) * 1024 bytes -- rocprofv3's KB units; on gfx950 FETCH_SIZE is
-calibrated only for 16-B-per-lane streaming reads (MI355X_MICROARCH.md §HBM), these loads
-are 4 B per lane, so the read side is reported raw and marked uncalibrated.
+HBM traffic per launch = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 bytes (rocprofv3's KB units).  On
+gfx950 FETCH_SIZE reports half the bytes of coalesced buffer loads: MI355X_MICROARCH.md §HBM for
+16 B / lane, and tools/fetch_cal.hip (profiles/fetch_cal_r02.txt) for this kernel's 4 B / lane
+A-word loads as well (1 GiB read -> 512 MiB FETCH_SIZE for both widths); WRITE_SIZE is exact for
+4 and 16 B / lane stores.
 """
+FETCH_CAL = 2.0  # bytes read per FETCH_SIZE byte (tools/fetch_cal.hip)
 import argparse
 import collections
 import csv
@@ -73,8 +75,8 @@ def main():
         res["pmc_avg_per_dispatch"] = {k: sum(v) / len(v) for k, v in counters.items()}
         pm = res["pmc_avg_per_dispatch"]
         if "FETCH_SIZE" in pm and "WRITE_SIZE" in pm:
-            res["bytes_per_launch"] = (pm["FETCH_SIZE"] + pm["WRITE_SIZE"]) * 1024.0
-            res["traffic_note"] = "FETCH_SIZE uncalibrated for 4-byte-per-lane loads (raw KB x 1024)"
+            res["bytes_per_launch"] = (FETCH_CAL * pm["FETCH_SIZE"] + pm["WRITE_SIZE"]) * 1024.0
+            res["traffic_note"] = "(2 x FETCH_SIZE + WRITE_SIZE) x 1024: FETCH_SIZE calibrated at 1/2 (tools/fetch_cal.hip)"
         if "SQ_INSTS_VALU" in pm and "SQ_WAVES" in pm:
             res["valu_instr_per_wave"] = pm["SQ_INSTS_VALU"] / pm["SQ_WAVES"]
     if counters and a.pmc_json:
@@ -82,10 +84,11 @@ def main():
         pj = dict(source="rocprofv3 --kernel-trace --pmc (separate passes per counter group, "
                          f"--kernel-include-regex {KERNEL}) on bench.py --steps 2 --warmup 1",
                   note=f"per {KERNEL} dispatch, averaged; FETCH_SIZE/WRITE_SIZE in KB (x1024 = bytes); "
-                       "FETCH_SIZE uncalibrated for 4-byte-per-lane loads (MI355X_MICROARCH.md HBM section)",
+                       "bytes_per_launch = (2 x FETCH_SIZE + WRITE_SIZE) x 1024: FETCH_SIZE reads half the bytes of "
+                       "4- and 16-B-per-lane buffer loads (tools/fetch_cal.hip, MI355X_MICROARCH.md HBM section)",
                   arch=a.arch, E=a.E, M=a.M)
         if "FETCH_SIZE" in pm and "WRITE_SIZE" in pm:
-            pj.update(kernel=KERNEL, bytes_per_launch=(pm["FETCH_SIZE"] + pm["WRITE_SIZE"]) * 1024.0,
+            pj.update(kernel=KERNEL, bytes_per_launch=(FETCH_CAL * pm["FETCH_SIZE"] + pm["WRITE_SIZE"]) * 1024.0,
                       fetch_kb=pm["FETCH_SIZE"], write_kb=pm["WRITE_SIZE"])
         if "SQ_INSTS_VALU" in pm and "GRBM_GUI_ACTIVE" in pm:
             # GRBM_GUI_ACTIVE is summed over the 8 XCDs; 1024 SIMDs; a wave64 VALU op issues in 2 cycles
