@@ -1090,15 +1090,18 @@ static void launch_fast(int mode, const GemmArgs &a, hipStream_t s) {
         const int bm = a.ttf7 ? Tt16Cfg<true>::BMR : Tt16Cfg<false>::BMR;
         const dim3 g16((unsigned)(((a.M + bm - 1) / bm) * ((a.N + BN - 1) / BN) * a.splits));
         a.ttf7 ? gemm_tt16_kernel<true><<<g16, NT, 0, s>>>(a) : gemm_tt16_kernel<false><<<g16, NT, 0, s>>>(a);
-        // gated: reruns the launch in the f32 form when a tile left the f16 window (flag bit 1)
+        // gated: reruns the launch in the f32 form when a tile left the f16 window (flag bits 1-4)
         a.ttf7 ? gemm_tt_kernel<4, true, true><<<grid, NT, 0, s>>>(a) : gemm_tt_kernel<4, false, true><<<grid, NT, 0, s>>>(a);
         return;
     }
     if (a.aw && a.wfmt == 1) {  // the tile-table kernel on pre-decoded operands (run_gemm)
-        if (a.Mw == 4)
+        if (a.Mw == 4) {
             a.ttf7 ? gemm_tt_kernel<4, true, false><<<grid, NT, 0, s>>>(a) : gemm_tt_kernel<4, false, false><<<grid, NT, 0, s>>>(a);
-        else
-            gemm_tt_kernel<5, false, false><<<grid, NT, 0, s>>>(a);
+        } else {  // 128-row tiles on 8-wave workgroups
+            static_assert(tt_rh<5>() == 2 && tt_rh<4>() == 1, "gemm_tt_kernel launch shapes");
+            const dim3 g5((unsigned)(((a.M + 127) / 128) * ((a.N + BN - 1) / BN) * a.splits));
+            gemm_tt_kernel<5, false, false><<<g5, 2 * NT, 0, s>>>(a);
+        }
         return;
     }
     if (mode == TM_F8) {  // s2n + qbma, no golden clip (selected in run_gemm)

@@ -78,6 +78,10 @@ __global__ __launch_bounds__(256) void tt_decode_b(const GemmArgs p, int64_t kpa
     if (p.wfmt == 2 && __syncthreads_or(win ? 0 : 1) && threadIdx.x == 0) atomicOr(p.flag, 8u);  // (B, image)
 }
 
+// Row halves per tile: E2M5 runs 128-row tiles on 8-wave workgroups that share one table build
+// (its 32-row table makes the build ~20 % of the work at 64 rows; 99.5 -> 79.8 ms on the ResNet-18
+// layer set), E3M4 64-row tiles (128 rows measured +-0 there).
+template <int MW> constexpr int tt_rh() { return MW == 5 ? 2 : 1; }
 template <int MW, bool F7> struct TtSmem {
     using C = TtCfg<MW, F7>;
     union {
@@ -85,16 +89,17 @@ template <int MW, bool F7> struct TtSmem {
             float tt[C::XK][C::NM][TT_RS];  // V c_b
             float tg[F7 ? C::XK : 1][F7 ? C::NM : 1][TT_RS];  // sig_a sig_b c_b (F7)
         } t;
-        float ct[BM * XM_CP];  // epilogue transpose tile
+        float ct[64 * XM_CP];  // epilogue transpose slice
     } u;
     float img[F7 ? TT_IMG_FLOATS : TT_IMG_FLOATS / 2];
-    uint32_t aw[C::XK][BM];
+    uint32_t aw[C::XK][64 * tt_rh<MW>()];
 };
 
 // A16: the A words are gemm_tt16_kernel's (E3M4; c_a 2^bA as f16 in the high half, m_a x 68 in the
 // low bits), and the kernel runs only when that kernel left its f16 window (flag bit 1).
 template <int MW, bool F7, bool A16>
-__global__ __launch_bounds__(NT) void gemm_tt_kernel(const GemmArgs p) {
+__global__ __launch_bounds__(NT * tt_rh<MW>()) void gemm_tt_kernel(const GemmArgs p) {
+    constexpr int TT_RH = tt_rh<MW>();
     using C = TtCfg<MW, F7>;
     if (A16 && (__hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 30u) == 0u) return;
     constexpr int NM = C::NM, XK = C::XK;
@@ -105,12 +110,14 @@ __global__ __launch_bounds__(NT) void gemm_tt_kernel(const GemmArgs p) {
     auto &img = sm.img;
     auto &aw = sm.aw;
 
+    constexpr int BMT = 64 * TT_RH;  // tile rows
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wvu = __builtin_amdgcn_readfirstlane(wv);
-    const int64_t num_mt = (p.M + BM - 1) / BM;
+    const int wc = wvu & 3, wr = wvu >> 2;  // the wave's column group and row half
+    const int64_t num_mt = (p.M + BMT - 1) / BMT;
     const int64_t tiles = num_mt * ((p.N + BN - 1) / BN);
     const int64_t bid = (int64_t)blockIdx.x % tiles, split = (int64_t)blockIdx.x / tiles;
-    const int64_t m0 = (bid % num_mt) * BM;
+    const int64_t m0 = (bid % num_mt) * BMT;
     const int64_t n0 = (bid / num_mt) * BN;
     const int kbeg = (int)(split * p.kchunk), kend = (int)min(p.K, (int64_t)kbeg + p.kchunk), K32 = (int)p.K;
     const int bR = *p.bR, bA16 = A16 ? *p.bA : 0;
@@ -118,7 +125,7 @@ __global__ __launch_bounds__(NT) void gemm_tt_kernel(const GemmArgs p) {
     const float kc15 = 1.5f * p2(23 - MW), cmin = 1.5f * p2(1 - bR + 23 - MW), thr = p2(-bR - MW);
 
     // static image: V (and sig_a sig_b for F7), [m_b][m_a]
-    for (int e = tid; e < NM * NM; e += NT) {
+    for (int e = tid; e < NM * NM; e += NT * TT_RH) {
         img[e] = reinterpret_cast<const float *>(p.lutw)[e];
         if (F7) img[TT_IMG_FLOATS / 2 + e] = reinterpret_cast<const float *>(p.lutw)[TT_IMG_FLOATS / 2 + e];
     }
@@ -131,10 +138,10 @@ __global__ __launch_bounds__(NT) void gemm_tt_kernel(const GemmArgs p) {
     const __amdgpu_buffer_rsrc_t brsrc =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint2 *>(p.bqw), (short)0, -1, 0x00020000);
 
-    // A staging: one word per thread (threads < XK x 64; conv: lane = row, K-step = wave; matrix:
-    // XK threads per row).  Rows past M re-read row M - 1.
-    const bool astage = tid < XK * BM;
-    const int arow = p.conv ? lane : (tid / XK), akk = p.conv ? wvu : (tid % XK);
+    // A staging: one word per thread (threads < XK x BMT; conv: lane = row, K-step and row half
+    // from the wave; matrix: XK threads per row).  Rows past M re-read row M - 1.
+    const bool astage = tid < XK * BMT;
+    const int arow = p.conv ? lane + 64 * (wvu / XK) : (tid / XK), akk = p.conv ? wvu % XK : (tid % XK);
     uint32_t aoff;
     const uint32_t phw = (uint32_t)(p.awH * p.awW), uW = (uint32_t)p.awW;
     {
@@ -175,7 +182,7 @@ __global__ __launch_bounds__(NT) void gemm_tt_kernel(const GemmArgs p) {
     float acc[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[j] = 0.0f;
-    const uint32_t wvo = (uint32_t)wvu * 64u;  // the wave's 16 columns, bytes into a table row
+    const uint32_t wvo = (uint32_t)wc * 64u;  // the wave's 16 columns, bytes into a table row
     __syncthreads();  // the static image is in LDS
 
     for (int k0 = kbeg; k0 < kend; k0 += XK) {
@@ -209,7 +216,7 @@ __global__ __launch_bounds__(NT) void gemm_tt_kernel(const GemmArgs p) {
 
 #pragma unroll
         for (int kk = 0; kk < XK; ++kk) {
-            const uint32_t w = aw[kk][lane];
+            const uint32_t w = aw[kk][64 * wr + lane];
             float ca;
             uint32_t off;
             if (A16) {  // c_a = the f16 high half / 2^bA; row offset in 2-byte units of the f16 table
@@ -251,16 +258,25 @@ __global__ __launch_bounds__(NT) void gemm_tt_kernel(const GemmArgs p) {
         __syncthreads();
     }
 
-    // lane = row, 16 columns -> [BM][BN] tile in LDS -> each thread's 4x4 block (store_tile)
+    // lane = row, 16 columns -> per row half a [64][BN] slice in LDS -> each thread's 4x4 block
+    // (threads < 256, store_tile)
     float *ct = sm.u.ct;
+    const int ety = tid & 15, etx = (tid >> 4) & 15;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) ct[lane * XM_CP + 16 * wv + j] = acc[j];
-    __syncthreads();
-    const int ety = tid & 15, etx = tid >> 4;
-    float o[TM][TN];
+    for (int hs = 0; hs < TT_RH; ++hs) {
+        if (hs > 0) __syncthreads();
+        if (wr == hs) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+            for (int j = 0; j < 16; ++j) ct[lane * XM_CP + 16 * wc + j] = acc[j];
+        }
+        __syncthreads();
+        if (tid < NT) {
+            float o[TM][TN];
 #pragma unroll
-        for (int j = 0; j < TN; ++j) o[i][j] = ct[(ety * TM + i) * XM_CP + etx * TN + j];
-    store_tile(p, split, m0, n0, ety, etx, o);
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) o[i][j] = ct[(ety * TM + i) * XM_CP + etx * TN + j];
+            store_tile(p, split, m0 + 64 * hs, n0, ety, etx, o);
+        }
+    }
 }
