@@ -31,7 +31,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 ARCH_NAMES = {"resnet18": "ResNet-18", "resnet50": "ResNet-50", "mobilenet_v2": "MobileNetV2",
-              "vit_fc": "ViT-B/16 fc1 (768x3072)"}
+              "vit_fc": "ViT-B/16 fc1 (768x3072)", "vit_b16": "ViT-B/16"}
+# images per GPU per step when --batch is not given: 256 for the CNNs (the round-1/2 protocol);
+# ViT-B/16 is BASELINE config 4, batch 512 over 8 GPUs = 64 per GPU
+DEFAULT_BATCH = {"vit_b16": 64}
 FP32_VALU_PEAK_TFLOPS = 157.3  # MI355X fp32 vector (= fp32 MFMA) peak, MI355X_MICROARCH.md
 
 
@@ -63,20 +66,24 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=256, help="images per GPU per step")
+    ap.add_argument("--batch", type=int, default=None, help="images per GPU per step (default 256; vit_b16 64)")
     ap.add_argument("--cal-batch", type=int, default=64)
     ap.add_argument("--with-comp", action="store_true", help="withComp=True (E4M3: all-zero error table)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-columns", type=int, default=48, help="output columns per layer in the CPU sample")
-    ap.add_argument("--arch", default="resnet18", choices=["resnet18", "resnet50", "mobilenet_v2", "vit_fc"],
+    ap.add_argument("--arch", default="resnet18", choices=sorted(ARCH_NAMES),
                     help="resnet18 = the headline (BASELINE configs[1]); the others are BASELINE configs 3-5 "
-                         "measured the same way (vit_fc: the 768x3072 QCustomLinearTorch on [B, 197, 768])")
+                         "measured the same way (vit_b16: the whole ViT-B/16 of vit_quantized_approx; vit_fc: its "
+                         "768x3072 QCustomLinearTorch alone on [B, 197, 768])")
     ap.add_argument("--bn-stats-batches", type=int, default=4,
                     help="synthetic batches that set the random-init float model's BN statistics (0 = keep the "
                          "default (0, 1) statistics)")
     ap.add_argument("--expo-width", type=int, default=4)
     ap.add_argument("--mant-width", type=int, default=3)
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.batch is None:
+        args.batch = DEFAULT_BATCH.get(args.arch, 256)
+    return args
 
 
 def synthetic_images(n, seed, device, shape=(3, 224, 224)):
@@ -96,6 +103,10 @@ def build_workload(arch, cfg, bn_batches=0, device=None):
     if arch == "mobilenet_v2":
         from fp8_quantization_amd.mobilenet_workload import mobilenet_v2_approx
         return mobilenet_v2_approx(**bn, **cfg), (3, 224, 224), "mobilenet_v2"
+    if arch == "vit_b16":  # no BN: the random-init (HF initialisation) network is used as is
+        from fp8_quantization_amd.vit_workload import vit_b16_approx
+        return vit_b16_approx(**cfg), (3, 224, 224), ("vit_b16 (vit_quantized_approx module tree: 72 approx "
+                                                      "QCustomLinearTorch on [B, 197, *] token rows + classifier)")
     from fp8_quantization_amd.approx_calculation import QCustomLinearTorch
     from fp8_quantization_amd.model_wrap import QuantizedModel
 
@@ -247,7 +258,7 @@ def main():
                             f"withComp={args.with_comp}, with_s2nn2s_opt, quant_btw_mult_accu, res_quantizer, fixed "
                             "ranges), ImageNet-shaped synthetic batch, random-init weights"
                             + (f" with BN statistics estimated on {args.bn_stats_batches} synthetic batches"
-                               if args.bn_stats_batches and args.arch != "vit_fc" else ""),
+                               if args.bn_stats_batches and not args.arch.startswith("vit") else ""),
                 "global_batch": world * args.batch,
                 "per_gpu_batch": args.batch,
                 "input_shape_per_image": list(in_shape),

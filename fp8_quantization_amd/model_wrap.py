@@ -9,15 +9,17 @@ their output quantizer to the preceding layer's.  A float model passed through
 ``quantize_model`` gets the same module tree (and state_dict keys) as with the reference.
 
 Only the approx path is mapped: Conv2d (+BN) -> QCustomBNConv2dTorch, Conv2d without BN ->
-QCustomConv2dTorch (exact product, as in the reference), Linear -> QCustomLinearTorch.  The
-reference's non-approx quantized layers (Conv1d, ConvTranspose, LayerNorm, Linear + BN) are
-outside the hot path and raise NotImplementedError here.
+QCustomConv2dTorch (exact product, as in the reference), Linear -> QCustomLinearTorch, and
+LayerNorm -> QuantLayerNorm (the ViT caller's norms).  The reference's other non-approx
+quantized layers (Conv1d, ConvTranspose, Linear + BN) are outside the hot path and
+raise NotImplementedError here.
 """
 import os
 import copy
 import warnings
 
 import torch
+import torch.nn.functional as F
 from torch import nn
 from torch.nn.modules.conv import _ConvNd
 from torch.nn.modules.pooling import _AdaptiveAvgPoolNd, _AvgPoolNd
@@ -25,16 +27,26 @@ from torch.nn.modules.pooling import _AdaptiveAvgPoolNd, _AvgPoolNd
 from .approx_calculation import QCustomBNConv2dTorch, QCustomConv2dTorch, QCustomLinearTorch
 from .quantization.base_quantized_classes import (QuantizedActivation, QuantizedModule, _set_layer_approx_calculation,
                                                   _set_layer_estimate_ranges, _set_layer_fix_ranges)
-from .quantization.hijacker import activations_set
+from .quantization.hijacker import QuantizationHijacker, activations_set
 from .quantization.quantization_manager import QuantizationManager
 
-__all__ = ["QuantizedModel", "QuantizedActivationWrapper", "Flattener", "fold_bn", "quantize_sequential",
-           "quantize_model", "non_bn_module_map", "bn_module_map"]
+__all__ = ["QuantizedModel", "QuantizedActivationWrapper", "Flattener", "QuantLayerNorm", "fold_bn",
+           "quantize_sequential", "quantize_model", "non_bn_module_map", "bn_module_map"]
 
-non_bn_module_map = {nn.Conv2d: QCustomConv2dTorch, nn.Linear: QCustomLinearTorch}
+
+
+class QuantLayerNorm(QuantizationHijacker, nn.LayerNorm):
+    """autoquant_utils.py:166-174: FP8-quantized input and (per-channel) weight, then a plain
+    fp32 layer norm -- not an approx product."""
+
+    def run_forward(self, x, weight, bias, offsets=None):
+        return F.layer_norm(x.contiguous(), self.normalized_shape, weight.contiguous(), bias.contiguous(), self.eps)
+
+
+non_bn_module_map = {nn.Conv2d: QCustomConv2dTorch, nn.Linear: QCustomLinearTorch, nn.LayerNorm: QuantLayerNorm}
 bn_module_map = {nn.Conv2d: QCustomBNConv2dTorch}
 non_param_modules = (_AdaptiveAvgPoolNd, _AvgPoolNd)
-_OFF_PATH = (nn.Conv1d, nn.ConvTranspose1d, nn.ConvTranspose2d, nn.LayerNorm)
+_OFF_PATH = (nn.Conv1d, nn.ConvTranspose1d, nn.ConvTranspose2d)
 
 
 class QuantizedModel(nn.Module):
@@ -146,6 +158,8 @@ def _module_args(mod, act):
                   bias=mod.bias is not None)
     elif isinstance(mod, nn.Linear):
         kw = dict(in_features=mod.in_features, out_features=mod.out_features, bias=mod.bias is not None)
+    elif isinstance(mod, nn.LayerNorm):  # replace_operations_with_approx_ops.py:240-242
+        kw = dict(normalized_shape=mod.normalized_shape, eps=mod.eps)
     else:
         raise ValueError(f"no approx operator for {type(mod).__name__}")
     kw["activation"] = act
