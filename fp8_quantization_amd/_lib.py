@@ -19,7 +19,8 @@ SYMBOLS = ("fp8a_version", "fp8a_last_error", "fp8a_decompose", "fp8a_quant", "f
            "fp8a_matmul_workspace_size_mnk", "fp8a_matmul", "fp8a_terms", "fp8a_conv2d_workspace_size", "fp8a_conv2d",
            "fp8a_conv2d_bn_act", "fp8a_conv2d_qin_workspace_size", "fp8a_conv2d_qin",
            "fp8a_conv2d_block_workspace_size", "fp8a_conv2d_block", "fp8a_max_pool2d", "fp8a_im2col",
-           "fp8a_fp8_quantize", "fp8a_matmul_qamaa", "fp8a_conv2d_qamaa")
+           "fp8a_fp8_quantize", "fp8a_matmul_qamaa", "fp8a_conv2d_qamaa", "fp8a_matmul_block_workspace_size",
+           "fp8a_matmul_block")
 
 _lib = None
 
@@ -65,6 +66,9 @@ def load():
         "fp8a_fp8_quantize": ([P, I64, I64, P, I, I, I, I, P, P, P, P], I),
         "fp8a_matmul_qamaa": ([P, I64, P, I64, I64, P, I64, I64, I64, P, I, I, I, P], I),
         "fp8a_conv2d_qamaa": ([P, P, P, I64, I64, I64, I64, I64, I, I, I, I, I, I, I, I, I, P, I, I, I, P], I),
+        "fp8a_matmul_block_workspace_size": ([I64, I64, I64], SZ),
+        "fp8a_matmul_block": ([P, I64, P, I64, I64, P, I64, I64, I64, I64, I, I, P, P, I64, P, P, U, P, I, F, F, P, I, I,
+                               I, P, P, P, I, F, F, P, I, I, I, P, P, P, SZ, P], I),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -13,13 +13,15 @@ per-group, per-output-column Python loop (approx_calculation.py:774-799):
 The behaviour lives in mixins so the same run_forward can sit on the reference's own
 QuantizationHijacker / BNFusedHijacker (see ``bind_operator_classes`` and INTEGRATION.md).
 """
+import os
+
 import torch
 import torch.nn.functional as F
 from torch import nn
 
 from . import _lib
-from .approx_ops import (_res_quant_params, approx_conv2d, approx_matmul, make_flags, make_flags_v5, qamaa_conv2d,
-                         qamaa_matmul)
+from .approx_ops import (_res_quant_params, approx_conv2d, approx_matmul, approx_matmul_block, make_flags,
+                         make_flags_v5, qamaa_conv2d, qamaa_matmul)
 from .error_tables import get_comp_table_NN_v5, get_error_table_NN
 from .quantization.hijacker import QuantizationHijacker
 from .quantization.quantized_folded_bn import BNFusedHijacker
@@ -158,10 +160,33 @@ class ApproxLinearMixin(ApproxOpMixin):
     Like the reference, only 2-D inputs are accepted (a 3-D [B, T, K] input fails the
     A.shape[1] == B.shape[0] assertion); set ``flatten_leading_dims = True`` on
     the class or instance for the extension that folds leading dims into rows (ViT linears).
+
+    The approx product, the linear's bias and -- in the fixed-range eval forward -- the input
+    quantizer (``qin``) and a caller's residual tail (``post``) run as one fp8a_matmul_block
+    launch; same values as the reference's separate passes (quantize, product, ``out += bias``,
+    add, quantize).  ``fuse_linear_block = False`` (or FP8A_FUSE_LINEAR=0) keeps the separate
+    passes.
     """
     flatten_leading_dims = False
+    fuse_linear_block = os.environ.get("FP8A_FUSE_LINEAR", "1") != "0"
 
-    def run_forward(self, x, weight, bias, offsets=None):
+    @property
+    def supports_input_quant_fusion(self):
+        return self.fuse_linear_block and self.out_features != 1
+
+    def _block_ok(self):
+        p = self.custom_approx_params
+        return (self.fuse_linear_block and self.approx_flag and self.out_features != 1
+                and p.get("approx_version", 9) != 5 and self.get_weights_fp_bias() is not None)
+
+    def tail_ok(self):
+        """Whether forward(x, post=...) fuses a caller's residual tail: the fixed-range eval
+        forward reduces to this one approx product and nothing follows it inside the layer."""
+        return (self._block_ok() and self.fix_ranges_flag and not self.original_quantize_res and not self.training
+                and self.res_quantizer_flag and not self.quantize_after_mult_and_add
+                and self.activation_function is None and (self.quantize_input or not self._qa()))
+
+    def run_forward(self, x, weight, bias, offsets=None, qin=None, post=None):
         x = x.contiguous()
         weight = weight.contiguous()
         lead = None
@@ -170,10 +195,29 @@ class ApproxLinearMixin(ApproxOpMixin):
                 raise AssertionError(f"approx linear expects a 2-D input, got {tuple(x.shape)} (SURVEY F4)")
             lead = x.shape[:-1]
             x = x.reshape(-1, x.shape[-1])
-        out = self.approx_multiply(x.detach(), weight.detach().t(), self.get_acts_fp_bias(),
-                                   self.get_weights_fp_bias(), self.get_res_fp_bias())
-        if bias is not None:
-            out += bias
+        if self._block_ok():
+            E, M, table, flags = self._approx_config()
+            qt = lambda q: (q.maxval, q.n_bits, q._mbits_int, q.sign_bits)  # noqa: E731
+            pq, pt = None, None
+            if post is not None:
+                pq = post[4]
+                pt = (post[0].reshape(-1, weight.shape[0]),) + tuple(post[1:4]) + ((qt(pq) if pq is not None else None),)
+            out, ib, ob = approx_matmul_block(
+                x.detach(), weight.detach().t(), E, M,
+                None if qin is not None else self._default_bias(self.get_acts_fp_bias(), E, x.device),
+                self.get_weights_fp_bias(), self._default_bias(self.get_res_fp_bias(), E, x.device), table, flags,
+                bias=bias.detach() if bias is not None else None, qin=qt(qin) if qin is not None else None, post=pt)
+            if qin is not None:
+                qin.custom_bias = ib
+            if pq is not None:
+                pq.custom_bias = ob
+        else:
+            if qin is not None or post is not None:
+                raise AssertionError("fused input quantization / tail without the fused linear launch")
+            out = self.approx_multiply(x.detach(), weight.detach().t(), self.get_acts_fp_bias(),
+                                       self.get_weights_fp_bias(), self.get_res_fp_bias())
+            if bias is not None:
+                out += bias
         if lead is not None:
             out = out.reshape(*lead, out.shape[-1])
         return out

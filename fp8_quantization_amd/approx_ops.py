@@ -20,7 +20,7 @@ from torch import nn
 from . import _lib
 from .error_tables import get_error_table_NN  # noqa: F401  (re-exported, v9:555)
 
-__all__ = ["custom_matmul_vectorize", "approx_matmul", "approx_terms", "approx_conv2d", "qamaa_matmul", "qamaa_conv2d",
+__all__ = ["custom_matmul_vectorize", "approx_matmul", "approx_matmul_block", "approx_terms", "approx_conv2d", "qamaa_matmul", "qamaa_conv2d",
            "quant_to_fp_any_vectorize_torch", "float_to_fpany_absint_torch", "get_error_table_NN",
            "make_flags", "make_flags_v5", "fp8_fake_quantize", "bn_act_epilogue"]
 
@@ -154,6 +154,87 @@ def approx_matmul(A, B, E, M, bA, bB, bR, table=None, flags=None, **flag_kwargs)
     C = _matmul_op(A, B, _bias_dev(bA, dev), bB_, _bias_dev(bR, dev), tab, int(E), int(M), int(flags))
     _prof_end(ev, A.shape[0] * A.shape[1] * B.shape[1])
     return C
+
+
+@torch.library.custom_op("fp8approx::matmul_block", mutates_args=())
+def _matmul_block_op(A: torch.Tensor, B: torch.Tensor, bA: Optional[torch.Tensor], bB: torch.Tensor,
+                     bR: torch.Tensor, table: torch.Tensor, E: int, M: int, flags: int, bn: Optional[torch.Tensor],
+                     in_maxval: Optional[torch.Tensor], in_nbits: int, in_mbits: int, in_sign_bits: int,
+                     res: Optional[torch.Tensor], post_act: int, post_lo: float, post_hi: float,
+                     out_maxval: Optional[torch.Tensor], out_nbits: int, out_mbits: int, out_sign_bits: int
+                     ) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
+    """fp8a_matmul_block: C = fq_out(clamp(bn(fq_in(A) @ B) + res)); returns C and the input /
+    output quantizers' float and int32 biases (1-element tensors, unset when unused)."""
+    L = _lib.load()
+    dev = A.device
+    A = A.contiguous()
+    Mr, K = A.shape
+    N = B.shape[1]
+    C = torch.empty((Mr, N), dtype=torch.float32, device=dev)
+    ib, iib = torch.empty(1, device=dev), torch.empty(1, dtype=torch.int32, device=dev)
+    ob, oib = torch.empty(1, device=dev), torch.empty(1, dtype=torch.int32, device=dev)
+    if res is not None:
+        res = res.contiguous()
+        if res.shape != C.shape or res.dtype != torch.float32 or res.device != dev:
+            raise AssertionError(f"approx_matmul_block: residual must be float32 {tuple(C.shape)} on {dev}")
+    if bn is not None and (bn.shape != (N, 2) or bn.dtype != torch.float32 or not bn.is_contiguous()):
+        raise AssertionError(f"approx_matmul_block: epilogue parameters must be contiguous float32 [{N}, 2]")
+    ws = _workspace(dev, L.fp8a_matmul_block_workspace_size(Mr, N, K))
+    opt = lambda t: _lib.dev_ptr(t) if t is not None else None  # noqa: E731
+    rc = L.fp8a_matmul_block(_lib.dev_ptr(A), K, _lib.dev_ptr(B), B.stride(0), B.stride(1), _lib.dev_ptr(C), N, Mr,
+                             N, K, E, M, opt(bA), _lib.dev_ptr(bB), 0 if bB.numel() == 1 else 1, _lib.dev_ptr(bR),
+                             _lib.host_ptr(table), flags, opt(bn), 0, 0.0, 0.0, opt(in_maxval), int(in_nbits),
+                             int(in_mbits), int(in_sign_bits), _lib.dev_ptr(ib), _lib.dev_ptr(iib), opt(res),
+                             int(post_act), float(post_lo), float(post_hi), opt(out_maxval), int(out_nbits),
+                             int(out_mbits), int(out_sign_bits), _lib.dev_ptr(ob), _lib.dev_ptr(oib), _lib.dev_ptr(ws),
+                             ws.numel(), _lib.stream_ptr(dev))
+    _lib.check(rc, "fp8a_matmul_block")
+    return C, ib, iib, ob, oib
+
+
+@_matmul_block_op.register_fake
+def _(A, B, bA, bB, bR, table, E, M, flags, bn, in_maxval, in_nbits, in_mbits, in_sign_bits, res, post_act, post_lo,
+      post_hi, out_maxval, out_nbits, out_mbits, out_sign_bits):
+    one = A.new_empty((1,))
+    onei = A.new_empty((1,), dtype=torch.int32)
+    return A.new_empty((A.shape[0], B.shape[1])), one, onei, one.clone(), onei.clone()
+
+
+def approx_matmul_block(A, B, E, M, bA, bB, bR, table=None, flags=None, bias=None, qin=None, post=None):
+    """approx_matmul with the linear layer's neighbours fused into the same launch:
+    C = fq_out(clamp(fq_in(A) @ B + bias + residual)).
+
+    bias: the linear's bias [N] or None (applied as the store's x * 1 + bias, i.e. exactly the
+    reference's ``out += bias``).  qin / post: as approx_conv2d (per-tensor quantizer tuples; A is
+    then UNQUANTIZED and bA unused).  Returns ``(C, input quantizer bias or None, output quantizer
+    bias or None)``."""
+    if A.dim() != 2 or B.dim() != 2 or A.shape[1] != B.shape[0]:
+        raise AssertionError(f"approx_matmul: shape mismatch {tuple(A.shape)} @ {tuple(B.shape)}")  # v9:20
+    A, B = _as_f32(A), _as_f32(B)
+    if B.stride(0) != 1 and B.stride(1) != 1:
+        B = B.contiguous()
+    dev = A.device
+    tab = _table_host(table, M, _uses_table(flags))
+    bB_ = _bias_dev(bB, dev)
+    if bB_.numel() not in (1, B.shape[1]):
+        raise AssertionError(f"approx_matmul: {bB_.numel()} column biases for {B.shape[1]} columns")
+    bn = None
+    if bias is not None:
+        b = _as_f32(bias).reshape(-1).to(dev)
+        bn = torch.stack((torch.ones_like(b), b), dim=1).contiguous()
+    iq = _quantizer_args(qin) if qin is not None else (None, 0, 0, 0)
+    res, pact, plo, phi, oq = post if post is not None else (None, 0, 0.0, 0.0, None)
+    oq = _quantizer_args(oq) if oq is not None else (None, 0, 0, 0)
+    ev = _prof_start()
+    C, ib, iib, ob, oib = _matmul_block_op(
+        A, B, None if qin is not None else _bias_dev(bA, dev), bB_, _bias_dev(bR, dev), tab, int(E), int(M),
+        int(flags), bn, iq[0].to(dev) if iq[0] is not None else None, iq[1], iq[2], iq[3],
+        _as_f32(res) if res is not None else None, int(pact), float(plo), float(phi),
+        oq[0].to(dev) if oq[0] is not None else None, oq[1], oq[2], oq[3])
+    _prof_end(ev, A.shape[0] * A.shape[1] * B.shape[1])
+    ib._fp8a_i32 = iib
+    ob._fp8a_i32 = oib
+    return C, (ib if qin is not None else None), (ob if oq[0] is not None else None)
 
 
 def approx_terms(A, B, E, M, bA, bB, bR, table=None, flags=None, **flag_kwargs):

@@ -756,9 +756,15 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs p) {
     }
 }
 
-// A(m, k) for the exact kernels: matrix or implicit im2col.
+// A(m, k) for the exact kernels: matrix or implicit im2col (through the fused input quantizer
+// when there is one).
 __device__ __forceinline__ float load_A(const GemmArgs &p, int64_t m, int64_t k) {
-    if (!p.conv) return p.A[m * p.lda + k];
+    if (!p.conv) {
+        const float v = p.A[m * p.lda + k];
+        if (p.fqin.mx == nullptr) return v;
+        const float mx = *p.fqin.mx;
+        return fq_apply(v, mx, fq_bias(mx, p.fqin.E, p.fqin.M), p.fqin.M, p.fqin.S);
+    }
     const int64_t hw = p.Ho * p.Wo, img = m / hw, pix = m - img * hw;
     const int64_t ho = pix / p.Wo, wo = pix - ho * p.Wo;
     const int64_t taps = (int64_t)p.kh * p.kw, c = k / taps, t = k - c * taps, ky = t / p.kw, kx = t - ky * p.kw;
@@ -1740,6 +1746,88 @@ int fp8a_conv2d_block(const float *x, const float *w, float *y, int64_t Bn, int6
     return conv2d_impl(x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups, E, Mw,
                        fin.mx ? nullptr : bA, bW, bR, table, flags, bn, act, act_lo, act_hi, workspace, rest, s, fin,
                        in_bias_out, in_ibias_out, xq, res, post_act, post_lo, post_hi, fout);
+}
+
+size_t fp8a_matmul_block_workspace_size(int64_t M, int64_t N, int64_t K) {
+    const size_t n = fp8a_matmul_workspace_size_mnk(M, N, K);
+    return n == 0 ? 0 : align256(n) + align256((size_t)(M * K) * sizeof(float));
+}
+
+// A linear layer with its neighbours fused (QCustomLinearTorch.run_forward + the callers'
+// elementwise tails, vit_quantized_approx.py:117-156): C = fq_out(clamp(bn_act(fq_in(A) @ B) + res)).
+// Same contract as fp8a_conv2d_block with the row-major matrix operands of fp8a_matmul; with
+// in_maxval, A must be dense (lda == K).
+int fp8a_matmul_block(const float *A, int64_t lda, const float *B, int64_t sbk, int64_t sbn, float *C, int64_t ldc,
+                      int64_t M, int64_t N, int64_t K, int E, int Mw, const int32_t *bA, const int32_t *bB,
+                      int64_t bB_stride, const int32_t *bR, const int32_t *table, uint32_t flags, const float *bn,
+                      int act, float act_lo, float act_hi, const float *in_maxval, int in_nbits, int in_mbits,
+                      int in_sign_bits, float *in_bias_out, int32_t *in_ibias_out, const float *res, int post_act,
+                      float post_lo, float post_hi, const float *out_maxval, int out_nbits, int out_mbits,
+                      int out_sign_bits, float *out_bias_out, int32_t *out_ibias_out, void *workspace,
+                      size_t workspace_bytes, fp8a_stream_t stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (lda < K || ldc < N) return fail(FP8A_EINVAL, "leading dimension smaller than extent");
+    if (flags & (F_TB | F_V5)) return fail(FP8A_EINVAL, "matmul_block: int-bias v9 path only");
+    if (bn && (((uintptr_t)bn) & 7) != 0) return fail(FP8A_EINVAL, "bn parameters must be 8-byte aligned");
+    if (res && (res == C || (((uintptr_t)res) & 15) != 0))
+        return fail(FP8A_EINVAL, "the residual must be a 16-byte aligned tensor other than the output");
+    FqIn fin{}, fout{};
+    if (in_maxval) {
+        const int qE = in_nbits - in_sign_bits - in_mbits;
+        if (in_mbits < 1 || qE < 1) return fail(FP8A_EFORMAT, "bad FP8 quantizer format");
+        if (!in_bias_out || !in_ibias_out) return fail(FP8A_EINVAL, "null pointer");
+        if (lda != K) return fail(FP8A_EINVAL, "matmul_block: fused input quantization needs a dense A");
+        fin = FqIn{in_maxval, qE, in_mbits, in_sign_bits};
+    } else if (!bA) {
+        return fail(FP8A_EINVAL, "null pointer");
+    }
+    if (out_maxval) {
+        const int qE = out_nbits - out_sign_bits - out_mbits;
+        if (out_mbits < 1 || qE < 1) return fail(FP8A_EFORMAT, "bad FP8 quantizer format");
+        if (!out_bias_out || !out_ibias_out) return fail(FP8A_EINVAL, "null pointer");
+        fout = FqIn{out_maxval, qE, out_mbits, out_sign_bits};
+        fq_bias_kernel<<<1, 1, 0, s>>>(fout, out_bias_out, out_ibias_out);
+        int rc = hip_check("fp8a output-quantizer bias");
+        if (rc) return rc;
+    }
+    const size_t xq_bytes = fin.mx ? align256((size_t)(M * K) * sizeof(float)) : 0;
+    if (workspace == nullptr || workspace_bytes < FLAG_BYTES + xq_bytes)
+        return fail(FP8A_EINVAL, "matmul_block workspace too small");
+    const size_t rest = (workspace_bytes - xq_bytes) & ~(size_t)255;
+    GemmArgs a = make_args(A, lda, B, sbk, sbn, C, ldc, M, N, K, E, Mw, fin.mx ? in_ibias_out : bA, bB, bB_stride, bR,
+                           flags);
+    a.ep = reinterpret_cast<const float2 *>(bn); a.ep_act = act; a.ep_lo = act_lo; a.ep_hi = act_hi;
+    a.res = res; a.post_act = post_act; a.post_lo = post_lo; a.post_hi = post_hi; a.post_fq = fout;
+    if (fin.mx && M > 0 && K > 0) {
+        // fuse into the matrix-core pre-decode only where run_gemm will take that path (as conv2d_impl)
+        TablePack tp;
+        int mode;
+        int rc = check_format(E, Mw);
+        if (rc) return rc;
+        rc = pack_table(table, Mw, (flags & F_APPROX) != 0, tp, mode);
+        if (rc) return rc;
+        const int64_t kpad = (K + BK - 1) / BK * BK, npad = (N + BN - 1) / BN * BN, a_words = M * kpad;
+        const bool fused = f8_form(E, Mw, flags, mode) && !no_mx() && a_words < (1ll << 30) &&
+                           kpad * npad * 4 < (1ll << 32) && rest >= gemm_workspace_bytes(M, N, K, a_words);
+        if (fused) {
+            a.fqin = fin;
+            a.fq_bias = in_bias_out;
+            a.fq_ibias = in_ibias_out;  // written by the A pre-decode before any kernel reads it
+        } else {  // one fake-quant pass into the workspace's end, then the plain path on it
+            float *xq = (float *)((char *)workspace + rest);
+            const int64_t nx = M * K;
+            fp8_quantize_kernel<<<(unsigned)std::max<int64_t>(1, std::min<int64_t>((nx + 255) / 256, 65536)), 256, 0,
+                                  s>>>(A, 1, nx, fin.mx, 0, fin.E, fin.M, fin.S, xq, in_bias_out, in_ibias_out);
+            rc = hip_check("fp8a input fake-quant");
+            if (rc) return rc;
+            a.A = xq;
+        }
+    } else if (fin.mx) {  // empty product: the quantizer's bias is still set, as its forward would
+        fq_bias_kernel<<<1, 1, 0, s>>>(fin, in_bias_out, in_ibias_out);
+        int rc = hip_check("fp8a input-quantizer bias");
+        if (rc) return rc;
+    }
+    return run_gemm(a, table, workspace, rest, s);
 }
 
 int fp8a_max_pool2d(const float *x, float *y, int64_t Bn, int64_t C, int64_t H, int64_t W, int kh, int kw, int sh,

@@ -291,3 +291,28 @@ def fused_block_tail(block, features, x, residual_fn, clamp):
     h = features[:-1](x) if len(features) > 1 else x
     lo, hi = clamp if clamp is not None else (0.0, 0.0)
     return last(h, post=(residual, int(clamp is not None), lo, hi, q))
+
+
+def fused_linear_tail(block, dense, x, residual, dropout=None):
+    """block.quantize_activations(dropout(dense(x)) + residual) as one launch of dense's fused
+    linear (fp8a_matmul_block), for the ViT blocks (vit_quantized_approx.py:137-156, 256-262):
+    same conditions as fused_block_tail (per-tensor FPQuantizer in the fixed-range state, or
+    activation quantization off) plus an inactive dropout.  Returns None when the tail must run
+    unfused.  Same result bit for bit as the reference's order (product, + bias, + residual,
+    quantize)."""
+    from .quantization.fp8_quantizer import FPQuantizer
+    from .quantization.quantization_manager import Qstates
+    if not FUSE_BLOCK or not hasattr(dense, "tail_ok") or not dense.tail_ok():
+        return None
+    if dropout is not None and dropout.training and dropout.p > 0:
+        return None
+    q = None
+    if block._qa():
+        mgr = block.activation_quantizer
+        q = getattr(mgr, "quantizer", None)
+        if getattr(mgr, "state", None) != Qstates.fix_ranges or not isinstance(q, FPQuantizer) \
+                or q.maxval.numel() != 1:
+            return None
+    if residual.shape[:-1] != x.shape[:-1] or residual.shape[-1] != dense.out_features:
+        return None
+    return dense(x, post=(residual, 0, 0.0, 0.0, q))

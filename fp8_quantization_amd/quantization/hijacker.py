@@ -96,8 +96,13 @@ class QuantizationHijacker(QuantizedModule):
             res = self.activation_quantizer(res)
         return res
 
-    def forward(self, x, offsets=None):
-        res, qa = self._core(x, offsets)
+    def forward(self, x, offsets=None, post=None):
+        """post: ``(residual, clamp, lo, hi, output FPQuantizer or None)`` -- a caller's tail
+        q(clamp(y + residual)) fused into the approx op's store (only where the operator's
+        ``tail_ok()`` holds; the ViT blocks use it)."""
+        if post is not None and not (hasattr(self, "tail_ok") and self.tail_ok()):
+            raise AssertionError("fused tail requested where the fused store does not run")
+        res, qa = self._core(x, offsets, post=post)
         return self._epilogue(res, qa)
 
     def get_params(self):

@@ -25,7 +25,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from .approx_calculation import QCustomLinearTorch
-from .model_wrap import QuantizedModel, quantize_model
+from .model_wrap import QuantizedModel, fused_linear_tail, quantize_model
 from .quantization.base_quantized_classes import QuantizedActivation
 
 
@@ -248,6 +248,9 @@ class QuantizedViTOutput(QuantizedActivation):
         self.dropout = orig.dropout
 
     def forward(self, h, input_tensor):
+        fused = fused_linear_tail(self, self.dense, h, input_tensor, self.dropout)
+        if fused is not None:
+            return fused
         return self.quantize_activations(self.dropout(self.dense(h)) + input_tensor)
 
 
@@ -310,7 +313,12 @@ class QuantizedViTLayer(QuantizedActivation):
         self.layernorm_after = quantize_model(orig.layernorm_after, **quant_params)
 
     def forward(self, hidden_states, head_mask=None, output_attentions=False):
-        h = self.quantize_activations(self.attention(self.layernorm_before(hidden_states)) + hidden_states)
+        att = self.attention
+        ctx = att.attention(self.layernorm_before(hidden_states))
+        h = fused_linear_tail(self, att.output.dense, ctx, hidden_states, att.output.dropout) \
+            if isinstance(att, QuantizedViTSdpaAttention) and isinstance(att.output, QuantizedViTSelfOutput) else None
+        if h is None:
+            h = self.quantize_activations(att.output(ctx) + hidden_states)
         return self.output(self.intermediate(self.layernorm_after(h)), h)
 
 

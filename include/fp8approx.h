@@ -179,6 +179,30 @@ int fp8a_conv2d_block(const float *x, const float *w, float *y, int64_t Bn, int6
                       size_t workspace_bytes, fp8a_stream_t stream);
 
 /*
+ * A linear layer with its neighbours' elementwise work fused (QCustomLinearTorch.run_forward,
+ * approx_calculation.py:1007-1023, plus the callers' tails in vit_quantized_approx.py:117-156):
+ *   C = fq_out(clamp(bn_act(fq_in(A) @ B) + res, post_lo, post_hi))
+ * Operands as fp8a_matmul.  bn: NULL or [N][2] {scale, shift} per output column (the linear's bias
+ * is {1, bias}: x * 1 + bias is the reference's `out += bias`), act / act_lo / act_hi a clamp.
+ * in_maxval NULL: A is already quantized and bA is used; else A (dense: lda == K) is quantized
+ * by that per-tensor FP8 quantizer inside the operand pre-decode where the E4M3 matrix-core
+ * path runs (else by one pass into the workspace) and its bias is written to in_bias_out /
+ * in_ibias_out.  res: NULL or a 16-byte aligned [M][ldc] tensor (not C).  post / out_* as
+ * fp8a_conv2d_block.  int-bias v9 path only (no TB / V5 flags).
+ * workspace: fp8a_matmul_block_workspace_size() bytes.
+ */
+size_t fp8a_matmul_block_workspace_size(int64_t M, int64_t N, int64_t K);
+int fp8a_matmul_block(const float *A, int64_t lda, const float *B, int64_t sbk, int64_t sbn, float *C,
+                      int64_t ldc, int64_t M, int64_t N, int64_t K, int E, int Mw, const int32_t *bA,
+                      const int32_t *bB, int64_t bB_stride, const int32_t *bR, const int32_t *table,
+                      uint32_t flags, const float *bn, int act, float act_lo, float act_hi,
+                      const float *in_maxval, int in_nbits, int in_mbits, int in_sign_bits,
+                      float *in_bias_out, int32_t *in_ibias_out, const float *res, int post_act,
+                      float post_lo, float post_hi, const float *out_maxval, int out_nbits,
+                      int out_mbits, int out_sign_bits, float *out_bias_out, int32_t *out_ibias_out,
+                      void *workspace, size_t workspace_bytes, fp8a_stream_t stream);
+
+/*
  * nn.MaxPool2d (dilation 1, floor mode, padding <= half the window) on NCHW fp32 y[Bn][C][Ho][Wo]:
  * the ResNet stem pooling on the benchmarked step (not an approx op).
  */

@@ -1,0 +1,85 @@
+"""fp8a_matmul_block (the fused linear launch of QCustomLinearTorch) against the separate passes
+the reference runs (approx_calculation.py:1007-1023 and its ViT callers,
+vit_quantized_approx.py:137-156): input fake-quant -> approx product -> ``out += bias`` ->
+``+ residual`` -> output fake-quant.  Every case must be bit-identical to the unfused sequence
+of this library's own ops (each of which is pinned to the oracle elsewhere), and the quantizer
+biases it reports must equal the ones the quantizers compute."""
+import numpy as np
+import pytest
+import torch
+
+from fp8_quantization_amd import approx_ops as ao
+from fp8_quantization_amd.error_tables import get_error_table_NN
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device")
+    from fp8_quantization_amd import _lib
+    _lib.load()
+
+
+def _operands(Mr, K, N, E, M, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn((Mr, K), generator=g).to(DEV)
+    w = (torch.randn((N, K), generator=g) * 0.05).to(DEV)
+    mxw = w.abs().amax(dim=1)
+    wq, bw = ao.fp8_fake_quantize(w, mxw, 8, M, per_row=True)
+    bias = (torch.randn(N, generator=g) * 0.1).to(DEV)
+    res = torch.randn((Mr, N), generator=g).to(DEV)
+    return x, wq, bw, bias, res
+
+
+def _bits(t):
+    return t.detach().cpu().numpy().view(np.uint32)
+
+
+CASES = [  # (M rows, K, N, E, M, with qin, with post)
+    (300, 192, 160, 4, 3, False, False),
+    (300, 192, 160, 4, 3, True, False),
+    (257, 768, 96, 4, 3, True, True),
+    (64, 4096, 128, 4, 3, True, True),     # split-K
+    (200, 256, 64, 3, 4, True, True),      # E3M4: materialized input quantization, tile-table kernel
+    (130, 96, 72, 2, 5, False, True),      # E2M5
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}x{c[1]}x{c[2]}-E{c[3]}M{c[4]}-q{int(c[5])}p{int(c[6])}"
+                                             for c in CASES])
+def test_matmul_block_equals_separate_passes(case):
+    Mr, K, N, E, M, with_qin, with_post = case
+    x, wq, bw, bias, res = _operands(Mr, K, N, E, M, seed=Mr + K + N)
+    table = get_error_table_NN(E, M, withComp=False, dnsmp_factor=3)
+    flags = ao.make_flags(with_approx=True, with_s2nn2s_opt=True, quant_btw_mult_accu=True)
+    in_mx = x.abs().amax().reshape(1)
+    xq, bx = ao.fp8_fake_quantize(x, in_mx, 8, M)
+    out_mx = torch.tensor([7.5], device=DEV)
+    bR = 2 ** (E - 1) + 3
+
+    # reference order, one pass each
+    ref = ao.approx_matmul(xq, wq.t(), E, M, bx, bw, bR, table, flags=flags)
+    ref = ref + bias
+    if with_post:
+        ref, bo = ao.fp8_fake_quantize(ref + res, out_mx, 8, M)
+
+    qin = (in_mx, 8, M, 1) if with_qin else None
+    post = (res, 0, 0.0, 0.0, (out_mx, 8, M, 1)) if with_post else None
+    got, ib, ob = ao.approx_matmul_block(x if with_qin else xq, wq.t(), E, M, None if with_qin else bx, bw, bR,
+                                         table, flags=flags, bias=bias, qin=qin, post=post)
+    assert np.array_equal(_bits(got), _bits(ref)), np.abs(got - ref).max().item()
+    if with_qin:
+        assert ib.item() == bx.reshape(-1)[0].item()
+    if with_post:
+        assert ob.item() == bo.reshape(-1)[0].item()
+
+
+def test_matmul_block_rejects_bad_residual():
+    x, wq, bw, bias, res = _operands(16, 32, 8, 4, 3, seed=1)
+    flags = ao.make_flags(with_approx=True, with_s2nn2s_opt=True, quant_btw_mult_accu=True)
+    with pytest.raises(AssertionError):
+        ao.approx_matmul_block(x, wq.t(), 4, 3, 12, bw, 15, None, flags=flags,
+                               post=(res[:, :4], 0, 0.0, 0.0, None))

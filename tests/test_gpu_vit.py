@@ -7,7 +7,9 @@ Checks:
   * every approx product of the forward (per layer Q, K, V, attention output, MLP up / down on
     [B * 17, *] token rows, plus the classifier on the class tokens) against the CPU oracle on the
     captured operands and biases: sums within 1e-5 * sum|term| (the bar of every parity test);
-  * the forward is deterministic (bit-identical logits on a second run);
+  * the forward is deterministic (bit-identical logits on a second run), and the fused forward
+    (input quantizer, bias and residual tails inside fp8a_matmul_block) gives logits
+    bit-identical to the unfused one;
   * with the F4 extension switched off the encoder linears raise AssertionError on their 3-D
     inputs, as the reference's do (approx_matmul_whole_v9.py:20).
 Reference-side parity of the whole model is unpinned: the reference cannot run this model
@@ -59,12 +61,20 @@ def _ib(t):
 @pytest.mark.parametrize("fmt", [(4, 3, False), (3, 4, True)], ids=["E4M3", "E3M4-comp"])
 def test_vit_layers_match_oracle(fmt, monkeypatch):
     from fp8_quantization_amd import approx_calculation as ac
+    from fp8_quantization_amd import model_wrap
+    from fp8_quantization_amd.quantization.hijacker import QuantizationHijacker
     E, M, comp = fmt
     model, xcal, xev = _model(E, M, with_comp=comp)
     _calibrate(model, xcal)
     with torch.no_grad():
-        first = model(xev).cpu().numpy()
+        fused = model(xev).cpu().numpy()
+        fused2 = model(xev).cpu().numpy()
+    assert np.array_equal(fused.view(np.uint32), fused2.view(np.uint32)), "forward is not deterministic"
 
+    # unfused: separate input quantizer, product, bias, residual and block-quantizer passes
+    monkeypatch.setattr(QuantizationHijacker, "fuse_input_quant", False)
+    monkeypatch.setattr(ac.ApproxLinearMixin, "fuse_linear_block", False)
+    monkeypatch.setattr(model_wrap, "FUSE_BLOCK", False)
     calls = []
     mm0 = ac.approx_matmul
 
@@ -76,7 +86,7 @@ def test_vit_layers_match_oracle(fmt, monkeypatch):
     monkeypatch.setattr(ac, "approx_matmul", mm)
     with torch.no_grad():
         logits = model(xev).cpu().numpy()
-    assert np.array_equal(first.view(np.uint32), logits.view(np.uint32)), "forward is not deterministic"
+    assert np.array_equal(fused.view(np.uint32), logits.view(np.uint32)), "fused and unfused logits differ"
     assert np.isfinite(logits).all()
     assert len(calls) == SMALL["layers"] * 6 + 1, len(calls)
 
