@@ -63,6 +63,7 @@ def test_resnet18_layers_match_oracle(fmt, monkeypatch):
     monkeypatch.setattr(QuantizationHijacker, "fuse_input_quant", False)
     monkeypatch.setattr(BNFusedHijacker, "fuse_bn_act", False)
     monkeypatch.setattr(model_wrap, "FUSE_BLOCK", False)
+    monkeypatch.setattr(ac.ApproxLinearMixin, "fuse_linear_block", False)
     calls = []
     conv0, mm0 = ac.approx_conv2d, ac.approx_matmul
 

@@ -79,6 +79,7 @@ def test_model_logits_identical_with_and_without_fusion(arch):
     from fp8_quantization_amd import model_wrap
     from fp8_quantization_amd.mobilenet_workload import mobilenet_v2_approx
     from fp8_quantization_amd.quantization.hijacker import QuantizationHijacker
+    from fp8_quantization_amd.approx_calculation import ApproxLinearMixin
     from fp8_quantization_amd.resnet_workload import resnet18_approx, resnet50_approx
     torch.manual_seed(0)
     if arch.startswith("resnet"):
@@ -99,13 +100,16 @@ def test_model_logits_identical_with_and_without_fusion(arch):
         try:
             QuantizationHijacker.fuse_input_quant = False
             model_wrap.FUSE_BLOCK = False
+            ApproxLinearMixin.fuse_linear_block = False
             ref = model(x)
             QuantizationHijacker.fuse_input_quant = True
+            ApproxLinearMixin.fuse_linear_block = True
             got_qin = model(x)
             model_wrap.FUSE_BLOCK = True
             got = model(x)
         finally:
             QuantizationHijacker.fuse_input_quant = True
+            ApproxLinearMixin.fuse_linear_block = True
             model_wrap.FUSE_BLOCK = True
     torch.cuda.synchronize()
     assert torch.equal(got_qin.view(torch.int32), ref.view(torch.int32)), "logits differ with the input fusion on"
