@@ -113,6 +113,254 @@ __global__ __launch_bounds__(256) void onehot_gemm(const uint2 *__restrict__ A1,
     (void)nbn;
 }
 
+// Compact form: A and B as one byte per element (the operand's own e4m3-like code: sign, the
+// exponent field, the mantissa m in the low 3 bits), expanded to the one-hot / L-row operands in
+// registers.  A byte a -> 8 bytes (a & 0xF8) << 8 (a & 7); B byte b -> the L row of m_b with
+// (e_b - 9) added to every byte's exponent field and the sign bit set by s_b.  Workgroup 256 x 128
+// (4 waves of 128 x 64), K chunks of 16.
+constexpr int TM2 = 256, TN2 = 128;
+__global__ __launch_bounds__(256) void onehot_gemm2(const uint8_t *__restrict__ Ac, const uint8_t *__restrict__ Bc,
+                                                    const uint2 *__restrict__ lut, const float *__restrict__ cscale,
+                                                    float *__restrict__ C, int M, int N, int K) {
+    __shared__ uint32_t As[TM2 * 4];  // [row][4 dwords = 16 k]
+    __shared__ uint32_t Bs[TN2 * 4];
+    __shared__ uint2 Ls[8];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wr = wv >> 1, wc = wv & 1;
+    const int nbm = M / TM2;
+    const int bm = blockIdx.x % nbm, bn = blockIdx.x / nbm;
+    const int m0 = bm * TM2, n0 = bn * TN2;
+    if (tid < 8) Ls[tid] = lut[tid];
+    uint4 ra, rb = make_uint4(0, 0, 0, 0);
+    auto gload = [&](int k0) {
+        ra = *reinterpret_cast<const uint4 *>(Ac + (size_t)(m0 + tid) * K + k0);
+        if (tid < TN2) rb = *reinterpret_cast<const uint4 *>(Bc + (size_t)(n0 + tid) * K + k0);
+    };
+    v4f acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+    gload(0);
+    const int r16 = lane & 15, g = lane >> 4;
+    for (int k0 = 0; k0 < K; k0 += KC) {
+        *reinterpret_cast<uint4 *>(&As[4 * tid]) = ra;
+        if (tid < TN2) *reinterpret_cast<uint4 *>(&Bs[4 * tid]) = rb;
+        __syncthreads();
+        if (k0 + KC < K) gload(k0 + KC);
+        v8i bf[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t w = Bs[4 * (64 * wc + 16 * j + r16) + g];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t b = (w >> (8 * e)) & 0xFFu;
+                const uint2 l = Ls[b & 7u];
+                const uint32_t add = (((b >> 3) & 15u) - 9u) * 0x08080808u;
+                const uint32_t sg = (b & 0x80u) ? 0x80808080u : 0u;
+                // a zero (or small) weight: all-zero operand bytes
+                bf[j][2 * e] = b ? (int)((l.x + add) ^ sg) : 0;
+                bf[j][2 * e + 1] = b ? (int)((l.y + add) ^ sg) : 0;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t w = As[4 * (128 * wr + 16 * i + r16) + g];
+            v8i af;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t a = (w >> (8 * e)) & 0xFFu;
+                const uint64_t x = (uint64_t)(a & 0xF8u) << (8 * (a & 7u));
+                af[2 * e] = (int)(uint32_t)x;
+                af[2 * e + 1] = (int)(uint32_t)(x >> 32);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bf[j], acc[i][j], 0, 0, 0, 127, 0,
+                                                                            127);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int col = n0 + 64 * wc + 16 * j + (lane & 15);
+            const float sc = cscale[col];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = m0 + 128 * wr + 16 * i + 4 * (lane >> 4) + r;
+                C[(size_t)row * N + col] = acc[i][j][r] * sc;
+            }
+        }
+}
+
+// Mixed form: A as one byte per element expanded in registers (as onehot_gemm2), B' as the 8-B
+// L-row image of onehot_gemm (weights are static: a per-layer pre-pass).  Workgroup 128 x 128,
+// 64 x 64 per wave (64 accumulator registers: 2 waves / SIMD).
+__global__ __launch_bounds__(256) void onehot_gemm3(const uint8_t *__restrict__ Ac, const uint2 *__restrict__ B1,
+                                                    const float *__restrict__ cscale, float *__restrict__ C, int M,
+                                                    int N, int K) {
+    __shared__ uint32_t As[TM * 4];
+    __shared__ __attribute__((aligned(16))) char Bs[TN * RS];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wr = wv >> 1, wc = wv & 1;
+    const int nbm = M / TM;
+    const int bm = blockIdx.x % nbm, bn = blockIdx.x / nbm;
+    const int m0 = bm * TM, n0 = bn * TN;
+    uint4 ra = make_uint4(0, 0, 0, 0), rb[4];
+    auto gload = [&](int k0) {
+        if (tid < TM) ra = *reinterpret_cast<const uint4 *>(Ac + (size_t)(m0 + tid) * K + k0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int e = tid + 256 * i, r = e >> 3, pc = e & 7;
+            rb[i] = *reinterpret_cast<const uint4 *>(B1 + (size_t)(n0 + r) * K + k0 + 2 * pc);
+        }
+    };
+    v4f acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+    gload(0);
+    const int r16 = lane & 15, g = lane >> 4;
+    for (int k0 = 0; k0 < K; k0 += KC) {
+        if (tid < TM) *reinterpret_cast<uint4 *>(&As[4 * tid]) = ra;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int e = tid + 256 * i, r = e >> 3, pc = e & 7;
+            *reinterpret_cast<uint4 *>(Bs + r * RS + 16 * pc) = rb[i];
+        }
+        __syncthreads();
+        if (k0 + KC < K) gload(k0 + KC);
+        v8i bf[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const char *pb = Bs + (64 * wc + 16 * j + r16) * RS + 32 * g;
+            const uint4 b0 = *reinterpret_cast<const uint4 *>(pb), b1 = *reinterpret_cast<const uint4 *>(pb + 16);
+            bf[j] = (v8i){(int)b0.x, (int)b0.y, (int)b0.z, (int)b0.w, (int)b1.x, (int)b1.y, (int)b1.z, (int)b1.w};
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t w = As[4 * (64 * wr + 16 * i + r16) + g];
+            v8i af;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t a = (w >> (8 * e)) & 0xFFu;
+                const uint64_t x = (uint64_t)(a & 0xF8u) << (8 * (a & 7u));
+                af[2 * e] = (int)(uint32_t)x;
+                af[2 * e + 1] = (int)(uint32_t)(x >> 32);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bf[j], acc[i][j], 0, 0, 0, 127, 0,
+                                                                            127);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int col = n0 + 64 * wc + 16 * j + (lane & 15);
+            const float sc = cscale[col];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = m0 + 64 * wr + 16 * i + 4 * (lane >> 4) + r;
+                C[(size_t)row * N + col] = acc[i][j][r] * sc;
+            }
+        }
+}
+
+// onehot_gemm3 with KCH original k per staged chunk (KCH / 16 MFMA k-steps between barriers).
+template <int KCH>
+__global__ __launch_bounds__(256) void onehot_gemm4(const uint8_t *__restrict__ Ac, const uint2 *__restrict__ B1,
+                                                    const float *__restrict__ cscale, float *__restrict__ C, int M,
+                                                    int N, int K) {
+    constexpr int AW = KCH / 4;           // A dwords per row
+    constexpr int BRS = 8 * KCH + 16;     // B' row stride (bytes)
+    constexpr int APT = TM * KCH / 16;    // 16-B A pieces per chunk
+    constexpr int BPT = TN * KCH / 2 / 256;  // 16-B B' pieces per thread
+    __shared__ uint32_t As[TM * AW];
+    __shared__ __attribute__((aligned(16))) char Bs[TN * BRS];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wr = wv >> 1, wc = wv & 1;
+    const int nbm = M / TM;
+    const int bm = blockIdx.x % nbm, bn = blockIdx.x / nbm;
+    const int m0 = bm * TM, n0 = bn * TN;
+    uint4 ra = make_uint4(0, 0, 0, 0), rb[BPT];
+    auto gload = [&](int k0) {
+        if (tid < APT) {
+            const int r = tid / (KCH / 16), pc = tid % (KCH / 16);
+            ra = *reinterpret_cast<const uint4 *>(Ac + (size_t)(m0 + r) * K + k0 + 16 * pc);
+        }
+#pragma unroll
+        for (int i = 0; i < BPT; ++i) {
+            const int e = tid + 256 * i, r = e / (KCH / 2), pc = e % (KCH / 2);
+            rb[i] = *reinterpret_cast<const uint4 *>(B1 + (size_t)(n0 + r) * K + k0 + 2 * pc);
+        }
+    };
+    v4f acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+    gload(0);
+    const int r16 = lane & 15, g = lane >> 4;
+    for (int k0 = 0; k0 < K; k0 += KCH) {
+        if (tid < APT) {
+            const int r = tid / (KCH / 16), pc = tid % (KCH / 16);
+            *reinterpret_cast<uint4 *>(&As[r * AW + 4 * pc]) = ra;
+        }
+#pragma unroll
+        for (int i = 0; i < BPT; ++i) {
+            const int e = tid + 256 * i, r = e / (KCH / 2), pc = e % (KCH / 2);
+            *reinterpret_cast<uint4 *>(Bs + r * BRS + 16 * pc) = rb[i];
+        }
+        __syncthreads();
+        if (k0 + KCH < K) gload(k0 + KCH);
+#pragma unroll
+        for (int ks = 0; ks < KCH / 16; ++ks) {
+            v8i bf[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const char *pb = Bs + (64 * wc + 16 * j + r16) * BRS + 128 * ks + 32 * g;
+                const uint4 b0 = *reinterpret_cast<const uint4 *>(pb), b1 = *reinterpret_cast<const uint4 *>(pb + 16);
+                bf[j] = (v8i){(int)b0.x, (int)b0.y, (int)b0.z, (int)b0.w, (int)b1.x, (int)b1.y, (int)b1.z, (int)b1.w};
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t w = As[(64 * wr + 16 * i + r16) * AW + 4 * ks + g];
+                v8i af;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const uint32_t a = (w >> (8 * e)) & 0xFFu;
+                    const uint64_t x = (uint64_t)(a & 0xF8u) << (8 * (a & 7u));
+                    af[2 * e] = (int)(uint32_t)x;
+                    af[2 * e + 1] = (int)(uint32_t)(x >> 32);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bf[j], acc[i][j], 0, 0, 0, 127, 0,
+                                                                                127);
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int col = n0 + 64 * wc + 16 * j + (lane & 15);
+            const float sc = cscale[col];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = m0 + 64 * wr + 16 * i + 4 * (lane >> 4) + r;
+                C[(size_t)row * N + col] = acc[i][j][r] * sc;
+            }
+        }
+}
+
 // ---- host: the reference's E4M3 term, scalar, in double
 static double rne(double x) { return std::nearbyint(x); }  // default rounding mode: nearest-even
 
@@ -137,8 +385,8 @@ struct Code {
 int main(int argc, char **argv) {
     const int M = argc > 1 ? atoi(argv[1]) : 8192, N = argc > 2 ? atoi(argv[2]) : 512,
               K = argc > 3 ? atoi(argv[3]) : 2304;
-    if (M % TM || N % TN || K % KC) {
-        fprintf(stderr, "M, N must be multiples of 128 and K of 16\n");
+    if (M % TM2 || N % TN || K % 32) {
+        fprintf(stderr, "M must be a multiple of 256, N of 128 and K of 32\n");
         return 2;
     }
     const int bA = 12, bR = 14;
@@ -221,57 +469,110 @@ int main(int argc, char **argv) {
     printf("M %d N %d K %d  tA %d  small A %.4f of nonzero, small B %.4f of nonzero\n", M, N, K, tA,
            (double)loA / std::max<size_t>(nzA, 1), (double)loB / std::max<size_t>(nzB, 1));
 
-    uint2 *dA, *dB;
+    // compact operands: A byte = sign | e_a << 3 | m_a (0 for zero / small), B byte likewise;
+    // lut[m_b] = the 8 bytes e4m3(L(j, m_b)) (exponent field p + 7), the kernel adds e_b - 9
+    std::vector<uint8_t> Ac((size_t)M * K), Bc((size_t)N * K);
+    for (size_t i = 0; i < a.size(); ++i)
+        Ac[i] = (a[i].e && a[i].e >= tA) ? (uint8_t)((a[i].s << 7) | (a[i].e << 3) | a[i].m) : 0;
+    for (int n = 0; n < N; ++n)
+        for (int k = 0; k < K; ++k) {
+            const Code c = b[(size_t)n * K + k];
+            Bc[(size_t)n * K + k] = (c.e && c.e >= tB[n]) ? (uint8_t)((c.s << 7) | (c.e << 3) | c.m) : 0;
+        }
+    std::vector<uint2> lut(8);
+    for (int mb = 0; mb < 8; ++mb) {
+        uint64_t w = 0;
+        for (int j = 0; j < 8; ++j) {
+            int p;
+            const double f = std::frexp(L[j][mb], &p);
+            w |= (uint64_t)((((p - 1) + 7) << 3) | (int)rne((2 * f - 1) * 8)) << (8 * j);
+        }
+        lut[mb] = make_uint2((uint32_t)w, (uint32_t)(w >> 32));
+    }
+
+    uint2 *dA, *dB, *dL;
+    uint8_t *dAc, *dBc;
     float *dC, *dS;
     CK(hipMalloc(&dA, A1.size() * 8));
     CK(hipMalloc(&dB, B1.size() * 8));
+    CK(hipMalloc(&dAc, Ac.size()));
+    CK(hipMalloc(&dBc, Bc.size()));
+    CK(hipMalloc(&dL, 64));
     CK(hipMalloc(&dC, (size_t)M * N * 4));
     CK(hipMalloc(&dS, N * 4));
     CK(hipMemcpy(dA, A1.data(), A1.size() * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(dB, B1.data(), B1.size() * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dAc, Ac.data(), Ac.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(dBc, Bc.data(), Bc.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(dL, lut.data(), 64, hipMemcpyHostToDevice));
     CK(hipMemcpy(dS, cs.data(), N * 4, hipMemcpyHostToDevice));
-    const dim3 grid((M / TM) * (N / TN));
-    hipLaunchKernelGGL(onehot_gemm, grid, dim3(256), 0, 0, dA, dB, dS, dC, M, N, K);
-    CK(hipDeviceSynchronize());
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const int reps = 20;
-    CK(hipEventRecord(e0));
-    for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(onehot_gemm, grid, dim3(256), 0, 0, dA, dB, dS, dC, M, N, K);
-    CK(hipEventRecord(e1));
-    CK(hipEventSynchronize(e1));
-    float ms;
-    CK(hipEventElapsedTime(&ms, e0, e1));
-    ms /= reps;
     const double prods = (double)M * N * K;
-    printf("dense one-hot kernel: %.3f ms, %.2f T products/s (%.1f products / cycle / SIMD at 2.4 GHz)\n", ms,
-           prods / ms / 1e9, prods / (ms * 1e-3) / (1024 * 2.4e9));
     std::vector<float> C((size_t)M * N);
-    CK(hipMemcpy(C.data(), dC, C.size() * 4, hipMemcpyDeviceToHost));
-    // check sampled rows against the reference term over hi x hi pairs
-    int bad = 0, checked = 0;
-    double worst = 0;
-    for (int t = 0; t < 48; ++t) {
-        const int m = (int)((t * 2654435761u) % (unsigned)M);
-        for (int n = 0; n < N; ++n) {
-            double s = 0, sa = 0;
-            for (int k = 0; k < K; ++k) {
-                const Code ca = a[(size_t)m * K + k], cb = b[(size_t)n * K + k];
-                if (!ca.e || !cb.e || ca.e < tA || cb.e < tB[n]) continue;
-                const double v = ((1 + ca.m / 8.0) * (1 + cb.m / 8.0) - T[ca.m][cb.m] / 8.0) *
-                                 std::ldexp(1.0, ca.e - bA + cb.e - bB[n]) * ((ca.s ^ cb.s) ? -1 : 1);
-                const double term = q_r(v, bR);
-                s += term;
-                sa += std::fabs(term);
+    int bad_total = 0;
+    for (int form = 1; form <= 5; ++form) {
+        if (form == 5 && K % 64) continue;
+        auto launch = [&]() {
+            if (form == 1)
+                hipLaunchKernelGGL(onehot_gemm, dim3((M / TM) * (N / TN)), dim3(256), 0, 0, dA, dB, dS, dC, M, N, K);
+            else if (form == 2)
+                hipLaunchKernelGGL(onehot_gemm2, dim3((M / TM2) * (N / TN2)), dim3(256), 0, 0, dAc, dBc, dL, dS, dC,
+                                   M, N, K);
+            else if (form == 3)
+                hipLaunchKernelGGL(onehot_gemm3, dim3((M / TM) * (N / TN)), dim3(256), 0, 0, dAc, dB, dS, dC, M, N, K);
+            else if (form == 4)
+                hipLaunchKernelGGL(onehot_gemm4<32>, dim3((M / TM) * (N / TN)), dim3(256), 0, 0, dAc, dB, dS, dC, M, N,
+                                   K);
+            else
+                hipLaunchKernelGGL(onehot_gemm4<64>, dim3((M / TM) * (N / TN)), dim3(256), 0, 0, dAc, dB, dS, dC, M, N,
+                                   K);
+        };
+        CK(hipMemset(dC, 0xFF, (size_t)M * N * 4));
+        launch();
+        CK(hipDeviceSynchronize());
+        const int reps = 20;
+        CK(hipEventRecord(e0));
+        for (int r = 0; r < reps; ++r) launch();
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        ms /= reps;
+        printf("%s: %.3f ms, %.2f T products/s (%.1f products / cycle / SIMD at 2.4 GHz)\n",
+               form == 1 ? "dense one-hot, 8-B operand images"
+               : form == 2 ? "dense one-hot, 1-B operands expanded in registers"
+               : form == 3 ? "dense one-hot, 1-B A expanded in registers, 8-B B' image"
+               : form == 4 ? "  same, 32 k per staged chunk"
+                           : "  same, 64 k per staged chunk",
+               ms, prods / ms / 1e9, prods / (ms * 1e-3) / (1024 * 2.4e9));
+        CK(hipMemcpy(C.data(), dC, C.size() * 4, hipMemcpyDeviceToHost));
+        // check sampled rows against the reference term over hi x hi pairs
+        int bad = 0, checked = 0;
+        double worst = 0;
+        for (int t = 0; t < 32; ++t) {
+            const int m = (int)((t * 2654435761u) % (unsigned)M);
+            for (int n = 0; n < N; ++n) {
+                double s = 0, sa = 0;
+                for (int k = 0; k < K; ++k) {
+                    const Code ca = a[(size_t)m * K + k], cb = b[(size_t)n * K + k];
+                    if (!ca.e || !cb.e || ca.e < tA || cb.e < tB[n]) continue;
+                    const double v = ((1 + ca.m / 8.0) * (1 + cb.m / 8.0) - T[ca.m][cb.m] / 8.0) *
+                                     std::ldexp(1.0, ca.e - bA + cb.e - bB[n]) * ((ca.s ^ cb.s) ? -1 : 1);
+                    const double term = q_r(v, bR);
+                    s += term;
+                    sa += std::fabs(term);
+                }
+                const double d = std::fabs(C[(size_t)m * N + n] - s);
+                worst = std::max(worst, d / (sa + 1e-30));
+                bad += !(d <= 1e-5 * sa + 1e-30);
+                ++checked;
             }
-            const double d = std::fabs(C[(size_t)m * N + n] - s);
-            const double tol = 1e-5 * sa + 1e-30;
-            worst = std::max(worst, d / (sa + 1e-30));
-            bad += d > tol;
-            ++checked;
         }
+        printf("  check: %d of %d sampled outputs outside 1e-5 sum|term| (worst rel %.3g)\n", bad, checked, worst);
+        bad_total += bad;
     }
-    printf("check: %d of %d sampled outputs outside 1e-5 sum|term| (worst rel %.3g)\n", bad, checked, worst);
+    const int bad = bad_total;
     return bad ? 1 : 0;
 }
