@@ -172,7 +172,7 @@ class ApproxLinearMixin(ApproxOpMixin):
 
     @property
     def supports_input_quant_fusion(self):
-        return self.fuse_linear_block and self.out_features != 1
+        return self._block_ok()
 
     def _block_ok(self):
         p = self.custom_approx_params

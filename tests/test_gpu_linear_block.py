@@ -83,3 +83,29 @@ def test_matmul_block_rejects_bad_residual():
     with pytest.raises(AssertionError):
         ao.approx_matmul_block(x, wq.t(), 4, 3, 12, bw, 15, None, flags=flags,
                                post=(res[:, :4], 0, 0.0, 0.0, None))
+
+
+@pytest.mark.parametrize("version", [9, 5])
+def test_linear_operator_fixed_range_forward(version):
+    """QCustomLinearTorch in the fixed-range approx forward (input quantizer and bias fused into
+    the launch for v9; v5 keeps its own path) equals the explicit sequence: quantize the input,
+    approx_multiply, + bias."""
+    from fp8_quantization_amd.approx_calculation import QCustomLinearTorch
+    from fp8_quantization_amd.resnet_workload import approx_qparams
+    qp = approx_qparams(expo_width=4, mant_width=3) if version == 9 else \
+        approx_qparams(expo_width=3, mant_width=4, withComp=True)
+    if version == 5:
+        qp["custom_approx_params"].update(approx_version=5, sim_hw_add_OFUF=True)
+    torch.manual_seed(2)
+    m = QCustomLinearTorch(in_features=48, out_features=24, bias=True, **qp).to(DEV).eval()
+    x = torch.randn(10, 48, device=DEV)
+    with torch.no_grad():
+        m.quantized()
+        m.estimate_ranges()
+        m(x)
+        m.fix_ranges()
+        got = m(x)
+        xq = m.activation_quantizer(x)
+        wq, b = m.get_params()
+        ref = m.approx_multiply(xq, wq.t(), m.get_acts_fp_bias(), m.get_weights_fp_bias(), m.get_res_fp_bias()) + b
+    assert np.array_equal(_bits(got), _bits(ref))

@@ -72,6 +72,21 @@ def layer_stats(A, B, bR, rows=2048):
         if tot < best[0]:
             best = (tot, tau, fa, fb)
     out.update(split_best=best[0], split_tau=best[1], split_fa=best[2], split_fb=best[3])
+    # compaction cost of that split (the round-3 small-set path): per 16-row block, every row's
+    # small A entries padded to the block's longest list (lanes of a wave = the block's rows), and
+    # per 16-column block the same for small weights; eff = entries / padded slots
+    if best[1] is not None:
+        tau = best[1]
+        small_a = (nz_a & (ea < tau)).sum(dim=1).float()  # [rows]
+        nb = small_a.numel() // 16
+        if nb:
+            blk = small_a[:nb * 16].view(nb, 16)
+            out["rowpad_eff_a"] = float(blk.sum() / (16 * blk.amax(dim=1)).sum().clamp(min=1))
+        small_b = (nz_b & (eb < thr - tau)).sum(dim=0).float()  # [cols]
+        nbb = small_b.numel() // 16
+        if nbb:
+            blk = small_b[:nbb * 16].view(nbb, 16)
+            out["colpad_eff_b"] = float(blk.sum() / (16 * blk.amax(dim=1)).sum().clamp(min=1))
     # per-(k, 32-column block) percentile thresholds: small b = below the block's q-quantile,
     # small a = e_a < thr - (q-quantile exponent)
     for q in (0.05, 0.1, 0.2):
