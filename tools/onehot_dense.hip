@@ -119,32 +119,34 @@ __global__ __launch_bounds__(256) void onehot_gemm(const uint2 *__restrict__ A1,
 // (e_b - 9) added to every byte's exponent field and the sign bit set by s_b.  Workgroup 256 x 128
 // (4 waves of 128 x 64), K chunks of 16.
 constexpr int TM2 = 256, TN2 = 128;
+template <int RB>  // 16-row blocks per wave: 8 -> 256 x 128 workgroup tiles, 4 -> 128 x 128
 __global__ __launch_bounds__(256) void onehot_gemm2(const uint8_t *__restrict__ Ac, const uint8_t *__restrict__ Bc,
                                                     const uint2 *__restrict__ lut, const float *__restrict__ cscale,
                                                     float *__restrict__ C, int M, int N, int K) {
-    __shared__ uint32_t As[TM2 * 4];  // [row][4 dwords = 16 k]
+    constexpr int TMR = 32 * RB;
+    __shared__ uint32_t As[TMR * 4];  // [row][4 dwords = 16 k]
     __shared__ uint32_t Bs[TN2 * 4];
     __shared__ uint2 Ls[8];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wr = wv >> 1, wc = wv & 1;
-    const int nbm = M / TM2;
+    const int nbm = M / TMR;
     const int bm = blockIdx.x % nbm, bn = blockIdx.x / nbm;
-    const int m0 = bm * TM2, n0 = bn * TN2;
+    const int m0 = bm * TMR, n0 = bn * TN2;
     if (tid < 8) Ls[tid] = lut[tid];
     uint4 ra, rb = make_uint4(0, 0, 0, 0);
     auto gload = [&](int k0) {
-        ra = *reinterpret_cast<const uint4 *>(Ac + (size_t)(m0 + tid) * K + k0);
+        if (tid < TMR) ra = *reinterpret_cast<const uint4 *>(Ac + (size_t)(m0 + tid) * K + k0);
         if (tid < TN2) rb = *reinterpret_cast<const uint4 *>(Bc + (size_t)(n0 + tid) * K + k0);
     };
-    v4f acc[8][4];
+    v4f acc[RB][4];
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < RB; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
     gload(0);
     const int r16 = lane & 15, g = lane >> 4;
     for (int k0 = 0; k0 < K; k0 += KC) {
-        *reinterpret_cast<uint4 *>(&As[4 * tid]) = ra;
+        if (tid < TMR) *reinterpret_cast<uint4 *>(&As[4 * tid]) = ra;
         if (tid < TN2) *reinterpret_cast<uint4 *>(&Bs[4 * tid]) = rb;
         __syncthreads();
         if (k0 + KC < K) gload(k0 + KC);
@@ -164,8 +166,8 @@ __global__ __launch_bounds__(256) void onehot_gemm2(const uint8_t *__restrict__ 
             }
         }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const uint32_t w = As[4 * (128 * wr + 16 * i + r16) + g];
+        for (int i = 0; i < RB; ++i) {
+            const uint32_t w = As[4 * (16 * RB * wr + 16 * i + r16) + g];
             v8i af;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -182,14 +184,14 @@ __global__ __launch_bounds__(256) void onehot_gemm2(const uint8_t *__restrict__ 
         __syncthreads();
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < RB; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int col = n0 + 64 * wc + 16 * j + (lane & 15);
             const float sc = cscale[col];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int row = m0 + 128 * wr + 16 * i + 4 * (lane >> 4) + r;
+                const int row = m0 + 16 * RB * wr + 16 * i + 4 * (lane >> 4) + r;
                 C[(size_t)row * N + col] = acc[i][j][r] * sc;
             }
         }
@@ -513,16 +515,19 @@ int main(int argc, char **argv) {
     const double prods = (double)M * N * K;
     std::vector<float> C((size_t)M * N);
     int bad_total = 0;
-    for (int form = 1; form <= 4; ++form) {
+    for (int form = 1; form <= 5; ++form) {
         auto launch = [&]() {
             if (form == 1)
                 hipLaunchKernelGGL(onehot_gemm, dim3((M / TM) * (N / TN)), dim3(256), 0, 0, dA, dB, dS, dC, M, N, K);
             else if (form == 2)
-                hipLaunchKernelGGL(onehot_gemm2, dim3((M / TM2) * (N / TN2)), dim3(256), 0, 0, dAc, dBc, dL, dS, dC,
+                hipLaunchKernelGGL(onehot_gemm2<8>, dim3((M / TM2) * (N / TN2)), dim3(256), 0, 0, dAc, dBc, dL, dS, dC,
+                                   M, N, K);
+            else if (form == 5)
+                hipLaunchKernelGGL(onehot_gemm2<4>, dim3((M / 128) * (N / TN2)), dim3(256), 0, 0, dAc, dBc, dL, dS, dC,
                                    M, N, K);
             else if (form == 3)
                 hipLaunchKernelGGL(onehot_gemm3, dim3((M / TM) * (N / TN)), dim3(256), 0, 0, dAc, dB, dS, dC, M, N, K);
-            else
+            else if (form == 4)
                 hipLaunchKernelGGL(onehot_gemm4<32>, dim3((M / TM) * (N / TN)), dim3(256), 0, 0, dAc, dB, dS, dC, M, N,
                                    K);
         };
@@ -541,7 +546,8 @@ int main(int argc, char **argv) {
                form == 1 ? "dense one-hot, 8-B operand images"
                : form == 2 ? "dense one-hot, 1-B operands expanded in registers"
                : form == 3 ? "dense one-hot, 1-B A expanded in registers, 8-B B' image"
-                           : "  same, 32 k per staged chunk",
+               : form == 4 ? "  same, 32 k per staged chunk"
+                           : "1-B operands expanded in registers, 128 x 128 tiles (64 x 64 per wave)",
                ms, prods / ms / 1e9, prods / (ms * 1e-3) / (1024 * 2.4e9));
         CK(hipMemcpy(C.data(), dC, C.size() * 4, hipMemcpyDeviceToHost));
         // check sampled rows against the reference term over hi x hi pairs
