@@ -45,20 +45,21 @@ CASES = [  # (M rows, K, N, E, M, with qin, with post)
     (64, 4096, 128, 4, 3, True, True),     # split-K
     (200, 256, 64, 3, 4, True, True),      # E3M4: materialized input quantization, tile-table kernel
     (130, 96, 72, 2, 5, False, True),      # E2M5
+    (96, 160, 64, 4, 3, True, True, 1),    # bR = 1: terms beyond the e4m3 range -> gated exact kernel with qin
 ]
 
 
 @pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}x{c[1]}x{c[2]}-E{c[3]}M{c[4]}-q{int(c[5])}p{int(c[6])}"
-                                             for c in CASES])
+                                             + (f"-bR{c[7]}" if len(c) > 7 else "") for c in CASES])
 def test_matmul_block_equals_separate_passes(case):
-    Mr, K, N, E, M, with_qin, with_post = case
+    Mr, K, N, E, M, with_qin, with_post = case[:7]
     x, wq, bw, bias, res = _operands(Mr, K, N, E, M, seed=Mr + K + N)
     table = get_error_table_NN(E, M, withComp=False, dnsmp_factor=3)
     flags = ao.make_flags(with_approx=True, with_s2nn2s_opt=True, quant_btw_mult_accu=True)
     in_mx = x.abs().amax().reshape(1)
     xq, bx = ao.fp8_fake_quantize(x, in_mx, 8, M)
     out_mx = torch.tensor([7.5], device=DEV)
-    bR = 2 ** (E - 1) + 3
+    bR = case[7] if len(case) > 7 else 2 ** (E - 1) + 3
 
     # reference order, one pass each
     ref = ao.approx_matmul(xq, wq.t(), E, M, bx, bw, bR, table, flags=flags)
