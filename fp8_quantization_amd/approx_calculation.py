@@ -20,8 +20,8 @@ import torch.nn.functional as F
 from torch import nn
 
 from . import _lib
-from .approx_ops import (_res_quant_params, approx_conv2d, approx_matmul, approx_matmul_block, make_flags,
-                         make_flags_v5, qamaa_conv2d, qamaa_matmul)
+from .approx_ops import (_res_quant_params, approx_conv2d, approx_matmul, approx_matmul_block, bias_epilogue,
+                         make_flags, make_flags_v5, qamaa_conv2d, qamaa_matmul)
 from .error_tables import get_comp_table_NN_v5, get_error_table_NN
 from .quantization.hijacker import QuantizationHijacker
 from .quantization.quantized_folded_bn import BNFusedHijacker
@@ -186,6 +186,17 @@ class ApproxLinearMixin(ApproxOpMixin):
                 and self.res_quantizer_flag and not self.quantize_after_mult_and_add
                 and self.activation_function is None and (self.quantize_input or not self._qa()))
 
+    def _bias_epilogue(self, bias, device):
+        """{1, bias} store epilogue, rebuilt only when the bias tensor changes."""
+        if bias is None:
+            return None
+        key = (bias._version, bias.data_ptr(), device)
+        cached = getattr(self, "_bias_epi_cache", None)
+        if cached is None or cached[0] != key:
+            cached = (key, bias_epilogue(bias, device))
+            self._bias_epi_cache = cached
+        return cached[1]
+
     def run_forward(self, x, weight, bias, offsets=None, qin=None, post=None):
         x = x.contiguous()
         weight = weight.contiguous()
@@ -206,7 +217,7 @@ class ApproxLinearMixin(ApproxOpMixin):
                 x.detach(), weight.detach().t(), E, M,
                 None if qin is not None else self._default_bias(self.get_acts_fp_bias(), E, x.device),
                 self.get_weights_fp_bias(), self._default_bias(self.get_res_fp_bias(), E, x.device), table, flags,
-                bias=bias.detach() if bias is not None else None, qin=qt(qin) if qin is not None else None, post=pt)
+                bias_epi=self._bias_epilogue(bias, x.device), qin=qt(qin) if qin is not None else None, post=pt)
             if qin is not None:
                 qin.custom_bias = ib
             if pq is not None:

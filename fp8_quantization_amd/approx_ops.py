@@ -200,12 +200,21 @@ def _(A, B, bA, bB, bR, table, E, M, flags, bn, in_maxval, in_nbits, in_mbits, i
     return A.new_empty((A.shape[0], B.shape[1])), one, onei, one.clone(), onei.clone()
 
 
-def approx_matmul_block(A, B, E, M, bA, bB, bR, table=None, flags=None, bias=None, qin=None, post=None):
+def bias_epilogue(bias, device):
+    """The store epilogue {1, bias} per column for a linear's bias: x * 1 + bias is exactly the
+    reference's ``out += bias``."""
+    with torch.no_grad():
+        b = _as_f32(bias.detach()).reshape(-1).to(device)
+        return torch.stack((torch.ones_like(b), b), dim=1).contiguous()
+
+
+def approx_matmul_block(A, B, E, M, bA, bB, bR, table=None, flags=None, bias=None, qin=None, post=None,
+                        bias_epi=None):
     """approx_matmul with the linear layer's neighbours fused into the same launch:
     C = fq_out(clamp(fq_in(A) @ B + bias + residual)).
 
     bias: the linear's bias [N] or None (applied as the store's x * 1 + bias, i.e. exactly the
-    reference's ``out += bias``).  qin / post: as approx_conv2d (per-tensor quantizer tuples; A is
+    reference's ``out += bias``); bias_epi: the same as a prebuilt ``bias_epilogue`` tensor.  qin / post: as approx_conv2d (per-tensor quantizer tuples; A is
     then UNQUANTIZED and bA unused).  Returns ``(C, input quantizer bias or None, output quantizer
     bias or None)``."""
     if A.dim() != 2 or B.dim() != 2 or A.shape[1] != B.shape[0]:
@@ -218,10 +227,7 @@ def approx_matmul_block(A, B, E, M, bA, bB, bR, table=None, flags=None, bias=Non
     bB_ = _bias_dev(bB, dev)
     if bB_.numel() not in (1, B.shape[1]):
         raise AssertionError(f"approx_matmul: {bB_.numel()} column biases for {B.shape[1]} columns")
-    bn = None
-    if bias is not None:
-        b = _as_f32(bias).reshape(-1).to(dev)
-        bn = torch.stack((torch.ones_like(b), b), dim=1).contiguous()
+    bn = bias_epi if bias_epi is not None else (bias_epilogue(bias, dev) if bias is not None else None)
     iq = _quantizer_args(qin) if qin is not None else (None, 0, 0, 0)
     res, pact, plo, phi, oq = post if post is not None else (None, 0, 0.0, 0.0, None)
     oq = _quantizer_args(oq) if oq is not None else (None, 0, 0, 0)
