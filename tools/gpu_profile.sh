@@ -22,5 +22,5 @@ timeout -k 10 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIV
     python $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/pmc_sq.log 2>&1 ; \
 cd $R && python tools/prof_summary.py --trace $(ls $OUT/trace/*kernel_trace.csv) --stats $(ls $OUT/trace/*kernel_stats.csv) \
     --pmc $(ls $OUT/pmc_*/*counter_collection.csv 2>/dev/null) --timed-launches $((STEPS*LAUNCH_PER_STEP)) \
-    --out $OUT/summary --pmc-json $OUT/pmc.json --note "bench.py --steps $STEPS --warmup 2 (resnet18 E4M3 approx_v9, batch 256)" ; \
+    --out $OUT/summary --pmc-json $OUT/pmc.json --note "bench.py --steps $STEPS --warmup 2 (resnet18 E4M3 approx_v9, batch 512)" --batch 512 ; \
 cat $OUT/bench.json
