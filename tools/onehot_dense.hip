@@ -364,6 +364,106 @@ __global__ __launch_bounds__(256) void onehot_gemm4(const uint8_t *__restrict__ 
         }
 }
 
+// Both operands as 1-B codes in HBM; per 32-k chunk the workgroup expands B into the 8-B L-row
+// operand ONCE in LDS (shared by the two row-waves of each column half), A is expanded in
+// registers.  128 x 128 tiles, 64 x 64 per wave.
+__global__ __launch_bounds__(256) void onehot_gemm5(const uint8_t *__restrict__ Ac, const uint8_t *__restrict__ Bc,
+                                                    const uint2 *__restrict__ lut, const float *__restrict__ cscale,
+                                                    float *__restrict__ C, int M, int N, int K) {
+    constexpr int KCH = 32, BRS5 = 8 * KCH + 16, AW5 = KCH / 4 + 1;  // B' row stride (bytes), A row (dwords)
+    __shared__ uint32_t As[TM * AW5];
+    __shared__ __attribute__((aligned(16))) char Bs[TN * BRS5];
+    __shared__ uint2 Ls[8];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wr = wv >> 1, wc = wv & 1;
+    const int nbm = M / TM;
+    const int bm = blockIdx.x % nbm, bn = blockIdx.x / nbm;
+    const int m0 = bm * TM, n0 = bn * TN;
+    if (tid < 8) Ls[tid] = lut[tid];
+    // thread t stages A row t / 2 (16 B half t & 1) and B column t / 2 (16 k half t & 1)
+    const int sr = tid >> 1, sh = tid & 1;
+    uint4 ra, rb;
+    auto gload = [&](int k0) {
+        ra = *reinterpret_cast<const uint4 *>(Ac + (size_t)(m0 + sr) * K + k0 + 16 * sh);
+        rb = *reinterpret_cast<const uint4 *>(Bc + (size_t)(n0 + sr) * K + k0 + 16 * sh);
+    };
+    v4f acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+    gload(0);
+    __syncthreads();  // Ls
+    const int r16 = lane & 15, g = lane >> 4;
+    for (int k0 = 0; k0 < K; k0 += KCH) {
+        // A codes as they are; B codes expanded to the L-row operand
+        As[sr * AW5 + 4 * sh + 0] = ra.x;
+        As[sr * AW5 + 4 * sh + 1] = ra.y;
+        As[sr * AW5 + 4 * sh + 2] = ra.z;
+        As[sr * AW5 + 4 * sh + 3] = ra.w;
+        {
+            const uint32_t wb[4] = {rb.x, rb.y, rb.z, rb.w};
+            char *dst = Bs + sr * BRS5 + 128 * sh;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                uint32_t o[8];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const uint32_t b = (wb[q] >> (8 * e)) & 0xFFu;
+                    const uint2 l = Ls[b & 7u];
+                    const uint32_t add = (((b >> 3) & 15u) - 9u) * 0x08080808u;
+                    const uint32_t sg = (b & 0x80u) ? 0x80808080u : 0u;
+                    o[2 * e] = b ? ((l.x + add) ^ sg) : 0u;
+                    o[2 * e + 1] = b ? ((l.y + add) ^ sg) : 0u;
+                }
+                *reinterpret_cast<uint4 *>(dst + 32 * q) = make_uint4(o[0], o[1], o[2], o[3]);
+                *reinterpret_cast<uint4 *>(dst + 32 * q + 16) = make_uint4(o[4], o[5], o[6], o[7]);
+            }
+        }
+        __syncthreads();
+        if (k0 + KCH < K) gload(k0 + KCH);
+#pragma unroll
+        for (int ks = 0; ks < KCH / 16; ++ks) {
+            v8i bf[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const char *pb = Bs + (64 * wc + 16 * j + r16) * BRS5 + 128 * ks + 32 * g;
+                const uint4 b0 = *reinterpret_cast<const uint4 *>(pb), b1 = *reinterpret_cast<const uint4 *>(pb + 16);
+                bf[j] = (v8i){(int)b0.x, (int)b0.y, (int)b0.z, (int)b0.w, (int)b1.x, (int)b1.y, (int)b1.z, (int)b1.w};
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t w = As[(64 * wr + 16 * i + r16) * AW5 + 4 * ks + g];
+                v8i af;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const uint32_t a = (w >> (8 * e)) & 0xFFu;
+                    const uint64_t x = (uint64_t)(a & 0xF8u) << (8 * (a & 7u));
+                    af[2 * e] = (int)(uint32_t)x;
+                    af[2 * e + 1] = (int)(uint32_t)(x >> 32);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bf[j], acc[i][j], 0, 0, 0, 127, 0,
+                                                                                127);
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int col = n0 + 64 * wc + 16 * j + (lane & 15);
+            const float sc = cscale[col];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = m0 + 64 * wr + 16 * i + 4 * (lane >> 4) + r;
+                C[(size_t)row * N + col] = acc[i][j][r] * sc;
+            }
+        }
+}
+
 // ---- host: the reference's E4M3 term, scalar, in double
 static double rne(double x) { return std::nearbyint(x); }  // default rounding mode: nearest-even
 
@@ -515,7 +615,7 @@ int main(int argc, char **argv) {
     const double prods = (double)M * N * K;
     std::vector<float> C((size_t)M * N);
     int bad_total = 0;
-    for (int form = 1; form <= 5; ++form) {
+    for (int form = 1; form <= 6; ++form) {
         auto launch = [&]() {
             if (form == 1)
                 hipLaunchKernelGGL(onehot_gemm, dim3((M / TM) * (N / TN)), dim3(256), 0, 0, dA, dB, dS, dC, M, N, K);
@@ -525,6 +625,9 @@ int main(int argc, char **argv) {
             else if (form == 5)
                 hipLaunchKernelGGL(onehot_gemm2<4>, dim3((M / 128) * (N / TN2)), dim3(256), 0, 0, dAc, dBc, dL, dS, dC,
                                    M, N, K);
+            else if (form == 6)
+                hipLaunchKernelGGL(onehot_gemm5, dim3((M / TM) * (N / TN)), dim3(256), 0, 0, dAc, dBc, dL, dS, dC, M, N,
+                                   K);
             else if (form == 3)
                 hipLaunchKernelGGL(onehot_gemm3, dim3((M / TM) * (N / TN)), dim3(256), 0, 0, dAc, dB, dS, dC, M, N, K);
             else if (form == 4)
@@ -547,7 +650,8 @@ int main(int argc, char **argv) {
                : form == 2 ? "dense one-hot, 1-B operands expanded in registers"
                : form == 3 ? "dense one-hot, 1-B A expanded in registers, 8-B B' image"
                : form == 4 ? "  same, 32 k per staged chunk"
-                           : "1-B operands expanded in registers, 128 x 128 tiles (64 x 64 per wave)",
+               : form == 5 ? "1-B operands expanded in registers, 128 x 128 tiles (64 x 64 per wave)"
+                           : "1-B operands, B expanded once per 32-k chunk into LDS, A in registers, 128 x 128",
                ms, prods / ms / 1e9, prods / (ms * 1e-3) / (1024 * 2.4e9));
         CK(hipMemcpy(C.data(), dC, C.size() * 4, hipMemcpyDeviceToHost));
         // check sampled rows against the reference term over hi x hi pairs
