@@ -135,6 +135,9 @@ def build_model(arch, weights, cfg, image_size=224):
             sd = torch.load(weights, map_location="cpu", weights_only=True)
             fp.load_state_dict(sd.get("state_dict", sd))
         return QuantizedMobileNetV2(fp, input_size=(1, 3, image_size, image_size), **rw.approx_qparams(**cfg))
+    if arch == "vit_b16":  # models/vit_quantized_approx.py (the registry's vit_quantized_approx)
+        from .vit_workload import vit_b16_approx
+        return vit_b16_approx(weights=weights, image_size=image_size, **cfg)
     raise ValueError(f"unknown architecture {arch}")
 
 
@@ -142,7 +145,7 @@ def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--images-dir", default=None)
     ap.add_argument("--synthetic", type=int, default=0, help="N random images instead of a dataset")
-    ap.add_argument("--arch", default="resnet18", choices=["resnet18", "resnet50", "mobilenet_v2"])
+    ap.add_argument("--arch", default="resnet18", choices=["resnet18", "resnet50", "mobilenet_v2", "vit_b16"])
     ap.add_argument("--weights", default=None, help="float (torchvision-format) state dict")
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--batch-size", type=int, default=16)

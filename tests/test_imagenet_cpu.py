@@ -65,3 +65,16 @@ def test_synthetic_images_are_deterministic():
     xa, ya = a[2]
     xb, yb = b[2]
     assert torch.equal(xa, xb) and ya == yb
+
+
+def test_build_model_knows_every_bench_architecture():
+    """The validate driver builds the same wrappers as bench.py (ViT-B/16 included)."""
+    from fp8_quantization_amd.approx_calculation import QCustomLinearTorch
+    from fp8_quantization_amd.imagenet import build_model
+    from fp8_quantization_amd.vit_workload import QuantizedVisionTransformerForImageClassification
+    cfg = dict(expo_width=4, mant_width=3, dnsmp_factor=3, withComp=False)
+    m = build_model("vit_b16", None, cfg)
+    assert isinstance(m, QuantizedVisionTransformerForImageClassification)
+    assert sum(isinstance(x, QCustomLinearTorch) for x in m.modules()) == 73
+    with pytest.raises(ValueError):
+        build_model("bert", None, cfg)
