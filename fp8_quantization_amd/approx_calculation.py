@@ -175,9 +175,12 @@ class ApproxLinearMixin(ApproxOpMixin):
         return self._block_ok()
 
     def _block_ok(self):
+        # (with autograd recording a trainable bias, the separate `out += bias` keeps its gradient)
         p = self.custom_approx_params
+        b = getattr(self, "bias", None)
         return (self.fuse_linear_block and self.approx_flag and self.out_features != 1
-                and p.get("approx_version", 9) != 5 and self.get_weights_fp_bias() is not None)
+                and p.get("approx_version", 9) != 5 and self.get_weights_fp_bias() is not None
+                and not (b is not None and b.requires_grad and torch.is_grad_enabled()))
 
     def tail_ok(self):
         """Whether forward(x, post=...) fuses a caller's residual tail: the fixed-range eval
