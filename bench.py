@@ -41,22 +41,28 @@ DEFAULT_BATCH = {"vit_b16": 64, "vit_fc": 256}
 FP32_VALU_PEAK_TFLOPS = 157.3  # MI355X fp32 vector (= fp32 MFMA) peak, MI355X_MICROARCH.md
 
 
-def metric_name(arch, E, M):
+def metric_name(arch, E, M, v5=False):
     """BASELINE.json's metric for the headline (ResNet-18 E4M3); the same wording for the other
     configs.  The top-1 clause is not part of it: top-1 is not measured here (no ImageNet or
     pretrained weights offline) -- see the line's ``top1_delta``."""
     fmt = "" if (E, M) == (4, 3) else f" E{E}M{M}"
-    return f"ImageNet val images/sec, {ARCH_NAMES[arch]} FP8{fmt} approx_v9"
+    return f"ImageNet val images/sec, {ARCH_NAMES[arch]} FP8{fmt} " + ("approx_v5 OFUF" if v5 else "approx_v9")
 
 
-def dominant_kernel(E, M):
+def dominant_kernel(E, M, v5=False):
     """(kernel name, description) of the approx GEMM kernel the bench's format runs on (run_gemm
     in csrc/fp8approx.hip; the bench uses s2n + qbma and the withComp=False tables): the E4M3
-    matrix-core form for E4M3, the tile-table kernel for E3M4 / E2M5 (their tables have no
-    negative entries), the VALU tiled kernel otherwise."""
+    matrix-core form for E4M3, the packed-f16 tile-table kernel for E3M4 (gemm_tt16_kernel on
+    every K >= 256 layer; gemm_tt_kernel<4> on the short-K ones), the f32 tile-table kernel for
+    E2M5, the VALU tiled kernel otherwise (E5M2, the v5 mode)."""
+    if v5:
+        return "gemm_fast_kernel", f"implicit-GEMM approx conv / linear on the VALU, E{E}M{M} v5 integer-adder terms"
     if (E, M) == (4, 3):
         return "gemm_f8mx_kernel", ("implicit-GEMM approx conv / linear, E4M3 terms by the hardware fp8 "
                                     "conversion, codes summed on the matrix core")
+    if (E, M) == (3, 4):
+        return "gemm_tt16_kernel", ("implicit-GEMM approx conv / linear, E3M4 terms in packed f16 from a per-tile "
+                                    "c_b-applied table, summed on the matrix core (gemm_tt_kernel<4> on K < 256)")
     if M in (4, 5):
         return "gemm_tt_kernel", (f"implicit-GEMM approx conv / linear on the VALU, E{E}M{M} terms from a "
                                   "per-tile c_b-applied table, one multiply + magic-constant Q_R + add per product")
@@ -64,7 +70,7 @@ def dominant_kernel(E, M):
                                 "term, arithmetic Q_R")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -83,7 +89,10 @@ def parse():
                          "default (0, 1) statistics)")
     ap.add_argument("--expo-width", type=int, default=4)
     ap.add_argument("--mant-width", type=int, default=3)
-    args = ap.parse_args()
+    ap.add_argument("--v5-ofuf", action="store_true",
+                    help="the opt-in v5 integer-adder mode with sim_hw_add_OFUF, with_OF_opt and with_UF_opt live "
+                         "(BASELINE config 3's switches, which v9 ignores: SURVEY F2)")
+    args = ap.parse_args(argv)
     if args.batch is None:
         args.batch = DEFAULT_BATCH.get(args.arch, 512)
     return args
@@ -143,16 +152,31 @@ def pmc_traffic(kernel, arch, E, M, batch):
     return None
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(shapes, table, cols):
     """Reference-cost CPU throughput on a bounded sample: for every distinct approx layer
     shape of ONE image, time `cols` output columns of the torch port, scale by the layer's
-    column count; images/s = 1 / projected seconds per image."""
+    column count; images/s = 1 / projected seconds per image.  The projection is checked on
+    the cheapest distinct layer, timed end to end (all its columns).  Threads: every core the
+    process may use, capped by OMP_NUM_THREADS when set (the GPU box's CPU share)."""
     from oracle import v9_torch_port as port
-    threads = min(16, os.cpu_count() or 1)
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = max(1, min(avail, omp) if omp > 0 else avail)
     torch.set_num_threads(threads)
     fa, fb = port._fmt(4, 3, 12), port._fmt(4, 3, 19)
     g = torch.Generator().manual_seed(7)
-    per_img, measured, cache = 0.0, 0.0, {}
+    per_img, measured, cache, ops = 0.0, 0.0, {}, {}
     for (_, Mi, K, N, groups) in shapes:
         key = (Mi, K)
         if key not in cache:
@@ -164,48 +188,62 @@ def cpu_baseline(shapes, table, cols):
                 port.column(A, B[:, c:c + 1], 4, 3, 12, 19, 15, table, approx=True, s2n=True, qbma=True)
             dt = (time.perf_counter() - t0) / nc
             cache[key] = dt
+            ops[key] = (A, N * groups)
             measured += dt * nc
         per_img += cache[key] * N * groups
+    # the projection on one whole layer: the cheapest distinct shape, every output column
+    convs = {k: v for k, v in ops.items() if k[0] > 1} or ops  # (a conv layer when there is one)
+    (Mi, K), (A, ncol) = min(convs.items(), key=lambda kv: kv[1][0].numel() * kv[1][1])
+    B = port._q(torch.randn((K, ncol), generator=g) * 0.05, fb, True)
+    t0 = time.perf_counter()
+    for c in range(ncol):
+        port.column(A, B[:, c:c + 1], 4, 3, 12, 19, 15, table, approx=True, s2n=True, qbma=True)
+    full = time.perf_counter() - t0
     return dict(value=1.0 / per_img, unit="images/s", cores=threads, kind="port",
+                cpu_model=cpu_model(), cpu_count=os.cpu_count(),
                 sample=(f"1 image: up to {cols} output columns of each of {len(cache)} distinct approx layer shapes "
                         f"(torch port of the v9 op sequence, {measured:.1f} s measured), scaled by each layer's "
-                        f"output-column count; {per_img:.1f} s/img projected"))
+                        f"output-column count; {per_img:.1f} s/img projected"),
+                full_layer_check=dict(shape=[Mi, K, ncol], measured_s=full, projected_s=cache[(Mi, K)] * ncol,
+                                      ratio=full / (cache[(Mi, K)] * ncol)))
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+def run(args, dev, rank=0, world=1):
+    """The benchmark on an initialised process group (world > 1) or alone; returns rank 0's
+    JSON dict (None on the other ranks).  On a CPU device (the gloo rehearsal in
+    tests/test_distributed_cpu.py, approx ops replaced by stand-ins) the control flow is the same
+    and the HIP-event roofline is omitted."""
+    cuda = dev.type == "cuda"
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
     torch.manual_seed(0)
 
     import fp8_quantization_amd as fa
     from fp8_quantization_amd import approx_ops as am
-    from fp8_quantization_amd.distributed import broadcast_quant_state, gather_logits
+    from fp8_quantization_amd.distributed import calibrate_on_rank0, gather_logits
     from fp8_quantization_amd.error_tables import get_error_table_NN
     from fp8_quantization_amd.resnet_workload import approx_layer_shapes, approx_macs_per_image
 
     fa._lib.load()
+    # formats the reference has no error table for (E5M2, configs 3 / 5) run with the opt-in
+    # all-zero table (approx_qparams: zero_table_ext)
     cfg = dict(expo_width=args.expo_width, mant_width=args.mant_width, dnsmp_factor=3, withComp=args.with_comp,
                with_approx=True, with_s2nn2s_opt=True, quant_btw_mult_accu=True)
+    if args.v5_ofuf:
+        cfg.update(approx_version=5, withComp=True, sim_hw_add_OFUF=True, with_OF_opt=True, with_UF_opt=True)
     model, in_shape, arch_desc = build_workload(args.arch, cfg, args.bn_stats_batches, dev)
     model = model.to(dev).eval()
 
-    # calibration (one batch, identical on every rank), then fixed ranges -- image_net.py:76-91
-    with torch.no_grad():
-        shapes, hooks = approx_layer_shapes(model)
-        model.quantized()
-        model.estimate_ranges()
-        model(synthetic_images(args.cal_batch, 1234, dev, in_shape))
-        model.fix_ranges()
-        for h in hooks:
-            h.remove()
-        broadcast_quant_state(model, src=0)  # identical bA/bB/bR on every rank
-    macs_img = approx_macs_per_image(shapes)
+    # calibration (one batch) on rank 0 alone, then fixed ranges -- image_net.py:76-91; the other
+    # ranks take rank 0's model state and FP8 ranges by broadcast (identical bA/bB/bR everywhere)
+    shapes, hooks = approx_layer_shapes(model)
+    calibrate_on_rank0(model, [synthetic_images(args.cal_batch, 1234, dev, in_shape)] if rank == 0 else [],
+                       quantized=True)
+    for h in hooks:
+        h.remove()
+    macs_img = approx_macs_per_image(shapes)  # (rank 0's calibration pass recorded the shapes)
 
     x = synthetic_images(args.batch, 10 + rank, dev, in_shape)  # this rank's shard of the validation batch
 
@@ -215,18 +253,23 @@ def main():
     with torch.no_grad():
         for _ in range(args.warmup):
             step()
-        torch.cuda.synchronize()
+        sync()
         if world > 1:
             dist.barrier()
-        am._PROFILE = []
+        am._PROFILE = [] if cuda else None
+        if cuda:
+            fa._lib.fallback_stats(reset=True)  # (synchronises: outside the timed region)
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step()
-        torch.cuda.synchronize()
+        sync()
         if world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t0
-        prof, am._PROFILE = am._PROFILE, None
+        prof, am._PROFILE = am._PROFILE or [], None
+    # how many launches / 64x64 output units of the timed steps left the fast path (a regression
+    # there would otherwise be invisible in the line)
+    fallback = fa._lib.fallback_stats() if cuda else None
 
     op_ms = sum(s.elapsed_time(e) for (s, e, _) in prof)
     op_macs = sum(m for (_, _, m) in prof)
@@ -237,12 +280,12 @@ def main():
     images = world * args.batch * args.steps
 
     if rank == 0:
-        kernel, kdesc = dominant_kernel(args.expo_width, args.mant_width)
-        launches = len(prof)
+        kernel, kdesc = dominant_kernel(args.expo_width, args.mant_width, args.v5_ofuf)
+        launches = max(1, len(prof))
         avg_s = op_ms / 1e3 / launches
-        achieved = 2.0 * (op_macs / launches) / avg_s / 1e12
+        achieved = 2.0 * (op_macs / launches) / avg_s / 1e12 if avg_s > 0 else None
         res = {
-            "metric": metric_name(args.arch, args.expo_width, args.mant_width),
+            "metric": metric_name(args.arch, args.expo_width, args.mant_width, args.v5_ofuf),
             "value": images / elapsed,
             "unit": "images/s",
             "n_gpus": world,
@@ -258,9 +301,13 @@ def main():
             "dtype": "fp32",
             "data": "synthetic",
             "config": {
-                "workload": f"{arch_desc} E{args.expo_width}M{args.mant_width} approx_v9 forward (dnsmp_factor=3, "
-                            f"withComp={args.with_comp}, with_s2nn2s_opt, quant_btw_mult_accu, res_quantizer, fixed "
-                            "ranges), ImageNet-shaped synthetic batch, random-init weights"
+                "workload": f"{arch_desc} E{args.expo_width}M{args.mant_width} "
+                            + ("approx_v5 integer-adder forward (withComp, sim_hw_add_OFUF, with_OF_opt, with_UF_opt, "
+                               if args.v5_ofuf else f"approx_v9 forward (dnsmp_factor=3, withComp={args.with_comp}, "
+                               "with_s2nn2s_opt, quant_btw_mult_accu, ")
+                            + ("zero error table (opt-in extension: the reference has none for this format), "
+                               if (args.expo_width, args.mant_width) not in ((4, 3), (3, 4), (2, 5)) else "")
+                            + "res_quantizer, fixed ranges), ImageNet-shaped synthetic batch, random-init weights"
                             + (f" with BN statistics estimated on {args.bn_stats_batches} synthetic batches"
                                if args.bn_stats_batches and not args.arch.startswith("vit") else ""),
                 "global_batch": world * args.batch,
@@ -276,17 +323,39 @@ def main():
                 "achieved": achieved,
                 "peak": FP32_VALU_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
-                "frac": achieved / FP32_VALU_PEAK_TFLOPS,
+                "frac": achieved / FP32_VALU_PEAK_TFLOPS if achieved else None,
                 "traffic": pmc_traffic(kernel, args.arch, args.expo_width, args.mant_width, args.batch),
                 "algorithmic": f"2 FLOP per approx-MAC; {op_macs / launches:.4g} approx-MAC per launch avg over "
                                f"{launches} launches, {avg_s * 1e3:.3f} ms avg launch (HIP events)",
-                "approx_macs_per_s": op_macs / (op_ms / 1e3),
+                "approx_macs_per_s": op_macs / (op_ms / 1e3) if op_ms > 0 else None,
                 "gemm_share_of_step": op_ms / 1e3 / elapsed,
             },
         }
+        if fallback is not None:
+            res["fallback"] = dict(fallback, approx_launches=len(prof),
+                                   note="timed steps only: exact_launches = launches whose gated exact kernel "
+                                        "recomputed exact_units 64x64 output units; f32_reruns = E3M4 launches "
+                                        "rerun in the f32 tile-table form; tb_launches = depthwise launches "
+                                        "recomputed by the literal restatement")
         if world == 1 and not args.no_cpu_baseline and (args.expo_width, args.mant_width) == (4, 3):
             res["cpu_baseline"] = cpu_baseline(shapes, get_error_table_NN(4, 3, args.with_comp, 3), args.cpu_columns)
             res["speedup_vs_cpu_baseline"] = res["value"] / res["cpu_baseline"]["value"]
+        if not cuda:
+            res.pop("roofline")
+        return res
+    return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    res = run(args, torch.device("cuda", local), rank, world)
+    if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

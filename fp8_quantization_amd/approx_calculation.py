@@ -15,6 +15,8 @@ QuantizationHijacker / BNFusedHijacker (see ``bind_operator_classes`` and INTEGR
 """
 import os
 
+import weakref
+
 import torch
 import torch.nn.functional as F
 from torch import nn
@@ -40,13 +42,16 @@ class ApproxOpMixin:
             # opt-in extension: the v5 integer-adder model with live sim_hw_add_OFUF /
             # with_OF_opt / with_UF_opt (approx_v5.py); without withComp, the zero table the v5
             # harness passes for "no compensation"
-            table = get_comp_table_NN_v5(E, M, True, p["dnsmp_factor"]) if p["withComp"] else \
+            table = get_comp_table_NN_v5(E, M, True, p["dnsmp_factor"], p.get("zero_table_ext", False)) \
+                if p["withComp"] else \
                 torch.zeros((2 ** M, 2 ** M), dtype=torch.int32)
             return E, M, table, make_flags_v5(p.get("sim_hw_add_OFUF", False), p.get("with_OF_opt", False),
                                               p.get("with_UF_opt", False))
         # get_error_table_NN runs first, as in the reference: unsupported formats raise
         # ValueError even when approx_flag is off (approx_calculation.py:772)
-        table = get_error_table_NN(E, M, withComp=p["withComp"], dnsmp_factor=p["dnsmp_factor"])
+        # (zero_table_ext: the opt-in all-zero table for formats the reference has none for, E5M2)
+        table = get_error_table_NN(E, M, withComp=p["withComp"], dnsmp_factor=p["dnsmp_factor"],
+                                   zero_table_ext=p.get("zero_table_ext", False))
         flags = make_flags(p["with_approx"], p["with_s2nn2s_opt"], p["quant_btw_mult_accu"], p["golden_clip_OF"])
         return E, M, table, flags
 
@@ -193,12 +198,14 @@ class ApproxLinearMixin(ApproxOpMixin):
         """{1, bias} store epilogue, rebuilt only when the bias tensor changes."""
         if bias is None:
             return None
+        # keyed on the tensor object as well: a replaced bias (new Parameter, load_state_dict with
+        # assign=True) may reuse the old storage address with a matching version counter
         key = (bias._version, bias.data_ptr(), device)
         cached = getattr(self, "_bias_epi_cache", None)
-        if cached is None or cached[0] != key:
-            cached = (key, bias_epilogue(bias, device))
+        if cached is None or cached[0] != key or cached[1]() is not bias:
+            cached = (key, weakref.ref(bias), bias_epilogue(bias, device))
             self._bias_epi_cache = cached
-        return cached[1]
+        return cached[2]
 
     def run_forward(self, x, weight, bias, offsets=None, qin=None, post=None):
         x = x.contiguous()

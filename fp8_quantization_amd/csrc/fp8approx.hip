@@ -135,7 +135,13 @@ struct GemmArgs {
     // output mapping: rowmajor C[m*ldc + n], or NCHW C[(m/hw)*ctot*hw + (coff+n)*hw + m%hw]
     int nchw;
     int64_t hw, ctot, coff;
-    uint32_t *flag;  // device word: set by the fast kernel when the exact kernel must run
+    uint32_t *flag;  // device word: set by the fast kernel when the exact kernel must run (FB_* bits)
+    // per-unit fallback marks (64 x 64 output units): urow[row unit] / ucol[column unit] for an
+    // operand outside the fast path's window, utile[row unit * nuc + column unit] for a tile whose
+    // terms left it; the gated exact kernel recomputes only the marked units.  nullptr (a
+    // workspace without room for them): any fallback recomputes the whole launch.
+    uint8_t *urow, *ucol, *utile;
+    int64_t nur, nuc;
     // split-K: block b works on tile b % tiles over k in [s*kchunk, (s+1)*kchunk), s = b / tiles;
     // with splits > 1 it writes its partial tile to part + s*M*N (the output layout with
     // ctot = N, coff = 0, ldc = N) and splitk_reduce_kernel sums the splits in order
@@ -181,6 +187,39 @@ struct GemmArgs {
     FqIn post_fq;
     TablePack tab;
 };
+
+// Fallback flag word bits: FB_ANY = some output unit needs the exact kernel, FB_ALL = every
+// unit does (a bias outside the exactness window, or no unit marks in the workspace).  (Bits
+// 1-4 belong to gemm_tt16_kernel's f16 window, gemm_tt16.h.)
+constexpr uint32_t FB_ANY = 1u, FB_ALL = 32u;
+
+// Fallback flag value of a block that found a bad operand: FB_ANY once the unit marks are
+// written, FB_ALL too without them (or when `all`).
+__device__ __forceinline__ uint32_t fb_bits(const GemmArgs &p, bool all = false) {
+    return (all || p.urow == nullptr) ? (FB_ANY | FB_ALL) : FB_ANY;
+}
+
+// Fallback statistics since load (or the last reset): [0] launches whose gated exact kernel
+// ran, [1] 64 x 64 output units it recomputed, [2] launches rerun in gemm_tt_kernel's f32 form
+// (gemm_tt16_kernel's f16 window left), [3] tensor-bias launches recomputed by
+// conv_tb_direct_kernel.  Read with fp8a_fallback_stats (include/fp8approx.h).
+__device__ unsigned long long g_fallback[4];
+
+// Mark the row units of output rows [m_lo, m_hi) / the column unit of column n / the units of
+// the output tile (m0 .. m0 + rows - 1, n0 .. n0 + 63) for the exact kernel (plain byte stores:
+// every writer stores 1).  The caller raises the flag word (fb_bits).
+__device__ __forceinline__ void fb_rows(const GemmArgs &p, int64_t m_lo, int64_t m_hi) {
+    if (p.urow == nullptr || m_hi <= m_lo) return;
+    for (int64_t u = m_lo >> 6; u <= (m_hi - 1) >> 6; ++u) p.urow[u] = 1;
+}
+__device__ __forceinline__ void fb_col(const GemmArgs &p, int64_t n) {
+    if (p.ucol != nullptr) p.ucol[n >> 6] = 1;
+}
+__device__ __forceinline__ void fb_tile(const GemmArgs &p, int64_t m0, int64_t rows, int64_t n0) {
+    if (p.utile == nullptr) return;
+    const int64_t hi = min(m0 + rows, p.M);
+    for (int64_t u = m0 >> 6; u <= (hi - 1) >> 6; ++u) p.utile[u * p.nuc + (n0 >> 6)] = 1;
+}
 
 // The block-output epilogue on one value / four values of the output at index o; pb = the post
 // quantizer's bias (post_bias()).
@@ -554,7 +593,10 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
         // Off-grid operands / biases outside the exact window: flag the launch; the gated
         // exact kernel that follows on the stream then recomputes the whole product.
         const int anybad = __syncthreads_or(bad ? 1 : 0);
-        if (anybad && tid == 0) atomicOr(p.flag, 1u);
+        if (anybad && tid == 0) {
+            fb_tile(p, m0, BM, n0);  // (every column tile staging the bad rows marks itself)
+            atomicOr(p.flag, fb_bits(p));
+        }
         if (k0 + BK < kend) load_tile(k0 + BK);  // next tile's loads fly during this tile's math
 
         // fp32 accumulation in k order: measured max |error| ~3e-7 x sum|terms| at K = 4608 on
@@ -686,7 +728,10 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j) nan |= __builtin_isnan(acc[i][j]);
-        if (__syncthreads_or(nan ? 1 : 0) && tid == 0) atomicOr(p.flag, 1u);
+        if (__syncthreads_or(nan ? 1 : 0) && tid == 0) {
+            fb_tile(p, m0, BM, n0);
+            atomicOr(p.flag, fb_bits(p));
+        }
     }
     // ---- epilogue
     store_tile(p, split, m0, n0, ty, tx, acc);
@@ -777,26 +822,68 @@ __device__ __forceinline__ float load_A(const GemmArgs &p, int64_t m, int64_t k)
 }
 
 __global__ __launch_bounds__(256) void gemm_exact_kernel(const GemmArgs p) {
-    // Gate: after a fast launch, run only if it flagged off-grid operands (uniform per grid;
-    // the grid is capped, so the no-op case costs one small launch).
-    if (p.flag != nullptr && (__hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1u) == 0u) return;
     const bool tb = p.flags & F_TB;
     const DFmt fA = dfmt(p.E, p.Mw, *p.bA, tb), fR = dfmt(p.E, p.Mw, *p.bR, tb);
-    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < p.M * p.N;
-         idx += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t m = idx % p.M, n = idx / p.M;
-        const DFmt fB = dfmt(p.E, p.Mw, p.bB[n * p.bBs], tb);
-        float s = 0.0f, part = 0.0f;
+    if (p.flag == nullptr) {  // the tensor-bias path: the exact kernel is the product itself
+        for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < p.M * p.N;
+             idx += (int64_t)gridDim.x * blockDim.x) {
+            const int64_t m = idx % p.M, n = idx / p.M;
+            const DFmt fB = dfmt(p.E, p.Mw, p.bB[n * p.bBs], tb);
+            float s = 0.0f, part = 0.0f;
+            for (int64_t k = 0; k < p.K; ++k) {
+                part += exact_term(load_A(p, m, k), p.B[k * p.sbk + n * p.sbn], fA, fB, fR, p.tab.raw, p.flags);
+                if ((k & 15) == 15) {
+                    s += part;
+                    part = 0.0f;
+                }
+            }
+            s += part;
+            const int64_t o = out_index(p, m, n);
+            p.C[o] = post1(p, o, epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, p.coff + n, s), post_bias(p));
+        }
+        return;
+    }
+    // Gated after a fast launch: nothing to do unless it flagged (uniform per grid; the grid is
+    // capped, so the no-op case costs one small launch); then only the marked 64 x 64 units
+    // (every unit with FB_ALL), one unit per block step: thread = (row, 16 columns).
+    const uint32_t f = __hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((f & FB_ANY) == 0u) return;
+    const bool all = (f & FB_ALL) != 0u || p.urow == nullptr;
+    const int64_t nur = (p.M + 63) >> 6, nuc = (p.N + 63) >> 6;
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_fallback[0], 1ull);
+    const float pb = post_bias(p);
+    for (int64_t u = blockIdx.x; u < nur * nuc; u += gridDim.x) {
+        const int64_t ur = u / nuc, uc = u - ur * nuc;
+        if (!all && !p.urow[ur] && !p.ucol[uc] && !p.utile[u]) continue;  // (block-uniform)
+        if (threadIdx.x == 0) atomicAdd(&g_fallback[1], 1ull);
+        const int64_t m = 64 * ur + (threadIdx.x & 63), nb = 64 * uc + 16 * (threadIdx.x >> 6);
+        if (m >= p.M) continue;
+        float s[16], part[16];
+        DFmt fB[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            s[j] = part[j] = 0.0f;
+            fB[j] = dfmt(p.E, p.Mw, p.bB[min(nb + j, p.N - 1) * p.bBs], tb);
+        }
         for (int64_t k = 0; k < p.K; ++k) {
-            part += exact_term(load_A(p, m, k), p.B[k * p.sbk + n * p.sbn], fA, fB, fR, p.tab.raw, p.flags);
-            if ((k & 15) == 15) {
-                s += part;
-                part = 0.0f;
+            const float a = load_A(p, m, k);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int64_t n = min(nb + j, p.N - 1);
+                part[j] += exact_term(a, p.B[k * p.sbk + n * p.sbn], fA, fB[j], fR, p.tab.raw, p.flags);
+                if ((k & 15) == 15) {
+                    s[j] += part[j];
+                    part[j] = 0.0f;
+                }
             }
         }
-        s += part;
-        const int64_t o = out_index(p, m, n);
-        p.C[o] = post1(p, o, epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, p.coff + n, s), post_bias(p));
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int64_t n = nb + j;
+            if (n >= p.N) break;
+            const int64_t o = out_index(p, m, n);
+            p.C[o] = post1(p, o, epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, p.coff + n, s[j] + part[j]), pb);
+        }
     }
 }
 
@@ -860,6 +947,7 @@ __global__ __launch_bounds__(256) void conv_tb_direct_kernel(const float *x, con
                                                              float ep_lo, float ep_hi, FqIn fq) {
     // after conv_tb_fast_kernel: run only if it flagged inputs outside its exactness window
     if (gate != nullptr && __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
+    if (gate != nullptr && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_fallback[3], 1ull);
     const int64_t total = Bn * Cout * Ho * Wo;
     const int64_t cpg = Cin / groups;   // input channels per group
     const DFmt fA = dfmt(E, Mw, *bA, true), fR = dfmt(E, Mw, *bR, true);
@@ -1207,6 +1295,13 @@ static size_t xm_operand_bytes(int64_t N, int64_t K, int64_t a_words) {
     return align256((size_t)a_words * 4) + align256((size_t)(kpad * npad / 2) * 8) + 16384;  // + table image
 }
 
+// The per-unit fallback marks after the flag word: urow [nur], ucol [nuc], utile [nur * nuc] bytes.
+static size_t unit_bytes(int64_t M, int64_t N) {
+    const int64_t nur = (M + 63) / 64, nuc = (N + 63) / 64;
+    return align256((size_t)(nur + nuc + nur * nuc));
+}
+static size_t head_bytes(int64_t M, int64_t N) { return FLAG_BYTES + unit_bytes(M, N); }
+
 static size_t splitk_bytes(int64_t M, int64_t N, int64_t K) {
     const int S = choose_splits(M, N, K);
     return S > 1 ? align256((size_t)S * (size_t)M * (size_t)N * sizeof(float)) : 0;
@@ -1215,7 +1310,7 @@ static size_t splitk_bytes(int64_t M, int64_t N, int64_t K) {
 // flag word + split-K partials + the pre-decoded operands (a_words: the A operand's element
 // count as the matrix-core E4M3 path stores it; 0 = no room for that path)
 static size_t gemm_workspace_bytes(int64_t M, int64_t N, int64_t K, int64_t a_words) {
-    return FLAG_BYTES + splitk_bytes(M, N, K) + (a_words > 0 ? xm_operand_bytes(N, K, a_words) : 0);
+    return head_bytes(M, N) + splitk_bytes(M, N, K) + (a_words > 0 ? xm_operand_bytes(N, K, a_words) : 0);
 }
 
 // The E4M3 table + hardware-fp8 form applies (TM_F8; run_gemm then takes the matrix-core kernel
@@ -1321,20 +1416,31 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     }
     if (ws == nullptr || ws_bytes < FLAG_BYTES) return fail(FP8A_EINVAL, "matmul workspace too small");
     a.flag = (uint32_t *)ws;
+    // the per-unit fallback marks when the workspace holds them (else a fallback reruns the launch)
+    const bool units = ws_bytes >= head_bytes(a.M, a.N);
+    const size_t head = units ? head_bytes(a.M, a.N) : FLAG_BYTES;
+    a.nur = (a.M + 63) / 64;
+    a.nuc = (a.N + 63) / 64;
+    a.urow = units ? (uint8_t *)ws + FLAG_BYTES : nullptr;
+    a.ucol = units ? a.urow + a.nur : nullptr;
+    a.utile = units ? a.ucol + a.nuc : nullptr;
     // split-K when the caller's workspace holds the partials (else one split)
     a.splits = choose_splits(a.M, a.N, a.K);
-    if (a.splits > 1 && ws_bytes < FLAG_BYTES + splitk_bytes(a.M, a.N, a.K)) a.splits = 1;
+    if (a.splits > 1 && ws_bytes < head + splitk_bytes(a.M, a.N, a.K)) a.splits = 1;
     const int64_t kt = (a.K + BK - 1) / BK;
     a.kchunk = ((kt + a.splits - 1) / a.splits) * BK;
-    a.part = a.splits > 1 ? (float *)((char *)ws + FLAG_BYTES) : nullptr;
-    if (hipMemsetAsync(ws, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a flag reset");
+    a.part = a.splits > 1 ? (float *)((char *)ws + head) : nullptr;
+    // flag word + unit marks zeroed by one fill
+    if (hipMemsetAsync(ws, 0, units ? FLAG_BYTES + (size_t)(a.nur + a.nuc + a.nur * a.nuc) : sizeof(uint32_t), s) !=
+        hipSuccess)
+        return hip_check("fp8a flag reset");
     // the matrix-core E4M3 kernel and the tile-table kernel (E3M4 / E2M5) need their pre-decoded
     // operands in the workspace (else gemm_fast_kernel runs); FP8A_NO_MX=1 forces the latter
     a.aw = nullptr;
     const bool tt = mode != TM_F8 && tt_form(a.Mw, a.flags, a.tab);
     if ((mode == TM_F8 || tt) && !no_mx()) {
         const int64_t kpad = kt * BK, npad = (a.N + BN - 1) / BN * BN;
-        const size_t off = FLAG_BYTES + (a.splits > 1 ? splitk_bytes(a.M, a.N, a.K) : 0);
+        const size_t off = head + (a.splits > 1 ? splitk_bytes(a.M, a.N, a.K) : 0);
         // gemm_f8mx_kernel reads its operands with 32-bit byte offsets
         const int64_t a_words = xm_a_words(a);
         const WordImage wi = word_image(a.H, a.W, a.ph, a.pw);
@@ -1376,7 +1482,8 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
         rc = hip_check("fp8a split-K reduce launch");
         if (rc) return rc;
     }
-    gemm_exact_kernel<<<eblocks, 256, 0, s>>>(a);
+    const unsigned ublocks = (unsigned)std::min<int64_t>(a.nur * a.nuc, 4096);
+    gemm_exact_kernel<<<ublocks, 256, 0, s>>>(a);
     rc = hip_check("fp8a gated exact gemm launch");
     static const bool dbg = getenv("FP8A_DEBUG_FLAGS") != nullptr;  // diagnostics: the flag word per launch
     if (!rc && dbg) {
@@ -1415,6 +1522,19 @@ extern "C" {
 const char *fp8a_version(void) { return "fp8approx gfx950 r1"; }
 
 const char *fp8a_last_error(void) { return g_err.c_str(); }
+
+int fp8a_fallback_stats(uint64_t *out, int reset) {
+    if (out == nullptr) return fail(FP8A_EINVAL, "null pointer");
+    unsigned long long v[4] = {0, 0, 0, 0};
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(v, HIP_SYMBOL(g_fallback), sizeof(v)) != hipSuccess)
+        return hip_check("fp8a_fallback_stats");
+    for (int i = 0; i < 4; ++i) out[i] = v[i];
+    if (reset) {
+        const unsigned long long z[4] = {0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_fallback), z, sizeof(z)) != hipSuccess) return hip_check("fp8a_fallback_stats");
+    }
+    return FP8A_OK;
+}
 
 int fp8a_decompose(const float *x, int64_t rows, int64_t cols, int64_t ld, int E, int M, const int32_t *bias,
                    int64_t bias_stride, uint32_t flags, int32_t *expo, int32_t *mant, fp8a_stream_t stream) {

@@ -178,7 +178,10 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
         *p.fq_ibias = bA;
     }
     const uint32_t emnA = (uint32_t)(128 - bA) << 23;
-    bool bad = !(xm_bias_ok(bA) && xm_bias_ok(bR)), win = true;
+    const bool biasbad = !(xm_bias_ok(bA) && xm_bias_ok(bR));  // every output unit falls back
+    bool bad = biasbad, win = true;
+    // conv: a bad input element marks its image's output rows; matrix: its row
+    const int64_t orows = p.conv ? p.Ho * p.Wo : 1;
     uint32_t *const out = const_cast<uint32_t *>(p.aw);
     const int64_t hw = p.H * p.W;
     const int64_t rows = p.conv ? p.M / (p.Ho * p.Wo) : p.M, cols = p.conv ? p.aw_c * p.awH * p.awW : p.awld;
@@ -202,6 +205,7 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
         for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) {
             const float *in = p.X + (r * p.Cin + p.cbase) * hw;
             uint32_t *o = out + r * cols;
+            bool badr = false;
             for (uint32_t e = per * t0; e < nin; e += per * tstride) {
                 const uint32_t c = e / hwin, t = e - c * hwin, hy = t / uW, wx = t - hy * uW;
                 uint32_t *d = o + (c * Hp + hy + ph) * Wp + pw + wx;
@@ -209,13 +213,15 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
                     const float4 v = *reinterpret_cast<const float4 *>(in + e);
                     bool ok0 = true, ok1 = true, ok2 = true, ok3 = true;
                     *reinterpret_cast<uint4 *>(d) = make_uint4(word(v.x, ok0), word(v.y, ok1), word(v.z, ok2), word(v.w, ok3));
-                    bad |= !(ok0 && ok1 && ok2 && ok3);
+                    badr |= !(ok0 && ok1 && ok2 && ok3);
                 } else {
                     bool ok = true;
                     d[0] = word(in[e], ok);
-                    bad |= !ok;
+                    badr |= !ok;
                 }
             }
+            if (badr) fb_rows(p, r * orows, (r + 1) * orows);
+            bad |= badr;
             for (uint32_t j = t0; j < (uint32_t)p.aw_c * nb; j += tstride) {
                 const uint32_t c = j / nb, t = j - c * nb;
                 uint32_t row, col;
@@ -231,7 +237,7 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
                 o[(c * Hp + row) * Wp + col] = zw;
             }
         }
-        if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, 1u);
+        if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, fb_bits(p, biasbad));
         if (__syncthreads_or(win ? 0 : 1) && threadIdx.x == 0) atomicOr(p.flag, 4u);  // gemm_tt16_kernel's window (A)
         return;
     }
@@ -245,6 +251,7 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
         const float *in = p.conv ? p.X + (r * p.Cin + p.cbase) * hw : p.A + r * p.lda;
         const int64_t lim = p.conv ? cols : p.K;
         uint32_t *o = out + r * cols;
+        bool badr = false;
         if (vec) {
             for (int64_t i = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x); i < cols;
                  i += 4 * (int64_t)gridDim.x * blockDim.x) {
@@ -253,19 +260,22 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
                     const float4 v = *reinterpret_cast<const float4 *>(in + i);
                     bool ok0 = true, ok1 = true, ok2 = true, ok3 = true;
                     w = make_uint4(word(v.x, ok0), word(v.y, ok1), word(v.z, ok2), word(v.w, ok3));
-                    bad |= !(ok0 && ok1 && ok2 && ok3);
+                    badr |= !(ok0 && ok1 && ok2 && ok3);
                 }
                 *reinterpret_cast<uint4 *>(o + i) = w;
             }
-            continue;
+        } else {
+            for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cols;
+                 i += (int64_t)gridDim.x * blockDim.x) {
+                bool ok = true;
+                o[i] = (i < lim) ? word(in[i], ok) : zw;
+                badr |= !ok;
+            }
         }
-        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cols; i += (int64_t)gridDim.x * blockDim.x) {
-            bool ok = true;
-            o[i] = (i < lim) ? word(in[i], ok) : zw;
-            bad |= !ok;
-        }
+        if (badr) fb_rows(p, r * orows, (r + 1) * orows);
+        bad |= badr;
     }
-    if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, 1u);
+    if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, fb_bits(p, biasbad));
     if (__syncthreads_or(win ? 0 : 1) && threadIdx.x == 0) atomicOr(p.flag, 4u);  // gemm_tt16_kernel's window (A)
 }
 
@@ -274,7 +284,8 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
 // static table ((code0 + 9 code1) * 32); out-of-range elements are zeros.
 __global__ __launch_bounds__(256) void xm_decode_b(const GemmArgs p, int64_t kpad) {
     const int bA = *p.bA, bR = *p.bR;
-    bool bad = !(xm_bias_ok(bA) && xm_bias_ok(bR));
+    const bool biasbad = !(xm_bias_ok(bA) && xm_bias_ok(bR));
+    bool bad = biasbad;
     const int64_t hq = p.npad / 2, n = kpad * hq;
     uint2 *const bq = const_cast<uint2 *>(p.bqw);
     if (blockIdx.x == 0)  // the table image every GEMM workgroup copies into LDS
@@ -292,8 +303,9 @@ __global__ __launch_bounds__(256) void xm_decode_b(const GemmArgs p, int64_t kpa
             if (k < p.K && col < p.N) {
                 const int bb = p.bB[col * p.bBs];
                 const bool ok = stage_decode(p.B[k * p.sbk + col * p.sbn], 3, (uint32_t)(128 - bb) << 23, true,
-                                             c[h], mc[h]);
-                bad |= !ok || !xm_bias_ok(bb);
+                                             c[h], mc[h]) && xm_bias_ok(bb);
+                if (!ok) fb_col(p, col);
+                bad |= !ok;
             }
         }
         uint32_t add = 0, code[2];
@@ -310,7 +322,7 @@ __global__ __launch_bounds__(256) void xm_decode_b(const GemmArgs p, int64_t kpa
         }
         bq[i] = make_uint2(add, (code[0] + 9u * code[1]) * 32u);
     }
-    if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, 1u);
+    if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, fb_bits(p, biasbad));
 }
 
 #ifndef XM_WAVES
@@ -388,7 +400,9 @@ __global__ __launch_bounds__(XM_NT, XM_WAVES) void gemm_f8mx_kernel(const GemmAr
         for (int r = 0; r < 2; ++r) {
             uint32_t ko;
             if (p.conv) {
-                const int k = k0 + 2 * akp + r;  // wave-uniform
+                // wave-uniform; past the group's last channel the address stays on channel K - 1 (the
+                // word image ends there: the zero word below replaces the value)
+                const int k = min(k0 + 2 * akp + r, K32 - 1);
                 const uint32_t c = fastdiv((uint32_t)k, p.kk_mul, p.kk_shift);
                 const uint32_t t = (uint32_t)k - c * (uint32_t)khw;
                 const uint32_t ky = fastdiv(t, p.kw_mul, p.kw_shift);
@@ -502,7 +516,10 @@ __global__ __launch_bounds__(XM_NT, XM_WAVES) void gemm_f8mx_kernel(const GemmAr
     for (int b = 0; b < XM_RB; ++b)
 #pragma unroll
         for (int i = 0; i < 4; ++i) nan |= __builtin_isnan(dq[b][i]);
-    if (__syncthreads_or(nan ? 1 : 0) && tid == 0) atomicOr(p.flag, 1u);
+    if (__syncthreads_or(nan ? 1 : 0) && tid == 0) {
+        fb_tile(p, m0, XM_BM, n0);
+        atomicOr(p.flag, fb_bits(p));
+    }
 
     // D (units of 2^(7-bR)) of row block b: lane l holds rows 4 (l >> 4) .. + 3, column l & 15
     // -> tile row 16 (XM_RB wr + b) + 4 (l >> 4) + i, column 16 wc + (l & 15) -> a [64][BN] slice in

@@ -36,7 +36,8 @@ template <int MW, bool F7> struct TtCfg {
 // and (block 0) the static image V / sig_a sig_b.
 __global__ __launch_bounds__(256) void tt_decode_b(const GemmArgs p, int64_t kpad) {
     const int bA = *p.bA, bR = *p.bR, M = p.Mw, nm = 1 << M;
-    bool bad = !(xm_bias_ok(bA) && xm_bias_ok(bR)), win = true;  // win: gemm_tt16_kernel's f16 window
+    const bool biasbad = !(xm_bias_ok(bA) && xm_bias_ok(bR));  // every output unit falls back
+    bool bad = biasbad, win = true;  // win: gemm_tt16_kernel's f16 window
     if (blockIdx.x == 0) {
         float *img = const_cast<float *>(reinterpret_cast<const float *>(p.lutw));
         const float ulp = p2(-M), kb = 2.0f - p2(-M) - p2(-22);
@@ -66,15 +67,17 @@ __global__ __launch_bounds__(256) void tt_decode_b(const GemmArgs p, int64_t kpa
             const int bb = p.bB[col * p.bBs];
             float c;
             uint32_t mc;
-            const bool ok = stage_decode(p.B[k * p.sbk + col * p.sbn], M, (uint32_t)(128 - bb) << 23, true, c, mc);
-            bad |= !ok || !xm_bias_ok(bb);
+            const bool ok = stage_decode(p.B[k * p.sbk + col * p.sbn], M, (uint32_t)(128 - bb) << 23, true, c, mc) &&
+                            xm_bias_ok(bb);
+            if (!ok) fb_col(p, col);
+            bad |= !ok;
             const uint32_t cb = __float_as_uint(c);
             win = win && ((cb >> 23) & 0xFFu) <= (uint32_t)(127 + 8 - bb);  // c_b at most one binade above the format's top
             if ((cb & 0x7FFFFFFFu) != 0u) w = (cb & TT_EXP) | mc;
         }
         bw[i] = w;
     }
-    if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, 1u);
+    if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, fb_bits(p, biasbad));
     if (p.wfmt == 2 && __syncthreads_or(win ? 0 : 1) && threadIdx.x == 0) atomicOr(p.flag, 8u);  // (B, image)
 }
 
@@ -101,7 +104,10 @@ template <int MW, bool F7, bool A16>
 __global__ __launch_bounds__(NT * tt_rh<MW>()) void gemm_tt_kernel(const GemmArgs p) {
     constexpr int TT_RH = tt_rh<MW>();
     using C = TtCfg<MW, F7>;
-    if (A16 && (__hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 30u) == 0u) return;
+    if (A16) {
+        if ((__hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 30u) == 0u) return;
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_fallback[2], 1ull);
+    }
     constexpr int NM = C::NM, XK = C::XK;
     static_assert(C::UNITS <= NT && XK >= 1 && XK <= 4, "tile-table configuration");
     __shared__ __attribute__((aligned(16))) TtSmem<MW, F7> sm;
@@ -161,7 +167,7 @@ __global__ __launch_bounds__(NT * tt_rh<MW>()) void gemm_tt_kernel(const GemmArg
         if (astage) {
             uint32_t ko;
             if (p.conv) {
-                const int k = k0 + akk;  // wave-uniform
+                const int k = min(k0 + akk, K32 - 1);  // wave-uniform; clamped: the word image ends at channel K - 1
                 const uint32_t c = fastdiv((uint32_t)k, p.kk_mul, p.kk_shift);
                 const uint32_t t = (uint32_t)k - c * (uint32_t)khw;
                 const uint32_t ky = fastdiv(t, p.kw_mul, p.kw_shift);

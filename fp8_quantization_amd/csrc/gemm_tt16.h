@@ -120,7 +120,7 @@ __global__ __launch_bounds__(NT, 6) void gemm_tt16_kernel(const GemmArgs p) {
     auto load_tile = [&](int k0) {
         uint32_t ko;
         if (p.conv) {
-            const int k = k0 + akk;  // wave-uniform
+            const int k = min(k0 + akk, K32 - 1);  // wave-uniform; clamped: the word image ends at channel K - 1
             const uint32_t c = fastdiv((uint32_t)k, p.kk_mul, p.kk_shift);
             const uint32_t t = (uint32_t)k - c * (uint32_t)khw;
             const uint32_t ky = fastdiv(t, p.kw_mul, p.kw_shift);

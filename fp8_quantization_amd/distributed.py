@@ -1,14 +1,19 @@
 """Multi-GPU plumbing of the approx validation path.
 
 Inference images are independent, so the validation set is sharded contiguously over ranks
-(one process per GPU) with no collective in the data path.  Exactly two collectives exist:
-  * broadcast_quant_state: rank 0's calibrated FP8 ranges (every FPQuantizer.maxval, a few KB)
-    go to every rank once, so all ranks use identical bA / bB / bR;
-  * gather_logits: one all-gather of the [B, classes] logits per validation batch (RCCL over
-    xGMI on MI355X; gloo on CPU), from which rank 0 scores top-1 / top-5.
+(one process per GPU) with no collective in the data path.  The collectives:
+  * once, before the data path: rank 0's float model state (parameters and buffers: the BN
+    statistics of a synthetic-weights model are estimated per process) and, after rank 0 alone
+    has calibrated, its FP8 ranges (every FPQuantizer.maxval / sign_bits, a few KB) are
+    broadcast, so all ranks use identical weights and bA / bB / bR (calibrate_on_rank0);
+  * per validation batch: ONE all-gather (RCCL over xGMI on MI355X; gloo on CPU) of a packed
+    [B, classes + 2] float tensor -- the logits, the label and a valid-row flag per row
+    (gather_scored) -- from which rank 0 scores top-1 / top-5 / loss.  The benchmark step
+    gathers the logits alone (gather_logits).
 """
 import torch
 import torch.distributed as dist
+import torch.nn.functional as F
 
 
 def world():
@@ -27,20 +32,61 @@ def quantizers(model):
     return [m for m in model.modules() if isinstance(m, FPQuantizer)]
 
 
+def broadcast_model_state(model, src=0):
+    """Every parameter and buffer of `model` from rank `src` (identical architecture on every
+    rank, so shapes agree): one broadcast per tensor, in module order."""
+    ws, _ = world()
+    if ws == 1:
+        return
+    with torch.no_grad():
+        for t in list(model.parameters()) + list(model.buffers()):
+            buf = t.detach().contiguous()
+            dist.broadcast(buf, src)
+            if buf.data_ptr() != t.data_ptr():
+                t.copy_(buf)
+
+
 def broadcast_quant_state(model, src=0):
-    """Make every rank's FP8 ranges identical to rank `src`'s (one broadcast per quantizer)."""
+    """Make every rank's FP8 ranges identical to rank `src`'s: per quantizer one broadcast of
+    (maxval element count, sign_bits) and one of maxval.  Ranks that never calibrated receive
+    the calibrated (e.g. per-channel) shapes."""
     ws, _ = world()
     if ws == 1:
         return
     for q in quantizers(model):
         mx = q.maxval.detach().clone().contiguous()
-        n = torch.tensor([mx.numel()], dtype=torch.int64, device=mx.device)
-        dist.broadcast(n, src)
-        if mx.numel() != int(n.item()):
-            mx = torch.empty(int(n.item()), dtype=mx.dtype, device=mx.device)
+        hdr = torch.tensor([mx.numel(), int(q.sign_bits)], dtype=torch.int64, device=mx.device)
+        dist.broadcast(hdr, src)
+        n, sb = int(hdr[0].item()), int(hdr[1].item())
+        if mx.numel() != n:
+            mx = torch.empty(n, dtype=mx.dtype, device=mx.device)
         dist.broadcast(mx, src)
         q.maxval = mx
-        q.sign_bits = int(q.sign_bits)
+        q.sign_bits = sb
+
+
+def calibrate_on_rank0(model, batches, src=0, quantized=False):
+    """The reference's calibration (image_net.py:76-91: estimate_ranges, forward the
+    calibration batches, fix_ranges) run by rank `src` alone; every other rank takes rank
+    `src`'s model state and FP8 ranges by broadcast.  `batches` is an iterable of input
+    tensors (only consumed on rank `src`).  quantized=True calls model.quantized() first (the
+    benchmark's order), else set_quant_state(True, True) around the pass (the validate
+    driver's)."""
+    _, rank = world()
+    broadcast_model_state(model, src)
+    if quantized:
+        model.quantized()
+    model.estimate_ranges()
+    if not quantized:
+        model.set_quant_state(True, True)
+    if rank == src:
+        with torch.no_grad():
+            for x in batches:
+                model(x)
+    if not quantized:
+        model.set_quant_state(True, True)
+    model.fix_ranges()
+    broadcast_quant_state(model, src)
 
 
 def gather_logits(logits):
@@ -53,7 +99,28 @@ def gather_logits(logits):
     return out
 
 
-def topk_correct(logits, labels, ks=(1, 5)):
+def gather_scored(logits, labels, batch):
+    """One all-gather per validation step: this rank's logits [n, C] (n <= batch; n = 0 for a
+    rank without a batch this step), its labels [n], padded to `batch` rows and packed with a
+    label column and a valid-row flag into float32 [batch, C + 2] (class indices < 2^24 are
+    exact).  Returns the valid rows of every rank in rank order: (logits [N, C], labels [N])."""
+    n, C = logits.shape
+    packed = torch.zeros((batch, C + 2), dtype=torch.float32, device=logits.device)
+    packed[:n, :C] = logits.float()
+    packed[:n, C] = labels.float()
+    packed[:n, C + 1] = 1.0
+    allp = gather_logits(packed)
+    valid = allp[:, C + 1] > 0
+    return allp[valid, :C], allp[valid, C].long()
+
+
+def score(logits, labels, ks=(1, 5)):
+    """(top-k hit counts, summed cross-entropy) of a scored batch."""
     top = logits.topk(max(ks), dim=1).indices
     hit = top.eq(labels.view(-1, 1))
-    return {k: int(hit[:, :k].any(dim=1).sum().item()) for k in ks}
+    return ({k: int(hit[:, :k].any(dim=1).sum().item()) for k in ks},
+            float(F.cross_entropy(logits, labels, reduction="sum")) if labels.numel() else 0.0)
+
+
+def topk_correct(logits, labels, ks=(1, 5)):
+    return score(logits, labels, ks)[0]

@@ -30,7 +30,6 @@ import time
 import numpy as np
 import torch
 import torch.distributed as dist
-import torch.nn.functional as F
 
 IMAGENET_MEAN = (0.485, 0.456, 0.406)
 IMAGENET_STD = (0.229, 0.224, 0.225)
@@ -170,52 +169,21 @@ def _loader(ds, batch, workers, indices=None):
     return torch.utils.data.DataLoader(ds, batch_size=batch, shuffle=False, num_workers=workers, pin_memory=True)
 
 
-def main(argv=None):
-    args = parse(argv)
-    ws = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if not torch.cuda.is_available():
-        raise RuntimeError("the approx path needs a HIP device")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if ws > 1:
-        dist.init_process_group("nccl", device_id=dev)
-    from .distributed import broadcast_quant_state, gather_logits
+def validate(model, val, train, args, dev, rank=0, ws=1, source=""):
+    """Calibrate on rank 0 (ranges broadcast), evaluate the (mini_test or full) batches sharded
+    over ranks with one packed all-gather per step; rank 0 returns the result dict (None on
+    the other ranks).  `model` is already on `dev` in eval mode."""
+    from .distributed import calibrate_on_rank0, gather_scored, score
 
-    if args.synthetic:
-        val = SyntheticImages(args.synthetic, args.image_size)
-        train = SyntheticImages(args.batch_size * args.num_est_batches, args.image_size, seed=1)
-        source = f"synthetic ({args.synthetic} random images)"
-    else:
-        val = NumericImageFolder(os.path.join(args.images_dir, "val"), args.image_size)
-        tdir = os.path.join(args.images_dir, "train")
-        train = NumericImageFolder(tdir, args.image_size) if os.path.isdir(tdir) else val
-        source = args.images_dir + ("" if train is not val else " (calibrated on val: no train split)")
-
-    cfg = dict(expo_width=args.expo_width, mant_width=args.mant_width, dnsmp_factor=args.dnsmp_factor,
-               withComp=args.with_comp, with_approx=True, with_s2nn2s_opt=not args.no_s2n,
-               quant_btw_mult_accu=not args.no_qbma)
-    if args.no_approx:
-        cfg["run_method"] = dict(approx_flag=False, quantize_after_mult_and_add=False, res_quantizer_flag=True,
-                                 original_quantize_res=False)
-    model = build_model(args.arch, args.weights, cfg, args.image_size).to(dev).eval()
-
-    # calibration on rank 0, ranges broadcast (identical biases everywhere)
-    model.estimate_ranges()
-    model.set_quant_state(True, True)
-    with torch.no_grad():
-        cal = _loader(train, args.batch_size, args.num_workers)
-        for i, (x, _) in enumerate(cal):
-            model(x.to(dev, non_blocking=True))
+    def cal_batches():
+        for i, (x, _) in enumerate(_loader(train, args.batch_size, args.num_workers)):
+            yield x.to(dev, non_blocking=True)
             if i >= args.num_est_batches - 1:
                 break
-    model.set_quant_state(True, True)
-    model.fix_ranges()
-    broadcast_quant_state(model, src=0)
+    calibrate_on_rank0(model, cal_batches())
 
     # evaluated batches (mini_test or all), sharded over ranks; each global step every rank
-    # runs one batch and the logits are all-gathered
+    # runs one batch (or none) and the packed logits / labels are all-gathered once
     nb = (len(val) + args.batch_size - 1) // args.batch_size
     batches = mini_test_batches(nb) if args.mini_test else list(range(nb))
     if args.max_batches:
@@ -232,40 +200,68 @@ def main(argv=None):
         for s in range(steps):
             if s < len(mine):
                 x, y = next(it)
-                y = y.to(dev)
                 logits = model(x.to(dev, non_blocking=True))
-                n_valid = torch.tensor([x.shape[0]], device=dev)
-            else:  # this rank has no batch left: contribute padding the scorer skips
-                logits = torch.zeros((args.batch_size, n_cls), device=dev)
-                y = torch.zeros(args.batch_size, dtype=torch.long, device=dev)
-                n_valid = torch.tensor([0], device=dev)
-            pad = args.batch_size - logits.shape[0]
-            if pad:
-                logits = F.pad(logits, (0, 0, 0, pad))
-                y = F.pad(y, (0, pad))
-            L = gather_logits(logits.float())
-            Y = gather_logits(y.view(-1, 1)).view(-1)
-            N = gather_logits(n_valid.view(1, 1)).view(-1)
-            if rank == 0:
-                for r in range(ws):
-                    n = int(N[r])
-                    if n == 0:
-                        continue
-                    lr = L[r * args.batch_size:r * args.batch_size + n]
-                    yr = Y[r * args.batch_size:r * args.batch_size + n]
-                    top = lr.topk(5, dim=1).indices
-                    hit = top.eq(yr.view(-1, 1))
-                    correct1 += int(hit[:, :1].any(1).sum())
-                    correct5 += int(hit.any(1).sum())
-                    loss_sum += float(F.cross_entropy(lr, yr, reduction="sum"))
-                    seen += n
-    torch.cuda.synchronize()
+                y = y.to(dev)
+            else:  # this rank has no batch left this step: it contributes no valid rows
+                logits = torch.zeros((0, n_cls), device=dev)
+                y = torch.zeros(0, dtype=torch.long, device=dev)
+            L, Y = gather_scored(logits, y, args.batch_size)
+            if rank == 0 and Y.numel():
+                hits, loss = score(L, Y)
+                correct1 += hits[1]
+                correct5 += hits[5]
+                loss_sum += loss
+                seen += int(Y.numel())
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if rank != 0:
+        return None
+    return dict(arch=args.arch, data=source, images=seen, top_1_accuracy=correct1 / max(1, seen),
+                top_5_accuracy=correct5 / max(1, seen), loss=loss_sum / max(1, seen), images_per_s=seen / elapsed,
+                n_gpus=ws, evaluate_param="mini_test" if args.mini_test else "full_test")
+
+
+def datasets(args):
+    if args.synthetic:
+        val = SyntheticImages(args.synthetic, args.image_size)
+        train = SyntheticImages(args.batch_size * args.num_est_batches, args.image_size, seed=1)
+        return val, train, f"synthetic ({args.synthetic} random images)"
+    val = NumericImageFolder(os.path.join(args.images_dir, "val"), args.image_size)
+    tdir = os.path.join(args.images_dir, "train")
+    train = NumericImageFolder(tdir, args.image_size) if os.path.isdir(tdir) else val
+    return val, train, args.images_dir + ("" if train is not val else " (calibrated on val: no train split)")
+
+
+def approx_cfg(args):
+    cfg = dict(expo_width=args.expo_width, mant_width=args.mant_width, dnsmp_factor=args.dnsmp_factor,
+               withComp=args.with_comp, with_approx=True, with_s2nn2s_opt=not args.no_s2n,
+               quant_btw_mult_accu=not args.no_qbma)
+    if args.no_approx:
+        # the reference's canonical no-approx run (scripts/image_net.sh:42-45): exact product, then
+        # the res quantizer through the original_quantize_res branch
+        cfg["run_method"] = dict(approx_flag=False, quantize_after_mult_and_add=False, res_quantizer_flag=True,
+                                 original_quantize_res=True)
+    return cfg
+
+
+def main(argv=None):
+    args = parse(argv)
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if not torch.cuda.is_available():
+        raise RuntimeError("the approx path needs a HIP device")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if ws > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    val, train, source = datasets(args)
+    cfg = approx_cfg(args)
+    model = build_model(args.arch, args.weights, cfg, args.image_size).to(dev).eval()
+    res = validate(model, val, train, args, dev, rank, ws, source)
     if rank == 0:
-        res = dict(arch=args.arch, data=source, images=seen, top_1_accuracy=correct1 / max(1, seen),
-                   top_5_accuracy=correct5 / max(1, seen), loss=loss_sum / max(1, seen),
-                   images_per_s=seen / elapsed, n_gpus=ws, evaluate_param="mini_test" if args.mini_test else "full_test",
-                   approx_params=cfg)
+        res["approx_params"] = cfg
         print(json.dumps(res), flush=True)
         if args.output:
             with open(args.output, "w") as f:

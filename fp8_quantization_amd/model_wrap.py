@@ -315,4 +315,6 @@ def fused_linear_tail(block, dense, x, residual, dropout=None):
             return None
     if residual.shape[:-1] != x.shape[:-1] or residual.shape[-1] != dense.out_features:
         return None
+    if residual.dtype != torch.float32 or not residual.is_contiguous() or residual.data_ptr() % 16:
+        return None  # fp8a_matmul_block takes a dense, 16-byte aligned float32 residual
     return dense(x, post=(residual, 0, 0.0, 0.0, q))

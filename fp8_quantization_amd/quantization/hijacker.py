@@ -87,6 +87,9 @@ class QuantizationHijacker(QuantizedModule):
                 kw["post"] = post  # a residual block's tail (BNFusedHijacker.forward)
             res = self.run_forward(x, weight, bias, offsets=offsets, **kw)
         self._check_res_flag()
+        if res is None:  # fixed ranges, no approx / qamaa product and original_quantize_res off: the
+            # reference then reads an unassigned `res` (hijacker.py:110, quantized_folded_bn.py:66)
+            raise UnboundLocalError("local variable 'res' referenced before assignment")
         return res, qa
 
     def _epilogue(self, res, qa, activation_done=False):

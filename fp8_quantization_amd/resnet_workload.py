@@ -21,10 +21,18 @@ from .quantization.base_quantized_classes import FP32Acts, QuantizedActivation
 
 
 def approx_qparams(expo_width=4, mant_width=3, dnsmp_factor=3, withComp=False, with_approx=True,
-                   with_s2nn2s_opt=True, quant_btw_mult_accu=True, golden_clip_OF=False, n_bits=8, run_method=None):
+                   with_s2nn2s_opt=True, quant_btw_mult_accu=True, golden_clip_OF=False, n_bits=8, run_method=None,
+                   zero_table_ext=None, approx_version=9, sim_hw_add_OFUF=False, with_OF_opt=False,
+                   with_UF_opt=False):
     """qparams exactly as the reference scripts build them (utils/click_options.py:544-606,
     scripts/generated_scripts.py): per-channel current_minmax weights, allminmax activations,
-    quantize_input, FP8 quantizer with set_maxval, approx + res_quantizer run method."""
+    quantize_input, FP8 quantizer with set_maxval, approx + res_quantizer run method.
+
+    Extensions (not in the reference): zero_table_ext (None = on exactly for formats the
+    reference has no error table for, E5M2: error_tables.get_error_table_NN) and approx_version 5
+    (the v5 integer-adder model with live sim_hw_add_OFUF / with_OF_opt / with_UF_opt)."""
+    if zero_table_ext is None:
+        zero_table_ext = (expo_width, mant_width) not in ((4, 3), (3, 4), (2, 5))
     return dict(
         method=FPQuantizer, act_method=FPQuantizer, n_bits=n_bits, n_bits_act=n_bits, per_channel_weights=True,
         weight_range_method=RangeEstimators.current_minmax.cls, weight_range_options={},
@@ -33,9 +41,11 @@ def approx_qparams(expo_width=4, mant_width=3, dnsmp_factor=3, withComp=False, w
                         learn_mantissa_bits=False, mse_include_mantissa_bits=False, allow_unsigned=False),
         custom_approx_params=dict(expo_width=expo_width, mant_width=mant_width, dnsmp_factor=dnsmp_factor,
                                   withComp=withComp, with_approx=with_approx, with_s2nn2s_opt=with_s2nn2s_opt,
-                                  sim_hw_add_OFUF=False, with_OF_opt=False, with_UF_opt=False,
+                                  sim_hw_add_OFUF=sim_hw_add_OFUF, with_OF_opt=with_OF_opt, with_UF_opt=with_UF_opt,
                                   golden_clip_OF=golden_clip_OF, quant_btw_mult_accu=quant_btw_mult_accu,
-                                  debug_mode=False, self_check_mode=False),
+                                  debug_mode=False, self_check_mode=False,
+                                  **({"zero_table_ext": True} if zero_table_ext else {}),
+                                  **({"approx_version": 5} if approx_version == 5 else {})),
         run_method=dict(run_method) if run_method else dict(
             approx_flag=True, quantize_after_mult_and_add=False, res_quantizer_flag=True, original_quantize_res=False))
 

@@ -52,6 +52,20 @@ const char *fp8a_version(void);
 const char *fp8a_last_error(void);
 
 /*
+ * Fallback counters of the library since it was loaded (or last reset), out[4]:
+ *   [0] launches whose gated exact kernel ran (an operand off its FP8 grid or outside the fast
+ *       path's exactness window, a bias outside the window, or a term beyond the e4m3 range),
+ *   [1] 64 x 64 output units that kernel recomputed (only the marked units are: an off-grid A
+ *       row marks its row units, a B column its column unit, a tile's out-of-range term its
+ *       own units; a bias outside the window marks them all),
+ *   [2] launches rerun in gemm_tt_kernel's f32 form (E3M4 left gemm_tt16_kernel's f16 window),
+ *   [3] tensor-bias (depthwise) launches recomputed by the literal restatement.
+ * Synchronises the device (diagnostics / benchmark reporting, not for the hot path); reset != 0
+ * zeroes the counters after reading.
+ */
+int fp8a_fallback_stats(uint64_t *out, int reset);
+
+/*
  * Element decomposition DEC of float_to_fpany_absint_torch (approx_matmul_whole_v9.py:233-291)
  * over a rows x cols matrix with row stride ld.  bias: device int32, bias_stride 0 = one bias
  * for all elements, 1 = one bias per ROW (per-channel weights).  flags: FP8A_TB selects the
@@ -75,10 +89,12 @@ int fp8a_quant(const float *x, int64_t n, int E, int M, const int32_t *bias, uin
  * v9:555-592) or NULL for all-zero; it is packed into the launch arguments, so the call stays
  * asynchronous.  C is row-major with leading dimension ldc.  workspace: device scratch of at
  * least fp8a_matmul_workspace_size() bytes (holds the off-grid flag that gates the exact
- * re-computation when an operand is not exactly representable in its FP8 code); a workspace
- * of fp8a_matmul_workspace_size_mnk(M, N, K) bytes also holds split-K partial sums, which the
- * launch then uses when the shape fills the GPU in a fractional number of waves (the partials
- * are summed in a fixed order: results stay deterministic).
+ * re-computation when an operand is not exactly representable in its FP8 code -- with this
+ * minimal workspace any fallback recomputes the whole product); a workspace of
+ * fp8a_matmul_workspace_size_mnk(M, N, K) bytes also holds the per-64x64-unit fallback marks
+ * (only the affected output units are recomputed) and split-K partial sums, which the launch
+ * then uses when the shape fills the GPU in a fractional number of waves (the partials are
+ * summed in a fixed order: results stay deterministic).
  */
 size_t fp8a_matmul_workspace_size(void);
 size_t fp8a_matmul_workspace_size_mnk(int64_t M, int64_t N, int64_t K);

@@ -80,12 +80,15 @@ from quantization.range_estimators import RangeEstimators  # noqa: E402
 FORMATS = [(4, 3), (3, 4), (2, 5), (5, 2)]
 
 
-def table(E, M, with_comp, dnsmp):
+def table(E, M, with_comp=False, dnsmp_factor=3, withComp=None):
     """Error table as the operator would pick it; E5M2 (unsupported by the reference,
-    SURVEY F3) gets an all-zero table so its arithmetic can still be pinned."""
+    SURVEY F3) gets an all-zero table so its arithmetic can still be pinned.  (Also stands in
+    for the reference's get_error_table_NN signature, withComp= keyword included.)"""
+    if withComp is not None:
+        with_comp = withComp
     if (E, M) == (5, 2):
         return torch.zeros((4, 4), dtype=torch.int32)
-    return v9.get_error_table_NN(E, M, withComp=with_comp, dnsmp_factor=dnsmp)
+    return v9.get_error_table_NN(E, M, withComp=with_comp, dnsmp_factor=dnsmp_factor)
 
 
 TABLE_VARIANTS = {
@@ -317,7 +320,9 @@ def gen_g6():
 
 
 # ----------------------------------------------------------------------------- G7
-V5_TABLES = {(4, 3): [3], (3, 4): [3, 4], (2, 5): [3, 4, 5]}
+# (E5M2 last, so the seeded draws of the other formats are unchanged: v5 has no E5M2 table
+# either -- get_comp_table_NN raises for it -- so it runs with the zero table only)
+V5_TABLES = {(4, 3): [3], (3, 4): [3, 4], (2, 5): [3, 4, 5], (5, 2): []}
 V5_FLAGS = [(False, False, False), (True, False, False), (True, True, False), (True, False, True),
             (True, True, True)]
 
@@ -385,9 +390,21 @@ def gen_g8():
     from models.mobilenet_v2 import MobileNetV2 as RefMobileNetV2  # reference, unmodified
     from models.mobilenet_v2_quantized_approx import QuantizedMobileNetV2 as RefQuantizedMobileNetV2
     out, meta = {}, []
-    run_method = dict(approx_flag=True, quantize_after_mult_and_add=False, res_quantizer_flag=True,
-                      original_quantize_res=False)
-    for (name, (E, M), wc) in [("mbv2_e4m3", (4, 3), False)]:
+    approx_rm = dict(approx_flag=True, quantize_after_mult_and_add=False, res_quantizer_flag=True,
+                     original_quantize_res=False)
+    # the reference's canonical --no-approx_flag run (scripts/image_net.sh:42-45): the exact product
+    # then the res quantizer, through the original_quantize_res branch (quantized_folded_bn.py:40-48;
+    # without it the fixed-range forward reads an unassigned `res`)
+    exact_rm = dict(approx_rm, approx_flag=False, original_quantize_res=True)
+    # mbv2_e4m3: BASELINE config 3's network in E4M3; mbv2_e4m3_noapprox: BASELINE config 1 (E4M3
+    # PTQ, --no-approx_flag: the quantizers around the exact product, hijacker.py:88-115);
+    # mbv2_e5m2: config 3's format, which the reference's get_error_table_NN rejects (v9:588-590,
+    # SURVEY F3) -- the generator gives the reference's operators an all-zero E5M2 table (the
+    # engine's opt-in zero_table_ext), everything else is the reference's own code
+    cases = [("mbv2_e4m3", (4, 3), False, approx_rm), ("mbv2_e4m3_noapprox", (4, 3), False, exact_rm),
+             ("mbv2_e5m2", (5, 2), False, approx_rm)]
+    for (name, (E, M), wc, run_method) in cases:
+        ac.get_error_table_NN = table if (E, M) == (5, 2) else v9.get_error_table_NN
         torch.manual_seed(88)
         fp = RefMobileNetV2(n_class=10, input_size=32, width_mult=0.25)
         with torch.no_grad():
@@ -426,7 +443,9 @@ def gen_g8():
         out[f"{name}__x_cal"], out[f"{name}__x_ev"] = x_cal.numpy(), x_ev.numpy()
         out[f"{name}__logits"] = logits.numpy()
         meta.append(dict(name=name, E=E, M=M, with_comp=wc, width_mult=0.25, input_size=32, n_class=10,
+                         run_method=run_method, zero_table_ext=(E, M) == (5, 2),
                          state_keys=list(state.keys()), approx_layers=biases))
+    ac.get_error_table_NN = v9.get_error_table_NN
     np.savez_compressed(os.path.join(HERE, "g8_mbv2.npz"), **out)
     return meta
 
@@ -510,15 +529,28 @@ def gen_g5():
     return meta
 
 
-def main():
+GROUPS = dict(g1=lambda: gen_g1(), g2=lambda: gen_g2(), g3=lambda: gen_g3(), g4=lambda: gen_g4(),
+              g5=lambda: gen_g5(), g6=lambda: gen_g6(), g7=lambda: gen_g7(), g8=lambda: gen_g8())
+
+
+def main(argv):
+    """All groups, or only the named ones (e.g. `gen_golden.py g7 g8`): meta.json keeps the other
+    groups' entries."""
     torch.set_num_threads(os.cpu_count() or 1)
-    meta = dict(torch_version=torch.__version__, reference="revollllt/FP8_quantization@2024-11-08",
-                g1=gen_g1(), g2=gen_g2(), g3=gen_g3(), g4=gen_g4(), g5=gen_g5(), g6=gen_g6(), g7=gen_g7(), g8=gen_g8())
-    with open(os.path.join(HERE, "meta.json"), "w") as f:
+    names = argv or list(GROUPS)
+    mpath = os.path.join(HERE, "meta.json")
+    meta = {}
+    if argv and os.path.exists(mpath):
+        with open(mpath) as f:
+            meta = json.load(f)
+    meta.update(torch_version=torch.__version__, reference="revollllt/FP8_quantization@2024-11-08")
+    for n in names:
+        meta[n] = GROUPS[n]()
+    with open(mpath, "w") as f:
         json.dump(meta, f, indent=1)
     sizes = {f: os.path.getsize(os.path.join(HERE, f)) for f in os.listdir(HERE) if f.endswith(".npz")}
     print(json.dumps(sizes))
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])

@@ -7,6 +7,10 @@ c_b, rounded by the gfx950 scaled fp8 conversion.  Checked here:
     bit-exact against the oracle, for several bias triples, with the launch's fallback flag
     read back to prove the fast form (not the exact kernel) produced them;
   * terms beyond the e4m3 range raise the flag and the exact kernel's result is returned;
+  * a fallback recomputes only the affected 64 x 64 output units (one out-of-range term: its
+    tile; an off-grid A element: its row unit; an off-grid B element: its column unit) and
+    every other output is bit-identical to the fast path's, with the library's fallback
+    counters (fp8a_fallback_stats) recording the units;
   * sums at realistic shapes stay within the 1e-5 * sum|term| bar.
 """
 import numpy as np
@@ -113,3 +117,56 @@ def test_sums_within_bar(shape):
     Cref, S = orc.matmul(A, B, 4, 3, bA, bB, bR, tab, fl, with_abs=True)
     assert flag == 0
     assert np.all(np.abs(C.astype(np.float64) - Cref) <= gio.sum_tolerance(S.astype(np.float64)))
+
+
+def _sum_operands(Mr, K, N, seed):
+    rng = np.random.default_rng(seed)
+    bA, bR = 9, 3
+    bB = rng.integers(11, 15, size=N).astype(np.int32)
+    e = rng.integers(3, 16, size=(Mr, K))
+    m = rng.integers(0, 8, size=(Mr, K))
+    A = np.ldexp(1.0 + m / 8.0, e - bA) * rng.choice([-1.0, 1.0], size=(Mr, K))
+    A[rng.random((Mr, K)) < 0.4] = 0.0
+    e = rng.integers(5, 16, size=(K, N))
+    m = rng.integers(0, 8, size=(K, N))
+    B = np.ldexp(1.0 + m / 8.0, e - bB[None, :]) * rng.choice([-1.0, 1.0], size=(K, N))
+    return A.astype(np.float32), B.astype(np.float32), bA, bB, bR
+
+
+@pytest.mark.parametrize("case", ["term_out_of_range", "off_grid_a", "off_grid_b"])
+def test_fallback_recomputes_only_marked_units(case):
+    from fp8_quantization_amd import _lib
+    Mr, K, N = 520, 600, 200  # 9 x 4 output units, split-K shape
+    A, B, bA, bB, bR = _sum_operands(Mr, K, N, 17)
+    tab = gio.load("g2_matmul.npz")["E4M3_table_nocomp"]
+    fl = orc.flags_of(approx=True, s2n=True, qbma=True)
+    C0, flag0 = _matmul_raw(A, B, bA, bB, bR, tab, fl)
+    assert flag0 == 0
+    r, k0, n = 300, 77, 131
+    A2, B2 = A.copy(), B.copy()
+    if case == "term_out_of_range":  # on the grid (any exponent), ONE product beyond the e4m3 range of bR
+        A2[r, k0] = 1024.0
+        B2[k0, :] /= 16.0  # (the row's other products stay in range)
+        B2[k0, n] = 30.0
+    elif case == "off_grid_a":
+        A2[r, k0] = 1.0 + 2.0 ** -10
+    else:
+        B2[k0, n] = 1.0 + 2.0 ** -12
+    _lib.fallback_stats(reset=True)
+    C2, flag2 = _matmul_raw(A2, B2, bA, bB, bR, tab, fl)
+    st = _lib.fallback_stats()
+    assert flag2 & 1 and not flag2 & 32, flag2  # some units, not all
+    assert st["exact_launches"] == 1
+    ur, uc = np.arange(Mr) // 64, np.arange(N) // 64
+    if case == "term_out_of_range":  # the 128-row tile holding (r, n)
+        marked = ((ur[:, None] // 2) == (r // 128)) & (uc[None, :] == n // 64)
+    elif case == "off_grid_a":
+        marked = (ur[:, None] == r // 64) & (uc[None, :] >= 0)
+    else:
+        marked = (ur[:, None] >= 0) & (uc[None, :] == n // 64)
+    units = {(a, b) for a, b in zip(*np.nonzero(marked)) for a, b in [(a // 64, b // 64)]}
+    assert st["exact_units"] == len(units), (st, len(units))
+    # outside the marked units: the fast path's bits; inside: the exact kernel, within the bar
+    assert np.array_equal(C2[~marked].view(np.uint32), C0[~marked].view(np.uint32))
+    Cref, S = orc.matmul(A2, B2, 4, 3, bA, bB, bR, tab, fl, with_abs=True)
+    assert np.all(np.abs(C2.astype(np.float64) - Cref) <= gio.sum_tolerance(S.astype(np.float64)))

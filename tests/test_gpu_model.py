@@ -1,6 +1,9 @@
-"""Model-level parity (G8): the reference's QuantizedMobileNetV2 (width 0.25, 32x32, E4M3
-approx_v9, random weights and BN statistics) rebuilt from the drop-in operators, given the
-reference's initial state, goes through estimate -> fix -> approx on the GPU.
+"""Model-level parity (G8): the reference's QuantizedMobileNetV2 (width 0.25, 32x32, random
+weights and BN statistics) rebuilt from the drop-in operators, given the reference's initial
+state, goes through estimate -> fix -> approx on the GPU.  Cases: E4M3 approx_v9; E4M3 with
+approx_flag off (BASELINE config 1: the reference's canonical --no-approx_flag
+--original-quantize-res run, exact product + quantizers); E5M2 approx_v9 with the opt-in zero
+table (BASELINE config 3's format; the reference was given the same zero table).
 
 Bars: every approx layer's bA / per-channel bB / bR identical (calibration reproduced through
 the whole network); logits within a summation-order tolerance; top-1 identical."""
@@ -21,7 +24,8 @@ def test_mobilenet_v2_model_level(case):
     g = gio.load("g8_mbv2.npz")
     name = case["name"]
     m = mobilenet_v2_approx(input_size=case["input_size"], width_mult=case["width_mult"], n_class=case["n_class"],
-                            expo_width=case["E"], mant_width=case["M"], withComp=case["with_comp"])
+                            expo_width=case["E"], mant_width=case["M"], withComp=case["with_comp"],
+                            run_method=case.get("run_method"), zero_table_ext=case.get("zero_table_ext", False))
     state = {k: torch.from_numpy(g[f"{name}__state__{k}"]) for k in case["state_keys"]}
     missing, unexpected = torch.nn.Module.load_state_dict(m, state, strict=False)
     assert not unexpected and not missing, (missing, unexpected)

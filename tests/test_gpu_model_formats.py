@@ -1,9 +1,11 @@
-"""Model-level parity for the non-E4M3 formats with withComp=False (BASELINE configs 3 and 5).
+"""Network-level parity of every approx product, per format (BASELINE configs 2 and 5).
 
-A ResNet-18 (random init, BN statistics from synthetic batches, 64x64 inputs) is quantized
-as E3M4 / E2M5 approx_v9 (dnsmp_factor 3, withComp False: the E3M4 16x16 and E2M5 32x32
-error tables, s2n, qbma), calibrated on one batch and run in the fixed-range state.  Two checks:
-  * every approx product of the forward (20 convs + fc), run unfused so its operands are
+A ResNet-18 and a ResNet-50 (random init, BN statistics from synthetic batches, 64x64 inputs)
+are quantized as E4M3 / E3M4 / E2M5 approx_v9 (dnsmp_factor 3, withComp False: the E4M3 8x8
+{0,1}, E3M4 16x16 and E2M5 32x32 error tables, s2n, qbma), calibrated on one batch and run in
+the fixed-range state.  Two checks:
+  * every approx product of the forward (ResNet-18: 20 convs + fc; ResNet-50: 53 convs + fc),
+    run unfused so its operands are
     visible, against the CPU oracle on the captured operands and biases (im2col for convs):
     sums within 1e-5 * sum|term|; this pins the whole network's data, biases included, through
     the GPU path layer by layer;
@@ -30,10 +32,10 @@ def _native():
     _lib.load()
 
 
-def _model(E, M):
-    from fp8_quantization_amd.resnet_workload import resnet18_approx
+def _model(E, M, arch="resnet18", batch=2):
+    from fp8_quantization_amd import resnet_workload as rw
     torch.manual_seed(E * 10 + M)
-    m = resnet18_approx(bn_stats_batches=2, device=DEV, expo_width=E, mant_width=M, withComp=False)
+    m = getattr(rw, arch + "_approx")(bn_stats_batches=2, device=DEV, expo_width=E, mant_width=M, withComp=False)
     m = m.to(DEV).eval()
     g = torch.Generator().manual_seed(5)
     m.quantized()
@@ -41,21 +43,22 @@ def _model(E, M):
     with torch.no_grad():
         m(torch.randn((4, 3, 64, 64), generator=g).to(DEV))
     m.fix_ranges()
-    return m, torch.randn((2, 3, 64, 64), generator=g).to(DEV)
+    return m, torch.randn((batch, 3, 64, 64), generator=g).to(DEV)
 
 
 def _ib(t):
     return int(t.reshape(-1)[0].item()) if isinstance(t, torch.Tensor) else int(t)
 
 
-@pytest.mark.parametrize("fmt", [(3, 4), (2, 5)], ids=["E3M4", "E2M5"])
-def test_resnet18_layers_match_oracle(fmt, monkeypatch):
+@pytest.mark.parametrize("fmt", [(4, 3), (3, 4), (2, 5)], ids=["E4M3", "E3M4", "E2M5"])
+@pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
+def test_resnet_layers_match_oracle(arch, fmt, monkeypatch):
     from fp8_quantization_amd import approx_calculation as ac
     from fp8_quantization_amd import model_wrap
     from fp8_quantization_amd.quantization.hijacker import QuantizationHijacker
     from fp8_quantization_amd.quantization.quantized_folded_bn import BNFusedHijacker
     E, M = fmt
-    model, x = _model(E, M)
+    model, x = _model(E, M, arch, batch=2 if arch == "resnet18" else 1)
 
     with torch.no_grad():
         fused = model(x).cpu().numpy()
@@ -82,7 +85,7 @@ def test_resnet18_layers_match_oracle(fmt, monkeypatch):
     with torch.no_grad():
         unfused = model(x).cpu().numpy()
     assert np.array_equal(fused.view(np.uint32), unfused.view(np.uint32)), "fused and unfused logits differ"
-    assert len(calls) == 21, len(calls)  # 20 convs + fc
+    assert len(calls) == (21 if arch == "resnet18" else 54), len(calls)  # convs + fc
 
     for i, (kind, a, b, bA, bB, bR, table, kw, out) in enumerate(calls):
         tab = np.ascontiguousarray(table.numpy(), np.int32)
