@@ -140,14 +140,15 @@ def test_fallback_recomputes_only_marked_units(case):
     A, B, bA, bB, bR = _sum_operands(Mr, K, N, 17)
     tab = gio.load("g2_matmul.npz")["E4M3_table_nocomp"]
     fl = orc.flags_of(approx=True, s2n=True, qbma=True)
-    C0, flag0 = _matmul_raw(A, B, bA, bB, bR, tab, fl)
-    assert flag0 == 0
     r, k0, n = 300, 77, 131
+    if case == "term_out_of_range":  # (row k0 of B small, but for column n: the baseline stays in range)
+        B[k0, :] /= 16.0
+        B[k0, n] = 30.0
+    C0, flag0 = _matmul_raw(A, B, bA, bB, bR, tab, fl)  # the fast path's bits, no fallback
+    assert flag0 == 0
     A2, B2 = A.copy(), B.copy()
-    if case == "term_out_of_range":  # on the grid (any exponent), ONE product beyond the e4m3 range of bR
+    if case == "term_out_of_range":  # on the grid (any exponent): ONE product beyond the e4m3 range of bR
         A2[r, k0] = 1024.0
-        B2[k0, :] /= 16.0  # (the row's other products stay in range)
-        B2[k0, n] = 30.0
     elif case == "off_grid_a":
         A2[r, k0] = 1.0 + 2.0 ** -10
     else:
@@ -167,6 +168,7 @@ def test_fallback_recomputes_only_marked_units(case):
     units = {(a, b) for a, b in zip(*np.nonzero(marked)) for a, b in [(a // 64, b // 64)]}
     assert st["exact_units"] == len(units), (st, len(units))
     # outside the marked units: the fast path's bits; inside: the exact kernel, within the bar
-    assert np.array_equal(C2[~marked].view(np.uint32), C0[~marked].view(np.uint32))
+    same = ~marked & (np.arange(Mr)[:, None] != r)  # (row r's other outputs use the changed A element)
+    assert np.array_equal(C2[same].view(np.uint32), C0[same].view(np.uint32))
     Cref, S = orc.matmul(A2, B2, 4, 3, bA, bB, bR, tab, fl, with_abs=True)
     assert np.all(np.abs(C2.astype(np.float64) - Cref) <= gio.sum_tolerance(S.astype(np.float64)))

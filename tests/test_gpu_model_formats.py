@@ -9,8 +9,9 @@ the fixed-range state.  Two checks:
     visible, against the CPU oracle on the captured operands and biases (im2col for convs):
     sums within 1e-5 * sum|term|; this pins the whole network's data, biases included, through
     the GPU path layer by layer;
-  * the fused forward (input quantization, BN + ReLU and residual tails in the kernels) gives
-    logits bit-identical to the unfused one.
+  * the fused forward (input quantization and residual tails in the kernels) gives logits
+    bit-identical to the unfused one (the BN + ReLU epilogue on in both: it is within one fp32
+    rounding of F.batch_norm, not bit-identical -- tests/test_gpu_fused_bn.py).
 """
 import numpy as np
 import pytest
@@ -63,10 +64,16 @@ def test_resnet_layers_match_oracle(arch, fmt, monkeypatch):
     with torch.no_grad():
         fused = model(x).cpu().numpy()
 
+    # the input-quantizer, block-tail and linear fusions are bit-identical to the separate passes;
+    # the BN epilogue (fma(acc, scale, shift)) is within one fp32 rounding of F.batch_norm, so the
+    # bit comparison keeps it on, and the operand capture below runs with it off
     monkeypatch.setattr(QuantizationHijacker, "fuse_input_quant", False)
-    monkeypatch.setattr(BNFusedHijacker, "fuse_bn_act", False)
     monkeypatch.setattr(model_wrap, "FUSE_BLOCK", False)
     monkeypatch.setattr(ac.ApproxLinearMixin, "fuse_linear_block", False)
+    with torch.no_grad():
+        unfused = model(x).cpu().numpy()
+    assert np.array_equal(fused.view(np.uint32), unfused.view(np.uint32)), "fused and unfused logits differ"
+    monkeypatch.setattr(BNFusedHijacker, "fuse_bn_act", False)
     calls = []
     conv0, mm0 = ac.approx_conv2d, ac.approx_matmul
 
@@ -83,8 +90,7 @@ def test_resnet_layers_match_oracle(arch, fmt, monkeypatch):
     monkeypatch.setattr(ac, "approx_conv2d", conv)
     monkeypatch.setattr(ac, "approx_matmul", mm)
     with torch.no_grad():
-        unfused = model(x).cpu().numpy()
-    assert np.array_equal(fused.view(np.uint32), unfused.view(np.uint32)), "fused and unfused logits differ"
+        model(x)
     assert len(calls) == (21 if arch == "resnet18" else 54), len(calls)  # convs + fc
 
     for i, (kind, a, b, bA, bB, bR, table, kw, out) in enumerate(calls):
