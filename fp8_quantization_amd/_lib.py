@@ -15,7 +15,7 @@ APPROX, S2N, QBMA, GCLIP, TB = 1, 2, 4, 8, 16
 V5, OFUF, OF_OPT, UF_OPT = 32, 64, 128, 256  # v5 integer-adder model (include/fp8approx.h)
 OK, EINVAL, EFORMAT, EHIP = 0, -1, -2, -3
 
-SYMBOLS = ("fp8a_version", "fp8a_last_error", "fp8a_fallback_stats", "fp8a_decompose", "fp8a_quant", "fp8a_matmul_workspace_size",
+SYMBOLS = ("fp8a_version", "fp8a_last_error", "fp8a_fallback_stats", "fp8a_path_stats", "fp8a_set_option", "fp8a_decompose", "fp8a_quant", "fp8a_matmul_workspace_size",
            "fp8a_matmul_workspace_size_mnk", "fp8a_matmul", "fp8a_terms", "fp8a_conv2d_workspace_size", "fp8a_conv2d",
            "fp8a_conv2d_bn_act", "fp8a_conv2d_qin_workspace_size", "fp8a_conv2d_qin",
            "fp8a_conv2d_block_workspace_size", "fp8a_conv2d_block", "fp8a_max_pool2d", "fp8a_im2col",
@@ -45,6 +45,8 @@ def load():
         "fp8a_version": ([], ctypes.c_char_p),
         "fp8a_last_error": ([], ctypes.c_char_p),
         "fp8a_fallback_stats": ([P, I], I),
+        "fp8a_path_stats": ([P, I], I),
+        "fp8a_set_option": ([ctypes.c_char_p, I], I),
         "fp8a_decompose": ([P, I64, I64, I64, I, I, P, I64, U, P, P, P], I),
         "fp8a_quant": ([P, I64, I, I, P, U, P, P], I),
         "fp8a_matmul_workspace_size": ([], SZ),
@@ -119,3 +121,22 @@ def fallback_stats(reset=False):
     out = (ctypes.c_uint64 * 4)()
     check(L.fp8a_fallback_stats(ctypes.cast(out, ctypes.c_void_p), 1 if reset else 0), "fp8a_fallback_stats")
     return dict(exact_launches=int(out[0]), exact_units=int(out[1]), f32_reruns=int(out[2]), tb_launches=int(out[3]))
+
+
+PATHS = ("one_hot", "f8mx", "tt", "tt16", "fast", "exact", "reserved6", "reserved7")
+
+
+def path_stats(reset=False):
+    """fp8a_path_stats: launches per GEMM path since load / the last reset."""
+    L = load()
+    out = (ctypes.c_uint64 * 8)()
+    check(L.fp8a_path_stats(ctypes.cast(out, ctypes.c_void_p), 1 if reset else 0), "fp8a_path_stats")
+    return {k: int(v) for k, v in zip(PATHS, out)}
+
+
+def set_option(name, value):
+    """fp8a_set_option: returns the previous value."""
+    rc = load().fp8a_set_option(name.encode(), int(value))
+    if rc < 0:
+        check(rc, "fp8a_set_option")
+    return rc

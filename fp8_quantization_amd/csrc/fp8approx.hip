@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -169,9 +170,17 @@ struct GemmArgs {
     int64_t awld, aw_c;
     int64_t awH, awW;  // conv: the word image's height / width (H + 2 ph, W + 2 pw when zero-padded)
     int awph, awpw;    // conv: x's offset inside the word image (the zero border's width)
-    int wfmt;          // pre-decoded operand format: 0 = gemm_f8mx_kernel's, 1 = gemm_tt_kernel's, 2 = gemm_tt16_kernel's
+    int wfmt;          // pre-decoded operand format: 0 = gemm_f8mx_kernel's, 1 = gemm_tt_kernel's, 2 = gemm_tt16_kernel's,
+                       // 3 = gemm_oh_kernel's (u16 A codes in the same image layout, gemm_oh.h)
     int ttf7;          // gemm_tt_kernel: the table has negative entries (the F7 sign rule)
     const uint2 *bqw;
+    // the one-hot E4M3 path (gemm_oh.h): B codes [npad][kpad] (u8), B block scales [npad][kpad / 4]
+    // (E8M0), the sorted candidate lists [kpad][npad / 64][64] (u32) and their count blocks
+    // [kpad][npad / 64][OH_CB] (u8) and the correction slice (split-K partial layout); the A shift
+    // sA = 6 - bA is derived on the device (bA may be the fused input quantizer's)
+    const uint8_t *ohb, *ohs, *ohc;
+    const uint32_t *ohl;
+    float *ohd;
     const uint32_t *lutw;  // the LDS table image (XM_LUT_WORDS words), written by xm_decode_b
     int64_t npad;
     // fused input quantization (fp8a_conv2d_qin): A = fq(X); the quantizer's bias is written to
@@ -740,13 +749,14 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
 #include "gemm_f8mx.h"
 #include "gemm_tt.h"
 #include "gemm_tt16.h"
+#include "gemm_oh.h"
 
 // Sums the split-K partials in split order (deterministic) and writes the output mapping.
 // Partial layout: row-major [M][N] (rowmajor output) or [img][N][hw] (NCHW output).
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs p) {
     const int64_t MN = p.M * p.N;
     const float pb = post_bias(p);
-    const int S = p.splits;
+    const int S = p.splits + (p.ohd ? 1 : 0);  // (the one-hot path's correction slice follows the partials)
     const bool vec = p.nchw ? ((p.hw & 3) == 0) : ((p.N & 3) == 0 && (p.ldc & 3) == 0);
     const bool aligned = ((((uintptr_t)p.C) & 15) == 0) && ((((uintptr_t)p.part) & 15) == 0) && ((MN & 3) == 0) &&
                          ((((uintptr_t)p.res) & 15) == 0);
@@ -1227,6 +1237,15 @@ static int check_format(int E, int Mw) {
 
 constexpr size_t FLAG_BYTES = 256;  // workspace prefix holding the off-grid flag word
 
+// Launch paths taken by run_gemm since load (fp8a_path_stats): host-side counters.
+enum { PATH_OH = 0, PATH_F8MX = 1, PATH_TT = 2, PATH_TT16 = 3, PATH_FAST = 4, PATH_EXACT = 5, PATH_N = 8 };
+static std::atomic<uint64_t> g_paths[PATH_N];
+// Options (fp8a_set_option): "one_hot" -- the E4M3 one-hot path (gemm_oh.h), default on
+// (FP8A_NO_OH=1 in the environment turns it off at load).
+static bool g_opt_one_hot = getenv("FP8A_NO_OH") == nullptr;
+// "oh_correct" (diagnostics): 0 skips the one-hot path's correction kernel (dense terms only)
+static bool g_opt_oh_correct = true;
+
 // Compute units of the current device (cached); 256 (MI355X) when no device is visible.
 static int device_cus() {
     static int cache[64] = {0};
@@ -1254,6 +1273,39 @@ static int device_cus() {
 // multiplies the tile count and divides the round length, and adds a pass that writes and
 // re-reads S*M*N partial floats (charged at 2 TB/s).  Each split keeps at least 16 K-tiles.
 // FP8A_SPLITK=<S> forces S (experiments).
+// The one-hot path's split-K factor (gemm_oh.h): the same round model for its tiles (256 x 64 or
+// 128 x 128, 2 workgroups per CU, ~2e11 products/s per workgroup slot); splits are multiples of
+// OH_KC and keep at least 8 chunks each.  FP8A_SPLITK_OH=<S> forces S.
+static int oh_tnw(int64_t N) { return (N % 128 == 0) ? 2 : 1; }
+static int choose_splits_oh(int64_t M, int64_t N, int64_t K) {
+    static int forced = -1;
+    if (forced < 0) {
+        const char *e = getenv("FP8A_SPLITK_OH");
+        forced = e ? std::max(0, atoi(e)) : 0;
+    }
+    const int64_t kc = (K + 31) / 32;
+    if (forced > 0) return (int)std::max<int64_t>(1, std::min<int64_t>(forced, kc));
+    const int tnw = oh_tnw(N);
+    const int64_t tm = 256 / tnw, tn = 64 * tnw;
+    const int64_t tiles = ((M + tm - 1) / tm) * ((N + tn - 1) / tn);
+    const double slots = 2.0 * device_cus();
+    const double t_round = (double)tm * tn * K / 2.0e11;
+    const double t_split = 2.0 * (double)M * N * sizeof(float) / 2.0e12;
+    double best = 1e300;
+    int bs = 1;
+    for (int S = 1; S <= 8; ++S) {
+        if (S > 1 && kc < 8 * S) break;
+        const double q = (double)tiles * S / slots, fl = std::floor(q), fr = q - fl;
+        const double rounds = fl + (fr > 1e-9 ? std::min(1.0, 0.4 + 1.1 * fr) : 0.0);
+        const double t = rounds / S * t_round + (S > 1 ? S * t_split : 0.0);
+        if (t < best * (1.0 - 1e-3)) {
+            best = t;
+            bs = S;
+        }
+    }
+    return bs;
+}
+
 static int choose_splits(int64_t M, int64_t N, int64_t K) {
     static int forced = -1;
     if (forced < 0) {
@@ -1307,10 +1359,27 @@ static size_t splitk_bytes(int64_t M, int64_t N, int64_t K) {
     return S > 1 ? align256((size_t)S * (size_t)M * (size_t)N * sizeof(float)) : 0;
 }
 
-// flag word + split-K partials + the pre-decoded operands (a_words: the A operand's element
-// count as the matrix-core E4M3 path stores it; 0 = no room for that path)
-static size_t gemm_workspace_bytes(int64_t M, int64_t N, int64_t K, int64_t a_words) {
-    return head_bytes(M, N) + splitk_bytes(M, N, K) + (a_words > 0 ? xm_operand_bytes(N, K, a_words) : 0);
+// The one-hot path's buffers after the head (gemm_oh.h): the split-K partials plus the correction
+// slice ((S + 1) x M x N floats), the u16 A codes, the B codes / block scales and the candidate
+// lists / count blocks.  conv_words: the conv word image's element count (0: a matrix A).
+static int64_t oh_kpad(int64_t K) { return (K + 31) / 32 * 32; }
+static int64_t oh_npad(int64_t N) { return (N + 127) / 128 * 128; }
+static size_t oh_operand_bytes(int64_t M, int64_t N, int64_t K, int64_t conv_words) {
+    const int64_t kpad = oh_kpad(K), npad = oh_npad(N), nct = npad / 64;
+    const int64_t aw = conv_words > 0 ? conv_words : M * kpad;
+    const int S = choose_splits_oh(M, N, K);
+    return align256((size_t)(S + 1) * M * N * sizeof(float)) + align256((size_t)aw * 2) +
+           align256((size_t)(npad * kpad)) + align256((size_t)(npad * kpad / 4)) +
+           align256((size_t)(kpad * nct * 64 * 4)) + align256((size_t)(kpad * nct * 72));
+}
+
+// flag word + unit marks + the larger of the two E4M3 pre-decoded paths: split-K partials + the
+// matrix-core kernel's operands (gemm_f8mx.h), or the one-hot path's (gemm_oh.h).  conv_words:
+// the conv word image's element count, 0 for a matrix A.
+static size_t gemm_workspace_bytes(int64_t M, int64_t N, int64_t K, int64_t conv_words) {
+    const int64_t a_words = conv_words > 0 ? conv_words : M * ((K + BK - 1) / BK * BK);
+    const size_t xm = splitk_bytes(M, N, K) + xm_operand_bytes(N, K, a_words);
+    return head_bytes(M, N) + std::max(xm, oh_operand_bytes(M, N, K, conv_words));
 }
 
 // The E4M3 table + hardware-fp8 form applies (TM_F8; run_gemm then takes the matrix-core kernel
@@ -1411,6 +1480,7 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     const unsigned eblocks = (unsigned)std::min<int64_t>((total + 255) / 256, 4096);
     if (a.flags & F_TB) {
         a.flag = nullptr;
+        ++g_paths[PATH_EXACT];
         gemm_exact_kernel<<<eblocks, 256, 0, s>>>(a);
         return hip_check("fp8a exact gemm launch");
     }
@@ -1435,6 +1505,67 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     if (hipMemsetAsync(ws, 0, units ? FLAG_BYTES + (size_t)(a.nur + a.nuc + a.nur * a.nuc) : sizeof(uint32_t), s) !=
         hipSuccess)
         return hip_check("fp8a flag reset");
+    // E4M3 (TM_F8 flags): the one-hot dense matrix-core GEMM + candidate correction (gemm_oh.h) when
+    // the workspace holds its buffers; FP8A_NO_OH=1 keeps gemm_f8mx_kernel
+    if (mode == TM_F8 && g_opt_one_hot && !no_mx() && units) {
+        const int64_t kpad = oh_kpad(a.K), npad = oh_npad(a.N), nct = npad / 64;
+        const WordImage wi = word_image(a.H, a.W, a.ph, a.pw);
+        const int64_t conv_words = a.conv ? (a.M / (a.Ho * a.Wo)) * a.aw_c * wi.H * wi.W : 0;
+        const int64_t a_words = a.conv ? conv_words : a.M * kpad;
+        const int S = choose_splits_oh(a.M, a.N, a.K);
+        const bool fits32 = a_words < (1ll << 30) && npad * kpad < (1ll << 31) && kpad * nct * 64 * 4 < (1ll << 31);
+        if (fits32 && ws_bytes >= head + oh_operand_bytes(a.M, a.N, a.K, conv_words)) {
+            a.awH = wi.H; a.awW = wi.W; a.awph = wi.ph; a.awpw = wi.pw;
+            const size_t MN4 = (size_t)a.M * a.N * sizeof(float);
+            char *base = (char *)ws + head;
+            a.splits = S;
+            a.kchunk = ((kpad / 32 + S - 1) / S) * 32;  // split boundaries on chunk boundaries
+            a.part = (float *)base;
+            a.ohd = (float *)(base + (size_t)(S > 1 ? S : 0) * MN4);  // the correction slice after the partials
+            base += align256((size_t)(S + 1) * MN4);
+            a.aw = (const uint32_t *)base;
+            base += align256((size_t)a_words * 2);
+            a.ohb = (const uint8_t *)base;
+            base += align256((size_t)(npad * kpad));
+            a.ohs = (const uint8_t *)base;
+            base += align256((size_t)(npad * kpad / 4));
+            a.ohl = (const uint32_t *)base;
+            base += align256((size_t)(kpad * nct * 64 * 4));
+            a.ohc = (const uint8_t *)base;
+            a.awld = kpad;
+            a.npad = npad;
+            a.wfmt = 3;
+            const int64_t rows = a.conv ? a.M / (a.Ho * a.Wo) : a.M, cols = a_words / std::max<int64_t>(rows, 1);
+            const dim3 ga((unsigned)std::min<int64_t>((cols + 255) / 256, 64), (unsigned)std::min<int64_t>(rows, 1024));
+            xm_decode_a<<<ga, 256, 0, s>>>(a);
+            oh_decode_b<<<dim3((unsigned)(kpad / 4), (unsigned)nct), 64, 0, s>>>(a, kpad);
+            rc = hip_check("fp8a one-hot pre-decode launch");
+            if (rc) return rc;
+            const int64_t ctiles = ((a.M + 127) / 128) * ((a.N + OH_CT - 1) / OH_CT);
+            if (g_opt_oh_correct) oh_correct_kernel<<<(unsigned)ctiles, 256, 0, s>>>(a);
+            else if (hipMemsetAsync(a.ohd, 0, (size_t)a.M * a.N * sizeof(float), s) != hipSuccess)
+                return hip_check("fp8a correction slice fill");
+            rc = hip_check("fp8a one-hot correction launch");
+            if (rc) return rc;
+            const int tnw = oh_tnw(a.N);
+            const int64_t tm = 256 / tnw, tn = 64 * tnw;
+            const unsigned g = (unsigned)(((a.M + tm - 1) / tm) * ((a.N + tn - 1) / tn) * S);
+            if (tnw == 2) gemm_oh_kernel<2><<<g, 256, 0, s>>>(a);
+            else gemm_oh_kernel<1><<<g, 256, 0, s>>>(a);
+            rc = hip_check("fp8a one-hot gemm launch");
+            if (rc) return rc;
+            if (S > 1) {
+                const unsigned rb = (unsigned)std::min<int64_t>((a.M * a.N / 4 + 255) / 256 + 1, 8192);
+                splitk_reduce_kernel<<<rb, 256, 0, s>>>(a);
+                rc = hip_check("fp8a split-K reduce launch");
+                if (rc) return rc;
+            }
+            const unsigned ublocks = (unsigned)std::min<int64_t>(a.nur * a.nuc, 4096);
+            gemm_exact_kernel<<<ublocks, 256, 0, s>>>(a);
+            ++g_paths[PATH_OH];
+            return hip_check("fp8a gated exact gemm launch");
+        }
+    }
     // the matrix-core E4M3 kernel and the tile-table kernel (E3M4 / E2M5) need their pre-decoded
     // operands in the workspace (else gemm_fast_kernel runs); FP8A_NO_MX=1 forces the latter
     a.aw = nullptr;
@@ -1473,6 +1604,7 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     }
     if (a.fqin.mx && !a.aw)  // the caller (conv2d_impl) only fuses where the pre-decode runs
         return fail(FP8A_EINVAL, "internal: fused input quantization without the matrix-core path");
+    ++g_paths[!a.aw ? PATH_FAST : a.wfmt == 0 ? PATH_F8MX : a.wfmt == 1 ? PATH_TT : PATH_TT16];
     launch_fast(mode, a, s);
     rc = hip_check("fp8a fast gemm launch");
     if (rc) return rc;
@@ -1523,6 +1655,27 @@ extern "C" {
 const char *fp8a_version(void) { return "fp8approx gfx950 r1"; }
 
 const char *fp8a_last_error(void) { return g_err.c_str(); }
+
+int fp8a_path_stats(uint64_t *out, int reset) {
+    if (out == nullptr) return fail(FP8A_EINVAL, "null pointer");
+    for (int i = 0; i < PATH_N; ++i) out[i] = reset ? g_paths[i].exchange(0) : g_paths[i].load();
+    return FP8A_OK;
+}
+
+int fp8a_set_option(const char *name, int value) {
+    if (name == nullptr) return fail(FP8A_EINVAL, "null pointer");
+    if (strcmp(name, "one_hot") == 0) {
+        const int old = g_opt_one_hot ? 1 : 0;
+        g_opt_one_hot = value != 0;
+        return old;
+    }
+    if (strcmp(name, "oh_correct") == 0) {
+        const int old = g_opt_oh_correct ? 1 : 0;
+        g_opt_oh_correct = value != 0;
+        return old;
+    }
+    return fail(FP8A_EINVAL, std::string("unknown option ") + name);
+}
 
 int fp8a_fallback_stats(uint64_t *out, int reset) {
     if (out == nullptr) return fail(FP8A_EINVAL, "null pointer");
@@ -1575,7 +1728,7 @@ size_t fp8a_matmul_workspace_size(void) { return FLAG_BYTES; }
 
 size_t fp8a_matmul_workspace_size_mnk(int64_t M, int64_t N, int64_t K) {
     if (M <= 0 || N <= 0 || K <= 0) return FLAG_BYTES;
-    return gemm_workspace_bytes(M, N, K, M * ((K + BK - 1) / BK * BK));
+    return gemm_workspace_bytes(M, N, K, 0);
 }
 
 int fp8a_matmul(const float *A, int64_t lda, const float *B, int64_t sbk, int64_t sbn, float *C, int64_t ldc,
@@ -1929,7 +2082,7 @@ int fp8a_matmul_block(const float *A, int64_t lda, const float *B, int64_t sbk, 
         if (rc) return rc;
         const int64_t kpad = (K + BK - 1) / BK * BK, npad = (N + BN - 1) / BN * BN, a_words = M * kpad;
         const bool fused = f8_form(E, Mw, flags, mode) && !no_mx() && a_words < (1ll << 30) &&
-                           kpad * npad * 4 < (1ll << 32) && rest >= gemm_workspace_bytes(M, N, K, a_words);
+                           kpad * npad * 4 < (1ll << 32) && rest >= gemm_workspace_bytes(M, N, K, 0);
         if (fused) {
             a.fqin = fin;
             a.fq_bias = in_bias_out;

@@ -163,6 +163,21 @@ __device__ __forceinline__ uint32_t tt16_word_a(float x, uint32_t emnA, int bA, 
     return (h << 16) | h | (mc * TT16_RSH);
 }
 
+// gemm_oh_kernel's A code (wfmt 3, gemm_oh.h): u16, low byte the bf8 (e5m2) byte of sign(a) *
+// 2^(e_a - sA) -- the one-hot operand's nonzero byte --, high byte 8 m_a (its position); zeros 0.
+// ok = on the (3, bA) grid, e_a - sA inside bf8's normal exponents [-14, 15] and the correction's
+// fp8 conversion scale 2^(7 - bR - e_a) a normal E8M0 value.
+__device__ __forceinline__ uint32_t oh_code_a(float x, uint32_t emnA, int sA, int bR, bool &ok) {
+    float c;
+    uint32_t mc;
+    ok = stage_decode(x, 3, emnA, true, c, mc);
+    const uint32_t cb = __float_as_uint(c);
+    if ((cb & 0x7FFFFFFFu) == 0u) return 0u;
+    const int ea = (int)((cb >> 23) & 0xFFu) - 127, e = ea - sA + 15, se = 134 - bR - ea;
+    ok = ok && e >= 1 && e <= 30 && se >= 1 && se <= 254;
+    return ((cb >> 31) << 7) | ((uint32_t)min(max(e, 1), 30) << 2) | (mc << 11);
+}
+
 // A pre-pass, one (image | row) per blockIdx.y step.  conv: the group's channel slice of x
 // [Bn][Cin][H][W] (channels cbase..cbase+aw_c) -> words [Bn][aw_c][awH][awW], x at (awph, awpw)
 // inside a border of zero words (the padding the convolution reads, so the wave-independent
@@ -187,9 +202,21 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
     const int64_t rows = p.conv ? p.M / (p.Ho * p.Wo) : p.M, cols = p.conv ? p.aw_c * p.awH * p.awW : p.awld;
     auto word = [&](float v, bool &ok) {
         if (p.fqin.mx) v = fq_apply(v, fmx, fbias, p.fqin.M, p.fqin.S);
-        return p.wfmt == 2 ? tt16_word_a(v, emnA, bA, ok, win) : p.wfmt ? tt_word_a(v, p.Mw, emnA, ok) : xm_word_a(v, emnA, bR, ok);
+        return p.wfmt == 3 ? oh_code_a(v, emnA, 6 - bA, bR, ok) : p.wfmt == 2 ? tt16_word_a(v, emnA, bA, ok, win)
+               : p.wfmt ? tt_word_a(v, p.Mw, emnA, ok) : xm_word_a(v, emnA, bR, ok);
     };
     const uint32_t zw = p.wfmt ? 0u : XM_ZERO_WORD;  // the word of a zero (padding, columns >= K)
+    // stores: 32-bit words, or the one-hot path's 16-bit codes (wfmt 3) at the same indices
+    const bool u16 = p.wfmt == 3;
+    uint16_t *const out16 = reinterpret_cast<uint16_t *>(out);
+    auto st1 = [&](int64_t i, uint32_t w) {
+        if (u16) out16[i] = (uint16_t)w;
+        else out[i] = w;
+    };
+    auto st4 = [&](int64_t i, uint4 w) {  // i % 4 == 0
+        if (u16) *reinterpret_cast<uint2 *>(out16 + i) = make_uint2(w.x | (w.y << 16), w.z | (w.w << 16));
+        else *reinterpret_cast<uint4 *>(out + i) = w;
+    };
     if (p.conv && (p.awph | p.awpw)) {  // zero-bordered image (< 2^30 words, run_gemm): 32-bit index math
         // interior: four input elements per thread step along W, one 16-B load and one 16-B store
         // when W % 4 == 0 (run_gemm's word_image aligns the interior rows), else one element;
@@ -204,19 +231,19 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
         const uint32_t tstride = gridDim.x * blockDim.x, t0 = blockIdx.x * blockDim.x + threadIdx.x;
         for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) {
             const float *in = p.X + (r * p.Cin + p.cbase) * hw;
-            uint32_t *o = out + r * cols;
+            const int64_t o = r * cols;
             bool badr = false;
             for (uint32_t e = per * t0; e < nin; e += per * tstride) {
                 const uint32_t c = e / hwin, t = e - c * hwin, hy = t / uW, wx = t - hy * uW;
-                uint32_t *d = o + (c * Hp + hy + ph) * Wp + pw + wx;
+                const int64_t d = o + (c * Hp + hy + ph) * Wp + pw + wx;
                 if (v4) {
                     const float4 v = *reinterpret_cast<const float4 *>(in + e);
                     bool ok0 = true, ok1 = true, ok2 = true, ok3 = true;
-                    *reinterpret_cast<uint4 *>(d) = make_uint4(word(v.x, ok0), word(v.y, ok1), word(v.z, ok2), word(v.w, ok3));
+                    st4(d, make_uint4(word(v.x, ok0), word(v.y, ok1), word(v.z, ok2), word(v.w, ok3)));
                     badr |= !(ok0 && ok1 && ok2 && ok3);
                 } else {
                     bool ok = true;
-                    d[0] = word(in[e], ok);
+                    st1(d, word(in[e], ok));
                     badr |= !ok;
                 }
             }
@@ -234,7 +261,7 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
                     row = ph + rr;
                     col = sc < pw ? sc : uW + sc;
                 }
-                o[(c * Hp + row) * Wp + col] = zw;
+                st1(o + (c * Hp + row) * Wp + col, zw);
             }
         }
         if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, fb_bits(p, biasbad));
@@ -250,7 +277,7 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
     for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) {
         const float *in = p.conv ? p.X + (r * p.Cin + p.cbase) * hw : p.A + r * p.lda;
         const int64_t lim = p.conv ? cols : p.K;
-        uint32_t *o = out + r * cols;
+        const int64_t o = r * cols;
         bool badr = false;
         if (vec) {
             for (int64_t i = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x); i < cols;
@@ -262,13 +289,13 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
                     w = make_uint4(word(v.x, ok0), word(v.y, ok1), word(v.z, ok2), word(v.w, ok3));
                     badr |= !(ok0 && ok1 && ok2 && ok3);
                 }
-                *reinterpret_cast<uint4 *>(o + i) = w;
+                st4(o + i, w);
             }
         } else {
             for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cols;
                  i += (int64_t)gridDim.x * blockDim.x) {
                 bool ok = true;
-                o[i] = (i < lim) ? word(in[i], ok) : zw;
+                st1(o + i, (i < lim) ? word(in[i], ok) : zw);
                 badr |= !ok;
             }
         }

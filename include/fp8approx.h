@@ -66,6 +66,23 @@ const char *fp8a_last_error(void);
 int fp8a_fallback_stats(uint64_t *out, int reset);
 
 /*
+ * Launch paths the GEMM entry points took since load (host-side counters, no device sync), out[8]:
+ *   [0] E4M3 one-hot dense matrix-core GEMM + candidate correction (gemm_oh.h),
+ *   [1] E4M3 per-pair matrix-core kernel (gemm_f8mx.h), [2] gemm_tt_kernel (E3M4 / E2M5),
+ *   [3] gemm_tt16_kernel (E3M4), [4] gemm_fast_kernel (VALU tiled), [5] the exact kernel alone
+ *   (tensor-bias products), [6-7] reserved.  reset != 0 zeroes them after reading.
+ */
+int fp8a_path_stats(uint64_t *out, int reset);
+
+/*
+ * Runtime options (A/B measurements and tests): "one_hot" (default 1; the environment variable
+ * FP8A_NO_OH=1 sets 0 at load) -- whether E4M3 products take the one-hot path when the workspace
+ * holds its buffers, else gemm_f8mx_kernel.  Returns the previous value, or FP8A_EINVAL for an
+ * unknown name.  Not synchronised with launches in flight on other threads.
+ */
+int fp8a_set_option(const char *name, int value);
+
+/*
  * Element decomposition DEC of float_to_fpany_absint_torch (approx_matmul_whole_v9.py:233-291)
  * over a rows x cols matrix with row stride ld.  bias: device int32, bias_stride 0 = one bias
  * for all elements, 1 = one bias per ROW (per-channel weights).  flags: FP8A_TB selects the

@@ -41,6 +41,16 @@ def _units(M, N):
     return _a256(nur + nuc + nur * nuc)
 
 
+def _oh(M, N, K, conv_words=0, S=1):
+    """The one-hot E4M3 path's buffers (gemm_oh.h): partials + correction slice, u16 A codes, B
+    codes, block scales, candidate lists, count blocks (unsplit shapes: S = 1)."""
+    kpad, npad = (K + 31) // 32 * 32, (N + 127) // 128 * 128
+    nct = npad // 64
+    aw = conv_words if conv_words else M * kpad
+    return (_a256((S + 1) * M * N * 4) + _a256(aw * 2) + _a256(npad * kpad) + _a256(npad * kpad // 4) +
+            _a256(kpad * nct * 256) + _a256(kpad * nct * 72))
+
+
 def test_workspace_queries_are_host_only():
     L = _lib.load()
     assert L.fp8a_matmul_workspace_size() >= 4
@@ -50,8 +60,8 @@ def test_workspace_queries_are_host_only():
     # holds the matrix-core E4M3 path's pre-decoded operands (A words + B column pairs)
     Mr, N, K = 3211264, 64, 147
     kpad, npad = (K + 15) // 16 * 16, (N + 63) // 64 * 64
-    assert L.fp8a_matmul_workspace_size_mnk(Mr, N, K) == flag + _units(Mr, N) + _a256(Mr * kpad * 4) + \
-        _a256(kpad * npad // 2 * 8) + 16384
+    assert L.fp8a_matmul_workspace_size_mnk(Mr, N, K) == flag + _units(Mr, N) + max(
+        _a256(Mr * kpad * 4) + _a256(kpad * npad // 2 * 8) + 16384, _oh(Mr, N, K))
     Mr, N, K = 12544, 512, 4608
     assert L.fp8a_matmul_workspace_size_mnk(Mr, N, K) > flag + _a256(Mr * K * 4) + _a256(K * N // 2 * 8)  # split
     # depthwise (single output channel per group): the tensor-bias kernels need the flag word and
@@ -61,9 +71,11 @@ def test_workspace_queries_are_host_only():
     # border (ph rows above / below; W % 4 == 0: a 4-word left margin and rows rounded up to 4
     # words, here 8 + 4 + 1 -> 16), + B column pairs + the table image (unsplit here)
     n2 = L.fp8a_conv2d_workspace_size(2, 3, 8, 8, 4, 3, 3, 1, 1, 1, 1, 1, 1, 1)
-    assert n2 == flag + _units(2 * 8 * 8, 4) + _a256(2 * 3 * 10 * 16 * 4) + _a256(32 * 64 // 2 * 8) + 16384
+    assert n2 == flag + _units(2 * 8 * 8, 4) + max(_a256(2 * 3 * 10 * 16 * 4) + _a256(32 * 64 // 2 * 8) + 16384,
+                                                   _oh(2 * 8 * 8, 4, 27, 2 * 3 * 10 * 16))
     n3 = L.fp8a_conv2d_workspace_size(2, 3, 7, 7, 4, 3, 3, 1, 1, 1, 1, 1, 1, 1)  # W % 4 != 0: 9 x 9
-    assert n3 == flag + _units(2 * 7 * 7, 4) + _a256(2 * 3 * 9 * 9 * 4) + _a256(32 * 64 // 2 * 8) + 16384
+    assert n3 == flag + _units(2 * 7 * 7, 4) + max(_a256(2 * 3 * 9 * 9 * 4) + _a256(32 * 64 // 2 * 8) + 16384,
+                                                   _oh(2 * 7 * 7, 4, 27, 2 * 3 * 9 * 9))
     assert L.fp8a_conv2d_workspace_size(256, 3, 224, 224, 4, 7, 7, 2, 2, 3, 3, 1, 1, 1) >= flag + 256 * 3 * 230 * 230 * 4
 
 

@@ -32,6 +32,24 @@ def _native():
     _lib.load()
 
 
+@pytest.fixture(params=["one_hot", "f8mx"])
+def path(request):
+    """Both E4M3 paths: the one-hot dense GEMM + correction (gemm_oh.h, the default) and the
+    per-pair matrix-core kernel (gemm_f8mx.h); the launch's path is read back from the library's
+    path counters."""
+    from fp8_quantization_amd import _lib
+    old = _lib.set_option("one_hot", request.param == "one_hot")
+    _lib.path_stats(reset=True)
+    yield request.param
+    _lib.set_option("one_hot", old)
+
+
+def _ran(path):
+    from fp8_quantization_amd import _lib
+    st = _lib.path_stats(reset=True)
+    assert st[path] >= 1 and sum(v for k, v in st.items() if k != path) == 0, st
+
+
 def _all_codes(bias):
     """The 256 E4M3 values of the given bias (both zeros included)."""
     e = np.repeat(np.arange(16), 8)
@@ -73,7 +91,7 @@ def _terms_equal(got, ref):
 
 @pytest.mark.parametrize("table", ["nocomp", "comp", "none"])
 @pytest.mark.parametrize("biases", [(12, 12, 8), (10, 13, 7), (9, 9, 2), (12, 14, 0), (8, 8, -14), (20, 18, 22)])
-def test_every_code_pair_bitexact(biases, table):
+def test_every_code_pair_bitexact(biases, table, path):
     bA, bB, bR = biases
     A = _all_codes(bA).reshape(-1, 1)
     B = _all_codes(bB).reshape(1, -1)
@@ -84,21 +102,26 @@ def test_every_code_pair_bitexact(biases, table):
     _terms_equal(C, ref)
     # every term fits the e4m3 range of these biases: the fast form ran, nothing fell back
     assert flag == 0, "fallback flag raised: the fast form did not produce these terms"
+    _ran(path)
 
 
-def test_terms_beyond_e4m3_range_fall_back():
+def test_terms_beyond_e4m3_range(path):
+    """Products above the result grid's top binade (Q_R lets the exponent run past max_norm, F6):
+    the per-pair kernel's e4m3 conversion cannot hold them, so it flags and the exact kernel
+    reruns; the one-hot path's dense terms are exact at any height -- no fallback."""
     bA, bB, bR = 12, 12, 14  # products up to ~2^7 * 3.5 exceed the result grid's top binade
     A = _all_codes(bA).reshape(-1, 1)
     B = _all_codes(bB).reshape(1, -1)
     tab = gio.load("g2_matmul.npz")["E4M3_table_nocomp"]
     fl = orc.flags_of(approx=True, s2n=True, qbma=True)
     C, flag = _matmul_raw(A, B, bA, bB, bR, tab, fl)
-    assert flag != 0
+    assert (flag != 0) == (path == "f8mx"), flag
     _terms_equal(C, orc.terms(A, B, 4, 3, bA, bB, bR, tab, fl)[:, 0, :])
+    _ran(path)
 
 
 @pytest.mark.parametrize("shape", [(256, 576, 64), (130, 300, 129), (1, 4608, 7), (512, 1152, 256)])
-def test_sums_within_bar(shape):
+def test_sums_within_bar(shape, path):
     Mr, K, N = shape
     rng = np.random.default_rng(Mr + K + N)
     bA, bR = 9, 3  # no product reaches the result grid's top binade (bR <= bA + min bB - 16)
@@ -117,6 +140,7 @@ def test_sums_within_bar(shape):
     Cref, S = orc.matmul(A, B, 4, 3, bA, bB, bR, tab, fl, with_abs=True)
     assert flag == 0
     assert np.all(np.abs(C.astype(np.float64) - Cref) <= gio.sum_tolerance(S.astype(np.float64)))
+    _ran(path)
 
 
 def _sum_operands(Mr, K, N, seed):
@@ -134,8 +158,10 @@ def _sum_operands(Mr, K, N, seed):
 
 
 @pytest.mark.parametrize("case", ["term_out_of_range", "off_grid_a", "off_grid_b"])
-def test_fallback_recomputes_only_marked_units(case):
+def test_fallback_recomputes_only_marked_units(case, path):
     from fp8_quantization_amd import _lib
+    if case == "term_out_of_range" and path == "one_hot":
+        pytest.skip("the one-hot path has no e4m3 range limit (test_terms_beyond_e4m3_range)")
     Mr, K, N = 520, 600, 200  # 9 x 4 output units, split-K shape
     A, B, bA, bB, bR = _sum_operands(Mr, K, N, 17)
     tab = gio.load("g2_matmul.npz")["E4M3_table_nocomp"]
@@ -159,7 +185,7 @@ def test_fallback_recomputes_only_marked_units(case):
     assert flag2 & 1 and not flag2 & 32, flag2  # some units, not all
     assert st["exact_launches"] == 1
     ur, uc = np.arange(Mr) // 64, np.arange(N) // 64
-    if case == "term_out_of_range":  # the 128-row tile holding (r, n)
+    if case == "term_out_of_range":  # the 128-row tile holding (r, n) (gemm_f8mx_kernel's tile)
         marked = ((ur[:, None] // 2) == (r // 128)) & (uc[None, :] == n // 64)
     elif case == "off_grid_a":
         marked = (ur[:, None] == r // 64) & (uc[None, :] >= 0)
