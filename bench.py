@@ -259,6 +259,7 @@ def run(args, dev, rank=0, world=1):
         am._PROFILE = [] if cuda else None
         if cuda:
             fa._lib.fallback_stats(reset=True)  # (synchronises: outside the timed region)
+            fa._lib.path_stats(reset=True)
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step()
@@ -270,6 +271,7 @@ def run(args, dev, rank=0, world=1):
     # how many launches / 64x64 output units of the timed steps left the fast path (a regression
     # there would otherwise be invisible in the line)
     fallback = fa._lib.fallback_stats() if cuda else None
+    paths = {k: v for k, v in fa._lib.path_stats().items() if v} if cuda else None
 
     op_ms = sum(s.elapsed_time(e) for (s, e, _) in prof)
     op_macs = sum(m for (_, _, m) in prof)
@@ -337,6 +339,9 @@ def run(args, dev, rank=0, world=1):
                                         "recomputed exact_units 64x64 output units; f32_reruns = E3M4 launches "
                                         "rerun in the f32 tile-table form; tb_launches = depthwise launches "
                                         "recomputed by the literal restatement")
+        if paths is not None:
+            res["gemm_paths"] = dict(paths, note="timed steps only: approx GEMM launches per kernel path "
+                                                 "(fp8a_path_stats; one_hot = opt-in E4M3 one-hot path)")
         if world == 1 and not args.no_cpu_baseline and (args.expo_width, args.mant_width) == (4, 3):
             res["cpu_baseline"] = cpu_baseline(shapes, get_error_table_NN(4, 3, args.with_comp, 3), args.cpu_columns)
             res["speedup_vs_cpu_baseline"] = res["value"] / res["cpu_baseline"]["value"]

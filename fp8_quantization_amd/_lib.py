@@ -15,7 +15,7 @@ APPROX, S2N, QBMA, GCLIP, TB = 1, 2, 4, 8, 16
 V5, OFUF, OF_OPT, UF_OPT = 32, 64, 128, 256  # v5 integer-adder model (include/fp8approx.h)
 OK, EINVAL, EFORMAT, EHIP = 0, -1, -2, -3
 
-SYMBOLS = ("fp8a_version", "fp8a_last_error", "fp8a_fallback_stats", "fp8a_path_stats", "fp8a_set_option", "fp8a_decompose", "fp8a_quant", "fp8a_matmul_workspace_size",
+SYMBOLS = ("fp8a_version", "fp8a_last_error", "fp8a_fallback_stats", "fp8a_path_stats", "fp8a_set_option", "fp8a_debug_stats", "fp8a_decompose", "fp8a_quant", "fp8a_matmul_workspace_size",
            "fp8a_matmul_workspace_size_mnk", "fp8a_matmul", "fp8a_terms", "fp8a_conv2d_workspace_size", "fp8a_conv2d",
            "fp8a_conv2d_bn_act", "fp8a_conv2d_qin_workspace_size", "fp8a_conv2d_qin",
            "fp8a_conv2d_block_workspace_size", "fp8a_conv2d_block", "fp8a_max_pool2d", "fp8a_im2col",
@@ -47,6 +47,7 @@ def load():
         "fp8a_fallback_stats": ([P, I], I),
         "fp8a_path_stats": ([P, I], I),
         "fp8a_set_option": ([ctypes.c_char_p, I], I),
+        "fp8a_debug_stats": ([P, I], I),
         "fp8a_decompose": ([P, I64, I64, I64, I, I, P, I64, U, P, P, P], I),
         "fp8a_quant": ([P, I64, I, I, P, U, P, P], I),
         "fp8a_matmul_workspace_size": ([], SZ),
@@ -140,3 +141,12 @@ def set_option(name, value):
     if rc < 0:
         check(rc, "fp8a_set_option")
     return rc
+
+
+def debug_stats(reset=False):
+    """fp8a_debug_stats (counted while set_option("oh_stats", 1)): the one-hot path's candidate
+    entries, excluded weights, nonempty / examined (A element, 64-column tile) segments."""
+    L = load()
+    out = (ctypes.c_uint64 * 4)()
+    check(L.fp8a_debug_stats(ctypes.cast(out, ctypes.c_void_p), 1 if reset else 0), "fp8a_debug_stats")
+    return dict(entries=int(out[0]), excluded=int(out[1]), segments_nonempty=int(out[2]), segments=int(out[3]))

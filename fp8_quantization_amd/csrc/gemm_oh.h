@@ -33,6 +33,12 @@
 // only by order (1e-5 sum|term| bar).  About 1-3 % of the nonzero products are candidates on
 // the benchmark networks (profiles/unsafe_stats_r02*.json).
 
+// diagnostics switch (fp8a_set_option("oh_stats", 1)): the kernels count into g_ohstat
+#ifndef FP8A_OH_STATS
+#define FP8A_OH_STATS 1
+#endif
+#define g_opt_stats_dev (FP8A_OH_STATS && p.ohstats)
+
 constexpr int OH_KC = 32;               // k per staged chunk of gemm_oh_kernel (K' = 256: two MFMA K-steps)
 constexpr int OH_BRS = OH_KC * 8 + 16;  // B' LDS row (column n) stride, bytes
 constexpr int OH_ARS = OH_KC + 4;       // A code LDS row stride, u16 (72 B: 8-B aligned staging rows; the 4-B
@@ -167,6 +173,11 @@ __global__ __launch_bounds__(64) void oh_decode_b(const GemmArgs p, int64_t kpad
     }
     // a count table wider than 64 exponent levels (weights spanning > 62 binades in one k): the
     // launch falls back (never seen on the grid of one FP8 format)
+    if (g_opt_stats_dev) {
+        const int nx = __popcll(__ballot(excl[0])) + __popcll(__ballot(excl[1])) + __popcll(__ballot(excl[2])) +
+                       __popcll(__ballot(excl[3]));
+        if (lane == 0 && nx) atomicAdd(&g_ohstat[1], (unsigned long long)nx);
+    }
     if (__any(bad ? 1 : 0) && lane == 0) atomicOr(p.flag, fb_bits(p, biasbad));
     if (__any(wide ? 1 : 0) && lane == 0) atomicOr(p.flag, FB_ANY | FB_ALL);
 }
@@ -508,6 +519,16 @@ __global__ __launch_bounds__(256, 2) void oh_correct_kernel(const GemmArgs p) {
         }
         sm.lsum[wv][lane] = incl - v;  // exclusive prefix of position `lane`
         const uint32_t T = __shfl(incl, 63);
+        if (g_opt_stats_dev) {
+            uint32_t nzs = 0;
+            for (int s2 = 0; s2 < OC_KC / 2; ++s2) nzs += (seg[(lane & 31) * OC_KC + sk0 + s2] >> 16) != 0u;
+            for (int o = 32; o >= 1; o >>= 1) nzs += __shfl_xor(nzs, o);
+            if (lane == 0) {
+                atomicAdd(&g_ohstat[0], (unsigned long long)T);
+                atomicAdd(&g_ohstat[2], (unsigned long long)nzs);
+                atomicAdd(&g_ohstat[3], (unsigned long long)(32 * OC_KC));
+            }
+        }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

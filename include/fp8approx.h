@@ -75,12 +75,23 @@ int fp8a_fallback_stats(uint64_t *out, int reset);
 int fp8a_path_stats(uint64_t *out, int reset);
 
 /*
- * Runtime options (A/B measurements and tests): "one_hot" (default 1; the environment variable
- * FP8A_NO_OH=1 sets 0 at load) -- whether E4M3 products take the one-hot path when the workspace
- * holds its buffers, else gemm_f8mx_kernel.  Returns the previous value, or FP8A_EINVAL for an
- * unknown name.  Not synchronised with launches in flight on other threads.
+ * Runtime options (A/B measurements, tests, diagnostics): "one_hot" (default 0; the environment
+ * variable FP8A_ONE_HOT=1 sets 1 at load) -- whether E4M3 products take the one-hot path when the
+ * workspace holds its buffers, else gemm_f8mx_kernel (same results; the one-hot path is slower on
+ * the benchmark network); "oh_correct" (default 1; 0 leaves the
+ * one-hot path's candidate pairs uncorrected: NOT the reference's result, timing ablations only);
+ * "oh_stats" (default 0) -- count fp8a_debug_stats.  Returns the previous value, or FP8A_EINVAL
+ * for an unknown name.  Not synchronised with launches in flight on other threads.
  */
 int fp8a_set_option(const char *name, int value);
+
+/*
+ * Diagnostic counters of the E4M3 one-hot path, counted only while the option "oh_stats" is 1
+ * (out[4]): [0] candidate entries the correction kernel processed, [1] weights excluded from
+ * their MX block's window, [2] (A element, 64-column tile) segments holding a candidate, [3] (A
+ * element, 64-column tile) segments examined.  Synchronises the device; reset != 0 zeroes them.
+ */
+int fp8a_debug_stats(uint64_t *out, int reset);
 
 /*
  * Element decomposition DEC of float_to_fpany_absint_torch (approx_matmul_whole_v9.py:233-291)
