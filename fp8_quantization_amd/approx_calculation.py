@@ -26,10 +26,17 @@ from .approx_ops import (_res_quant_params, approx_conv2d, approx_matmul, approx
                          make_flags, make_flags_v5, qamaa_conv2d, qamaa_matmul)
 from .error_tables import get_comp_table_NN_v5, get_error_table_NN
 from .quantization.hijacker import QuantizationHijacker
+from .quantization.quantization_manager import QuantizationManager
+from .quantization.base_quantized_classes import QuantizedActivation, QuantizedModule
+from .quantization.hijacker import activations_set
 from .quantization.quantized_folded_bn import BNFusedHijacker
 
+# (the hijacker bases too: the reference's replace_operations_with_approx_ops takes them from its
+# `from approx.approx_calculation import *`, INTEGRATION.md §3 Option A)
 __all__ = ["QCustomBNConv2dTorch", "QCustomLinearTorch", "QCustomConv2dTorch", "ApproxOpMixin",
-           "ApproxConv2dMixin", "ApproxLinearMixin", "ExactConv2dMixin", "bind_operator_classes"]
+           "ApproxConv2dMixin", "ApproxLinearMixin", "ExactConv2dMixin", "bind_operator_classes",
+           "QuantizationHijacker", "BNFusedHijacker", "QuantizationManager",
+           "QuantizedActivation", "QuantizedModule", "activations_set"]
 
 
 class ApproxOpMixin:
@@ -73,10 +80,19 @@ class ApproxOpMixin:
                 return approx_matmul(x, y, E, M, x_bias, y_bias, res_bias, table, flags=flags)
             if self.quantize_after_mult_and_add:  # approx_calculation.py:787-795
                 return qamaa_matmul(x, y, *self._qamaa_params())
-            return x @ y
+            return self._exact_product(x, y, M)
         if self.approx_flag:  # single column: biases stay tensors -> tensor-bias semantics (F5)
             tb = 0 if flags & _lib.V5 else _lib.TB  # (v5 never had tensor-bias semantics)
             return approx_matmul(x, y, E, M, x_bias, y_bias, res_bias, table, flags=flags | tb)
+        return self._exact_product(x, y, M)
+
+    @staticmethod
+    def _exact_product(x, y, M):
+        """The non-approx ``x @ y`` (approx_calculation.py:797, 811): on the GPU the block-scaled
+        fp8 matrix-core product for FP8-grid operands (E4M3 / E5M2), else the fp32 contraction."""
+        fmt = dense_format(M)
+        if x.is_cuda and fmt is not None:
+            return dense_matmul(x, y, fmt)
         return x @ y
 
     def multiply(self, x, y):
@@ -142,7 +158,12 @@ class ApproxConv2dMixin(ApproxOpMixin):
             out = qamaa_conv2d(x.detach(), weight.detach(), *self._qamaa_params(), stride=self.stride,
                                padding=self.padding, dilation=self.dilation, groups=self.groups)
         else:  # exact product (also qamaa's single-column groups, approx_calculation.py:810-811)
-            out = F.conv2d(x.detach(), weight.detach(), None, self.stride, self.padding, self.dilation, self.groups)
+            fmt = dense_format(M)
+            if x.is_cuda and fmt is not None and self.groups == 1:
+                out = dense_conv2d(x.detach(), weight.detach(), fmt, self.stride, self.padding, self.dilation)
+            else:  # grouped (depthwise: one-column products) / wide-mantissa formats: the fp32 contraction
+                out = F.conv2d(x.detach(), weight.detach(), None, self.stride, self.padding, self.dilation,
+                               self.groups)
         if bias is not None:
             out += bias.view(1, -1, 1, 1)
         return out
