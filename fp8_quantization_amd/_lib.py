@@ -14,13 +14,15 @@ LIB_PATH = os.environ.get("FP8A_LIB_PATH") or os.path.join(HERE, "lib", "libfp8a
 APPROX, S2N, QBMA, GCLIP, TB = 1, 2, 4, 8, 16
 V5, OFUF, OF_OPT, UF_OPT = 32, 64, 128, 256  # v5 integer-adder model (include/fp8approx.h)
 OK, EINVAL, EFORMAT, EHIP = 0, -1, -2, -3
+DENSE_E4M3, DENSE_E5M2 = 0, 1  # fp8a_dense_* operand formats
 
 SYMBOLS = ("fp8a_version", "fp8a_last_error", "fp8a_fallback_stats", "fp8a_path_stats", "fp8a_set_option", "fp8a_debug_stats", "fp8a_decompose", "fp8a_quant", "fp8a_matmul_workspace_size",
            "fp8a_matmul_workspace_size_mnk", "fp8a_matmul", "fp8a_terms", "fp8a_conv2d_workspace_size", "fp8a_conv2d",
            "fp8a_conv2d_bn_act", "fp8a_conv2d_qin_workspace_size", "fp8a_conv2d_qin",
            "fp8a_conv2d_block_workspace_size", "fp8a_conv2d_block", "fp8a_max_pool2d", "fp8a_im2col",
            "fp8a_fp8_quantize", "fp8a_matmul_qamaa", "fp8a_conv2d_qamaa", "fp8a_matmul_block_workspace_size",
-           "fp8a_matmul_block")
+           "fp8a_matmul_block", "fp8a_dense_matmul_workspace_size", "fp8a_dense_matmul",
+           "fp8a_dense_conv2d_workspace_size", "fp8a_dense_conv2d", "fp8a_dense_stats", "fp8a_clock_stats")
 
 _lib = None
 
@@ -73,6 +75,12 @@ def load():
         "fp8a_matmul_block_workspace_size": ([I64, I64, I64], SZ),
         "fp8a_matmul_block": ([P, I64, P, I64, I64, P, I64, I64, I64, I64, I, I, P, P, I64, P, P, U, P, I, F, F, P, I, I,
                                I, P, P, P, I, F, F, P, I, I, I, P, P, P, SZ, P], I),
+        "fp8a_dense_matmul_workspace_size": ([I64, I64, I64], SZ),
+        "fp8a_dense_matmul": ([P, I64, I64, P, I64, I64, P, I64, I64, I64, I64, I, P, SZ, P], I),
+        "fp8a_dense_conv2d_workspace_size": ([I64, I64, I64, I64, I64, I, I, I, I, I, I, I, I], SZ),
+        "fp8a_dense_conv2d": ([P, P, P, I64, I64, I64, I64, I64, I, I, I, I, I, I, I, I, I, P, SZ, P], I),
+        "fp8a_dense_stats": ([P, I], I),
+        "fp8a_clock_stats": ([P, I], I),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -124,7 +132,7 @@ def fallback_stats(reset=False):
     return dict(exact_launches=int(out[0]), exact_units=int(out[1]), f32_reruns=int(out[2]), tb_launches=int(out[3]))
 
 
-PATHS = ("one_hot", "f8mx", "tt", "tt16", "fast", "exact", "reserved6", "reserved7")
+PATHS = ("one_hot", "f8mx", "tt", "tt16", "fast", "exact", "dense", "reserved7")
 
 
 def path_stats(reset=False):
@@ -150,3 +158,21 @@ def debug_stats(reset=False):
     out = (ctypes.c_uint64 * 4)()
     check(L.fp8a_debug_stats(ctypes.cast(out, ctypes.c_void_p), 1 if reset else 0), "fp8a_debug_stats")
     return dict(entries=int(out[0]), excluded=int(out[1]), segments_nonempty=int(out[2]), segments=int(out[3]))
+
+
+def dense_stats(reset=False):
+    """fp8a_dense_stats: dict(fp32_launches, fp32_units) -- dense exact-product launches with
+    64 x 64 units recomputed in fp32, and those units (synchronises the device)."""
+    L = load()
+    out = (ctypes.c_uint64 * 2)()
+    check(L.fp8a_dense_stats(ctypes.cast(out, ctypes.c_void_p), 1 if reset else 0), "fp8a_dense_stats")
+    return dict(fp32_launches=int(out[0]), fp32_units=int(out[1]))
+
+
+def clock_stats(reset=False):
+    """fp8a_clock_stats (a -DFP8A_CLOCK_STAMP=1 build): dict(memtime, realtime, workgroups, ghz)."""
+    L = load()
+    out = (ctypes.c_uint64 * 3)()
+    check(L.fp8a_clock_stats(ctypes.cast(out, ctypes.c_void_p), 1 if reset else 0), "fp8a_clock_stats")
+    t, r, n = int(out[0]), int(out[1]), int(out[2])
+    return dict(memtime=t, realtime=r, workgroups=n, ghz=(t / r * 0.1) if r else None)

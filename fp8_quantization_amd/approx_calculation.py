@@ -23,7 +23,8 @@ from torch import nn
 
 from . import _lib
 from .approx_ops import (_res_quant_params, approx_conv2d, approx_matmul, approx_matmul_block, bias_epilogue,
-                         make_flags, make_flags_v5, qamaa_conv2d, qamaa_matmul)
+                         dense_conv2d, dense_format, dense_matmul, make_flags, make_flags_v5, qamaa_conv2d,
+                         qamaa_matmul)
 from .error_tables import get_comp_table_NN_v5, get_error_table_NN
 from .quantization.hijacker import QuantizationHijacker
 from .quantization.quantization_manager import QuantizationManager

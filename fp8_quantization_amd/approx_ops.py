@@ -22,7 +22,8 @@ from .error_tables import get_error_table_NN  # noqa: F401  (re-exported, v9:555
 
 __all__ = ["custom_matmul_vectorize", "approx_matmul", "approx_matmul_block", "approx_terms", "approx_conv2d", "qamaa_matmul", "qamaa_conv2d",
            "quant_to_fp_any_vectorize_torch", "float_to_fpany_absint_torch", "get_error_table_NN",
-           "make_flags", "make_flags_v5", "fp8_fake_quantize", "bn_act_epilogue"]
+           "make_flags", "make_flags_v5", "fp8_fake_quantize", "bn_act_epilogue", "dense_format", "dense_matmul",
+           "dense_conv2d"]
 
 
 def make_flags(with_approx=True, with_s2nn2s_opt=False, quant_btw_mult_accu=True, golden_clip_OF=False,
@@ -589,6 +590,90 @@ def qamaa_conv2d(x, w, maxval, n_bits, mantissa_bits, sign_bits=1, stride=(1, 1)
                              _lib.dev_ptr(mx), int(n_bits), int(mantissa_bits), int(sign_bits),
                              _lib.stream_ptr(x.device))
     _lib.check(rc, "fp8a_conv2d_qamaa")
+    return y
+
+
+# ------------------------------------------------------------------- the exact product (dense)
+def dense_format(mant_width):
+    """fp8a_dense operand format for values on a grid with ``mant_width`` mantissa bits: e4m3 for
+    3 (E4M3), e5m2 for fewer (E5M2: the wider exponent range); None for wider mantissas (E3M4,
+    E2M5: not exact in OCP fp8 -- their exact product stays the fp32 torch contraction)."""
+    if mant_width == 3:
+        return _lib.DENSE_E4M3
+    if 0 < mant_width <= 2:
+        return _lib.DENSE_E5M2
+    return None
+
+
+@torch.library.custom_op("fp8approx::dense_matmul", mutates_args=())
+def _dense_matmul_op(A: torch.Tensor, B: torch.Tensor, fmt: int) -> torch.Tensor:
+    L = _lib.load()
+    dev = A.device
+    Mr, K = A.shape
+    N = B.shape[1]
+    C = torch.empty((Mr, N), dtype=torch.float32, device=dev)
+    ws = _workspace(dev, L.fp8a_dense_matmul_workspace_size(Mr, N, K))
+    rc = L.fp8a_dense_matmul(_lib.dev_ptr(A), A.stride(0), A.stride(1), _lib.dev_ptr(B), B.stride(0), B.stride(1),
+                             _lib.dev_ptr(C), N, Mr, N, K, int(fmt), _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(dev))
+    _lib.check(rc, "fp8a_dense_matmul")
+    return C
+
+
+@_dense_matmul_op.register_fake
+def _(A, B, fmt):
+    return A.new_empty((A.shape[0], B.shape[1]), dtype=torch.float32)
+
+
+def dense_matmul(A, B, fmt):
+    """A [M, K] @ B [K, N] (fp32 values on an FP8 grid, any strides) on the block-scaled fp8
+    matrix core: the reference's exact branch ``x @ y`` (approx_calculation.py:797, 811), equal to
+    the fp32 product up to summation order (off-grid values: their units in fp32)."""
+    if A.dim() != 2 or B.dim() != 2 or A.shape[1] != B.shape[0]:
+        raise AssertionError(f"dense_matmul: shape mismatch {tuple(A.shape)} @ {tuple(B.shape)}")
+    A, B = _as_f32(A), _as_f32(B)
+    ev = _prof_start()
+    C = _dense_matmul_op(A, B, int(fmt))
+    _prof_end(ev, A.shape[0] * A.shape[1] * B.shape[1])
+    return C
+
+
+@torch.library.custom_op("fp8approx::dense_conv2d", mutates_args=())
+def _dense_conv2d_op(x: torch.Tensor, w: torch.Tensor, fmt: int, stride: list[int], padding: list[int],
+                     dilation: list[int]) -> torch.Tensor:
+    L = _lib.load()
+    Bn, Cin, H, W = x.shape
+    Cout, _, kh, kw = w.shape
+    Ho = (H + 2 * padding[0] - dilation[0] * (kh - 1) - 1) // stride[0] + 1
+    Wo = (W + 2 * padding[1] - dilation[1] * (kw - 1) - 1) // stride[1] + 1
+    y = torch.empty((Bn, Cout, Ho, Wo), dtype=torch.float32, device=x.device)
+    geo = (Bn, Cin, H, W, Cout, kh, kw, stride[0], stride[1], padding[0], padding[1], dilation[0], dilation[1])
+    ws = _workspace(x.device, L.fp8a_dense_conv2d_workspace_size(*geo))
+    rc = L.fp8a_dense_conv2d(_lib.dev_ptr(x), _lib.dev_ptr(w), _lib.dev_ptr(y), *geo, int(fmt), _lib.dev_ptr(ws),
+                             ws.numel(), _lib.stream_ptr(x.device))
+    _lib.check(rc, "fp8a_dense_conv2d")
+    return y
+
+
+@_dense_conv2d_op.register_fake
+def _(x, w, fmt, stride, padding, dilation):
+    Bn, _, H, W = x.shape
+    Cout, _, kh, kw = w.shape
+    Ho = (H + 2 * padding[0] - dilation[0] * (kh - 1) - 1) // stride[0] + 1
+    Wo = (W + 2 * padding[1] - dilation[1] * (kw - 1) - 1) // stride[1] + 1
+    return x.new_empty((Bn, Cout, Ho, Wo), dtype=torch.float32)
+
+
+def dense_conv2d(x, w, fmt, stride=(1, 1), padding=(0, 0), dilation=(1, 1)):
+    """Exact-product convolution (groups = 1) on the block-scaled fp8 matrix core: the reference's
+    im2col + ``x @ y`` (approx_calculation.py:811) without the im2col image."""
+    if x.dim() != 4 or w.dim() != 4 or x.shape[1] != w.shape[1]:
+        raise AssertionError(f"dense_conv2d: shape mismatch {tuple(x.shape)} * {tuple(w.shape)}")
+    x = _as_f32(x).contiguous()
+    w = _as_f32(w).contiguous()
+    ev = _prof_start()
+    y = _dense_conv2d_op(x, w, int(fmt), [int(v) for v in stride], [int(v) for v in padding],
+                         [int(v) for v in dilation])
+    _prof_end(ev, y.shape[0] * y.shape[2] * y.shape[3] * w.shape[0] * w.shape[1] * w.shape[2] * w.shape[3])
     return y
 
 

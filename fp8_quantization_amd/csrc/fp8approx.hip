@@ -214,6 +214,27 @@ __device__ __forceinline__ uint32_t fb_bits(const GemmArgs &p, bool all = false)
 // (gemm_tt16_kernel's f16 window left), [3] tensor-bias launches recomputed by
 // conv_tb_direct_kernel.  Read with fp8a_fallback_stats (include/fp8approx.h).
 __device__ unsigned long long g_fallback[4];
+// In-kernel clock of gemm_f8mx_kernel (diagnostic build only: -DFP8A_CLOCK_STAMP=1, tools/clock_probe.py):
+// thread 0 of every workgroup adds its s_memtime and s_memrealtime (100 MHz) deltas; the clock the
+// chip held = sum dt / sum dr x 100 MHz (MI355X_MICROARCH.md, DVFS give-back item 6).  Nothing
+// else reads g_clk; the product build compiles no stamp.
+#ifndef FP8A_CLOCK_STAMP
+#define FP8A_CLOCK_STAMP 0
+#endif
+__device__ unsigned long long g_clk[3];
+#if FP8A_CLOCK_STAMP
+#define FP8A_CLK_BEGIN const uint64_t clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
+#define FP8A_CLK_END                                                                                   \
+    if (threadIdx.x == 0) {                                                                            \
+        const uint64_t clk_t1 = __builtin_amdgcn_s_memtime(), clk_r1 = __builtin_amdgcn_s_memrealtime(); \
+        atomicAdd(&g_clk[0], (unsigned long long)(clk_t1 - clk_t0));                                   \
+        atomicAdd(&g_clk[1], (unsigned long long)(clk_r1 - clk_r0));                                   \
+        atomicAdd(&g_clk[2], 1ull);                                                                    \
+    }
+#else
+#define FP8A_CLK_BEGIN
+#define FP8A_CLK_END
+#endif
 // Diagnostic counters of the one-hot path (fp8a_debug_stats): [0] candidate entries the correction
 // kernel processed, [1] excluded weights (outside their MX block's window), [2] (A element, 64-column
 // tile) segments with at least one candidate, [3] A elements x 64-column tiles examined.
@@ -755,6 +776,7 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
 #include "gemm_tt.h"
 #include "gemm_tt16.h"
 #include "gemm_oh.h"
+#include "gemm_dense.h"
 
 // Sums the split-K partials in split order (deterministic) and writes the output mapping.
 // Partial layout: row-major [M][N] (rowmajor output) or [img][N][hw] (NCHW output).
@@ -1243,7 +1265,8 @@ static int check_format(int E, int Mw) {
 constexpr size_t FLAG_BYTES = 256;  // workspace prefix holding the off-grid flag word
 
 // Launch paths taken by run_gemm since load (fp8a_path_stats): host-side counters.
-enum { PATH_OH = 0, PATH_F8MX = 1, PATH_TT = 2, PATH_TT16 = 3, PATH_FAST = 4, PATH_EXACT = 5, PATH_N = 8 };
+enum { PATH_OH = 0, PATH_F8MX = 1, PATH_TT = 2, PATH_TT16 = 3, PATH_FAST = 4, PATH_EXACT = 5, PATH_DENSE = 6,
+       PATH_N = 8 };
 static std::atomic<uint64_t> g_paths[PATH_N];
 // Options (fp8a_set_option): "one_hot" -- the E4M3 one-hot path (gemm_oh.h), default off: its
 // dense GEMM beats gemm_f8mx_kernel by 1.6x, but the 1.1% candidate pairs of the benchmark network
@@ -1654,6 +1677,71 @@ static int run_qamaa(GemmArgs &a, hipStream_t s) {
     return FP8A_OK;
 }
 
+// ------------------------------------------------------------------ the exact product (gemm_dense.h)
+static inline int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+static inline size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+static size_t dense_ws_bytes(int64_t M, int64_t N, int64_t K) {
+    const int64_t mpad = round_up(std::max<int64_t>(M, 1), DN_T), npad = round_up(std::max<int64_t>(N, 1), DN_T);
+    const int64_t kpad = round_up(std::max<int64_t>(K, 1), 32);
+    return al256((size_t)(mpad / DN_U + npad / DN_U)) + al256((size_t)(mpad * kpad)) + al256((size_t)(mpad * kpad / 32)) +
+           al256((size_t)(npad * kpad)) + al256((size_t)(npad * kpad / 32));
+}
+
+static int run_dense(DenseArgs a, void *ws, size_t wsb, hipStream_t s) {
+    if (a.M < 0 || a.N < 0 || a.K < 0) return fail(FP8A_EINVAL, "negative extent");
+    if (a.fmt != FP8A_DENSE_E4M3 && a.fmt != FP8A_DENSE_E5M2) return fail(FP8A_EINVAL, "unknown dense operand format");
+    if (a.M == 0 || a.N == 0) return FP8A_OK;
+    ++g_paths[PATH_DENSE];
+    if (a.K == 0) {
+        const hipError_t e = a.conv ? hipMemsetAsync(a.y, 0, (size_t)(a.M * a.N) * sizeof(float), s)
+                                    : hipMemset2DAsync(a.y, (size_t)a.ldc * sizeof(float), 0, (size_t)a.N * sizeof(float),
+                                                       (size_t)a.M, s);
+        return e == hipSuccess ? FP8A_OK : hip_check("fp8a dense fill");
+    }
+    a.mpad = round_up(a.M, DN_T);
+    a.npad = round_up(a.N, DN_T);
+    a.kpad = round_up(a.K, 32);
+    if (a.kpad / 32 > 65535) return fail(FP8A_EINVAL, "K too large for the dense path (> 2097120)");
+    if (ws == nullptr || wsb < dense_ws_bytes(a.M, a.N, a.K)) return fail(FP8A_EINVAL, "workspace too small");
+    uint8_t *w = static_cast<uint8_t *>(ws);
+    const size_t nmark = (size_t)(a.mpad / DN_U + a.npad / DN_U);
+    a.urow = w;
+    a.ucol = w + a.mpad / DN_U;
+    w += al256(nmark);
+    a.qa = w;  w += al256((size_t)(a.mpad * a.kpad));
+    a.qas = w; w += al256((size_t)(a.mpad * a.kpad / 32));
+    a.qb = w;  w += al256((size_t)(a.npad * a.kpad));
+    a.qbs = w;
+    if (hipMemsetAsync(a.urow, 0, nmark, s) != hipSuccess) return hip_check("fp8a dense marks");
+    const dim3 ga((unsigned)((a.mpad + 255) / 256), (unsigned)(a.kpad / 32));
+    const dim3 gb((unsigned)((a.npad + 255) / 256), (unsigned)(a.kpad / 32));
+    const unsigned tiles = (unsigned)((a.mpad / DN_T) * (a.npad / DN_T));
+    const unsigned units = (unsigned)((a.mpad / DN_U) * (a.npad / DN_U));
+    if (a.fmt == FP8A_DENSE_E4M3) {
+        dn_pack<false, 0><<<ga, 256, 0, s>>>(a);
+        dn_pack<true, 0><<<gb, 256, 0, s>>>(a);
+        if (a.conv) dn_gemm<0, true><<<tiles, 256, 0, s>>>(a);
+        else dn_gemm<0, false><<<tiles, 256, 0, s>>>(a);
+    } else {
+        dn_pack<false, 1><<<ga, 256, 0, s>>>(a);
+        dn_pack<true, 1><<<gb, 256, 0, s>>>(a);
+        if (a.conv) dn_gemm<1, true><<<tiles, 256, 0, s>>>(a);
+        else dn_gemm<1, false><<<tiles, 256, 0, s>>>(a);
+    }
+    dn_count<<<1, 64, 0, s>>>(a);
+    dn_fix<<<units, 256, 0, s>>>(a);
+    return hip_check("fp8a dense launch");
+}
+
+static DenseArgs dense_args() {
+    DenseArgs a;
+    memset(&a, 0, sizeof(a));
+    a.Ho = a.Wo = 1;
+    a.kh = a.kw = a.sh = a.sw = a.dh = a.dw = 1;
+    return a;
+}
+
 }  // namespace fp8a
 
 using namespace fp8a;
@@ -1712,6 +1800,71 @@ int fp8a_fallback_stats(uint64_t *out, int reset) {
     if (reset) {
         const unsigned long long z[4] = {0, 0, 0, 0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_fallback), z, sizeof(z)) != hipSuccess) return hip_check("fp8a_fallback_stats");
+    }
+    return FP8A_OK;
+}
+
+size_t fp8a_dense_matmul_workspace_size(int64_t M, int64_t N, int64_t K) { return dense_ws_bytes(M, N, K); }
+
+int fp8a_dense_matmul(const float *A, int64_t sam, int64_t sak, const float *B, int64_t sbk, int64_t sbn, float *C,
+                      int64_t ldc, int64_t M, int64_t N, int64_t K, int fmt, void *workspace, size_t workspace_bytes,
+                      fp8a_stream_t stream) {
+    if (ldc < N) return fail(FP8A_EINVAL, "leading dimension smaller than extent");
+    DenseArgs a = dense_args();
+    a.x = A; a.sam = sam; a.sak = sak; a.w = B; a.sbk = sbk; a.sbn = sbn; a.y = C; a.ldc = ldc;
+    a.M = M; a.N = N; a.K = K; a.fmt = fmt;
+    return run_dense(a, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+size_t fp8a_dense_conv2d_workspace_size(int64_t Bn, int64_t Cin, int64_t H, int64_t W, int64_t Cout, int kh, int kw,
+                                        int sh, int sw, int ph, int pw, int dh, int dw) {
+    const int64_t Ho = (H + 2 * ph - dh * (kh - 1) - 1) / sh + 1;
+    const int64_t Wo = (W + 2 * pw - dw * (kw - 1) - 1) / sw + 1;
+    if (Ho <= 0 || Wo <= 0) return 0;
+    return dense_ws_bytes(Bn * Ho * Wo, Cout, Cin * kh * kw);
+}
+
+int fp8a_dense_conv2d(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
+                      int64_t Cout, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw, int fmt,
+                      void *workspace, size_t workspace_bytes, fp8a_stream_t stream) {
+    if (kh < 1 || kw < 1 || sh < 1 || sw < 1 || dh < 1 || dw < 1 || ph < 0 || pw < 0 || Bn < 0 || Cin < 0 || Cout < 0)
+        return fail(FP8A_EINVAL, "bad convolution geometry");
+    const int64_t Ho = (H + 2 * ph - dh * (kh - 1) - 1) / sh + 1;
+    const int64_t Wo = (W + 2 * pw - dw * (kw - 1) - 1) / sw + 1;
+    if (Ho <= 0 || Wo <= 0) return fail(FP8A_EINVAL, "empty convolution output");
+    DenseArgs a = dense_args();
+    a.x = x; a.w = w; a.y = y; a.conv = 1;
+    a.C = Cin; a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo;
+    a.kh = kh; a.kw = kw; a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw; a.dh = dh; a.dw = dw;
+    a.M = Bn * Ho * Wo; a.N = Cout; a.K = Cin * kh * kw;
+    a.sbk = 1; a.sbn = a.K;  // w [Cout][Cin][kh][kw]: B(k, n) = w[n * K + k]
+    a.ldc = Cout; a.fmt = fmt;
+    return run_dense(a, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int fp8a_clock_stats(uint64_t *out, int reset) {
+    if (out == nullptr) return fail(FP8A_EINVAL, "null pointer");
+    unsigned long long v[3] = {0, 0, 0};
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(v, HIP_SYMBOL(g_clk), sizeof(v)) != hipSuccess)
+        return hip_check("fp8a_clock_stats");
+    for (int i = 0; i < 3; ++i) out[i] = v[i];
+    if (reset) {
+        const unsigned long long z[3] = {0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_clk), z, sizeof(z)) != hipSuccess) return hip_check("fp8a_clock_stats");
+    }
+    return FP8A_OK;
+}
+
+int fp8a_dense_stats(uint64_t *out, int reset) {
+    if (out == nullptr) return fail(FP8A_EINVAL, "null pointer");
+    unsigned long long v[2] = {0, 0};
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(v, HIP_SYMBOL(g_dense), sizeof(v)) != hipSuccess)
+        return hip_check("fp8a_dense_stats");
+    out[0] = v[0];
+    out[1] = v[1];
+    if (reset) {
+        const unsigned long long z[2] = {0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_dense), z, sizeof(z)) != hipSuccess) return hip_check("fp8a_dense_stats");
     }
     return FP8A_OK;
 }

@@ -1,0 +1,314 @@
+// gemm_dense.h -- the exact (non-approx) product on the matrix core (included by fp8approx.hip
+// inside namespace fp8a, after gemm_oh.h).  DESIGN.md §3e.
+//
+// The reference's non-approx branch is a plain fp32 contraction of FP8-quantized operands:
+// `x @ y` (approx_calculation.py:797, 811 -- the im2col form for convs; QuantizationHijacker
+// with approx_flag off, BASELINE config 1).  Every value on an E4M3 / E5M2 grid has at most 4 / 3
+// significant bits, so within one 32-k block it is EXACT in OCP e4m3 / e5m2 times a power-of-two
+// block scale, and the block-scaled MFMA (v_mfma_scale_f32_16x16x128_f8f6f4) forms each product
+// exactly and accumulates in fp32: the same sums up to summation order.
+//
+//   dn_pack<A|B>  -- one thread per (row, 32-k block): the block's largest magnitude picks the
+//                    E8M0 scale (e4m3: largest binade 8 when the top value fits 448, else 7;
+//                    e5m2: 15), the 32 values go to fp8 bytes, and each is converted back: a value
+//                    that does not round-trip (off the FP8 grid, more than ~16 / ~31 binades below
+//                    its block's largest, inf / NaN) marks its 64-row (A) / 64-column (B) unit.
+//                    A is gathered straight from NCHW for convs (implicit im2col).
+//   dn_gemm       -- 128 x 128 tiles, 4 waves of 64 x 64, per 128-k stage the byte images through
+//                    LDS and 128 block-scaled MFMAs per wave, each over 16 k of one MX block with
+//                    one value per 8-byte operand group (the matrix core's first summation stage
+//                    is narrow: see dn_gemm).  NCHW stores use the transposed
+//                    product (B as the MFMA's first operand) so consecutive lanes hold consecutive
+//                    pixels.
+//   dn_fix        -- the marked 64 x 64 units again in fp32 FMAs from the original operands (a
+//                    no-op launch when nothing is marked; counted by fp8a_dense_stats).
+
+constexpr int DN_T = 128;            // tile rows = tile columns
+constexpr int DN_KC = 128;           // k per LDS stage (one MFMA K-step)
+constexpr int DN_RS = DN_KC + 16;    // LDS row stride, bytes
+constexpr int DN_U = 64;             // fallback unit edge
+
+struct DenseArgs {
+    const float *x;            // A: matmul element (m, k) at x[m * sam + k * sak]; conv: the NCHW input
+    const float *w;            // B: element (k, n) at w[k * sbk + n * sbn]
+    float *y;                  // C: y[m * ldc + n], or NCHW (conv)
+    int64_t M, N, K, kpad, mpad, npad;
+    int64_t sam, sak, sbk, sbn, ldc;
+    int conv;
+    int64_t C, H, W, Ho, Wo;
+    int kh, kw, sh, sw, ph, pw, dh, dw;
+    uint8_t *qa, *qas, *qb, *qbs;  // byte images [mpad|npad][kpad] and E8M0 scales [..][kpad / 32]
+    uint8_t *urow, *ucol;          // unit marks [mpad / 64], [npad / 64]
+    int fmt;                       // FP8A_DENSE_E4M3 / FP8A_DENSE_E5M2
+};
+
+__device__ unsigned long long g_dense[2];  // [0] launches with marked units, [1] units recomputed
+
+__device__ __forceinline__ float dn_conv_elem(const DenseArgs &p, int64_t img, int64_t ho, int64_t wo, int64_t c,
+                                              int i, int j) {
+    const int64_t hi = ho * p.sh - p.ph + (int64_t)i * p.dh, wi = wo * p.sw - p.pw + (int64_t)j * p.dw;
+    if (hi < 0 || hi >= p.H || wi < 0 || wi >= p.W) return 0.0f;
+    return p.x[((img * p.C + c) * p.H + hi) * p.W + wi];
+}
+
+__device__ __forceinline__ float dn_a(const DenseArgs &p, int64_t m, int64_t k) {
+    if (!p.conv) return p.x[m * p.sam + k * p.sak];
+    const int64_t hw = p.Ho * p.Wo, img = m / hw, pix = m - img * hw, ho = pix / p.Wo, wo = pix - ho * p.Wo;
+    const int khw = p.kh * p.kw;
+    const int64_t c = k / khw;
+    const int t = (int)(k - c * khw), i = t / p.kw, j = t - i * p.kw;
+    return dn_conv_elem(p, img, ho, wo, c, i, j);
+}
+
+// fp8 bytes of two floats (scale 1: the caller has applied the block scale) and back
+template <int FMT>
+__device__ __forceinline__ uint32_t dn_cvt2(float a, float b, bool &ok) {
+    xm_s2 cv = {0, 0};
+    float ra, rb;
+    if constexpr (FMT == 0) {
+        cv = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(cv, a, b, 1.0f, false);
+        const uint32_t u = __builtin_bit_cast(uint32_t, cv);
+        ra = __builtin_amdgcn_cvt_scalef32_f32_fp8((int)u, 1.0f, 0);
+        rb = __builtin_amdgcn_cvt_scalef32_f32_fp8((int)u, 1.0f, 1);
+    } else {
+        cv = __builtin_amdgcn_cvt_scalef32_pk_bf8_f32(cv, a, b, 1.0f, false);
+        const uint32_t u = __builtin_bit_cast(uint32_t, cv);
+        ra = __builtin_amdgcn_cvt_scalef32_f32_bf8((int)u, 1.0f, 0);
+        rb = __builtin_amdgcn_cvt_scalef32_f32_bf8((int)u, 1.0f, 1);
+    }
+    ok = ok && ra == a && rb == b;
+    return __builtin_bit_cast(uint32_t, cv) & 0xFFFFu;
+}
+
+template <bool ISB, int FMT>
+__global__ __launch_bounds__(256) void dn_pack(const DenseArgs p) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t rows = ISB ? p.N : p.M, rpad = ISB ? p.npad : p.mpad;
+    if (r >= rpad) return;
+    const int kb = blockIdx.y;
+    const int64_t k0 = 32 * (int64_t)kb;
+    float v[32];
+#pragma unroll
+    for (int e = 0; e < 32; ++e) v[e] = 0.0f;
+    if (r < rows) {
+        if (ISB) {
+#pragma unroll
+            for (int e = 0; e < 32; ++e)
+                if (k0 + e < p.K) v[e] = p.w[(k0 + e) * p.sbk + r * p.sbn];
+        } else if (p.conv) {
+            const int64_t hw = p.Ho * p.Wo, img = r / hw, pix = r - img * hw, ho = pix / p.Wo, wo = pix - ho * p.Wo;
+            const int khw = p.kh * p.kw;
+            int64_t c = k0 / khw;
+            int t = (int)(k0 - c * khw), i = t / p.kw, j = t - i * p.kw;
+#pragma unroll
+            for (int e = 0; e < 32; ++e) {
+                if (k0 + e < p.K) v[e] = dn_conv_elem(p, img, ho, wo, c, i, j);
+                if (++j == p.kw) {
+                    j = 0;
+                    if (++i == p.kh) { i = 0; ++c; }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 32; ++e)
+                if (k0 + e < p.K) v[e] = p.x[r * p.sam + (k0 + e) * p.sak];
+        }
+    }
+    float amax = 0.0f;
+    bool ok = true;
+#pragma unroll
+    for (int e = 0; e < 32; ++e) {
+        amax = fmaxf(amax, fabsf(v[e]));
+        ok = ok && v[e] == v[e];  // NaN
+    }
+    int s = 0;
+    if (amax > 0.0f) {
+        if (!(amax <= 3.4028235e38f)) {
+            ok = false;
+        } else {
+            int e;
+            frexpf(amax, &e);
+            --e;  // floor(log2 amax)
+            s = FMT == 0 ? (ldexpf(amax, 8 - e) <= 448.0f ? e - 8 : e - 7) : e - 15;
+            if (s < -127 || s > 127) { ok = false; s = 0; }
+        }
+    }
+    uint32_t wd[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const uint32_t lo = dn_cvt2<FMT>(ldexpf(v[4 * q], -s), ldexpf(v[4 * q + 1], -s), ok);
+        const uint32_t hi = dn_cvt2<FMT>(ldexpf(v[4 * q + 2], -s), ldexpf(v[4 * q + 3], -s), ok);
+        wd[q] = lo | (hi << 16);
+    }
+    uint8_t *q = (ISB ? p.qb : p.qa) + r * p.kpad + k0;
+    *reinterpret_cast<uint4 *>(q) = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+    *reinterpret_cast<uint4 *>(q + 16) = make_uint4(wd[4], wd[5], wd[6], wd[7]);
+    (ISB ? p.qbs : p.qas)[r * (p.kpad / 32) + kb] = (uint8_t)(ok ? s + 127 : 127);
+    if (!ok) (ISB ? p.ucol : p.urow)[r / DN_U] = 1;
+}
+
+struct DnSmem {
+    uint8_t a[DN_T][DN_RS];
+    uint8_t b[DN_T][DN_RS];
+    uint32_t as[DN_T];  // the row's 4 block scales of the stage
+    uint32_t bs[DN_T];
+};
+
+template <int FMT, bool NCHW>
+__global__ __launch_bounds__(256, 2) void dn_gemm(const DenseArgs p) {
+    __shared__ __attribute__((aligned(16))) DnSmem sm;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wr = __builtin_amdgcn_readfirstlane(wv >> 1), wc = __builtin_amdgcn_readfirstlane(wv & 1);
+    const int64_t num_mt = p.mpad / DN_T;
+    const int64_t m0 = ((int64_t)blockIdx.x % num_mt) * DN_T, n0 = ((int64_t)blockIdx.x / num_mt) * DN_T;
+    const int64_t kpad = p.kpad, kb32 = kpad / 32;
+    // staging: thread = (row, 4 of the stage's 8 16-byte granules); even threads also the scales
+    const int srow = tid >> 1, sg0 = (tid & 1) * 4;
+    const uint8_t *ga = p.qa + (m0 + srow) * kpad, *gb = p.qb + (n0 + srow) * kpad;
+    const uint8_t *gas = p.qas + (m0 + srow) * kb32, *gbs = p.qbs + (n0 + srow) * kb32;
+    uint4 ra[4], rb[4];
+    uint32_t rsa = 0x7F7F7F7Fu, rsb = 0x7F7F7F7Fu;
+    auto load = [&](int64_t k0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t kk = k0 + 16 * (sg0 + q);
+            ra[q] = kk < kpad ? *reinterpret_cast<const uint4 *>(ga + kk) : make_uint4(0u, 0u, 0u, 0u);
+            rb[q] = kk < kpad ? *reinterpret_cast<const uint4 *>(gb + kk) : make_uint4(0u, 0u, 0u, 0u);
+        }
+        if ((tid & 1) == 0) {
+            rsa = rsb = 0u;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t b = k0 / 32 + q;
+                rsa |= (uint32_t)(b < kb32 ? gas[b] : 127) << (8 * q);
+                rsb |= (uint32_t)(b < kb32 ? gbs[b] : 127) << (8 * q);
+            }
+        }
+    };
+    xm_v4f acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (xm_v4f){0.0f, 0.0f, 0.0f, 0.0f};
+    const int r16 = lane & 15, g = lane >> 4;
+    load(0);
+    for (int64_t k0 = 0; k0 < kpad; k0 += DN_KC) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            *reinterpret_cast<uint4 *>(&sm.a[srow][16 * (sg0 + q)]) = ra[q];
+            *reinterpret_cast<uint4 *>(&sm.b[srow][16 * (sg0 + q)]) = rb[q];
+        }
+        if ((tid & 1) == 0) {
+            sm.as[srow] = rsa;
+            sm.bs[srow] = rsb;
+        }
+        __syncthreads();
+        if (k0 + DN_KC < kpad) load(k0 + DN_KC);  // the next stage's loads fly during the MFMAs
+        // One value per 8-byte group of the MFMA operand: the matrix core sums the products of each
+        // 8-byte group in a narrow first stage that drops a product ~2^13 or more below its
+        // neighbour (measured: tools/mfma_bf16_precision.hip, tools/debug_dense3.py),
+        // and adds the groups exactly.  So each MFMA takes 16 real k -- half an MX block, its scale
+        // in all four lane groups -- at slots 16 g, 16 g + 8, 64 + 16 g, 64 + 16 g + 8 of lane
+        // group g (operand K layout measured, tools/mfma_scale_layout.hip: lane group g's bytes 0-15
+        // are slots 16 g .., bytes 16-31 slots 64 + 16 g ..): k = 2 g, 2 g + 1, 8 + 2 g, 9 + 2 g.
+#pragma unroll
+        for (int ks = 0; ks < DN_KC / 16; ++ks) {
+            xm_v8i af[4], bf[4];
+            int sa[4], sb[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = 64 * wr + 16 * i + r16, col = 64 * wc + 16 * i + r16;
+                const uint32_t a0 = *reinterpret_cast<const uint16_t *>(&sm.a[row][16 * ks + 2 * g]);
+                const uint32_t a1 = *reinterpret_cast<const uint16_t *>(&sm.a[row][16 * ks + 8 + 2 * g]);
+                const uint32_t b0 = *reinterpret_cast<const uint16_t *>(&sm.b[col][16 * ks + 2 * g]);
+                const uint32_t b1 = *reinterpret_cast<const uint16_t *>(&sm.b[col][16 * ks + 8 + 2 * g]);
+                af[i] = (xm_v8i){(int)(a0 & 0xFFu), 0, (int)(a0 >> 8), 0, (int)(a1 & 0xFFu), 0, (int)(a1 >> 8), 0};
+                bf[i] = (xm_v8i){(int)(b0 & 0xFFu), 0, (int)(b0 >> 8), 0, (int)(b1 & 0xFFu), 0, (int)(b1 >> 8), 0};
+                sa[i] = (int)((sm.as[row] >> (8 * (ks >> 1))) & 0xFFu);
+                sb[i] = (int)((sm.bs[col] >> (8 * (ks >> 1))) & 0xFFu);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if constexpr (NCHW)  // D^T: rows = columns n, columns = rows m
+                        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bf[j], af[i], acc[i][j], FMT, FMT,
+                                                                                    0, sb[j], 0, sa[i]);
+                    else
+                        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bf[j], acc[i][j], FMT, FMT,
+                                                                                    0, sa[i], 0, sb[j]);
+                }
+        }
+        __syncthreads();
+    }
+    // lane (r16, g) holds D[4 g + r][r16] of each 16 x 16 block
+    const int64_t hw = p.Ho * p.Wo;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if constexpr (NCHW) {
+                    const int64_t m = m0 + 64 * wr + 16 * i + r16, n = n0 + 64 * wc + 16 * j + 4 * g + r;
+                    if (m < p.M && n < p.N) {
+                        const int64_t img = m / hw, pix = m - img * hw;
+                        p.y[(img * p.N + n) * hw + pix] = acc[i][j][r];
+                    }
+                } else {
+                    const int64_t m = m0 + 64 * wr + 16 * i + 4 * g + r, n = n0 + 64 * wc + 16 * j + r16;
+                    if (m < p.M && n < p.N) p.y[m * p.ldc + n] = acc[i][j][r];
+                }
+            }
+}
+
+// The marked units in fp32 (fmaf, k order) from the original operands.
+__global__ __launch_bounds__(256) void dn_fix(const DenseArgs p) {
+    const int64_t num_um = p.mpad / DN_U;
+    const int64_t um = (int64_t)blockIdx.x % num_um, un = (int64_t)blockIdx.x / num_um;
+    if (!(p.urow[um] | p.ucol[un])) return;
+    __shared__ float sa[16][DN_U + 1], sb[16][DN_U + 1];
+    const int tid = threadIdx.x, ty = tid & 15, tx = tid >> 4;
+    if (tid == 0) atomicAdd(&g_dense[1], 1ull);
+    const int64_t m0 = um * DN_U, n0 = un * DN_U;
+    float acc[4][4] = {};
+    for (int64_t k0 = 0; k0 < p.K; k0 += 16) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int idx = tid + 256 * e, kk = idx >> 6, rr = idx & 63;
+            const int64_t k = k0 + kk, m = m0 + rr, n = n0 + rr;
+            sa[kk][rr] = (k < p.K && m < p.M) ? dn_a(p, m, k) : 0.0f;
+            sb[kk][rr] = (k < p.K && n < p.N) ? p.w[k * p.sbk + n * p.sbn] : 0.0f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = __fmaf_rn(sa[kk][4 * ty + i], sb[kk][4 * tx + j], acc[i][j]);
+        __syncthreads();
+    }
+    const int64_t hw = p.Ho * p.Wo;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t m = m0 + 4 * ty + i, n = n0 + 4 * tx + j;
+            if (m >= p.M || n >= p.N) continue;
+            if (p.conv) {
+                const int64_t img = m / hw, pix = m - img * hw;
+                p.y[(img * p.N + n) * hw + pix] = acc[i][j];
+            } else {
+                p.y[m * p.ldc + n] = acc[i][j];
+            }
+        }
+}
+
+// one thread: whether any unit is marked (counts the launch)
+__global__ void dn_count(const DenseArgs p) {
+    bool any = false;
+    for (int64_t u = threadIdx.x; u < p.mpad / DN_U; u += blockDim.x) any |= p.urow[u] != 0;
+    for (int64_t u = threadIdx.x; u < p.npad / DN_U; u += blockDim.x) any |= p.ucol[u] != 0;
+    if (__any(any ? 1 : 0) && threadIdx.x == 0) atomicAdd(&g_dense[0], 1ull);
+}

@@ -366,6 +366,7 @@ __global__ __launch_bounds__(256) void xm_decode_b(const GemmArgs p, int64_t kpa
 // conv word image carries the zero padding (xm_decode_a), so the gather has no bounds checks.
 __global__ __launch_bounds__(XM_NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs p) {
     __shared__ __attribute__((aligned(16))) XmSmem sm;
+    FP8A_CLK_BEGIN
 
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wvu = __builtin_amdgcn_readfirstlane(wv);
@@ -577,4 +578,5 @@ __global__ __launch_bounds__(XM_NT, XM_WAVES) void gemm_f8mx_kernel(const GemmAr
             store_tile(p, split, m0 + 64 * h, n0, ety, etx, acc);
         }
     }
+    FP8A_CLK_END
 }

@@ -70,7 +70,7 @@ int fp8a_fallback_stats(uint64_t *out, int reset);
  *   [0] E4M3 one-hot dense matrix-core GEMM + candidate correction (gemm_oh.h),
  *   [1] E4M3 per-pair matrix-core kernel (gemm_f8mx.h), [2] gemm_tt_kernel (E3M4 / E2M5),
  *   [3] gemm_tt16_kernel (E3M4), [4] gemm_fast_kernel (VALU tiled), [5] the exact kernel alone
- *   (tensor-bias products), [6-7] reserved.  reset != 0 zeroes them after reading.
+ *   (tensor-bias products), [6] the dense exact product (fp8a_dense_*), [7] reserved.  reset != 0 zeroes them after reading.
  */
 int fp8a_path_stats(uint64_t *out, int reset);
 
@@ -92,6 +92,40 @@ int fp8a_set_option(const char *name, int value);
  * element, 64-column tile) segments examined.  Synchronises the device; reset != 0 zeroes them.
  */
 int fp8a_debug_stats(uint64_t *out, int reset);
+
+/*
+ * The exact (non-approx) product on the matrix core -- the reference's `x @ y` of FP8-quantized
+ * operands (approx_calculation.py:797, 811: QuantizationHijacker with approx_flag off, BASELINE
+ * config 1; the im2col form for convs).  Operands are fp32 values; per (row, 32-k block) they are
+ * converted to OCP fp8 with a power-of-two block scale (fmt FP8A_DENSE_E4M3: e4m3, for E4M3-grid
+ * values; FP8A_DENSE_E5M2: e5m2, for E5M2 / narrower grids) and multiplied exactly by the
+ * block-scaled MFMA with fp32 accumulation.  Values that are not exact in the block's fp8 format
+ * (off-grid, too far below the block's largest, inf / NaN) send their 64-row / 64-column output
+ * units to an fp32 FMA recompute, so ANY finite or non-finite input gives the fp32 product up to
+ * summation order.  fp8a_dense_matmul: A element (m, k) at A[m * sam + k * sak], B element (k, n)
+ * at B[k * sbk + n * sbn], C row-major with ldc.  fp8a_dense_conv2d: NCHW x, w [Cout][Cin][kh][kw],
+ * NCHW y, groups = 1.  Workspace: the *_workspace_size bytes.
+ */
+#define FP8A_DENSE_E4M3 0
+#define FP8A_DENSE_E5M2 1
+size_t fp8a_dense_matmul_workspace_size(int64_t M, int64_t N, int64_t K);
+int fp8a_dense_matmul(const float *A, int64_t sam, int64_t sak, const float *B, int64_t sbk, int64_t sbn, float *C,
+                      int64_t ldc, int64_t M, int64_t N, int64_t K, int fmt, void *workspace, size_t workspace_bytes,
+                      fp8a_stream_t stream);
+size_t fp8a_dense_conv2d_workspace_size(int64_t Bn, int64_t Cin, int64_t H, int64_t W, int64_t Cout, int kh, int kw,
+                                        int sh, int sw, int ph, int pw, int dh, int dw);
+int fp8a_dense_conv2d(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
+                      int64_t Cout, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw, int fmt,
+                      void *workspace, size_t workspace_bytes, fp8a_stream_t stream);
+/* Dense-path counters since load / the last reset (out[2]): [0] launches with units recomputed in
+ * fp32, [1] 64 x 64 units recomputed.  Synchronises the device. */
+int fp8a_dense_stats(uint64_t *out, int reset);
+
+/* Diagnostic: the in-kernel clock of gemm_f8mx_kernel, counted only by a library built with
+ * -DFP8A_CLOCK_STAMP=1 (tools/clock_probe.py; zeros otherwise), out[3]: sum over workgroups of
+ * the s_memtime delta, of the s_memrealtime (100 MHz) delta, and the workgroup count.
+ * Synchronises the device. */
+int fp8a_clock_stats(uint64_t *out, int reset);
 
 /*
  * Element decomposition DEC of float_to_fpany_absint_torch (approx_matmul_whole_v9.py:233-291)

@@ -3,7 +3,9 @@ weights and BN statistics) rebuilt from the drop-in operators, given the referen
 state, goes through estimate -> fix -> approx on the GPU.  Cases: E4M3 approx_v9; E4M3 with
 approx_flag off (BASELINE config 1: the reference's canonical --no-approx_flag
 --original-quantize-res run, exact product + quantizers); E5M2 approx_v9 with the opt-in zero
-table (BASELINE config 3's format; the reference was given the same zero table).
+table (BASELINE config 3's format; the reference was given the same zero table).  In the
+no-approx case the exact products (groups = 1) run on the block-scaled fp8 matrix core
+(csrc/gemm_dense.h), the depthwise ones as the fp32 contraction.
 
 Bars: every approx layer's bA / per-channel bB / bR identical (calibration reproduced through
 the whole network); logits within a summation-order tolerance; top-1 identical."""
@@ -35,8 +37,13 @@ def test_mobilenet_v2_model_level(case):
     with torch.no_grad():
         m(torch.from_numpy(g[f"{name}__x_cal"]).to(DEV))
     m.fix_ranges()
+    from fp8_quantization_amd import _lib
+    _lib.path_stats(reset=True)
     with torch.no_grad():
         logits = m(torch.from_numpy(g[f"{name}__x_ev"]).to(DEV)).cpu().numpy()
+    paths = _lib.path_stats(reset=True)
+    if not case["run_method"]["approx_flag"]:  # config 1: the exact products on the fp8 matrix core
+        assert paths["dense"] > 0 and paths["f8mx"] == 0, paths
     mods = dict(m.named_modules())
     for lname in case["approx_layers"]:
         mod = mods[lname]
