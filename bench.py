@@ -39,13 +39,17 @@ ARCH_NAMES = {"resnet18": "ResNet-18", "resnet50": "ResNet-50", "mobilenet_v2": 
 # GEMM keeps its round-1/2 shape (256 x 197 token rows).
 DEFAULT_BATCH = {"vit_b16": 64, "vit_fc": 256}
 FP32_VALU_PEAK_TFLOPS = 157.3  # MI355X fp32 vector (= fp32 MFMA) peak, MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0  # HBM3E spec, MI355X_MICROARCH.md
+FP8_MFMA_PEAK_TFLOPS = 5000.0  # dense fp8 MFMA, MI355X_MICROARCH.md
 
 
-def metric_name(arch, E, M, v5=False):
+def metric_name(arch, E, M, v5=False, no_approx=False):
     """BASELINE.json's metric for the headline (ResNet-18 E4M3); the same wording for the other
     configs.  The top-1 clause is not part of it: top-1 is not measured here (no ImageNet or
     pretrained weights offline) -- see the line's ``top1_delta``."""
     fmt = "" if (E, M) == (4, 3) else f" E{E}M{M}"
+    if no_approx:
+        return f"ImageNet val images/sec, {ARCH_NAMES[arch]} FP8{fmt} PTQ (approx off, exact product)"
     return f"ImageNet val images/sec, {ARCH_NAMES[arch]} FP8{fmt} " + ("approx_v5 OFUF" if v5 else "approx_v9")
 
 
@@ -89,6 +93,9 @@ def parse(argv=None):
                          "default (0, 1) statistics)")
     ap.add_argument("--expo-width", type=int, default=4)
     ap.add_argument("--mant-width", type=int, default=3)
+    ap.add_argument("--no-approx", action="store_true",
+                    help="approx_flag off (BASELINE config 1: the reference's canonical --no-approx_flag "
+                         "--original-quantize-res PTQ run): the exact products on the fp8 matrix core")
     ap.add_argument("--v5-ofuf", action="store_true",
                     help="the opt-in v5 integer-adder mode with sim_hw_add_OFUF, with_OF_opt and with_UF_opt live "
                          "(BASELINE config 3's switches, which v9 ignores: SURVEY F2)")
@@ -233,6 +240,9 @@ def run(args, dev, rank=0, world=1):
                with_approx=True, with_s2nn2s_opt=True, quant_btw_mult_accu=True)
     if args.v5_ofuf:
         cfg.update(approx_version=5, withComp=True, sim_hw_add_OFUF=True, with_OF_opt=True, with_UF_opt=True)
+    if args.no_approx:  # scripts/image_net.sh:42-45 (--no-approx_flag --original-quantize-res)
+        cfg.update(run_method=dict(approx_flag=False, quantize_after_mult_and_add=False, res_quantizer_flag=True,
+                                   original_quantize_res=True))
     model, in_shape, arch_desc = build_workload(args.arch, cfg, args.bn_stats_batches, dev)
     model = model.to(dev).eval()
 
@@ -260,6 +270,7 @@ def run(args, dev, rank=0, world=1):
         if cuda:
             fa._lib.fallback_stats(reset=True)  # (synchronises: outside the timed region)
             fa._lib.path_stats(reset=True)
+            fa._lib.dense_stats(reset=True)
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step()
@@ -272,9 +283,11 @@ def run(args, dev, rank=0, world=1):
     # there would otherwise be invisible in the line)
     fallback = fa._lib.fallback_stats() if cuda else None
     paths = {k: v for k, v in fa._lib.path_stats().items() if v} if cuda else None
+    dense_fb = fa._lib.dense_stats() if cuda else None
 
-    op_ms = sum(s.elapsed_time(e) for (s, e, _) in prof)
-    op_macs = sum(m for (_, _, m) in prof)
+    op_ms = sum(s.elapsed_time(e) for (s, e, _, _) in prof)
+    op_macs = sum(m for (_, _, m, _) in prof)
+    op_bytes = sum(b for (_, _, _, b) in prof)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -287,7 +300,7 @@ def run(args, dev, rank=0, world=1):
         avg_s = op_ms / 1e3 / launches
         achieved = 2.0 * (op_macs / launches) / avg_s / 1e12 if avg_s > 0 else None
         res = {
-            "metric": metric_name(args.arch, args.expo_width, args.mant_width, args.v5_ofuf),
+            "metric": metric_name(args.arch, args.expo_width, args.mant_width, args.v5_ofuf, args.no_approx),
             "value": images / elapsed,
             "unit": "images/s",
             "n_gpus": world,
@@ -304,7 +317,9 @@ def run(args, dev, rank=0, world=1):
             "data": "synthetic",
             "config": {
                 "workload": f"{arch_desc} E{args.expo_width}M{args.mant_width} "
-                            + ("approx_v5 integer-adder forward (withComp, sim_hw_add_OFUF, with_OF_opt, with_UF_opt, "
+                            + ("PTQ forward with approx_flag off (the exact product of the quantized operands, "
+                               "original_quantize_res, " if args.no_approx else
+                               "approx_v5 integer-adder forward (withComp, sim_hw_add_OFUF, with_OF_opt, with_UF_opt, "
                                if args.v5_ofuf else f"approx_v9 forward (dnsmp_factor=3, withComp={args.with_comp}, "
                                "with_s2nn2s_opt, quant_btw_mult_accu, ")
                             + ("zero error table (opt-in extension: the reference has none for this format), "
@@ -333,7 +348,27 @@ def run(args, dev, rank=0, world=1):
                 "gemm_share_of_step": op_ms / 1e3 / elapsed,
             },
         }
-        if fallback is not None:
+        if args.no_approx and cuda:
+            gbs = op_bytes / (op_ms / 1e3) / 1e9 if op_ms > 0 else None
+            res["roofline"] = {
+                "bound": "hbm",
+                "kernel": "dn_gemm (csrc/gemm_dense.h: the exact product on the block-scaled fp8 matrix core, "
+                          "implicit-GEMM conv / matmul; groups = 1 -- the depthwise convs stay torch's fp32 "
+                          "contraction); timed per op with its operand packing and gated fp32 units",
+                "achieved": gbs,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": gbs / HBM_PEAK_GBS if gbs else None,
+                "traffic": None,
+                "algorithmic": f"fp32 operands read once + fp32 output written once: {op_bytes / launches:.4g} B per "
+                               f"launch avg over {launches} launches, {avg_s * 1e3:.3f} ms avg launch (HIP events); "
+                               f"{2.0 * op_macs / (op_ms / 1e3) / 1e12 if op_ms > 0 else 0:.1f} TFLOP/s of exact "
+                               f"products (fp8 MFMA dense peak {FP8_MFMA_PEAK_TFLOPS:.0f})",
+                "gemm_share_of_step": op_ms / 1e3 / elapsed,
+            }
+            res["dense_fp32_units"] = dict(dense_fb, note="timed steps only: dense launches with 64x64 units "
+                                                          "recomputed in fp32 (blocks not exact in e4m3 / e5m2)")
+        if fallback is not None and not args.no_approx:
             res["fallback"] = dict(fallback, approx_launches=len(prof),
                                    note="timed steps only: exact_launches = launches whose gated exact kernel "
                                         "recomputed exact_units 64x64 output units; f32_reruns = E3M4 launches "
@@ -342,7 +377,8 @@ def run(args, dev, rank=0, world=1):
         if paths is not None:
             res["gemm_paths"] = dict(paths, note="timed steps only: approx GEMM launches per kernel path "
                                                  "(fp8a_path_stats; one_hot = opt-in E4M3 one-hot path)")
-        if world == 1 and not args.no_cpu_baseline and (args.expo_width, args.mant_width) == (4, 3):
+        if world == 1 and not args.no_cpu_baseline and (args.expo_width, args.mant_width) == (4, 3) \
+                and not args.no_approx:
             res["cpu_baseline"] = cpu_baseline(shapes, get_error_table_NN(4, 3, args.with_comp, 3), args.cpu_columns)
             res["speedup_vs_cpu_baseline"] = res["value"] / res["cpu_baseline"]["value"]
         if not cuda:

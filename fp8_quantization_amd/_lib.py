@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("FP8A_LIB_PATH") or os.path.join(HERE, "lib", "libfp8a
 APPROX, S2N, QBMA, GCLIP, TB = 1, 2, 4, 8, 16
 V5, OFUF, OF_OPT, UF_OPT = 32, 64, 128, 256  # v5 integer-adder model (include/fp8approx.h)
 OK, EINVAL, EFORMAT, EHIP = 0, -1, -2, -3
-DENSE_E4M3, DENSE_E5M2 = 0, 1  # fp8a_dense_* operand formats
+DENSE_E4M3, DENSE_E5M2, DENSE_BF16 = 0, 1, 2  # fp8a_dense_* operand formats
 
 SYMBOLS = ("fp8a_version", "fp8a_last_error", "fp8a_fallback_stats", "fp8a_path_stats", "fp8a_set_option", "fp8a_debug_stats", "fp8a_decompose", "fp8a_quant", "fp8a_matmul_workspace_size",
            "fp8a_matmul_workspace_size_mnk", "fp8a_matmul", "fp8a_terms", "fp8a_conv2d_workspace_size", "fp8a_conv2d",

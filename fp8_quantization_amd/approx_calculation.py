@@ -32,6 +32,9 @@ from .quantization.base_quantized_classes import QuantizedActivation, QuantizedM
 from .quantization.hijacker import activations_set
 from .quantization.quantized_folded_bn import BNFusedHijacker
 
+# the non-approx products on the fp8 matrix core (gemm_dense.h); FP8A_DENSE=0: torch's fp32 contraction
+DENSE_EXACT = os.environ.get("FP8A_DENSE", "1") != "0"
+
 # (the hijacker bases too: the reference's replace_operations_with_approx_ops takes them from its
 # `from approx.approx_calculation import *`, INTEGRATION.md §3 Option A)
 __all__ = ["QCustomBNConv2dTorch", "QCustomLinearTorch", "QCustomConv2dTorch", "ApproxOpMixin",
@@ -90,8 +93,9 @@ class ApproxOpMixin:
     @staticmethod
     def _exact_product(x, y, M):
         """The non-approx ``x @ y`` (approx_calculation.py:797, 811): on the GPU the block-scaled
-        fp8 matrix-core product for FP8-grid operands (E4M3 / E5M2), else the fp32 contraction."""
-        fmt = dense_format(M)
+        fp8 matrix-core product for FP8-grid operands (E4M3 / E5M2), else the fp32 contraction
+        (also with FP8A_DENSE=0: A/B measurements)."""
+        fmt = dense_format(M) if DENSE_EXACT else None
         if x.is_cuda and fmt is not None:
             return dense_matmul(x, y, fmt)
         return x @ y
@@ -159,7 +163,7 @@ class ApproxConv2dMixin(ApproxOpMixin):
             out = qamaa_conv2d(x.detach(), weight.detach(), *self._qamaa_params(), stride=self.stride,
                                padding=self.padding, dilation=self.dilation, groups=self.groups)
         else:  # exact product (also qamaa's single-column groups, approx_calculation.py:810-811)
-            fmt = dense_format(M)
+            fmt = dense_format(M) if DENSE_EXACT else None
             if x.is_cuda and fmt is not None and self.groups == 1:
                 out = dense_conv2d(x.detach(), weight.detach(), fmt, self.stride, self.padding, self.dilation)
             else:  # grouped (depthwise: one-column products) / wide-mantissa formats: the fp32 contraction

@@ -12,6 +12,7 @@ tensor-bias semantics (quirk F5 -- param_prepare's integer powers flush min_norm
 is what approx_multiply passes for single-column products (approx_calculation.py:800-809).
 """
 import ctypes
+import os
 from typing import Optional
 
 import torch
@@ -58,11 +59,13 @@ def _prof_start():
     return ev
 
 
-def _prof_end(start, macs):
+def _prof_end(start, macs, nbytes=0):
+    """nbytes: the launch's algorithmic HBM bytes (operands read once, output written once), for
+    the memory-bound dense exact product; 0 for the approx ops (priced by MACs)."""
     if start is not None:
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()
-        _PROFILE.append((start, ev, int(macs)))
+        _PROFILE.append((start, ev, int(macs), int(nbytes)))
 
 
 def _bias_dev(b, device, n=None):
@@ -595,9 +598,12 @@ def qamaa_conv2d(x, w, maxval, n_bits, mantissa_bits, sign_bits=1, stride=(1, 1)
 
 # ------------------------------------------------------------------- the exact product (dense)
 def dense_format(mant_width):
-    """fp8a_dense operand format for values on a grid with ``mant_width`` mantissa bits: e4m3 for
-    3 (E4M3), e5m2 for fewer (E5M2: the wider exponent range); None for wider mantissas (E3M4,
-    E2M5: not exact in OCP fp8 -- their exact product stays the fp32 torch contraction)."""
+    """fp8a_dense operand format for values on a grid with ``mant_width`` mantissa bits.  Default
+    bf16 (every FP8 / E3M4 / E2M5 grid value is exact in bf16 at any exponent; measured exact
+    accumulation); FP8A_DENSE_FMT=fp8 selects the block-scaled OCP fp8 form -- e4m3
+    for 3 mantissa bits, e5m2 for fewer, None (the fp32 contraction) for wider mantissas."""
+    if os.environ.get("FP8A_DENSE_FMT", "bf16") != "fp8":
+        return _lib.DENSE_BF16 if 0 < mant_width <= 7 else None
     if mant_width == 3:
         return _lib.DENSE_E4M3
     if 0 < mant_width <= 2:
@@ -633,7 +639,7 @@ def dense_matmul(A, B, fmt):
     A, B = _as_f32(A), _as_f32(B)
     ev = _prof_start()
     C = _dense_matmul_op(A, B, int(fmt))
-    _prof_end(ev, A.shape[0] * A.shape[1] * B.shape[1])
+    _prof_end(ev, A.shape[0] * A.shape[1] * B.shape[1], 4 * (A.numel() + B.numel() + C.numel()))
     return C
 
 
@@ -673,7 +679,8 @@ def dense_conv2d(x, w, fmt, stride=(1, 1), padding=(0, 0), dilation=(1, 1)):
     ev = _prof_start()
     y = _dense_conv2d_op(x, w, int(fmt), [int(v) for v in stride], [int(v) for v in padding],
                          [int(v) for v in dilation])
-    _prof_end(ev, y.shape[0] * y.shape[2] * y.shape[3] * w.shape[0] * w.shape[1] * w.shape[2] * w.shape[3])
+    _prof_end(ev, y.shape[0] * y.shape[2] * y.shape[3] * w.shape[0] * w.shape[1] * w.shape[2] * w.shape[3],
+              4 * (x.numel() + w.numel() + y.numel()))
     return y
 
 

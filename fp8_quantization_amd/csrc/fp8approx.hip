@@ -1684,13 +1684,15 @@ static inline size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
 static size_t dense_ws_bytes(int64_t M, int64_t N, int64_t K) {
     const int64_t mpad = round_up(std::max<int64_t>(M, 1), DN_T), npad = round_up(std::max<int64_t>(N, 1), DN_T);
     const int64_t kpad = round_up(std::max<int64_t>(K, 1), 32);
-    return al256((size_t)(mpad / DN_U + npad / DN_U)) + al256((size_t)(mpad * kpad)) + al256((size_t)(mpad * kpad / 32)) +
-           al256((size_t)(npad * kpad)) + al256((size_t)(npad * kpad / 32));
+    // byte images at 2 B per element (the bf16 form; the fp8 forms use the first half)
+    return al256((size_t)(mpad / DN_U + npad / DN_U) + 4) + al256((size_t)(2 * mpad * kpad)) +
+           al256((size_t)(mpad * kpad / 32)) + al256((size_t)(2 * npad * kpad)) + al256((size_t)(npad * kpad / 32));
 }
 
 static int run_dense(DenseArgs a, void *ws, size_t wsb, hipStream_t s) {
     if (a.M < 0 || a.N < 0 || a.K < 0) return fail(FP8A_EINVAL, "negative extent");
-    if (a.fmt != FP8A_DENSE_E4M3 && a.fmt != FP8A_DENSE_E5M2) return fail(FP8A_EINVAL, "unknown dense operand format");
+    if (a.fmt != FP8A_DENSE_E4M3 && a.fmt != FP8A_DENSE_E5M2 && a.fmt != FP8A_DENSE_BF16)
+        return fail(FP8A_EINVAL, "unknown dense operand format");
     if (a.M == 0 || a.N == 0) return FP8A_OK;
     ++g_paths[PATH_DENSE];
     if (a.K == 0) {
@@ -1705,20 +1707,25 @@ static int run_dense(DenseArgs a, void *ws, size_t wsb, hipStream_t s) {
     if (a.kpad / 32 > 65535) return fail(FP8A_EINVAL, "K too large for the dense path (> 2097120)");
     if (ws == nullptr || wsb < dense_ws_bytes(a.M, a.N, a.K)) return fail(FP8A_EINVAL, "workspace too small");
     uint8_t *w = static_cast<uint8_t *>(ws);
-    const size_t nmark = (size_t)(a.mpad / DN_U + a.npad / DN_U);
-    a.urow = w;
-    a.ucol = w + a.mpad / DN_U;
+    const size_t nmark = (size_t)(a.mpad / DN_U + a.npad / DN_U) + 4;
+    a.anymark = reinterpret_cast<uint32_t *>(w);
+    a.urow = w + 4;
+    a.ucol = w + 4 + a.mpad / DN_U;
     w += al256(nmark);
-    a.qa = w;  w += al256((size_t)(a.mpad * a.kpad));
+    a.qa = w;  w += al256((size_t)(2 * a.mpad * a.kpad));
     a.qas = w; w += al256((size_t)(a.mpad * a.kpad / 32));
-    a.qb = w;  w += al256((size_t)(a.npad * a.kpad));
+    a.qb = w;  w += al256((size_t)(2 * a.npad * a.kpad));
     a.qbs = w;
-    if (hipMemsetAsync(a.urow, 0, nmark, s) != hipSuccess) return hip_check("fp8a dense marks");
+    if (hipMemsetAsync(a.anymark, 0, nmark, s) != hipSuccess) return hip_check("fp8a dense marks");
     const dim3 ga((unsigned)((a.mpad + 255) / 256), (unsigned)(a.kpad / 32));
     const dim3 gb((unsigned)((a.npad + 255) / 256), (unsigned)(a.kpad / 32));
     const unsigned tiles = (unsigned)((a.mpad / DN_T) * (a.npad / DN_T));
     const unsigned units = (unsigned)((a.mpad / DN_U) * (a.npad / DN_U));
-    if (a.fmt == FP8A_DENSE_E4M3) {
+    if (a.fmt == FP8A_DENSE_BF16) {  // (A straight from its fp32 source)
+        dn_pack<true, 2><<<gb, 256, 0, s>>>(a);
+        if (a.conv) dn_gemm_bf16<true><<<tiles, 256, 0, s>>>(a);
+        else dn_gemm_bf16<false><<<tiles, 256, 0, s>>>(a);
+    } else if (a.fmt == FP8A_DENSE_E4M3) {
         dn_pack<false, 0><<<ga, 256, 0, s>>>(a);
         dn_pack<true, 0><<<gb, 256, 0, s>>>(a);
         if (a.conv) dn_gemm<0, true><<<tiles, 256, 0, s>>>(a);
@@ -1729,8 +1736,7 @@ static int run_dense(DenseArgs a, void *ws, size_t wsb, hipStream_t s) {
         if (a.conv) dn_gemm<1, true><<<tiles, 256, 0, s>>>(a);
         else dn_gemm<1, false><<<tiles, 256, 0, s>>>(a);
     }
-    dn_count<<<1, 64, 0, s>>>(a);
-    dn_fix<<<units, 256, 0, s>>>(a);
+    dn_fix<<<std::min(units, 2048u), 256, 0, s>>>(a);
     return hip_check("fp8a dense launch");
 }
 

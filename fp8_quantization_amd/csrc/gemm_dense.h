@@ -39,7 +39,8 @@ struct DenseArgs {
     int kh, kw, sh, sw, ph, pw, dh, dw;
     uint8_t *qa, *qas, *qb, *qbs;  // byte images [mpad|npad][kpad] and E8M0 scales [..][kpad / 32]
     uint8_t *urow, *ucol;          // unit marks [mpad / 64], [npad / 64]
-    int fmt;                       // FP8A_DENSE_E4M3 / FP8A_DENSE_E5M2
+    uint32_t *anymark;             // 1 once any unit is marked
+    int fmt;                       // FP8A_DENSE_E4M3 / FP8A_DENSE_E5M2 / FP8A_DENSE_BF16
 };
 
 __device__ unsigned long long g_dense[2];  // [0] launches with marked units, [1] units recomputed
@@ -114,6 +115,26 @@ __global__ __launch_bounds__(256) void dn_pack(const DenseArgs p) {
                 if (k0 + e < p.K) v[e] = p.x[r * p.sam + (k0 + e) * p.sak];
         }
     }
+    if constexpr (FMT == 2) {  // bf16: exact iff the low 16 bits are zero (finite, normal or zero)
+        bool ok = true;
+        uint32_t wd[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const uint32_t u0 = __float_as_uint(v[2 * q]), u1 = __float_as_uint(v[2 * q + 1]);
+            const uint32_t e0 = u0 & 0x7F800000u, e1 = u1 & 0x7F800000u;
+            ok = ok && (u0 & 0xFFFFu) == 0u && (u1 & 0xFFFFu) == 0u && e0 != 0x7F800000u && e1 != 0x7F800000u &&
+                 (e0 != 0u || (u0 & 0x7FFFFFFFu) == 0u) && (e1 != 0u || (u1 & 0x7FFFFFFFu) == 0u);
+            wd[q] = (u0 >> 16) | (u1 & 0xFFFF0000u);
+        }
+        uint4 *q = reinterpret_cast<uint4 *>((ISB ? p.qb : p.qa) + 2 * (r * p.kpad + k0));
+#pragma unroll
+        for (int t = 0; t < 4; ++t) q[t] = make_uint4(wd[4 * t], wd[4 * t + 1], wd[4 * t + 2], wd[4 * t + 3]);
+        if (!ok) {
+            (ISB ? p.ucol : p.urow)[r / DN_U] = 1;
+            *p.anymark = 1u;
+        }
+        return;
+    }
     float amax = 0.0f;
     bool ok = true;
 #pragma unroll
@@ -144,7 +165,10 @@ __global__ __launch_bounds__(256) void dn_pack(const DenseArgs p) {
     *reinterpret_cast<uint4 *>(q) = make_uint4(wd[0], wd[1], wd[2], wd[3]);
     *reinterpret_cast<uint4 *>(q + 16) = make_uint4(wd[4], wd[5], wd[6], wd[7]);
     (ISB ? p.qbs : p.qas)[r * (p.kpad / 32) + kb] = (uint8_t)(ok ? s + 127 : 127);
-    if (!ok) (ISB ? p.ucol : p.urow)[r / DN_U] = 1;
+    if (!ok) {
+        (ISB ? p.ucol : p.urow)[r / DN_U] = 1;
+        *p.anymark = 1u;
+    }
 }
 
 struct DnSmem {
@@ -262,13 +286,194 @@ __global__ __launch_bounds__(256, 2) void dn_gemm(const DenseArgs p) {
             }
 }
 
+// The bf16 form (fmt FP8A_DENSE_BF16, the default for the exact product): every value of an FP8 /
+// E3M4 / E2M5 grid (<= 6 significant bits) is exact in bf16 at any exponent, so no block scales and
+// no range limit; v_mfma_f32_16x16x32_bf16 forms the products exactly and adds them exactly down to
+// fp32's last bit at every K position (measured: tools/mfma_bf16_precision.hip) -- 32 real k per
+// MFMA, 4x the fp8 form's 16 at the same MFMA cycles.  A is read straight from the fp32 source
+// (implicit im2col for convs: thread = row, 32 consecutive k per stage, lanes on consecutive rows,
+// so every load instruction covers consecutive pixels) and truncated to bf16 in registers; a value
+// that is not exact (low 16 bits set, inf / NaN, fp32 denormal) marks its row unit for dn_fix.  B
+// comes from dn_pack's bf16 image.  128 x 128 tiles, 4 waves of 64 x 64, 64 k per LDS stage.
+constexpr int DN_BK = 64;                 // k per LDS stage of the bf16 form
+constexpr int DN_BRS = 2 * DN_BK + 16;    // bf16 LDS row stride, bytes
+struct DnSmem16 {
+    uint8_t a[DN_T][DN_BRS];
+    uint8_t b[DN_T][DN_BRS];
+};
+typedef __bf16 dn_v8bf __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ bool dn_bf16_exact(uint32_t u) {
+    const uint32_t e = u & 0x7F800000u;
+    return (u & 0xFFFFu) == 0u && e != 0x7F800000u && (e != 0u || (u & 0x7FFFFFFFu) == 0u);
+}
+
+template <bool CONV>
+__global__ __launch_bounds__(256, 2) void dn_gemm_bf16(const DenseArgs p) {
+    __shared__ __attribute__((aligned(16))) DnSmem16 sm;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wr = __builtin_amdgcn_readfirstlane(wv >> 1), wc = __builtin_amdgcn_readfirstlane(wv & 1);
+    const int64_t num_mt = p.mpad / DN_T;
+    const int64_t m0 = ((int64_t)blockIdx.x % num_mt) * DN_T, n0 = ((int64_t)blockIdx.x / num_mt) * DN_T;
+    const int64_t kpad = p.kpad;
+    // A staging: thread = (row ar, k half ah): 32 consecutive k of the stage
+    const int ar = tid & 127, ah = tid >> 7;
+    const int64_t am = m0 + ar;
+    const bool arow = am < p.M;
+    int64_t img = 0, hi0 = 0, wi0 = 0;
+    if (CONV && arow) {
+        const int64_t hw = p.Ho * p.Wo, pix = am - (am / hw) * hw, ho = pix / p.Wo, wo = pix - ho * p.Wo;
+        img = am / hw;
+        hi0 = ho * p.sh - p.ph;
+        wi0 = wo * p.sw - p.pw;
+    }
+    const float *xrow = CONV ? p.x + img * p.C * p.H * p.W : p.x + (arow ? am : 0) * p.sam;
+    const int khw = p.kh * p.kw;
+    float ra[32];
+    bool aok = true;
+    auto load_a = [&](int64_t k0) {
+        const int64_t kb = k0 + 32 * ah;
+        if (CONV) {
+            int64_t c = kb / khw;
+            int t = (int)(kb - c * khw), i = t / p.kw, j = t - i * p.kw;
+#pragma unroll
+            for (int e = 0; e < 32; ++e) {
+                const int64_t hi = hi0 + (int64_t)i * p.dh, wi = wi0 + (int64_t)j * p.dw;
+                ra[e] = (arow && kb + e < p.K && hi >= 0 && hi < p.H && wi >= 0 && wi < p.W)
+                            ? xrow[(c * p.H + hi) * p.W + wi] : 0.0f;
+                if (++j == p.kw) {
+                    j = 0;
+                    if (++i == p.kh) { i = 0; ++c; }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 32; ++e) ra[e] = (arow && kb + e < p.K) ? xrow[(kb + e) * p.sak] : 0.0f;
+        }
+    };
+    // B staging: thread = (column tid >> 1, 4 of the stage's 8 16-byte granules)
+    const int bcol = tid >> 1, bg0 = (tid & 1) * 4;
+    const uint8_t *gb = p.qb + 2 * (n0 + bcol) * kpad;
+    uint4 rb[4];
+    auto load_b = [&](int64_t k0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t kk = k0 + 8 * (bg0 + q);
+            rb[q] = kk < kpad ? *reinterpret_cast<const uint4 *>(gb + 2 * kk) : make_uint4(0u, 0u, 0u, 0u);
+        }
+    };
+    xm_v4f acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (xm_v4f){0.0f, 0.0f, 0.0f, 0.0f};
+    const int r16 = lane & 15, g = lane >> 4;
+    load_a(0);
+    load_b(0);
+    for (int64_t k0 = 0; k0 < kpad; k0 += DN_BK) {
+        {
+            uint32_t w[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const uint32_t u0 = __float_as_uint(ra[2 * q]), u1 = __float_as_uint(ra[2 * q + 1]);
+                aok = aok && dn_bf16_exact(u0) && dn_bf16_exact(u1);
+                w[q] = (u0 >> 16) | (u1 & 0xFFFF0000u);
+            }
+            uint4 *d = reinterpret_cast<uint4 *>(&sm.a[ar][64 * ah]);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) d[t] = make_uint4(w[4 * t], w[4 * t + 1], w[4 * t + 2], w[4 * t + 3]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) *reinterpret_cast<uint4 *>(&sm.b[bcol][16 * (bg0 + q)]) = rb[q];
+        }
+        __syncthreads();
+        if (k0 + DN_BK < kpad) {  // the next stage's loads fly during the MFMAs
+            load_a(k0 + DN_BK);
+            load_b(k0 + DN_BK);
+        }
+#pragma unroll
+        for (int ks = 0; ks < DN_BK / 32; ++ks) {
+            dn_v8bf af[4], bf[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {  // lane (r16, g): row / column r16, k 8 g .. 8 g + 7 of the step
+                const int row = 64 * wr + 16 * i + r16, col = 64 * wc + 16 * i + r16;
+                af[i] = __builtin_bit_cast(dn_v8bf, *reinterpret_cast<const uint4 *>(&sm.a[row][2 * (32 * ks + 8 * g)]));
+                bf[i] = __builtin_bit_cast(dn_v8bf, *reinterpret_cast<const uint4 *>(&sm.b[col][2 * (32 * ks + 8 * g)]));
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if constexpr (CONV)  // D^T: consecutive lanes on consecutive pixels for the NCHW store
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
+                    else
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+                }
+        }
+        __syncthreads();
+    }
+    if (!aok) {
+        p.urow[am / DN_U] = 1;
+        *p.anymark = 1u;
+    }
+    // epilogue through LDS, half the tile at a time (64 channels x 128 pixels for convs, 64 rows x
+    // 128 columns for matmuls), so every store instruction writes 64 consecutive floats of one
+    // output row / channel plane (full 128-B lines) instead of 16-float pieces
+    static_assert(sizeof(DnSmem16) >= 64 * (DN_T + 1) * sizeof(float), "epilogue slice fits the stage buffers");
+    float *ct = reinterpret_cast<float *>(&sm);
+    constexpr int CP = DN_T + 1;
+    const int64_t hw = p.Ho * p.Wo;
+    const int et = tid & 127, eq = tid >> 7;
+    int64_t eimg = 0, epix = 0;
+    if (CONV) {
+        const int64_t m = m0 + et;
+        eimg = m / hw;
+        epix = m - eimg * hw;
+    }
+    // (halves past the last channel / row are skipped: narrow layers fill few of the 128)
+    const int nh = (CONV ? (p.N - n0) : (p.M - m0)) > 64 ? 2 : 1;
+    for (int h = 0; h < nh; ++h) {
+        __syncthreads();
+        if ((CONV ? wc : wr) == h) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        if constexpr (CONV)  // D^T[n][m]: channel 16 j + 4 g + r of the half, pixel 64 wr + 16 i + r16
+                            ct[(16 * j + 4 * g + r) * CP + 64 * wr + 16 * i + r16] = acc[i][j][r];
+                        else  // D[m][n]: row 16 i + 4 g + r of the half, column 64 wc + 16 j + r16
+                            ct[(16 * i + 4 * g + r) * CP + 64 * wc + 16 * j + r16] = acc[i][j][r];
+                    }
+        }
+        __syncthreads();
+        const int64_t left = (CONV ? p.N - n0 : p.M - m0) - 64 * h;
+        const int nq = (int)min((int64_t)32, (left + 1) / 2);
+#pragma unroll 4
+        for (int q = 0; q < nq; ++q) {
+            const int c = eq + 2 * q;  // the half's channel (conv) / row (matmul)
+            if constexpr (CONV) {
+                const int64_t m = m0 + et, n = n0 + 64 * h + c;
+                if (m < p.M && n < p.N) p.y[(eimg * p.N + n) * hw + epix] = ct[c * CP + et];
+            } else {
+                const int64_t m = m0 + 64 * h + c, n = n0 + et;
+                if (m < p.M && n < p.N) p.y[m * p.ldc + n] = ct[c * CP + et];
+            }
+        }
+    }
+}
+
 // The marked units in fp32 (fmaf, k order) from the original operands.
+// A persistent grid over the units: nothing to do (one word read) unless a unit is marked.
 __global__ __launch_bounds__(256) void dn_fix(const DenseArgs p) {
-    const int64_t num_um = p.mpad / DN_U;
-    const int64_t um = (int64_t)blockIdx.x % num_um, un = (int64_t)blockIdx.x / num_um;
-    if (!(p.urow[um] | p.ucol[un])) return;
+    if (*p.anymark == 0u) return;
+    const int64_t num_um = p.mpad / DN_U, units = num_um * (p.npad / DN_U);
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_dense[0], 1ull);
     __shared__ float sa[16][DN_U + 1], sb[16][DN_U + 1];
     const int tid = threadIdx.x, ty = tid & 15, tx = tid >> 4;
+    for (int64_t u = blockIdx.x; u < units; u += gridDim.x) {
+    const int64_t um = u % num_um, un = u / num_um;
+    if (!(p.urow[um] | p.ucol[un])) continue;
     if (tid == 0) atomicAdd(&g_dense[1], 1ull);
     const int64_t m0 = um * DN_U, n0 = un * DN_U;
     float acc[4][4] = {};
@@ -303,12 +508,5 @@ __global__ __launch_bounds__(256) void dn_fix(const DenseArgs p) {
                 p.y[m * p.ldc + n] = acc[i][j];
             }
         }
-}
-
-// one thread: whether any unit is marked (counts the launch)
-__global__ void dn_count(const DenseArgs p) {
-    bool any = false;
-    for (int64_t u = threadIdx.x; u < p.mpad / DN_U; u += blockDim.x) any |= p.urow[u] != 0;
-    for (int64_t u = threadIdx.x; u < p.npad / DN_U; u += blockDim.x) any |= p.ucol[u] != 0;
-    if (__any(any ? 1 : 0) && threadIdx.x == 0) atomicAdd(&g_dense[0], 1ull);
+    }
 }

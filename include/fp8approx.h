@@ -108,6 +108,7 @@ int fp8a_debug_stats(uint64_t *out, int reset);
  */
 #define FP8A_DENSE_E4M3 0
 #define FP8A_DENSE_E5M2 1
+#define FP8A_DENSE_BF16 2  /* bf16 operands (any value with <= 8 significant bits, every exponent) */
 size_t fp8a_dense_matmul_workspace_size(int64_t M, int64_t N, int64_t K);
 int fp8a_dense_matmul(const float *A, int64_t sam, int64_t sak, const float *B, int64_t sbk, int64_t sbn, float *C,
                       int64_t ldc, int64_t M, int64_t N, int64_t K, int fmt, void *workspace, size_t workspace_bytes,

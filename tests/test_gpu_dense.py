@@ -56,12 +56,20 @@ def _check(C, A, B):
     assert not bad.any(), f"{bad.sum()} outputs outside the bar"
 
 
+FMTS = {"e4m3": (4, 3), "e5m2": (5, 2), "bf16": (4, 3)}  # (the bf16 form on E4M3-grid operands)
+
+
+def _fmt(name):
+    from fp8_quantization_amd import _lib
+    return {"e4m3": _lib.DENSE_E4M3, "e5m2": _lib.DENSE_E5M2, "bf16": _lib.DENSE_BF16}[name]
+
+
 def _stats():
     from fp8_quantization_amd import _lib
     return _lib.dense_stats(reset=True)
 
 
-@pytest.mark.parametrize("fmt", ["e4m3", "e5m2"])
+@pytest.mark.parametrize("fmt", ["e4m3", "e5m2", "bf16"])
 @pytest.mark.parametrize("shape", [(1, 1, 1), (7, 33, 5), (130, 300, 129), (256, 4608, 64), (1000, 147, 1),
                                    (513, 64, 1000), (3, 0, 4)])
 @pytest.mark.parametrize("layout", ["rowmajor", "transposed"])
@@ -69,7 +77,7 @@ def test_matmul_on_grid(shape, fmt, layout):
     from fp8_quantization_amd import _lib
     from fp8_quantization_amd.approx_ops import dense_matmul
     Mr, K, N = shape
-    E, M = (4, 3) if fmt == "e4m3" else (5, 2)
+    E, M = FMTS[fmt]
     A, B = _operands(Mr, K, N, E, M, sum(shape) + M)
     if layout == "rowmajor":
         tA, tB = torch.from_numpy(A).to(DEV), torch.from_numpy(B).to(DEV)
@@ -78,7 +86,7 @@ def test_matmul_on_grid(shape, fmt, layout):
         tB = torch.from_numpy(np.ascontiguousarray(B.T)).to(DEV).t()
     _stats()
     _lib.path_stats(reset=True)
-    C = dense_matmul(tA, tB, _lib.DENSE_E4M3 if fmt == "e4m3" else _lib.DENSE_E5M2).cpu().numpy()
+    C = dense_matmul(tA, tB, _fmt(fmt)).cpu().numpy()
     st = _stats()
     assert _lib.path_stats(reset=True)["dense"] == 1
     if K == 0:
@@ -88,15 +96,14 @@ def test_matmul_on_grid(shape, fmt, layout):
     # e4m3 holds (a column's 1.875 x 2^e maximum next to its smallest subnormal: ~19 binades vs
     # e4m3's 17.8) -- those few units run in fp32
     units = ((Mr + 127) // 128 * 2) * ((N + 127) // 128 * 2)
-    assert st["fp32_units"] <= units // 10, st
+    assert st["fp32_units"] <= (0 if fmt == "bf16" else units // 10), st
 
 
-@pytest.mark.parametrize("fmt", ["e4m3", "e5m2"])
+@pytest.mark.parametrize("fmt", ["e4m3", "e5m2", "bf16"])
 def test_off_grid_rows_take_the_fp32_units(fmt):
-    from fp8_quantization_amd import _lib
     from fp8_quantization_amd.approx_ops import dense_matmul
-    E, M = (4, 3) if fmt == "e4m3" else (5, 2)
-    f = _lib.DENSE_E4M3 if fmt == "e4m3" else _lib.DENSE_E5M2
+    E, M = FMTS[fmt]
+    f = _fmt(fmt)
     Mr, K, N = 300, 200, 129
     A, B = _operands(Mr, K, N, E, M, 11)
     A, B = _tame(A), np.ascontiguousarray(_tame(B.T).T)
@@ -156,7 +163,7 @@ def test_non_finite_like_torch():
     _stats()
 
 
-@pytest.mark.parametrize("fmt", ["e4m3", "e5m2"])
+@pytest.mark.parametrize("fmt", ["e4m3", "e5m2", "bf16"])
 @pytest.mark.parametrize("geo", [
     # (Bn, Cin, H, W, Cout, kh, kw, stride, padding, dilation)
     (2, 16, 15, 17, 24, 3, 3, (2, 1), (1, 2), (1, 2)),
@@ -168,14 +175,13 @@ def test_conv_on_grid(geo, fmt):
     from fp8_quantization_amd import _lib
     from fp8_quantization_amd.approx_ops import dense_conv2d
     Bn, Cin, H, W, Cout, kh, kw, st, pd, dl = geo
-    E, M = (4, 3) if fmt == "e4m3" else (5, 2)
+    E, M = FMTS[fmt]
     rng = np.random.default_rng(Cin + Cout)
     x = _q(np.maximum(rng.standard_normal((Bn, Cin, H, W)), 0).astype(np.float32), E, M)
     w = _q((rng.standard_normal((Cout, Cin * kh * kw)) * 0.1).astype(np.float32), E, M, per_row=True)
     w = _tame(w).reshape(Cout, Cin, kh, kw)
     _stats()
-    y = dense_conv2d(torch.from_numpy(x).to(DEV), torch.from_numpy(w).to(DEV),
-                     _lib.DENSE_E4M3 if fmt == "e4m3" else _lib.DENSE_E5M2, st, pd, dl).cpu().numpy()
+    y = dense_conv2d(torch.from_numpy(x).to(DEV), torch.from_numpy(w).to(DEV), _fmt(fmt), st, pd, dl).cpu().numpy()
     stt = _stats()
     tx, tw = torch.from_numpy(x).double(), torch.from_numpy(w).double()
     ref = F.conv2d(tx, tw, None, st, pd, dl).numpy()
@@ -217,7 +223,7 @@ def test_module_exact_branch_runs_dense():
     _stats()
 
 
-@pytest.mark.parametrize("fmt", ["e4m3", "e5m2"])
+@pytest.mark.parametrize("fmt", ["e4m3", "e5m2", "bf16"])
 def test_wide_range_pairs_exact(fmt):
     """Every pair of positions (i, j) of a 32-k block: 2^8 at i and 2^-9 at j (17 binades apart,
     both exact in the block's fp8 format) must sum exactly -- the matrix core's narrow first
@@ -225,7 +231,7 @@ def test_wide_range_pairs_exact(fmt):
     from fp8_quantization_amd import _lib
     from fp8_quantization_amd.approx_ops import dense_matmul
     pairs = [(i, j) for i in range(32) for j in range(32) if i != j]
-    lo = 2.0 ** -9 if fmt == "e4m3" else 2.0 ** -14
+    lo = 2.0 ** -9 if fmt == "e4m3" else 2.0 ** -14  # (bf16: 2^-14 too)
     A = np.zeros((len(pairs), 64), np.float32)
     for r, (i, j) in enumerate(pairs):
         A[r, i] = 256.0
@@ -234,9 +240,23 @@ def test_wide_range_pairs_exact(fmt):
         A[r, 32 + i] = lo
     B = np.ones((64, 16), np.float32)
     _stats()
-    C = dense_matmul(torch.from_numpy(A).to(DEV), torch.from_numpy(B).to(DEV),
-                     _lib.DENSE_E4M3 if fmt == "e4m3" else _lib.DENSE_E5M2).cpu().numpy()
+    C = dense_matmul(torch.from_numpy(A).to(DEV), torch.from_numpy(B).to(DEV), _fmt(fmt)).cpu().numpy()
     assert _stats()["fp32_units"] == 0
     want = np.float32(512.0 + 2 * lo)
     bad = [pairs[r] for r in range(len(pairs)) if C[r, 0] != want]
     assert not bad, f"{len(bad)} pairs lose the small product, e.g. {bad[:8]}"
+
+
+def test_bf16_form_has_no_range_limit():
+    """The bf16 form holds a whole E4M3 tensor's range (and E3M4 / E2M5 values) in one block:
+    no fp32 units where the e4m3 form needs them."""
+    from fp8_quantization_amd import _lib
+    from fp8_quantization_amd.approx_ops import dense_matmul
+    for (E, M) in ((4, 3), (3, 4), (2, 5)):
+        A, B = _operands(300, 256, 96, E, M, E)
+        A[:, 0] = np.float32(1.875 * 2.0 ** 3)
+        A[:, 1] = np.float32(2.0 ** -14)
+        _stats()
+        C = dense_matmul(torch.from_numpy(A).to(DEV), torch.from_numpy(B).to(DEV), _lib.DENSE_BF16).cpu().numpy()
+        assert _stats()["fp32_units"] == 0
+        _check(C, A, B)

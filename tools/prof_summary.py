@@ -34,7 +34,11 @@ def main():
     ap.add_argument("--trace", required=True)
     ap.add_argument("--stats")
     ap.add_argument("--pmc", nargs="*", default=[])
-    ap.add_argument("--timed-launches", type=int, required=True)
+    ap.add_argument("--timed-launches", type=int, default=0,
+                    help="the last N dispatches of --kernel are the timed ones (0: use --forwards)")
+    ap.add_argument("--forwards", default="",
+                    help="TRACE_FORWARDS:TIMED[,PMC_FORWARDS:TIMED]: every forward launches --kernel equally "
+                         "often, so the timed dispatches are the last total x TIMED / FORWARDS")
     ap.add_argument("--out", required=True)
     ap.add_argument("--note", default="")
     ap.add_argument("--pmc-json", default="", help="also write the per-launch PMC summary bench.py reads")
@@ -44,13 +48,17 @@ def main():
     ap.add_argument("--M", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256, help="images per step of the profiled bench run")
     ap.add_argument("--op-kernels", default=OP_KERNELS)
+    ap.add_argument("--pmc-launches", type=int, default=0,
+                    help="average PMC counters over the last N dispatches of --kernel per file (0 = all)")
     a = ap.parse_args()
     KERNEL = a.kernel
 
     trace = read_csv(a.trace)
     rows = [r for r in trace if KERNEL in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    timed = rows[-a.timed_launches:]
+    fw = [tuple(int(x) for x in f.split(":")) for f in a.forwards.split(",") if f]
+    n_timed = a.timed_launches or (len(rows) * fw[0][1] // fw[0][0] if fw else len(rows))
+    timed = rows[-n_timed:]
     durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in timed]
     # the op window: from the first timed dispatch's preceding pre-decode (if any) to the end
     t0 = int(timed[0]["Start_Timestamp"]) if timed else 0
@@ -67,11 +75,18 @@ def main():
     if a.stats:
         res["stats_top"] = [dict(name=r["Name"][:120], calls=int(r["Calls"]), avg_ns=float(r["AverageNs"]),
                                  pct=float(r["Percentage"])) for r in read_csv(a.stats)[:8]]
+    # per counter file: the LAST --pmc-launches dispatches of KERNEL (the PMC runs' timed steps;
+    # averaging over every dispatch would mix in the calibration pass's smaller launches)
     counters = collections.defaultdict(list)
     for p in a.pmc:
+        per = collections.defaultdict(lambda: collections.defaultdict(float))
         for r in read_csv(p):
             if KERNEL in r.get("Kernel_Name", ""):
-                counters[r["Counter_Name"]].append(float(r["Counter_Value"]))
+                per[int(r.get("Dispatch_Id", r.get("Correlation_Id", 0)))][r["Counter_Name"]] += float(r["Counter_Value"])
+        keep = a.pmc_launches or (len(per) * fw[1][1] // fw[1][0] if len(fw) > 1 else 0)
+        for d in sorted(per)[-keep:] if keep > 0 else sorted(per):
+            for k, v in per[d].items():
+                counters[k].append(v)
     if counters:
         res["pmc_avg_per_dispatch"] = {k: sum(v) / len(v) for k, v in counters.items()}
         pm = res["pmc_avg_per_dispatch"]
