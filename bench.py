@@ -140,15 +140,19 @@ def build_workload(arch, cfg, bn_batches=0, device=None):
     return VitFc(), (197, 768), "vit_b16 fc1 (768x3072 QCustomLinearTorch, 197 tokens/image)"
 
 
-PMC_FILES = ("pmc_r02b.json", "pmc_r02.json", "pmc_r01.json")
+def pmc_files():
+    """Committed PMC summaries, newest round first (profiles/pmc_r<NN>[...].json)."""
+    import glob
+    return sorted((os.path.basename(f) for f in glob.glob(os.path.join(ROOT, "profiles", "pmc_r*.json"))),
+                  key=lambda n: (n[5:7], n), reverse=True)
 
 
 def pmc_traffic(kernel, arch, E, M, batch):
     """Per-launch HBM bytes of the approx GEMM kernel from a committed rocprofv3 PMC summary
-    (profiles/pmc_<round>.json, tools/prof_summary.py) recorded for this same kernel, workload,
+    (profiles/pmc_r<round>*.json, tools/prof_summary.py) recorded for this same kernel, workload,
     format and batch (summaries without a batch field were taken at 256); None when no such
     summary exists."""
-    for name in PMC_FILES:
+    for name in pmc_files():
         try:
             with open(os.path.join(ROOT, "profiles", name)) as f:
                 j = json.load(f)
