@@ -173,6 +173,8 @@ struct GemmArgs {
     int wfmt;          // pre-decoded operand format: 0 = gemm_f8mx_kernel's, 1 = gemm_tt_kernel's, 2 = gemm_tt16_kernel's,
                        // 3 = gemm_oh_kernel's (u16 A codes in the same image layout, gemm_oh.h)
     int ttf7;          // gemm_tt_kernel: the table has negative entries (the F7 sign rule)
+    int af32;          // gemm_f8mx_kernel reads A as fp32 and decodes it while staging (no A pre-pass)
+    int xncg;          // gemm_f8mx_kernel's column groups per tile (4: 128 x 64, 2: 128 x 32, 1: 256 x 16)
     const uint2 *bqw;
     // the one-hot E4M3 path (gemm_oh.h): B codes [npad][kpad] (u8), B block scales [npad][kpad / 4]
     // (E8M0), the sorted candidate lists [kpad][npad / 64][64] (u32) and their count blocks
@@ -1210,6 +1212,39 @@ static void launch_fast_t(int mode, const GemmArgs &a, dim3 grid, hipStream_t s)
     }
 }
 
+template <int NCG, int RB>
+static void launch_f8mx_t(const GemmArgs &a, hipStream_t s) {
+    using Cf = XmCfg<NCG, RB>;
+    const int64_t xt = ((a.M + Cf::BMT - 1) / Cf::BMT) * ((a.N + Cf::BNT - 1) / Cf::BNT);
+    const dim3 g((unsigned)(xt * a.splits));
+    if (a.af32) gemm_f8mx_kernel<NCG, RB, true><<<g, Cf::NT, 0, s>>>(a);
+    else gemm_f8mx_kernel<NCG, RB, false><<<g, Cf::NT, 0, s>>>(a);
+}
+static void launch_f8mx(const GemmArgs &a, hipStream_t s) {
+    if (a.xncg == 1) launch_f8mx_t<1, 4>(a, s);
+    else if (a.xncg == 2) launch_f8mx_t<2, 4>(a, s);
+    else launch_f8mx_t<4, 8>(a, s);
+}
+
+// gemm_f8mx_kernel's tile width: the fewest padded columns, ties to the wider tile (N = 16 -> 16,
+// 24 / 32 / 96 / 160 -> 32, multiples of 64 -> 64).  Option "xm_ncg" / FP8A_XM_NCG=<1|2|4> forces it
+// (0 = this choice; A/B runs and identity tests).
+static int g_opt_xm_ncg = getenv("FP8A_XM_NCG") ? atoi(getenv("FP8A_XM_NCG")) : 0;  // option "xm_ncg"
+static int xm_ncg(int64_t N) {
+    const int forced = g_opt_xm_ncg;
+    if (forced == 1 || forced == 2 || forced == 4) return forced;
+    int best = 4;
+    int64_t bp = (N + 63) / 64 * 64;
+    for (int c : {2, 1}) {
+        const int64_t pad = (N + 16 * c - 1) / (16 * c) * (16 * c);
+        if (pad < bp) {
+            bp = pad;
+            best = c;
+        }
+    }
+    return best;
+}
+
 static void launch_fast(int mode, const GemmArgs &a, hipStream_t s) {
     const int64_t tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
     dim3 grid((unsigned)(tiles * a.splits));
@@ -1238,9 +1273,8 @@ static void launch_fast(int mode, const GemmArgs &a, hipStream_t s) {
     if (mode == TM_F8) {  // s2n + qbma, no golden clip (selected in run_gemm)
         // matrix-core accumulation on pre-decoded operands (gemm_f8mx.h) when run_gemm staged
         // them, else the VALU-accumulating form
-        if (a.aw) {
-            const int64_t xt = ((a.M + XM_BM - 1) / XM_BM) * ((a.N + BN - 1) / BN);
-            gemm_f8mx_kernel<<<dim3((unsigned)(xt * a.splits)), XM_NT, 0, s>>>(a);
+        if (a.aw || a.af32) {
+            launch_f8mx(a, s);
         }
         else
             gemm_fast_kernel<true, true, false, TM_F8><<<grid, NT, 0, s>>>(a);
@@ -1275,6 +1309,10 @@ static bool g_opt_one_hot = getenv("FP8A_ONE_HOT") != nullptr && atoi(getenv("FP
 // "oh_correct" (diagnostics): 0 skips the one-hot path's correction kernel (dense terms only)
 static bool g_opt_oh_correct = true;
 static bool g_opt_oh_stats = false;  // "oh_stats": the one-hot kernels count into g_ohstat
+// "dwx": the band-staged depthwise kernel (conv_dwx_kernel) instead of the word-image form
+// conv_tbx_kernel.  Default OFF: measured 1.3x slower on MobileNetV2; FP8A_DWX=1
+// turns it on at load.
+static bool g_opt_dwx = getenv("FP8A_DWX") != nullptr && atoi(getenv("FP8A_DWX")) != 0;
 
 // Compute units of the current device (cached); 256 (MI355X) when no device is visible.
 static int device_cus() {
@@ -1480,6 +1518,24 @@ static int64_t xm_a_words(const GemmArgs &a) {
     return (a.M / (a.Ho * a.Wo)) * a.aw_c * w.H * w.W;
 }
 
+// gemm_f8mx_kernel reads A as fp32 and decodes it while staging (no xm_decode_a pass) for a 1x1
+// unpadded conv or a matrix A whose source lies within 32-bit byte offsets, when the launch has at
+// most FP8A_AF32_MAXCT column tiles (default 4; 0 = never): each column tile decodes its A
+// elements again (~25 VALU operations each), against the pre-pass's 8 B of HBM traffic per element
+// (MobileNetV2's projections: 2.9 ms of pre-pass per forward at batch 512).
+static int g_opt_af32_maxct = getenv("FP8A_AF32_MAXCT") ? std::max(0, atoi(getenv("FP8A_AF32_MAXCT"))) : 4;
+static bool xm_af32(const GemmArgs &a) {
+    const int maxct = g_opt_af32_maxct;  // option "af32_maxct"
+    const int64_t bnt = 16 * a.xncg, ct = (a.N + bnt - 1) / bnt;
+    if (ct > maxct) return false;
+    if (a.conv) {
+        if (a.kh != 1 || a.kw != 1 || a.ph != 0 || a.pw != 0) return false;
+        const int64_t bn = a.M / (a.Ho * a.Wo);
+        return bn * a.Cin * a.H * a.W * 4 < (1ll << 32);
+    }
+    return a.A != nullptr && a.M * a.lda * 4 < (1ll << 32) && a.lda >= a.K;
+}
+
 // Fast tiled kernel + gated exact kernel (int-bias path), or the exact kernel alone (tb path).
 static int run_qamaa(GemmArgs &a, hipStream_t s);
 
@@ -1619,9 +1675,11 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
             a.ttf7 = 0;
             for (int i = 0; tt && i < (1 << (2 * a.Mw)); ++i) a.ttf7 |= a.tab.raw[i] < 0;
             a.wfmt = tt ? (tt16_form(a.Mw, a.ttf7, a.K) ? 2 : 1) : 0;
+            a.xncg = tt ? 4 : xm_ncg(a.N);
+            a.af32 = !tt && xm_af32(a) ? 1 : 0;
             const int64_t rows = a.conv ? a.M / (a.Ho * a.Wo) : a.M, cols = a_words / std::max<int64_t>(rows, 1);
             const dim3 ga((unsigned)std::min<int64_t>((cols + 255) / 256, 64), (unsigned)std::min<int64_t>(rows, 1024));
-            xm_decode_a<<<ga, 256, 0, s>>>(a);
+            if (!a.af32) xm_decode_a<<<ga, 256, 0, s>>>(a);
             if (tt) {  // B words [Kpad][Npad] (the same bytes as the E4M3 pair grid) + the static image
                 const unsigned gb = (unsigned)std::min<int64_t>((kpad * npad + 255) / 256, 4096);
                 tt_decode_b<<<gb, 256, 0, s>>>(a, kpad);  // (+ gemm_tt16_kernel's f16 image when wfmt == 2)
@@ -1774,6 +1832,21 @@ int fp8a_set_option(const char *name, int value) {
     if (strcmp(name, "oh_stats") == 0) {
         const int old = g_opt_oh_stats ? 1 : 0;
         g_opt_oh_stats = value != 0;
+        return old;
+    }
+    if (strcmp(name, "xm_ncg") == 0) {
+        const int old = g_opt_xm_ncg;
+        g_opt_xm_ncg = value;
+        return old;
+    }
+    if (strcmp(name, "af32_maxct") == 0) {
+        const int old = g_opt_af32_maxct;
+        g_opt_af32_maxct = std::max(0, value);
+        return old;
+    }
+    if (strcmp(name, "dwx") == 0) {
+        const int old = g_opt_dwx ? 1 : 0;
+        g_opt_dwx = value != 0;
         return old;
     }
     if (strcmp(name, "oh_correct") == 0) {
@@ -1980,6 +2053,43 @@ int fp8a_conv2d(const float *x, const float *w, float *y, int64_t Bn, int64_t Ci
 // (fp8_quantizer.py:97-173, per tensor) is applied inside the matrix-core / tensor-bias-table
 // pre-decodes (its bias written to fqb / fqi, which serve as bA), or -- for every other path --
 // into xq (numel(x) floats) by one fake-quant pass first.
+// Band shape of conv_dwx_kernel: NP planes x RG row groups of 4 output rows per 256-thread
+// workgroup, one thread per output column and row group; the shape maximises the fraction of busy
+// threads (rows past Ho in the last band, threads past NP * RG * Wo) within the LDS budget.
+static bool dwx_config(int64_t planes, int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo, int kh, int S, int ph,
+                       int pw, int dh, DwxArgs &d) {
+    if (kh != 3 || dh != 1 || Wo > 256 || H >= (1 << 30) || W >= (1 << 30)) return false;
+    const int IC = (int)(Wo - 1) * S + 3;
+    double best = 0.0;
+    int brg = 0, bnp = 0;
+    for (int rg = 1; rg * Wo <= 256 && 4 * (rg - 1) < Ho; ++rg) {
+        const int IR = (4 * rg - 1) * S + 3;
+        for (int np = 1; np * rg * Wo <= 256; ++np) {
+            if ((int64_t)np * IR * IC > DWX_LDS_WORDS) break;
+            const int64_t bands = (Ho + 4 * rg - 1) / (4 * rg);
+            const double eff = (double)Ho / (double)(bands * 4 * rg) * (double)(np * rg * Wo) / 256.0;
+            if (eff > best + 1e-9) {
+                best = eff;
+                brg = rg;
+                bnp = np;
+            }
+        }
+    }
+    if (brg == 0) return false;
+    d.planes = planes;
+    d.C = (int32_t)C; d.H = (int32_t)H; d.W = (int32_t)W; d.Ho = (int32_t)Ho; d.Wo = (int32_t)Wo;
+    d.kh = kh; d.ph = ph; d.pw = pw; d.dh = dh;
+    d.RG = brg; d.TH = 4 * brg; d.NP = bnp;
+    d.bands = (int32_t)((Ho + d.TH - 1) / d.TH);
+    d.IR = (d.TH - 1) * S + 3;
+    d.IC = IC;
+    fastdiv_params((uint32_t)d.IC, d.ic_mul, d.ic_shift);
+    fastdiv_params((uint32_t)d.IR, d.ir_mul, d.ir_shift);
+    fastdiv_params((uint32_t)(brg * Wo), d.tg_mul, d.tg_shift);
+    fastdiv_params((uint32_t)Wo, d.ng_mul, d.ng_shift);
+    return ((planes + bnp - 1) / bnp) * d.bands < (1ll << 31);
+}
+
 static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
                        int64_t Cout, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw, int groups,
                        int E, int Mw, const int32_t *bA, const int32_t *bW, const int32_t *bR, const int32_t *table,
@@ -2029,11 +2139,31 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
                             (flags & F_QBMA) && kw == 3 && dw == 1 && sh == sw && (sw == 1 || sw == 2) &&
                             items < (1ll << 31) && Ho * Wo < (1ll << 31) &&
                             workspace_bytes >= FLAG_BYTES + (size_t)(Bn * Cin * H * W) * 4;
-        if (fq.mx && !tbx_ok) {
+        // depthwise (one input channel per group): the band-staged form reading fp32 directly
+        // (conv_dwx_kernel), same terms and sum order as conv_tbx_kernel
+        DwxArgs da;
+        const bool dwx_ok = fast_ok && g_opt_dwx && E == 4 && Mw == 3 && (mode == TM_NONE || mode == TM_W1U) &&
+                            (flags & F_QBMA) && kw == 3 && dw == 1 && sh == sw && (sw == 1 || sw == 2) && cig == 1 &&
+                            Bn * Cin < (1ll << 40) && dwx_config(Bn * Cin, Cin, H, W, Ho, Wo, kh, sw, ph, pw, dh, da);
+        if (fq.mx && !tbx_ok && !dwx_ok) {
             rc = materialize();
             if (rc) return rc;
         }
-        if (tbx_ok) {
+        if (dwx_ok) {
+            gate = (uint32_t *)workspace;
+            if (hipMemsetAsync(gate, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a gate reset");
+            const unsigned gb = (unsigned)(((da.planes + da.NP - 1) / da.NP) * da.bands);
+            const size_t lds = (size_t)(((da.NP * da.IR * da.IC + 1) & ~1) + 2 * da.NP * kh * 3) * 4;
+            if (sw == 1)
+                conv_dwx_kernel<1><<<gb, 256, lds, s>>>(x, w, y, da, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi, fq,
+                                                      fqb, fqi);
+            else
+                conv_dwx_kernel<2><<<gb, 256, lds, s>>>(x, w, y, da, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi, fq,
+                                                      fqb, fqi);
+            if (fq.mx) bA = fqi;
+            rc = hip_check("fp8a_conv2d (depthwise, E4M3 table form, band-staged)");
+            if (rc) return rc;
+        } else if (tbx_ok) {
             gate = (uint32_t *)workspace;
             uint32_t *aw = (uint32_t *)((char *)workspace + FLAG_BYTES);
             if (hipMemsetAsync(gate, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a gate reset");

@@ -60,26 +60,44 @@ constexpr uint32_t XM_ROW_SHIFT = 3, XM_ROW_MASK = 0x78u;  // A word bits 3-6: r
 constexpr int XBK = 8;                         // K-steps per staged tile
 constexpr int XM_TTK = 16 * 32 + 16;           // tile-table words per K-step: [tx 16][row 16][j 2] + bank shift
 constexpr uint32_t XM_ZERO_WORD = 254u << 23;  // A = 0: cvt scale 2^127 (the code is 0), row 0
+constexpr int XM_CP = BN + 1;  // the 64-column epilogue slices of the other kernels: [64][BN + 1] floats
+
+// Tile shapes of gemm_f8mx_kernel<NCG, RB, AF32>: 4 waves; NCG column groups of 16 columns x
+// (4 / NCG) row groups of RB 16-row blocks.  NCG = 4 (128 x 64) is the round-2 kernel; the narrow
+// shapes (128 x 32, 256 x 16) serve layers with N = 16 / 24 / 32 / 96 / 160 (MobileNetV2's
+// projections), where a 64-column tile converted up to 4x the products the layer has.
 // A words in LDS: [kk / 2][row][kk % 2] -- one ds_write_b64 stores (and one ds_read_b64 reads) a
 // row's words of a K-step pair; the pair arrays sit 32 banks apart, so the math loop's reads
-// (lane groups of K-step pairs g, g + 1) and the staging's stores are conflict-free
-#ifndef XM_RB
-#define XM_RB 8  // 16-row blocks per wave
-#endif
-#ifndef XM_NWV
-#define XM_NWV 4  // waves per workgroup: 4 column groups x XM_NWV / 4 row groups
-#endif
-constexpr int XM_NT = 64 * XM_NWV;               // threads per workgroup
-constexpr int XM_BM = 16 * XM_RB * (XM_NWV / 4);  // tile rows
-static_assert((XM_RB == 4 || XM_RB == 8) && (XM_NWV == 4 || XM_NWV == 8), "gemm_f8mx_kernel tile shape");
-constexpr int XM_AWQ = 2 * XM_BM + 32;
-struct XmSmem {
-    uint32_t tt[XBK][XM_TTK];  // c_b-applied pairs [kk][tx][row][j] (first: its byte offsets are the reads' immediates)
-    uint32_t lut[XM_LUT_WORDS];
-    uint32_t aw[XBK / 2][XM_AWQ];  // A(m, k)'s word: cvt scale exponent << 23 | row << 3
+// (lane groups of K-step pairs g, g + 1) and the staging's stores are conflict-free.
+template <int NCG, int RB>
+struct XmCfg {
+    static constexpr int NT = 256;
+    static constexpr int BNT = 16 * NCG;          // tile columns
+    static constexpr int RG = 4 / NCG;            // row groups
+    static constexpr int BMT = 16 * RB * RG;      // tile rows
+    static constexpr int TXN = 4 * NCG;           // 4-column blocks of the tile table
+    // tile-table words per K-step: [tx][row 16][j 2] + a shift putting odd K-steps >= 16 banks over
+    static constexpr int TTK = TXN * 32 + 16;
+    static constexpr int AWQ = 2 * BMT + 32;
+    static constexpr int APR = BMT / 64;          // A rows per staging thread
+    static constexpr int NBU = 32 * TXN;          // table-build units per staged tile (8 K-steps x TXN x 4)
+    static constexpr int BU = (NBU + NT - 1) / NT;
+    static_assert(NT % (8 * TXN) == 0, "build units: one column block per thread");
+    static constexpr int SR = 4096 / BNT;         // epilogue slab: SR rows x BNT columns = 16 outputs per thread
+    static constexpr int CP = BNT + 1;
+    struct Stage {
+        uint32_t tt[XBK][TTK];  // c_b-applied pairs [kk][tx][row][j] (first: its byte offsets are the reads' immediates)
+        uint32_t lut[XM_LUT_WORDS];
+        uint32_t aw[XBK / 2][AWQ];  // A(m, k)'s word: cvt scale exponent << 23 | row << 3
+    };
+    union Smem {
+        Stage st;
+        float ct[SR * CP];  // epilogue transpose slab, aliased on the staging LDS
+    };
+    static_assert(NCG == 1 || NCG == 2 || NCG == 4, "column groups");
+    static_assert(BMT % 64 == 0 && BMT % SR == 0, "tile rows");
+    static_assert((TTK % 64) >= 16 && (TTK % 64) <= 48, "odd K-steps of the table build must not share banks");
 };
-constexpr int XM_CP = BN + 1;  // epilogue transpose slice [64][BN + 1] floats, aliased on XmSmem
-static_assert(sizeof(float) * 64 * XM_CP <= sizeof(XmSmem), "epilogue slice must fit the staging LDS");
 
 // Exactness / range window shared by the pre-passes (as bias_ok in gemm_fast_kernel)
 __device__ __forceinline__ bool xm_bias_ok(int b) { return b >= -100 && b <= 120; }
@@ -310,7 +328,8 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
 // ((s_b << 15) + (e_b << 7) per bf16 half, 0 for a zero B) and the pair's byte offset in the
 // static table ((code0 + 9 code1) * 32); out-of-range elements are zeros.
 __global__ __launch_bounds__(256) void xm_decode_b(const GemmArgs p, int64_t kpad) {
-    const int bA = *p.bA, bR = *p.bR;
+    // (af32: A's bias -- maybe the fused input quantizer's, not written yet -- is checked by the GEMM)
+    const int bA = p.af32 ? 0 : *p.bA, bR = *p.bR;
     const bool biasbad = !(xm_bias_ok(bA) && xm_bias_ok(bR));
     bool bad = biasbad;
     const int64_t hq = p.npad / 2, n = kpad * hq;
@@ -355,81 +374,122 @@ __global__ __launch_bounds__(256) void xm_decode_b(const GemmArgs p, int64_t kpa
 #ifndef XM_WAVES
 #define XM_WAVES 6  // register bound: 80 VGPRs, 6 waves / SIMD (the LDS allows 6 workgroups / CU)
 #endif
-// The GEMM.  Tile XM_BM x 64 (128 x 64), XM_NWV waves (4); wave wv = column group wc = wv & 3
-// (the 16 columns 16 wc .. 16 wc + 15, column blocks tx = 4 wc + c of the tile table) and row
-// group wr = wv >> 2 (16 XM_RB rows).  Math mapping: lane = (row r16 of each of the wave's XM_RB
-// 16-row blocks, K-step pair g of the 8-step tile).  Per A element (row, K-step): ONE v_and_or_b32 (row offset | the
-// wave's column base + the K-step's table offset; block c in the reads' immediates), four
-// ds_read_b64 (16 columns), eight conversions; per 16-row block and tile one 16x16x128 MFMA sums
-// the 4 lane groups' 2 K-steps.  Operands are read through buffer descriptors: uniform K-step
-// offsets in SGPRs, 32-bit lane offsets (run_gemm keeps the word images below 2^32 bytes); the
+// The GEMM.  Tile BMT x BNT (XmCfg), 4 waves; wave wv = column group wc = wv % NCG (the 16
+// columns 16 wc .. 16 wc + 15, column blocks tx = 4 wc + c of the tile table) and row group
+// wr = wv / NCG (16 RB rows).  Math mapping: lane = (row r16 of each of the wave's RB 16-row
+// blocks, K-step pair g of the 8-step tile).  Per A element (row, K-step): ONE v_and_or_b32 (row
+// offset | the wave's column base + the K-step's table offset; block c in the reads' immediates),
+// four ds_read_b64 (16 columns), eight conversions; per 16-row block and tile one 16x16x128 MFMA
+// sums the 4 lane groups' 2 K-steps.  Operands are read through buffer descriptors: uniform
+// K-step offsets in SGPRs, 32-bit lane offsets (run_gemm keeps the images below 2^32 bytes); the
 // conv word image carries the zero padding (xm_decode_a), so the gather has no bounds checks.
-__global__ __launch_bounds__(XM_NT, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs p) {
-    __shared__ __attribute__((aligned(16))) XmSmem sm;
+//
+// AF32: A is read as fp32 straight from its source (a 1x1 / unpadded conv's x, or the matrix A)
+// and turned into its word while it is staged -- the fused input quantizer, the on-grid / window
+// checks and the fallback marks included -- instead of by the xm_decode_a pre-pass.  That pass
+// writes and re-reads 8 B per A element through HBM; staging-time decoding costs ~25 VALU
+// operations per element per column tile, the cheaper choice up to a few column tiles (run_gemm).
+template <int NCG, int RB, bool AF32>
+__global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs p) {
+    using Cf = XmCfg<NCG, RB>;
+    constexpr int NT = Cf::NT, BMT = Cf::BMT, BNT = Cf::BNT, TTK = Cf::TTK, APR = Cf::APR;
+    constexpr int BU = Cf::BU, NBU = Cf::NBU, TXN = Cf::TXN, SR = Cf::SR, CP = Cf::CP;
+    __shared__ __attribute__((aligned(16))) typename Cf::Smem smu;
+    auto &sm = smu.st;
     FP8A_CLK_BEGIN
 
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wvu = __builtin_amdgcn_readfirstlane(wv);
-    const int wc = wvu & 3, wr = wvu >> 2;  // the wave's column group and row group
-    const int64_t num_mt = (p.M + XM_BM - 1) / XM_BM;
-    const int64_t tiles = num_mt * ((p.N + BN - 1) / BN);
+    const int wc = wvu % NCG, wr = wvu / NCG;  // the wave's column group and row group
+    const int64_t num_mt = (p.M + BMT - 1) / BMT;
+    const int64_t tiles = num_mt * ((p.N + BNT - 1) / BNT);
     const int64_t bid = (int64_t)blockIdx.x % tiles, split = (int64_t)blockIdx.x / tiles;
-    const int64_t m0 = (bid % num_mt) * XM_BM;
-    const int64_t n0 = (bid / num_mt) * BN;
+    const int64_t m0 = (bid % num_mt) * BMT;
+    const int64_t n0 = (bid / num_mt) * BNT;
     const int kbeg = (int)(split * p.kchunk), kend = (int)min(p.K, (int64_t)kbeg + p.kchunk), K32 = (int)p.K;
     const int bR = *p.bR;
+    // AF32: the A operand's bias (the fused input quantizer's, written once for the gated kernels)
+    float fmx = 0.0f, fbias = 0.0f;
+    int bA = 0;
+    bool abad = false, biasbad = false;
+    if (AF32) {
+        fmx = p.fqin.mx ? *p.fqin.mx : 0.0f;
+        fbias = p.fqin.mx ? fq_bias(fmx, p.fqin.E, p.fqin.M) : 0.0f;
+        bA = p.fqin.mx ? (int)fbias : *p.bA;
+        if (p.fqin.mx && blockIdx.x == 0 && tid == 0) {
+            *p.fq_bias = fbias;
+            *p.fq_ibias = bA;
+        }
+        biasbad = !(xm_bias_ok(bA) && xm_bias_ok(bR));  // every output unit falls back
+    }
+    const uint32_t emnA = (uint32_t)(128 - bA) << 23;
 
     // table: copied from the launch's pre-computed image (xm_decode_b), 16-B per thread and step
-    for (int e = 4 * tid; e < XM_LUT_WORDS; e += 4 * XM_NT)
+    for (int e = 4 * tid; e < XM_LUT_WORDS; e += 4 * NT)
         *reinterpret_cast<uint4 *>(&sm.lut[e]) = *reinterpret_cast<const uint4 *>(&p.lutw[e]);
 
-    // tile-table build units e = tid + XM_NT u (512 per tile): (m_a pair q4, column block btx,
+    // tile-table build units e = tid + NT u (NBU per tile): (m_a pair q4, column block btx,
     // K-step bkk[u]); the 8 lanes of a ds_write_b128 group are 4 q4 x an even and an odd K-step
-    // (16 banks apart)
-    constexpr int BU = 512 / XM_NT;
+    // (>= 16 banks apart)
     const uint32_t hq8 = (uint32_t)(p.npad / 2) * 8u;  // bytes per K-step of the B pair grid
-    const int q4 = tid & 3, btx = (tid >> 3) & 15;
+    // (NT is a multiple of 8 TXN, so the unit's column block is the same for every u)
+    const int q4 = tid & 3, btx = (tid >> 3) % TXN;
     int bkk[BU];
     uint32_t boff[BU];
 #pragma unroll
     for (int u = 0; u < BU; ++u) {
-        const int e = tid + XM_NT * u;
-        bkk[u] = 2 * (e >> 7) + ((e >> 2) & 1);
+        const int e = min(tid + NT * u, NBU - 1);
+        bkk[u] = 2 * (e / (8 * TXN)) + ((e >> 2) & 1);
         boff[u] = (uint32_t)(kbeg + bkk[u]) * hq8 + (uint32_t)(n0 / 2 + 2 * btx) * 8u;  // pair 2 btx: 16-B aligned
     }
+    const bool build = NBU % NT == 0 || tid < NBU;  // (NCG = 1: half the threads build)
     const __amdgpu_buffer_rsrc_t brsrc =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint2 *>(p.bqw), (short)0, -1, 0x00020000);
 
-    // A staging: thread = (rows arow + XM_NT / 4 i, K-step pair kp), K-steps 2 kp + r.  conv:
-    // lane = row (consecutive pixels), kp = the wave's column group (wave-uniform: the k -> (c, ky,
-    // kx) split and the word offset run on the scalar unit); matrix: four threads per row.  Rows
-    // past M re-read row M - 1 (store_tile drops them).
-    constexpr int APR = XM_BM * 4 / XM_NT;  // rows per thread
-    const int arow = p.conv ? (lane + 64 * wr) : (tid >> 2), akp = p.conv ? wc : (tid & 3);
+    // A staging: thread = (rows arow + 64 i, K-step pair akp), K-steps 2 akp + r.  conv: lane =
+    // row (consecutive pixels), akp = the wave (wave-uniform: the k -> (c, ky, kx) split and the
+    // word offset run on the scalar unit); matrix: four threads per row.  Rows past M re-read row
+    // M - 1 (store_tile drops them).
+    const int arow = p.conv ? lane : (tid >> 2), akp = p.conv ? wvu : (tid & 3);
     uint32_t aoff[APR];
-    const uint32_t phw = (uint32_t)(p.awH * p.awW), uW = (uint32_t)p.awW;
+    const uint32_t phw = AF32 ? (uint32_t)(p.H * p.W) : (uint32_t)(p.awH * p.awW), uW = (uint32_t)p.awW;
 #pragma unroll
     for (int i = 0; i < APR; ++i) {
-        const int64_t m = min(m0 + arow + (XM_NT / 4) * i, p.M - 1);
+        const int64_t m = min(m0 + arow + 64 * i, p.M - 1);
         if (p.conv) {
             const int64_t hw = p.Ho * p.Wo, img = m / hw, pix = m - img * hw, ho = pix / p.Wo, wo = pix - ho * p.Wo;
-            aoff[i] = (uint32_t)(4 * (img * p.aw_c * (int64_t)phw + ho * p.sh * p.awW + wo * p.sw + (p.awpw - p.pw)));
+            if (AF32)  // 1x1, unpadded: x[img][cbase + k][ho sh][wo sw]
+                aoff[i] = (uint32_t)(4 * ((img * p.Cin + p.cbase) * (int64_t)phw + ho * p.sh * p.W + wo * p.sw));
+            else
+                aoff[i] = (uint32_t)(4 * (img * p.aw_c * (int64_t)phw + ho * p.sh * p.awW + wo * p.sw + (p.awpw - p.pw)));
         } else {
-            aoff[i] = (uint32_t)(4 * (m * p.awld + 2 * akp));
+            aoff[i] = (uint32_t)(4 * (m * (AF32 ? p.lda : p.awld) + 2 * akp));
         }
     }
     const __amdgpu_buffer_rsrc_t arsrc =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(p.aw), (short)0, -1, 0x00020000);
+        AF32 ? __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p.conv ? p.X : p.A), (short)0, -1, 0x00020000)
+             : __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(p.aw), (short)0, -1, 0x00020000);
     const int khw = p.kh * p.kw;
     uint32_t wa[APR][2];
     uint4 wbq[BU];
     auto load_tile = [&](int k0) {
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
+            if (AF32 && !p.conv) {
+                // matrix rows: k = k0 + 2 akp + r per lane, clamped to the row's last element (the
+                // value is replaced at staging) so that no load leaves the row
+                const uint32_t k = (uint32_t)min(k0 + 2 * akp + r, K32 - 1);
+#pragma unroll
+                for (int i = 0; i < APR; ++i)
+                    wa[i][r] = __builtin_amdgcn_raw_buffer_load_b32(arsrc, (int)(aoff[i] - 8u * (uint32_t)akp + 4u * k), 0, 0);
+                continue;
+            }
             uint32_t ko;
-            if (p.conv) {
+            if (AF32) {
+                ko = 4u * (uint32_t)min(k0 + 2 * akp + r, K32 - 1) * phw;  // channel plane (wave-uniform)
+            } else if (p.conv) {
                 // wave-uniform; past the group's last channel the address stays on channel K - 1 (the
-                // word image ends there: the zero word below replaces the value)
+                // word image ends there: the zero word at staging replaces the value)
                 const int k = min(k0 + 2 * akp + r, K32 - 1);
                 const uint32_t c = fastdiv((uint32_t)k, p.kk_mul, p.kk_shift);
                 const uint32_t t = (uint32_t)k - c * (uint32_t)khw;
@@ -443,13 +503,15 @@ __global__ __launch_bounds__(XM_NT, XM_WAVES) void gemm_f8mx_kernel(const GemmAr
 #pragma unroll
             for (int i = 0; i < APR; ++i) {
                 wa[i][r] = __builtin_amdgcn_raw_buffer_load_b32(arsrc, (int)aoff[i], (int)ko, 0);
-                if (p.conv && k0 + 2 * akp + r >= K32) wa[i][r] = XM_ZERO_WORD;  // past the group's last channel (uniform)
+                if (!AF32 && p.conv && k0 + 2 * akp + r >= K32) wa[i][r] = XM_ZERO_WORD;  // past the group's last channel (uniform)
             }
         }
-        const uint32_t kb = __builtin_amdgcn_readfirstlane((uint32_t)(k0 - kbeg) * hq8);
+        if (build) {
+            const uint32_t kb = __builtin_amdgcn_readfirstlane((uint32_t)(k0 - kbeg) * hq8);
 #pragma unroll
-        for (int u = 0; u < BU; ++u)  // (add0, off0, add1, off1) of pairs 2 btx, 2 btx + 1
-            wbq[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(brsrc, (int)boff[u], (int)kb, 0));
+            for (int u = 0; u < BU; ++u)  // (add0, off0, add1, off1) of pairs 2 btx, 2 btx + 1
+                wbq[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(brsrc, (int)boff[u], (int)kb, 0));
+        }
     };
     load_tile(kbeg);
 
@@ -468,9 +530,9 @@ __global__ __launch_bounds__(XM_NT, XM_WAVES) void gemm_f8mx_kernel(const GemmAr
             sel[v] = (int)w;
         }
     }
-    xm_v4f dq[XM_RB];  // one 16x16 accumulator per 16-row block
+    xm_v4f dq[RB];  // one 16x16 accumulator per 16-row block
 #pragma unroll
-    for (int b = 0; b < XM_RB; ++b) dq[b] = (xm_v4f){0.0f, 0.0f, 0.0f, 0.0f};
+    for (int b = 0; b < RB; ++b) dq[b] = (xm_v4f){0.0f, 0.0f, 0.0f, 0.0f};
     xm_v8i av = {0, 0, 0, 0, 0, 0, 0, 0};
     const char *lut = reinterpret_cast<const char *>(sm.lut);
     const uint32_t wvo = (uint32_t)wc * 512u;  // the wave's first column block (4 wc) in a K-step of the table
@@ -478,21 +540,43 @@ __global__ __launch_bounds__(XM_NT, XM_WAVES) void gemm_f8mx_kernel(const GemmAr
     __syncthreads();  // the static table is in LDS before the first build reads it
 
     for (int k0 = kbeg; k0 < kend; k0 += XBK) {
+        if (AF32) {  // the staged values become words here (the loads above have landed)
+#pragma unroll
+            for (int i = 0; i < APR; ++i)
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    if (k0 + 2 * akp + r >= K32) {
+                        wa[i][r] = XM_ZERO_WORD;
+                    } else {
+                        float v = __uint_as_float(wa[i][r]);
+                        if (p.fqin.mx) v = fq_apply(v, fmx, fbias, p.fqin.M, p.fqin.S);
+                        bool ok = true;
+                        wa[i][r] = xm_word_a(v, emnA, bR, ok);
+                        if (!ok) {  // the output row this A row feeds (1x1 conv / matrix), as the pre-pass marks it
+                            const int64_t m = min(m0 + arow + 64 * i, p.M - 1);
+                            fb_rows(p, m, m + 1);
+                            abad = true;
+                        }
+                    }
+                }
+        }
 #pragma unroll
         for (int i = 0; i < APR; ++i)
-            *reinterpret_cast<uint2 *>(&sm.aw[akp][2 * (arow + (XM_NT / 4) * i)]) = make_uint2(wa[i][0], wa[i][1]);
+            *reinterpret_cast<uint2 *>(&sm.aw[akp][2 * (arow + 64 * i)]) = make_uint2(wa[i][0], wa[i][1]);
         // build: rows 2 q4, 2 q4 + 1 of both signs for the unit's two column pairs
+        if (build) {
 #pragma unroll
-        for (int u = 0; u < BU; ++u) {
-            const uint4 b = wbq[u];
-            const uint2 s0 = *reinterpret_cast<const uint2 *>(lut + b.y + 8 * q4);
-            const uint2 s1 = *reinterpret_cast<const uint2 *>(lut + b.w + 8 * q4);
-            const xm_u2 a0 = __builtin_bit_cast(xm_u2, b.x), a1 = __builtin_bit_cast(xm_u2, b.z);
-            const xm_u2 n0 = __builtin_bit_cast(xm_u2, b.x ^ 0x80008000u), n1 = __builtin_bit_cast(xm_u2, b.z ^ 0x80008000u);
-            auto pk = [](uint32_t v, xm_u2 ad) { return __builtin_bit_cast(uint32_t, __builtin_bit_cast(xm_u2, v) + ad); };
-            uint32_t *d = &sm.tt[bkk[u]][btx * 32 + q4 * 4];
-            *reinterpret_cast<uint4 *>(d) = make_uint4(pk(s0.x, a0), pk(s1.x, a1), pk(s0.y, a0), pk(s1.y, a1));
-            *reinterpret_cast<uint4 *>(d + 16) = make_uint4(pk(s0.x, n0), pk(s1.x, n1), pk(s0.y, n0), pk(s1.y, n1));
+            for (int u = 0; u < BU; ++u) {
+                const uint4 b = wbq[u];
+                const uint2 s0 = *reinterpret_cast<const uint2 *>(lut + b.y + 8 * q4);
+                const uint2 s1 = *reinterpret_cast<const uint2 *>(lut + b.w + 8 * q4);
+                const xm_u2 a0 = __builtin_bit_cast(xm_u2, b.x), a1 = __builtin_bit_cast(xm_u2, b.z);
+                const xm_u2 n0 = __builtin_bit_cast(xm_u2, b.x ^ 0x80008000u), n1 = __builtin_bit_cast(xm_u2, b.z ^ 0x80008000u);
+                auto pk = [](uint32_t v, xm_u2 ad) { return __builtin_bit_cast(uint32_t, __builtin_bit_cast(xm_u2, v) + ad); };
+                uint32_t *d = &sm.tt[bkk[u]][btx * 32 + q4 * 4];
+                *reinterpret_cast<uint4 *>(d) = make_uint4(pk(s0.x, a0), pk(s1.x, a1), pk(s0.y, a0), pk(s1.y, a1));
+                *reinterpret_cast<uint4 *>(d + 16) = make_uint4(pk(s0.x, n0), pk(s1.x, n1), pk(s0.y, n0), pk(s1.y, n1));
+            }
         }
         __syncthreads();
         if (k0 + XBK < kend) load_tile(k0 + XBK);  // next tile's loads fly during this tile's math
@@ -502,11 +586,11 @@ __global__ __launch_bounds__(XM_NT, XM_WAVES) void gemm_f8mx_kernel(const GemmAr
         // block's 8 K-steps (4 lane groups x 2) -- half the matrix-pipe cycles of the 32x32 form
         {
             const int r16 = lane & 15, g = lane >> 4;
-            const uint32_t base = wvo + (uint32_t)(2 * g) * (uint32_t)(XM_TTK * 4);  // multiple of 128 B
+            const uint32_t base = wvo + (uint32_t)(2 * g) * (uint32_t)(TTK * 4);  // multiple of 128 B
             const char *tt0 = reinterpret_cast<const char *>(&sm.tt[0][0]);
 #pragma unroll
-            for (int b = 0; b < XM_RB; ++b) {
-                const uint2 aw2 = *reinterpret_cast<const uint2 *>(&sm.aw[g][2 * (16 * (XM_RB * wr + b) + r16)]);
+            for (int b = 0; b < RB; ++b) {
+                const uint2 aw2 = *reinterpret_cast<const uint2 *>(&sm.aw[g][2 * (16 * (RB * wr + b) + r16)]);
                 const uint32_t awh[2] = {aw2.x, aw2.y};
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
@@ -515,7 +599,7 @@ __global__ __launch_bounds__(XM_NT, XM_WAVES) void gemm_f8mx_kernel(const GemmAr
                     __builtin_assume((a & 7u) == 0u);
                     // (volatile: otherwise the two halves, used as different types, are split into
                     // two loads and re-merged into a ds_read2_b32 -- half the LDS rate of ds_read_b64)
-                    xm_lds_u64 *ttk = (xm_lds_u64 *)(tt0 + h * XM_TTK * 4);
+                    xm_lds_u64 *ttk = (xm_lds_u64 *)(tt0 + h * TTK * 4);
                     uint2 v[4];
 #pragma unroll
                     for (int c = 0; c < 4; ++c) {
@@ -538,45 +622,46 @@ __global__ __launch_bounds__(XM_NT, XM_WAVES) void gemm_f8mx_kernel(const GemmAr
     }
 
     // a term beyond the e4m3 range came back NaN (and poisons its column): the exact kernel
-    // reruns the launch
+    // recomputes the tile; (AF32) an A operand off the grid / outside the window marked its row
+    // above, a bias outside the window every unit
     bool nan = false;
 #pragma unroll
-    for (int b = 0; b < XM_RB; ++b)
+    for (int b = 0; b < RB; ++b)
 #pragma unroll
         for (int i = 0; i < 4; ++i) nan |= __builtin_isnan(dq[b][i]);
-    if (__syncthreads_or(nan ? 1 : 0) && tid == 0) {
-        fb_tile(p, m0, XM_BM, n0);
-        atomicOr(p.flag, fb_bits(p));
+    const bool tnan = __syncthreads_or(nan ? 1 : 0) != 0;
+    const bool tbad = AF32 && __syncthreads_or((abad || biasbad) ? 1 : 0) != 0;
+    if ((tnan || tbad) && tid == 0) {
+        if (tnan) fb_tile(p, m0, BMT, n0);
+        atomicOr(p.flag, fb_bits(p, biasbad));
     }
 
     // D (units of 2^(7-bR)) of row block b: lane l holds rows 4 (l >> 4) .. + 3, column l & 15
-    // -> tile row 16 (XM_RB wr + b) + 4 (l >> 4) + i, column 16 wc + (l & 15) -> a [64][BN] slice in
-    // LDS per 64 tile rows -> each thread's 4x4 block (threads < 256), epilogue mapping with
-    // consecutive lanes on consecutive pixels
+    // -> tile row 16 (RB wr + b) + 4 (l >> 4) + i, column 16 wc + (l & 15) -> an [SR][BNT] slab in
+    // LDS per SR tile rows -> each thread's 4x4 block (64-row sub-slab sub, 4-column block cb),
+    // epilogue mapping with consecutive lanes on consecutive pixels
     const float f8S = __uint_as_float((uint32_t)min(max(134 - bR, 1), 254) << 23);
-    float *ct = reinterpret_cast<float *>(&sm);
-    const int ety = tid & 15, etx = (tid >> 4) & 15;
+    float *ct = smu.ct;
+    const int ety = tid & 15, etx = tid >> 4, cb = etx % (BNT / 4), sub = etx / (BNT / 4);
 #pragma unroll
-    for (int h = 0; h < XM_BM / 64; ++h) {
-        if (h > 0) __syncthreads();  // the previous slice is read
+    for (int h = 0; h < BMT / SR; ++h) {
+        if (h > 0) __syncthreads();  // the previous slab is read (the K loop's last barrier covers h = 0)
 #pragma unroll
-        for (int b = 0; b < XM_RB; ++b) {
-            const int rb = 16 * (XM_RB * wr + b) - 64 * h;  // the block's first row in the slice (wave-uniform)
-            if (rb >= 0 && rb < 64) {
+        for (int b = 0; b < RB; ++b) {
+            const int rb = 16 * (RB * wr + b) - SR * h;  // the block's first row in the slab (wave-uniform)
+            if (rb >= 0 && rb < SR) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                    ct[(rb + 4 * (lane >> 4) + i) * XM_CP + 16 * wc + (lane & 15)] = dq[b][i] * f8S;
+                    ct[(rb + 4 * (lane >> 4) + i) * CP + 16 * wc + (lane & 15)] = dq[b][i] * f8S;
             }
         }
         __syncthreads();
-        if (tid < NT) {
-            float acc[TM][TN];
+        float acc[TM][TN];
 #pragma unroll
-            for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-                for (int j = 0; j < TN; ++j) acc[i][j] = ct[(ety * TM + i) * XM_CP + etx * TN + j];
-            store_tile(p, split, m0 + 64 * h, n0, ety, etx, acc);
-        }
+            for (int j = 0; j < TN; ++j) acc[i][j] = ct[(64 * sub + ety * TM + i) * CP + cb * TN + j];
+        store_tile(p, split, m0 + SR * h + 64 * sub, n0, ety, cb, acc);
     }
     FP8A_CLK_END
 }

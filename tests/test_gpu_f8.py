@@ -157,11 +157,24 @@ def _sum_operands(Mr, K, N, seed):
     return A.astype(np.float32), B.astype(np.float32), bA, bB, bR
 
 
+@pytest.mark.parametrize("ncg", [4, 1])
 @pytest.mark.parametrize("case", ["term_out_of_range", "off_grid_a", "off_grid_b"])
-def test_fallback_recomputes_only_marked_units(case, path):
+def test_fallback_recomputes_only_marked_units(case, path, ncg):
+    """ncg: gemm_f8mx_kernel's tile (4: 128 x 64, 1: 256 x 16 -- option "xm_ncg")."""
     from fp8_quantization_amd import _lib
     if case == "term_out_of_range" and path == "one_hot":
         pytest.skip("the one-hot path has no e4m3 range limit (test_terms_beyond_e4m3_range)")
+    if ncg != 4 and path == "one_hot":
+        pytest.skip("tile shapes of gemm_f8mx_kernel only")
+    old_ncg = _lib.set_option("xm_ncg", ncg)
+    try:
+        _fallback_case(case, ncg)
+    finally:
+        _lib.set_option("xm_ncg", old_ncg)
+
+
+def _fallback_case(case, ncg):
+    from fp8_quantization_amd import _lib
     Mr, K, N = 520, 600, 200  # 9 x 4 output units, split-K shape
     A, B, bA, bB, bR = _sum_operands(Mr, K, N, 17)
     tab = gio.load("g2_matmul.npz")["E4M3_table_nocomp"]
@@ -185,8 +198,9 @@ def test_fallback_recomputes_only_marked_units(case, path):
     assert flag2 & 1 and not flag2 & 32, flag2  # some units, not all
     assert st["exact_launches"] == 1
     ur, uc = np.arange(Mr) // 64, np.arange(N) // 64
-    if case == "term_out_of_range":  # the 128-row tile holding (r, n) (gemm_f8mx_kernel's tile)
-        marked = ((ur[:, None] // 2) == (r // 128)) & (uc[None, :] == n // 64)
+    if case == "term_out_of_range":  # the tile holding (r, n): 128 or 256 rows (gemm_f8mx_kernel's tile)
+        tr = 128 if ncg == 4 else 256
+        marked = ((ur[:, None] // (tr // 64)) == (r // tr)) & (uc[None, :] == n // 64)
     elif case == "off_grid_a":
         marked = (ur[:, None] == r // 64) & (uc[None, :] >= 0)
     else:
