@@ -1309,10 +1309,10 @@ static bool g_opt_one_hot = getenv("FP8A_ONE_HOT") != nullptr && atoi(getenv("FP
 // "oh_correct" (diagnostics): 0 skips the one-hot path's correction kernel (dense terms only)
 static bool g_opt_oh_correct = true;
 static bool g_opt_oh_stats = false;  // "oh_stats": the one-hot kernels count into g_ohstat
-// "dwx": the band-staged depthwise kernel (conv_dwx_kernel) instead of the word-image form
-// conv_tbx_kernel.  Default OFF: measured 1.3x slower on MobileNetV2; FP8A_DWX=1
-// turns it on at load.
-static bool g_opt_dwx = getenv("FP8A_DWX") != nullptr && atoi(getenv("FP8A_DWX")) != 0;
+// "dwx": the E4M3 depthwise form -- 0 the word-image gather conv_tbx_kernel (+ tbx_decode_a),
+// 1 the band-staged conv_dwx_kernel (measured 1.3x slower on MobileNetV2), 2 the
+// fp32 gather conv_dwg_kernel.  FP8A_DW=<n> sets it at load.
+static int g_opt_dwx = getenv("FP8A_DW") ? atoi(getenv("FP8A_DW")) : 0;
 
 // Compute units of the current device (cached); 256 (MI355X) when no device is visible.
 static int device_cus() {
@@ -1845,8 +1845,8 @@ int fp8a_set_option(const char *name, int value) {
         return old;
     }
     if (strcmp(name, "dwx") == 0) {
-        const int old = g_opt_dwx ? 1 : 0;
-        g_opt_dwx = value != 0;
+        const int old = g_opt_dwx;
+        g_opt_dwx = value;
         return old;
     }
     if (strcmp(name, "oh_correct") == 0) {
@@ -2141,15 +2141,39 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
                             workspace_bytes >= FLAG_BYTES + (size_t)(Bn * Cin * H * W) * 4;
         // depthwise (one input channel per group): the band-staged form reading fp32 directly
         // (conv_dwx_kernel), same terms and sum order as conv_tbx_kernel
+        // the fp32 gather form (conv_dwg_kernel): 3x3, undilated, one input channel per group
+        DwgArgs dg;
+        const int64_t rgn = (Ho + 3) / 4, gitems = Bn * Cout * rgn * Wo;
+        const bool dwg_ok = fast_ok && g_opt_dwx == 2 && E == 4 && Mw == 3 && (mode == TM_NONE || mode == TM_W1U) &&
+                            (flags & F_QBMA) && kh == 3 && kw == 3 && dh == 1 && dw == 1 && sh == sw &&
+                            (sw == 1 || sw == 2) && cig == 1 && gitems < (1ll << 31);
         DwxArgs da;
-        const bool dwx_ok = fast_ok && g_opt_dwx && E == 4 && Mw == 3 && (mode == TM_NONE || mode == TM_W1U) &&
+        const bool dwx_ok = !dwg_ok && fast_ok && g_opt_dwx == 1 && E == 4 && Mw == 3 && (mode == TM_NONE || mode == TM_W1U) &&
                             (flags & F_QBMA) && kw == 3 && dw == 1 && sh == sw && (sw == 1 || sw == 2) && cig == 1 &&
                             Bn * Cin < (1ll << 40) && dwx_config(Bn * Cin, Cin, H, W, Ho, Wo, kh, sw, ph, pw, dh, da);
-        if (fq.mx && !tbx_ok && !dwx_ok) {
+        if (fq.mx && !tbx_ok && !dwx_ok && !dwg_ok) {
             rc = materialize();
             if (rc) return rc;
         }
-        if (dwx_ok) {
+        if (dwg_ok) {
+            gate = (uint32_t *)workspace;
+            if (hipMemsetAsync(gate, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a gate reset");
+            dg.C = (int32_t)Cout; dg.H = (int32_t)H; dg.W = (int32_t)W; dg.Ho = (int32_t)Ho; dg.Wo = (int32_t)Wo;
+            dg.ph = ph; dg.pw = pw; dg.RGn = (int32_t)rgn;
+            dg.items = (uint32_t)gitems;
+            fastdiv_params((uint32_t)Wo, dg.wo_mul, dg.wo_shift);
+            fastdiv_params((uint32_t)rgn, dg.rg_mul, dg.rg_shift);
+            const unsigned gb = (unsigned)std::min<int64_t>((gitems + 255) / 256, 16 * 1024);
+            if (sw == 1)
+                conv_dwg_kernel<1><<<gb, 256, 0, s>>>(x, w, y, dg, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi, fq,
+                                                      fqb, fqi);
+            else
+                conv_dwg_kernel<2><<<gb, 256, 0, s>>>(x, w, y, dg, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi, fq,
+                                                      fqb, fqi);
+            if (fq.mx) bA = fqi;
+            rc = hip_check("fp8a_conv2d (depthwise, E4M3 table form, fp32 gather)");
+            if (rc) return rc;
+        } else if (dwx_ok) {
             gate = (uint32_t *)workspace;
             if (hipMemsetAsync(gate, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a gate reset");
             const unsigned gb = (unsigned)(((da.planes + da.NP - 1) / da.NP) * da.bands);

@@ -80,9 +80,9 @@ int fp8a_path_stats(uint64_t *out, int reset);
  * workspace holds its buffers, else gemm_f8mx_kernel (same results; the one-hot path is slower on
  * the benchmark network); "oh_correct" (default 1; 0 leaves the
  * one-hot path's candidate pairs uncorrected: NOT the reference's result, timing ablations only);
- * "oh_stats" (default 0) -- count fp8a_debug_stats; "dwx" (default 0; FP8A_DWX=1 sets 1 at
- * load) -- E4M3 depthwise convolutions in the band-staged form (conv_dwx_kernel) rather than the
- * word-image form (conv_tbx_kernel): identical sums, the former reads fp32 input directly;
+ * "oh_stats" (default 0) -- count fp8a_debug_stats; "dwx" (FP8A_DW=<n> sets it at load) -- the
+ * E4M3 depthwise form: 0 the word-image gather (tbx_decode_a + conv_tbx_kernel), 1 the
+ * band-staged conv_dwx_kernel, 2 the fp32 gather conv_dwg_kernel (identical sums);
  * "xm_ncg" (default 0 = by N; FP8A_XM_NCG) -- gemm_f8mx_kernel's tile width forced to 16 x 1 / 2
  * / 4 columns; "af32_maxct" (default 4; FP8A_AF32_MAXCT) -- the most column tiles for which a 1x1
  * conv / matrix A is decoded inside gemm_f8mx_kernel instead of by its pre-pass (0 = never).

@@ -1,13 +1,12 @@
-"""The band-staged depthwise kernel conv_dwx_kernel (csrc/conv_tbx.h) against the word-image form
-conv_tbx_kernel it replaces on E4M3 depthwise layers.
+"""The depthwise forms conv_dwx_kernel (band-staged) and conv_dwg_kernel (fp32 gather)
+(csrc/conv_tbx.h) against the word-image form conv_tbx_kernel on E4M3 depthwise layers.
 
-Both compute the same tensor-bias table terms in the same (ky, kx) order, so the outputs must be
+All compute the same tensor-bias table terms in the same (ky, kx) order, so the outputs must be
 BIT-identical; conv_tbx_kernel itself is pinned to the oracle per term and per layer in
-tests/test_gpu_tbx.py (which now runs on conv_dwx_kernel by default, i.e. the new kernel is also
-checked against the oracle directly there).  Covered here: every MobileNetV2 depthwise shape
+tests/test_gpu_tbx.py (which runs on the default form).  Covered here: every MobileNetV2 depthwise shape
 (batch 2), ragged widths (Wo % 4 != 0, 1-pixel planes), a 5x3 kernel with dilation, the fused
 input quantizer (qin), the BN + ReLU6 epilogue, and an off-grid input (gate raised: both return
-the gated exact kernel's result).  The per-launch path option is fp8a_set_option("dwx", 0 / 1).
+the gated exact kernel's result).  The per-launch path option is fp8a_set_option("dwx", 0 / 1 / 2).
 """
 import numpy as np
 import pytest
@@ -37,23 +36,35 @@ def _grid(rng, shape, bias, zero_frac=0.0, lo=3):
     return v.astype(np.float32)
 
 
+class _Both:
+    """fn() under each depthwise form (option "dwx": 1 band-staged, 2 fp32 gather), each paired
+    with the word-image form (0) for _same."""
+
+    def __init__(self, fn):
+        from fp8_quantization_amd import _lib
+        old = _lib.set_option("dwx", 0)
+        try:
+            self.ref = fn()
+            self.runs = []
+            for mode in (1, 2):
+                _lib.set_option("dwx", mode)
+                self.runs.append((mode, fn()))
+        finally:
+            _lib.set_option("dwx", old)
+
+
 def _both(fn):
-    """fn() with the band-staged kernel, then with the word-image kernel."""
-    from fp8_quantization_amd import _lib
-    old = _lib.set_option("dwx", 1)
-    try:
-        a = fn()
-        _lib.set_option("dwx", 0)
-        b = fn()
-    finally:
-        _lib.set_option("dwx", old)
-    return a, b
+    return _Both(fn)
 
 
-def _same(a, b, what):
-    a, b = a.cpu().numpy(), b.cpu().numpy()
-    same = (a.view(np.uint32) == b.view(np.uint32)) | ((a == 0) & (b == 0))
-    assert same.all(), f"{what}: {np.count_nonzero(~same)} outputs differ, first at {np.argwhere(~same)[0]}"
+def _same(both, what):
+    def bits(t):
+        return t.cpu().numpy() if torch.is_tensor(t) else t
+    b = bits(both.ref)
+    for mode, a in both.runs:
+        a = bits(a)
+        same = (a.view(np.uint32) == b.view(np.uint32)) | ((a == 0) & (b == 0))
+        assert same.all(), f"{what} (dwx={mode}): {np.count_nonzero(~same)} outputs differ, first at {np.argwhere(~same)[0]}"
 
 
 # (C, H, stride): the 17 depthwise layers of MobileNetV2 at 224 (distinct shapes)
@@ -77,10 +88,10 @@ def test_mbv2_depthwise_identical(C, H, s):
     x = torch.from_numpy(_grid(rng, (2, C, H, H), bA, zero_frac=0.4)).to(DEV)
     bW = rng.integers(12, 16, size=C).astype(np.int32)
     w = torch.from_numpy(_grid(rng, (C, 1, 3, 3), bW[:, None, None, None])).to(DEV)
-    a, b = _both(lambda: approx_conv2d(x, w, E, M, bA, torch.from_numpy(bW), bR, _tab(), with_approx=True,
-                                       with_s2nn2s_opt=True, quant_btw_mult_accu=True, stride=(s, s),
-                                       padding=(1, 1), groups=C))
-    _same(a, b, f"C={C} H={H} s={s}")
+    r = _both(lambda: approx_conv2d(x, w, E, M, bA, torch.from_numpy(bW), bR, _tab(), with_approx=True,
+                                    with_s2nn2s_opt=True, quant_btw_mult_accu=True, stride=(s, s),
+                                    padding=(1, 1), groups=C))
+    _same(r, f"C={C} H={H} s={s}")
 
 
 @pytest.mark.parametrize("shape", [(3, 5, 9, 9, 1, (3, 3), (1, 1), (1, 1)),
@@ -97,10 +108,10 @@ def test_ragged_shapes_identical(shape):
     x = torch.from_numpy(_grid(rng, (Bn, C, H, W), bA, zero_frac=0.3)).to(DEV)
     bW = rng.integers(11, 16, size=C).astype(np.int32)
     w = torch.from_numpy(_grid(rng, (C, 1) + k, bW[:, None, None, None])).to(DEV)
-    a, b = _both(lambda: approx_conv2d(x, w, E, M, bA, torch.from_numpy(bW), bR, _tab(), with_approx=True,
-                                       with_s2nn2s_opt=True, quant_btw_mult_accu=True, stride=(s, s), padding=pad,
-                                       dilation=dil, groups=C))
-    _same(a, b, f"shape {shape}")
+    r = _both(lambda: approx_conv2d(x, w, E, M, bA, torch.from_numpy(bW), bR, _tab(), with_approx=True,
+                                    with_s2nn2s_opt=True, quant_btw_mult_accu=True, stride=(s, s), padding=pad,
+                                    dilation=dil, groups=C))
+    _same(r, f"shape {shape}")
 
 
 @pytest.mark.parametrize("C,H,s", [(96, 28, 2), (144, 14, 1), (24, 9, 1)])
@@ -121,10 +132,12 @@ def test_fused_input_quantizer_and_bn_identical(C, H, s):
         y, ib, _ = approx_conv2d(x, w, E, M, None, torch.from_numpy(bW), 9, _tab(), with_approx=True,
                                  with_s2nn2s_opt=True, quant_btw_mult_accu=True, stride=(s, s), padding=(1, 1),
                                  groups=C, epilogue=ep, qin=(mx, 8, 3, 1))
-        return y, ib
-    (ya, ia), (yb, ib) = _both(run)
-    _same(ya, yb, f"qin C={C} H={H} s={s}")
-    assert float(ia) == float(ib)
+        return y.cpu().numpy(), float(ib)
+    r = _both(run)
+    ys = _Both.__new__(_Both)
+    ys.ref, ys.runs = r.ref[0], [(m, v[0]) for m, v in r.runs]
+    _same(ys, f"qin C={C} H={H} s={s}")
+    assert all(v[1] == r.ref[1] for _, v in r.runs)
 
 
 def test_off_grid_input_gated_identical():
@@ -136,6 +149,6 @@ def test_off_grid_input_gated_identical():
     x = torch.from_numpy(xn).to(DEV)
     bW = np.full(8, 13, np.int32)
     w = torch.from_numpy(_grid(rng, (8, 1, 3, 3), 13)).to(DEV)
-    a, b = _both(lambda: approx_conv2d(x, w, E, M, bA, torch.from_numpy(bW), bR, _tab(), with_approx=True,
-                                       with_s2nn2s_opt=True, quant_btw_mult_accu=True, padding=(1, 1), groups=8))
-    _same(a, b, "off-grid")
+    r = _both(lambda: approx_conv2d(x, w, E, M, bA, torch.from_numpy(bW), bR, _tab(), with_approx=True,
+                                    with_s2nn2s_opt=True, quant_btw_mult_accu=True, padding=(1, 1), groups=8))
+    _same(r, "off-grid")

@@ -1,0 +1,16 @@
+#!/bin/bash
+# depthwise forms: identity tests, MobileNetV2 E4M3 bench per form, trace of the fp32-gather form
+set -o pipefail
+OUT=gpurun_out/dwg; mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest tests/test_gpu_dwx.py tests/test_gpu_tbx.py -m gpu -q --maxfail 10 --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1
+rc=$?; grep -E "^FAILED|passed|failed" $OUT/tests.log | tail -12
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+B="python bench.py --arch mobilenet_v2 --steps 5 --warmup 2 --no-cpu-baseline"
+for m in 0 2; do
+    FP8A_DW=$m timeout -k 10 300 $B > $OUT/mb_dw$m.json 2> $OUT/mb_dw$m.err || exit $?
+    python -c "import json; d=json.load(open('$OUT/mb_dw$m.json')); print('dw$m', round(d['value'],1), round(d['ms_per_step'],3), round(d['roofline']['approx_macs_per_s']/1e12,2), d['fallback'])"
+done
+R=$(pwd); cd /tmp && export TMPDIR=/tmp
+FP8A_DW=2 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $R/$OUT/trace -o run -- python $R/bench.py --arch mobilenet_v2 --steps 3 --warmup 1 --no-cpu-baseline > $R/$OUT/trace.log 2>&1 || exit $?
+cd $R && python tools/trace_breakdown.py $(ls $OUT/trace/*kernel_trace.csv) --forwards 5:3 --out $OUT/breakdown.txt | head -14
+grep conv_dwg $OUT/breakdown.txt | tail -17
