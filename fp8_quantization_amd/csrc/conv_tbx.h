@@ -315,7 +315,9 @@ struct DwgArgs {
     uint32_t wo_mul, wo_shift, rg_mul, rg_shift;
 };
 
-template <int SW>
+// WORDS: read the word image tbx_decode_a wrote (x is then that image, reinterpreted) instead of
+// the fp32 input -- the column mapping's contiguous loads without the per-load decode.
+template <int SW, bool WORDS>
 __global__ __launch_bounds__(256) void conv_dwg_kernel(const float *x, const float *w, float *y, DwgArgs t,
                                                        const int32_t *bA, const int32_t *bW, const int32_t *bR,
                                                        TablePack tab, uint32_t *gate, const float2 *ep, int ep_act,
@@ -324,9 +326,9 @@ __global__ __launch_bounds__(256) void conv_dwg_kernel(const float *x, const flo
     constexpr int KW = 3, NR = (TBX_TW - 1) * SW + KW;
     __shared__ float2 sL[64];
     const int tid = threadIdx.x;
-    const float fmx = fq.mx ? *fq.mx : 0.0f, fbias = fq.mx ? fq_bias(fmx, fq.E, fq.M) : 0.0f;
-    const int a_b = fq.mx ? (int)fbias : *bA, r_b = *bR;
-    if (fq.mx && blockIdx.x == 0 && tid == 0) {
+    const float fmx = (!WORDS && fq.mx) ? *fq.mx : 0.0f, fbias = (!WORDS && fq.mx) ? fq_bias(fmx, fq.E, fq.M) : 0.0f;
+    const int a_b = (!WORDS && fq.mx) ? (int)fbias : *bA, r_b = *bR;
+    if (!WORDS && fq.mx && blockIdx.x == 0 && tid == 0) {
         *fq_bias_out = fbias;
         *fq_ibias_out = a_b;
     }
@@ -382,6 +384,10 @@ __global__ __launch_bounds__(256) void conv_dwg_kernel(const float *x, const flo
         for (int i = 0; i < NR; ++i)
 #pragma unroll
             for (int kx = 0; kx < KW; ++kx) {
+                if (WORDS) {  // (checked by tbx_decode_a)
+                    wd[i][kx] = __float_as_uint(xv[i][kx]);
+                    continue;
+                }
                 float v = xv[i][kx];
                 if (fq.mx) v = fq_apply(v, fmx, fbias, fq.M, fq.S);
                 const uint32_t u = __float_as_uint(v), ua = u & 0x7FFFFFFFu;

@@ -976,6 +976,10 @@ __global__ __launch_bounds__(256) void im2col_kernel(const float *x, float *out,
 }
 
 // Single-output-channel groups (depthwise): tensor-bias semantics, direct from NCHW x.
+// TB = false: the same literal restatement with int-bias semantics -- the v5 model's depthwise
+// convolutions (v5 has no tensor-bias path: its products are the GEMM path's, with a zero
+// operand's NONZERO term at every padded position, as the reference's im2col supplies them).
+template <bool TB>
 __global__ __launch_bounds__(256) void conv_tb_direct_kernel(const float *x, const float *w, float *y, int64_t Bn,
                                                              int64_t Cin, int64_t H, int64_t W, int64_t Cout,
                                                              int kh, int kw, int sh, int sw, int ph, int pw, int dh,
@@ -989,13 +993,13 @@ __global__ __launch_bounds__(256) void conv_tb_direct_kernel(const float *x, con
     if (gate != nullptr && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_fallback[3], 1ull);
     const int64_t total = Bn * Cout * Ho * Wo;
     const int64_t cpg = Cin / groups;   // input channels per group
-    const DFmt fA = dfmt(E, Mw, *bA, true), fR = dfmt(E, Mw, *bR, true);
+    const DFmt fA = dfmt(E, Mw, *bA, TB), fR = dfmt(E, Mw, *bR, TB);
     const float fmx = fq.mx ? *fq.mx : 0.0f, fbias = fq.mx ? fq_bias(fmx, fq.E, fq.M) : 0.0f;
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
          idx += (int64_t)gridDim.x * blockDim.x) {
         const int64_t wo = idx % Wo, ho = (idx / Wo) % Ho, co = (idx / (Wo * Ho)) % Cout, b = idx / (Wo * Ho * Cout);
         const int64_t g = co / (Cout / groups);
-        const DFmt fB = dfmt(E, Mw, bW[co], true);
+        const DFmt fB = dfmt(E, Mw, bW[co], TB);
         float s = 0.0f, part = 0.0f;
         int cnt = 0;
         for (int64_t c = 0; c < cpg; ++c)
@@ -1006,7 +1010,7 @@ __global__ __launch_bounds__(256) void conv_tb_direct_kernel(const float *x, con
                                   ? x[((b * Cin + g * cpg + c) * H + hi) * W + wi] : 0.0f;
                     if (fq.mx) a = fq_apply(a, fmx, fbias, fq.M, fq.S);
                     const float bv = w[((co * cpg + c) * kh + ky) * kw + kx];
-                    part += exact_term(a, bv, fA, fB, fR, tab.raw, flags | F_TB);
+                    part += exact_term(a, bv, fA, fB, fR, tab.raw, TB ? (flags | F_TB) : flags);
                     if (++cnt == 16) {
                         s += part;
                         part = 0.0f;
@@ -1311,7 +1315,8 @@ static bool g_opt_oh_correct = true;
 static bool g_opt_oh_stats = false;  // "oh_stats": the one-hot kernels count into g_ohstat
 // "dwx": the E4M3 depthwise form -- 0 the word-image gather conv_tbx_kernel (+ tbx_decode_a),
 // 1 the band-staged conv_dwx_kernel (measured 1.3x slower on MobileNetV2), 2 the
-// fp32 gather conv_dwg_kernel.  FP8A_DW=<n> sets it at load.
+// fp32 gather conv_dwg_kernel (5 % slower), 3 conv_dwg_kernel's column mapping over
+// tbx_decode_a's word image.  FP8A_DW=<n> sets it at load.
 static int g_opt_dwx = getenv("FP8A_DW") ? atoi(getenv("FP8A_DW")) : 0;
 
 // Compute units of the current device (cached); 256 (MI355X) when no device is visible.
@@ -2144,7 +2149,8 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
         // the fp32 gather form (conv_dwg_kernel): 3x3, undilated, one input channel per group
         DwgArgs dg;
         const int64_t rgn = (Ho + 3) / 4, gitems = Bn * Cout * rgn * Wo;
-        const bool dwg_ok = fast_ok && g_opt_dwx == 2 && E == 4 && Mw == 3 && (mode == TM_NONE || mode == TM_W1U) &&
+        const bool dwg_words = g_opt_dwx == 3;  // the same kernel over tbx_decode_a's word image
+        const bool dwg_ok = fast_ok && (g_opt_dwx == 2 || (dwg_words && workspace_bytes >= FLAG_BYTES + (size_t)(Bn * Cin * H * W) * 4)) && E == 4 && Mw == 3 && (mode == TM_NONE || mode == TM_W1U) &&
                             (flags & F_QBMA) && kh == 3 && kw == 3 && dh == 1 && dw == 1 && sh == sw &&
                             (sw == 1 || sw == 2) && cig == 1 && gitems < (1ll << 31);
         DwxArgs da;
@@ -2164,12 +2170,27 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
             fastdiv_params((uint32_t)Wo, dg.wo_mul, dg.wo_shift);
             fastdiv_params((uint32_t)rgn, dg.rg_mul, dg.rg_shift);
             const unsigned gb = (unsigned)std::min<int64_t>((gitems + 255) / 256, 16 * 1024);
-            if (sw == 1)
-                conv_dwg_kernel<1><<<gb, 256, 0, s>>>(x, w, y, dg, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi, fq,
-                                                      fqb, fqi);
-            else
-                conv_dwg_kernel<2><<<gb, 256, 0, s>>>(x, w, y, dg, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi, fq,
-                                                      fqb, fqi);
+            const float *src = x;
+            if (dwg_words) {
+                uint32_t *aw = (uint32_t *)((char *)workspace + FLAG_BYTES);
+                const int64_t nx = Bn * Cin * H * W;
+                tbx_decode_a<<<(unsigned)std::min<int64_t>((nx + 255) / 256, 8192), 256, 0, s>>>(x, nx, aw, gate, fq,
+                                                                                                    fqb, fqi);
+                if (fq.mx) bA = fqi;
+                src = reinterpret_cast<const float *>(aw);
+                if (sw == 1)
+                    conv_dwg_kernel<1, true><<<gb, 256, 0, s>>>(src, w, y, dg, bA, bW, bR, tp, gate, ep, act, act_lo,
+                                                                act_hi, fq, fqb, fqi);
+                else
+                    conv_dwg_kernel<2, true><<<gb, 256, 0, s>>>(src, w, y, dg, bA, bW, bR, tp, gate, ep, act, act_lo,
+                                                                act_hi, fq, fqb, fqi);
+            } else if (sw == 1) {
+                conv_dwg_kernel<1, false><<<gb, 256, 0, s>>>(x, w, y, dg, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi,
+                                                             fq, fqb, fqi);
+            } else {
+                conv_dwg_kernel<2, false><<<gb, 256, 0, s>>>(x, w, y, dg, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi,
+                                                             fq, fqb, fqi);
+            }
             if (fq.mx) bA = fqi;
             rc = hip_check("fp8a_conv2d (depthwise, E4M3 table form, fp32 gather)");
             if (rc) return rc;
@@ -2219,11 +2240,11 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
         }
         const unsigned eb = (unsigned)(fast_ok ? std::min<int64_t>((total + 255) / 256, 4096) : (total + 255) / 256);
         if (fast_ok) {  // gated, grid-capped: a no-op launch unless the fast kernel flagged
-            conv_tb_direct_kernel<<<eb, 256, 0, s>>>(x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw,
+            conv_tb_direct_kernel<true><<<eb, 256, 0, s>>>(x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw,
                                                     groups, Ho, Wo, E, Mw, bA, bW, bR, tp, flags | F_TB, gate, ep,
                                                     act, act_lo, act_hi, fq);
         } else {
-            conv_tb_direct_kernel<<<eb, 256, 0, s>>>(x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw,
+            conv_tb_direct_kernel<true><<<eb, 256, 0, s>>>(x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw,
                                                      groups, Ho, Wo, E, Mw, bA, bW, bR, tp, flags | F_TB, nullptr, ep,
                                                      act, act_lo, act_hi, FqIn{});
         }
@@ -2248,6 +2269,24 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
             rc = materialize();
             if (rc) return rc;
         }
+    }
+    // v5 depthwise: one direct launch (a GEMM per single-column group would be `groups` launches of
+    // N = 1 tiles: MobileNetV2 E5M2 v5 ran at ~500 images/s that way)
+    if ((flags & F_V5) && cog == 1 && !post && groups > 1) {
+        if (fq.mx) {
+            rc = materialize();
+            if (rc) return rc;
+        }
+        TablePack tp;
+        int mode;
+        rc = pack_table(table, Mw, true, tp, mode);
+        if (rc) return rc;
+        const int64_t total = Bn * Cout * Ho * Wo;
+        ++g_paths[PATH_EXACT];
+        conv_tb_direct_kernel<false><<<(unsigned)std::min<int64_t>((total + 255) / 256, 16384), 256, 0, s>>>(
+            x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups, Ho, Wo, E, Mw, bA, bW, bR, tp, flags,
+            nullptr, ep, act, act_lo, act_hi, FqIn{});
+        return hip_check("fp8a_conv2d (v5 depthwise, direct)");
     }
     for (int g = 0; g < groups; ++g) {
         GemmArgs a = make_args(nullptr, 0, w + g * cog * Kg, 1, Kg, y, 0, Mrows, cog, Kg, E, Mw, bA, bW + g * cog, 1,

@@ -82,7 +82,8 @@ int fp8a_path_stats(uint64_t *out, int reset);
  * one-hot path's candidate pairs uncorrected: NOT the reference's result, timing ablations only);
  * "oh_stats" (default 0) -- count fp8a_debug_stats; "dwx" (FP8A_DW=<n> sets it at load) -- the
  * E4M3 depthwise form: 0 the word-image gather (tbx_decode_a + conv_tbx_kernel), 1 the
- * band-staged conv_dwx_kernel, 2 the fp32 gather conv_dwg_kernel (identical sums);
+ * band-staged conv_dwx_kernel, 2 the fp32 gather conv_dwg_kernel, 3 conv_dwg_kernel over the
+ * word image (identical sums);
  * "xm_ncg" (default 0 = by N; FP8A_XM_NCG) -- gemm_f8mx_kernel's tile width forced to 16 x 1 / 2
  * / 4 columns; "af32_maxct" (default 4; FP8A_AF32_MAXCT) -- the most column tiles for which a 1x1
  * conv / matrix A is decoded inside gemm_f8mx_kernel instead of by its pre-pass (0 = never).

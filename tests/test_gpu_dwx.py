@@ -6,7 +6,7 @@ BIT-identical; conv_tbx_kernel itself is pinned to the oracle per term and per l
 tests/test_gpu_tbx.py (which runs on the default form).  Covered here: every MobileNetV2 depthwise shape
 (batch 2), ragged widths (Wo % 4 != 0, 1-pixel planes), a 5x3 kernel with dilation, the fused
 input quantizer (qin), the BN + ReLU6 epilogue, and an off-grid input (gate raised: both return
-the gated exact kernel's result).  The per-launch path option is fp8a_set_option("dwx", 0 / 1 / 2).
+the gated exact kernel's result).  The per-launch path option is fp8a_set_option("dwx", 0 / 1 / 2 / 3).
 """
 import numpy as np
 import pytest
@@ -37,7 +37,8 @@ def _grid(rng, shape, bias, zero_frac=0.0, lo=3):
 
 
 class _Both:
-    """fn() under each depthwise form (option "dwx": 1 band-staged, 2 fp32 gather), each paired
+    """fn() under each depthwise form (option "dwx": 1 band-staged, 2 fp32 gather, 3 column gather
+    over the word image), each paired
     with the word-image form (0) for _same."""
 
     def __init__(self, fn):
@@ -46,7 +47,7 @@ class _Both:
         try:
             self.ref = fn()
             self.runs = []
-            for mode in (1, 2):
+            for mode in (1, 2, 3):
                 _lib.set_option("dwx", mode)
                 self.runs.append((mode, fn()))
         finally:
