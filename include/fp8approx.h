@@ -85,7 +85,7 @@ int fp8a_path_stats(uint64_t *out, int reset);
  * band-staged conv_dwx_kernel, 2 the fp32 gather conv_dwg_kernel, 3 conv_dwg_kernel over the
  * word image (identical sums);
  * "xm_ncg" (default 0 = by N; FP8A_XM_NCG) -- gemm_f8mx_kernel's tile width forced to 16 x 1 / 2
- * / 4 columns; "af32_maxct" (default 4; FP8A_AF32_MAXCT) -- the most column tiles for which a 1x1
+ * / 4 columns; "af32_maxct" (default 3; FP8A_AF32_MAXCT) -- the most column tiles for which a 1x1
  * conv / matrix A is decoded inside gemm_f8mx_kernel instead of by its pre-pass (0 = never).
  * All of these change the schedule only: the outputs are bit-identical.  Returns the previous value, or FP8A_EINVAL
  * for an unknown name.  Not synchronised with launches in flight on other threads.
