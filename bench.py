@@ -8,9 +8,10 @@ activation / weight / result quantizers) over a batch of synthetic ImageNet-shap
 E4M3, dnsmp_factor=3, with_s2nn2s_opt, quant_btw_mult_accu.  Random-init weights (no network
 for checkpoints), synthetic data (no ImageNet here).
 
-N>1 (torch.distributed.run, one rank per GPU, RCCL): the validation batch is sharded --
-each rank runs its own B images (weak scaling) and the logits are all-gathered once per step,
-as the validate driver does.
+N>1 (one rank per GPU, RCCL; under torch.distributed.run, or `--gpus N` alone, which spawns the N
+ranks itself before anything touches the GPU): the validation batch is sharded -- each rank runs
+its own B images (weak scaling) and the logits are all-gathered once per step, as the validate
+driver does.
 
 Prints ONE JSON line (rank 0).  `roofline` is for the dominant kernel family, the fused
 approx GEMM/conv launches (fp8a_conv2d / fp8a_matmul), timed with HIP events on the stream
@@ -76,7 +77,10 @@ def dominant_kernel(E, M, v5=False):
 
 def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without a launcher's WORLD_SIZE, N > 1 spawns the N ranks itself")
+    ap.add_argument("--device", default="cuda", choices=("cuda", "cpu"),
+                    help="cpu = the gloo rehearsal of the multi-rank flow (tests; approx ops need stand-ins)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=None, help="images per GPU per step (default 512; vit_b16 64, vit_fc 256)")
@@ -396,15 +400,55 @@ def run(args, dev, rank=0, world=1):
     return None
 
 
-def main():
-    args = parse()
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawned(local_rank, world, port, argv, worker_init):
+    """One rank of a `--gpus N` launch: the environment torch.distributed.run would give it,
+    then the same entry point."""
+    os.environ.update(RANK=str(local_rank), LOCAL_RANK=str(local_rank), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if worker_init is not None:
+        worker_init()
+    main(argv)
+
+
+def launch(args, argv, worker_init=None):
+    """`--gpus N` without a launcher: start N fresh rank processes (spawn) from this process,
+    which has not touched the GPU (it only parsed arguments), and wait for them.  Rank 0 prints
+    the line.  `worker_init` (a picklable top-level function) runs first in every rank: the CPU
+    rehearsal's stand-ins (tests/test_distributed_cpu.py)."""
+    import torch.multiprocessing as mp
+    mp.start_processes(_spawned, args=(args.gpus, _free_port(), argv, worker_init), nprocs=args.gpus,
+                       join=True, start_method="spawn")
+
+
+def main(argv=None, worker_init=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch(args, argv, worker_init)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}; reporting {world} GPUs", file=sys.stderr)
+    if args.device == "cpu":  # the gloo rehearsal (tests): same control flow, no GPU
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+    else:
+        dev = torch.device("cuda", local)
+        if world > 1:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=dev)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    res = run(args, torch.device("cuda", local), rank, world)
+        world = dist.get_world_size()
+    res = run(args, dev, rank, world)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

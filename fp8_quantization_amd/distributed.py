@@ -32,37 +32,76 @@ def quantizers(model):
     return [m for m in model.modules() if isinstance(m, FPQuantizer)]
 
 
+def comm_device():
+    """The device a collective's tensors must live on: the current GPU for RCCL ("nccl"), the
+    host for gloo."""
+    if dist.get_backend() == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
 def broadcast_model_state(model, src=0):
     """Every parameter and buffer of `model` from rank `src` (identical architecture on every
-    rank, so shapes agree): one broadcast per tensor, in module order."""
+    rank, so shapes agree): ONE broadcast per dtype of the flattened tensors, on the
+    collective's device, copied back in place."""
     ws, _ = world()
     if ws == 1:
         return
+    dev = comm_device()
+    groups = {}
+    for t in list(model.parameters()) + list(model.buffers()):
+        groups.setdefault(t.dtype, []).append(t)
     with torch.no_grad():
-        for t in list(model.parameters()) + list(model.buffers()):
-            buf = t.detach().contiguous()
-            dist.broadcast(buf, src)
-            if buf.data_ptr() != t.data_ptr():
-                t.copy_(buf)
+        for dtype, ts in groups.items():
+            wire = torch.uint8 if dtype == torch.bool else dtype
+            flat = torch.cat([t.detach().reshape(-1).to(device=dev, dtype=wire) for t in ts])
+            dist.broadcast(flat, src)
+            off = 0
+            for t in ts:
+                n = t.numel()
+                t.copy_(flat[off:off + n].view(t.shape).to(dtype))
+                off += n
+
+
+_HDR = 8  # per quantizer: numel, sign_bits, ndim, up to 5 dims
 
 
 def broadcast_quant_state(model, src=0):
-    """Make every rank's FP8 ranges identical to rank `src`'s: per quantizer one broadcast of
-    (maxval element count, sign_bits) and one of maxval.  Ranks that never calibrated receive
-    the calibrated (e.g. per-channel) shapes."""
-    ws, _ = world()
+    """Make every rank's FP8 ranges identical to rank `src`'s with two broadcasts in all: one
+    int64 header [quantizers, 8] (maxval element count, sign_bits, maxval shape) and one float32
+    buffer of every quantizer's maxval.  Ranks that never calibrated receive the calibrated
+    (e.g. per-channel) shapes.  Both tensors are built on the collective's device (RCCL rejects
+    host tensors; a quantizer that never ran a forward still holds its maxval on the host), and
+    each received maxval stays there -- the GPU the forward runs on under RCCL."""
+    ws, rank = world()
     if ws == 1:
         return
-    for q in quantizers(model):
-        mx = q.maxval.detach().clone().contiguous()
-        hdr = torch.tensor([mx.numel(), int(q.sign_bits)], dtype=torch.int64, device=mx.device)
-        dist.broadcast(hdr, src)
-        n, sb = int(hdr[0].item()), int(hdr[1].item())
-        if mx.numel() != n:
-            mx = torch.empty(n, dtype=mx.dtype, device=mx.device)
-        dist.broadcast(mx, src)
-        q.maxval = mx
+    qs = quantizers(model)
+    if not qs:
+        return
+    dev = comm_device()
+    hdr = torch.zeros((len(qs), _HDR), dtype=torch.int64)
+    if rank == src:
+        for i, q in enumerate(qs):
+            shp = list(q.maxval.shape)
+            if len(shp) > _HDR - 3:
+                raise ValueError(f"maxval of rank {rank} has {len(shp)} dims; at most {_HDR - 3} are supported")
+            hdr[i, :3 + len(shp)] = torch.tensor([q.maxval.numel(), int(q.sign_bits), len(shp)] + shp)
+    hdr = hdr.to(dev)
+    dist.broadcast(hdr, src)
+    hdr = hdr.cpu()
+    total = int(hdr[:, 0].sum())
+    if rank == src:
+        flat = torch.cat([q.maxval.detach().reshape(-1).to(device=dev, dtype=torch.float32) for q in qs])
+    else:
+        flat = torch.empty(total, dtype=torch.float32, device=dev)
+    dist.broadcast(flat, src)
+    off = 0
+    for q, h in zip(qs, hdr.tolist()):
+        n, sb, nd = h[0], h[1], h[2]
+        q.maxval = flat[off:off + n].clone().view(h[3:3 + nd])
         q.sign_bits = sb
+        off += n
 
 
 def calibrate_on_rank0(model, batches, src=0, quantized=False):

@@ -41,8 +41,27 @@ def _worker(rank, ws, port, q):
         holder = torch.nn.Module()
         holder.q = FPQuantizer(n_bits=8, mantissa_bits=3, set_maxval=True)
         holder.q.maxval = torch.tensor([1.0 + rank])
+        # a per-channel quantizer: rank 0 calibrated it ([3, 1] ranges, unsigned); the other rank
+        # never ran a forward and holds its maxval on a device the collective cannot use (here
+        # 'meta', on a GPU box the host while RCCL needs the GPU) -- it must not be touched
+        holder.w = FPQuantizer(n_bits=8, mantissa_bits=3, set_maxval=True)
+        if rank == 0:
+            holder.w.maxval = torch.tensor([[0.5], [2.0], [8.0]])
+            holder.w.sign_bits = 0
+        else:
+            holder.w.maxval = torch.empty(1, device="meta")
         broadcast_quant_state(holder, src=0)
-        q.put((rank, allg, topk_correct(allg, labels), float(holder.q.maxval[0]), (x @ w)))
+        # model state: one flattened broadcast per dtype (float parameters, int64 / bool buffers)
+        from fp8_quantization_amd.distributed import broadcast_model_state
+        m = torch.nn.Linear(3, 2)
+        with torch.no_grad():
+            m.weight.fill_(float(rank))
+        m.register_buffer("count", torch.tensor([7 * (rank + 1)], dtype=torch.int64))
+        m.register_buffer("mask", torch.tensor([rank == 0, rank == 1]))
+        broadcast_model_state(m, src=0)
+        state = dict(w=m.weight.tolist(), count=m.count.tolist(), mask=m.mask.tolist(), wdev=str(holder.w.maxval.device),
+                     wmax=holder.w.maxval.tolist(), wsign=holder.w.sign_bits)
+        q.put((rank, allg, topk_correct(allg, labels), float(holder.q.maxval[0]), (x @ w), state))
     finally:
         dist.destroy_process_group()
 
@@ -70,10 +89,12 @@ def test_gloo_world2_gather_and_broadcast():
         assert p.exitcode == 0
     res.sort(key=lambda t: t[0])
     full = res[0][4]
-    for rank, allg, acc, mx, _ in res:
+    for rank, allg, acc, mx, _, st in res:
         assert torch.equal(allg, full)          # gathered logits == unsharded logits
         assert mx == 1.0                        # rank 0's ranges everywhere
         assert acc == res[0][2]
+        assert st["wdev"] == "cpu" and st["wmax"] == [[0.5], [2.0], [8.0]] and st["wsign"] == 0
+        assert st["w"] == [[0.0] * 3] * 2 and st["count"] == [7] and st["mask"] == [True, False]
 
 
 # ---------------------------------------------------------------------------------------------
@@ -182,3 +203,20 @@ def test_gloo_world2_validate_and_bench_flow():
     assert r0["top_1_accuracy"] == single["top_1_accuracy"] and r0["top_5_accuracy"] == single["top_5_accuracy"]
     assert abs(r0["loss"] - single["loss"]) <= 1e-5 * abs(single["loss"])
     assert b0["n_gpus"] == 2 and b0["config"]["global_batch"] == 4 and b0["value"] > 0
+
+
+def test_bench_main_gpus2_spawns_ranks(capfd):
+    """`bench.py --gpus 2` with no launcher environment starts the two ranks itself (spawned
+    from a parent that touches no GPU) and rank 0 reports n_gpus = 2 -- the driver's scaling
+    command form (here on the CPU rehearsal device: gloo and torch stand-ins)."""
+    import bench
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        assert k not in os.environ
+    bench.main(["--gpus", "2", "--device", "cpu", "--arch", "mobilenet_v2", "--batch", "2", "--steps", "1",
+                "--warmup", "1", "--cal-batch", "2", "--bn-stats-batches", "0", "--no-cpu-baseline"],
+               worker_init=_install_standins)
+    lines = [ln for ln in capfd.readouterr().out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, lines  # rank 0 alone prints
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 4 and line["config"]["parallelism"] == "dp2"
+    assert line["value"] > 0

@@ -65,6 +65,8 @@ def _unfold_rows(x, kh, kw, stride, pad, picks):
     dict(name="resnet18 conv1 b64", cin=3, cout=64, hw=224, k=7, s=2, p=3, Bn=64, E=4, M=3, t="nocomp"),
     dict(name="resnet50 layer3 3x3 E2M5 b64", cin=256, cout=256, hw=14, k=3, s=1, p=1, Bn=64, E=2, M=5, t="comp3"),
     dict(name="resnet50 layer2 1x1 E3M4 b64", cin=512, cout=128, hw=28, k=1, s=1, p=0, Bn=64, E=3, M=4, t="comp3"),
+    dict(name="resnet50 layer3 3x3 E5M2 b64", cin=256, cout=256, hw=14, k=3, s=1, p=1, Bn=64, E=5, M=2, t="zero"),
+    dict(name="resnet50 layer1 1x1 E5M2 b32", cin=64, cout=256, hw=56, k=1, s=1, p=0, Bn=32, E=5, M=2, t="zero"),
 ])
 def test_conv_full_size_sampled(cfg):
     from fp8_quantization_amd.approx_ops import approx_conv2d, make_flags
