@@ -57,13 +57,14 @@ def metric_name(arch, E, M, v5=False, no_approx=False):
 def dominant_kernel(E, M, v5=False):
     """(kernel name, description) of the approx GEMM kernel the bench's format runs on (run_gemm
     in csrc/fp8approx.hip; the bench uses s2n + qbma and the withComp=False tables): the E4M3
-    matrix-core form for E4M3, the packed-f16 tile-table kernel for E3M4 (gemm_tt16_kernel on
-    every K >= 256 layer; gemm_tt_kernel<4> on the short-K ones), the f32 tile-table kernel for
-    E2M5, the VALU tiled kernel otherwise (E5M2, the v5 mode)."""
+    matrix-core form for E4M3 and E5M2 (bf8 conversion), the packed-f16 tile-table kernel for
+    E3M4 (gemm_tt16_kernel on every K >= 256 layer; gemm_tt_kernel<4> on the short-K ones), the
+    f32 tile-table kernel for E2M5, the VALU tiled kernel otherwise (the v5 mode)."""
     if v5:
         return "gemm_fast_kernel", f"implicit-GEMM approx conv / linear on the VALU, E{E}M{M} v5 integer-adder terms"
-    if (E, M) == (4, 3):
-        return "gemm_f8mx_kernel", ("implicit-GEMM approx conv / linear, E4M3 terms by the hardware fp8 "
+    if (E, M) in ((4, 3), (5, 2)):
+        cvt = "fp8 (e4m3)" if (E, M) == (4, 3) else "bf8 (e5m2)"
+        return "gemm_f8mx_kernel", (f"implicit-GEMM approx conv / linear, E{E}M{M} terms by the hardware {cvt} "
                                     "conversion, codes summed on the matrix core")
     if (E, M) == (3, 4):
         return "gemm_tt16_kernel", ("implicit-GEMM approx conv / linear, E3M4 terms in packed f16 from a per-tile "

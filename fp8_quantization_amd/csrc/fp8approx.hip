@@ -1216,18 +1216,24 @@ static void launch_fast_t(int mode, const GemmArgs &a, dim3 grid, hipStream_t s)
     }
 }
 
-template <int NCG, int RB>
+template <int NCG, int RB, int XF>
 static void launch_f8mx_t(const GemmArgs &a, hipStream_t s) {
     using Cf = XmCfg<NCG, RB>;
     const int64_t xt = ((a.M + Cf::BMT - 1) / Cf::BMT) * ((a.N + Cf::BNT - 1) / Cf::BNT);
     const dim3 g((unsigned)(xt * a.splits));
-    if (a.af32) gemm_f8mx_kernel<NCG, RB, true><<<g, Cf::NT, 0, s>>>(a);
-    else gemm_f8mx_kernel<NCG, RB, false><<<g, Cf::NT, 0, s>>>(a);
+    if (a.af32) gemm_f8mx_kernel<NCG, RB, true, XF><<<g, Cf::NT, 0, s>>>(a);
+    else gemm_f8mx_kernel<NCG, RB, false, XF><<<g, Cf::NT, 0, s>>>(a);
 }
+template <int XF>
+static void launch_f8mx_f(const GemmArgs &a, hipStream_t s) {
+    if (a.xncg == 1) launch_f8mx_t<1, 4, XF>(a, s);
+    else if (a.xncg == 2) launch_f8mx_t<2, 4, XF>(a, s);
+    else launch_f8mx_t<4, 8, XF>(a, s);
+}
+// E4M3 (XF 0) or E5M2 (XF 1, mant_width 2) result grid
 static void launch_f8mx(const GemmArgs &a, hipStream_t s) {
-    if (a.xncg == 1) launch_f8mx_t<1, 4>(a, s);
-    else if (a.xncg == 2) launch_f8mx_t<2, 4>(a, s);
-    else launch_f8mx_t<4, 8>(a, s);
+    if (a.Mw == 2) launch_f8mx_f<1>(a, s);
+    else launch_f8mx_f<0>(a, s);
 }
 
 // gemm_f8mx_kernel's tile width: the fewest padded columns, ties to the wider tile (N = 16 -> 16,
@@ -1455,12 +1461,16 @@ static size_t gemm_workspace_bytes(int64_t M, int64_t N, int64_t K, int64_t conv
     return head_bytes(M, N) + std::max(xm, oh_operand_bytes(M, N, K, conv_words));
 }
 
-// The E4M3 table + hardware-fp8 form applies (TM_F8; run_gemm then takes the matrix-core kernel
-// when the workspace holds its pre-decoded operands): E4M3, a {0,1} or zero table, s2n + qbma, no
-// golden clip, int-bias semantics, not v5.
+// The table + hardware-fp8 form applies (TM_F8; run_gemm then takes the matrix-core kernel when
+// the workspace holds its pre-decoded operands): E4M3 (e4m3 conversion) or E5M2 (bf8 conversion,
+// round 4), a {0,1} or zero table, s2n + qbma, no golden clip, int-bias semantics, not v5.
+// (E5M2 has no VALU TM_F8 form: without the pre-decoded operands it keeps its table mode.)
+// FP8A_NO_F8=1 keeps the arithmetic forms; FP8A_NO_F8_E5M2=1 only for E5M2 (A/B runs).
 static bool f8_form(int E, int Mw, uint32_t flags, int table_mode) {
     static const bool no_f8 = getenv("FP8A_NO_F8") != nullptr;
-    return !no_f8 && !(flags & F_V5) && E == 4 && Mw == 3 && (table_mode == TM_NONE || table_mode == TM_W1U) &&
+    static const bool no_f8_e5 = getenv("FP8A_NO_F8_E5M2") != nullptr;
+    const bool fmt = (E == 4 && Mw == 3) || (E == 5 && Mw == 2 && !no_f8_e5);
+    return !no_f8 && !(flags & F_V5) && fmt && (table_mode == TM_NONE || table_mode == TM_W1U) &&
            (flags & F_S2N) && (flags & F_QBMA) && !(flags & F_GCLIP) && !(flags & F_TB);
 }
 
@@ -1565,8 +1575,9 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     rc = pack_table(table, a.Mw, v5 || (a.flags & F_APPROX), a.tab, mode);
     if (rc) return rc;
     if (v5) mode = TM_V5;
-    // E4M3 with a {0,1} (or no) table, s2n and per-product quantization: the LUT + hardware-fp8
-    // form (FP8A_NO_F8=1 keeps the arithmetic form, for comparison)
+    const int mode0 = mode;
+    // E4M3 / E5M2 with a {0,1} (or no) table, s2n and per-product quantization: the LUT + hardware
+    // fp8 / bf8 form (FP8A_NO_F8=1 keeps the arithmetic form, for comparison)
     if (f8_form(a.E, a.Mw, a.flags, mode)) mode = TM_F8;
     const int64_t total = a.M * a.N;
     const unsigned eblocks = (unsigned)std::min<int64_t>((total + 255) / 256, 4096);
@@ -1599,7 +1610,7 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
         return hip_check("fp8a flag reset");
     // E4M3 (TM_F8 flags): the one-hot dense matrix-core GEMM + candidate correction (gemm_oh.h) when
     // the workspace holds its buffers and the option is on (default off)
-    if (mode == TM_F8 && g_opt_one_hot && !no_mx() && units) {
+    if (mode == TM_F8 && a.Mw == 3 && g_opt_one_hot && !no_mx() && units) {
         const int64_t kpad = oh_kpad(a.K), npad = oh_npad(a.N), nct = npad / 64;
         const WordImage wi = word_image(a.H, a.W, a.ph, a.pw);
         const int64_t conv_words = a.conv ? (a.M / (a.Ho * a.Wo)) * a.aw_c * wi.H * wi.W : 0;
@@ -1699,6 +1710,7 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     }
     if (a.fqin.mx && !a.aw)  // the caller (conv2d_impl) only fuses where the pre-decode runs
         return fail(FP8A_EINVAL, "internal: fused input quantization without the matrix-core path");
+    if (mode == TM_F8 && a.Mw != 3 && !a.aw) mode = mode0;  // (gemm_fast_kernel's TM_F8 form is E4M3 only)
     ++g_paths[!a.aw ? PATH_FAST : a.wfmt == 0 ? PATH_F8MX : a.wfmt == 1 ? PATH_TT : PATH_TT16];
     launch_fast(mode, a, s);
     rc = hip_check("fp8a fast gemm launch");

@@ -46,6 +46,17 @@
 // Static table layout [pair (code0 + 9 code1)][m_a] u32 for s_a = + (a negative A row is the same
 // pair with the sign bits flipped, folded into the build's addend); zero A operands take scale
 // 2^127 (the conversion returns 0), so their row is irrelevant.
+//
+// E5M2 (XF = 1, round 4) runs the same kernel: the E5M2 result grid of bias bR (binades from
+// 2^(1-bR), 2 mantissa bits, subnormal step 2^(-1-bR)) is the OCP e5m2 (bf8) grid scaled by
+// 2^(15-bR), so the conversion is v_cvt_scalef32_pk_bf8_bf16 with scale 2^(15-bR-e_a), the codes
+// enter the MFMA as bf8 (cbsz = 1) against the same e4m3 selection operand, and the sums are in
+// units of 2^(15-bR).  V' = sig_a sig_b - T 2^-2 has at most 6 significant bits (bf16-exact);
+// its pre-clamp bound is 1.6875 x binade: any bound in (1.625, 1.75) rounds to the saturating
+// mantissa 1.75 (F6) and keeps the subnormal band's top binade (x / step = 2 V') below the tie at
+// 3.5 that the reference clamps to the largest subnormal 3.  Rows are 8 s_a + m_a with m_a < 4;
+// B codes m_b < 4 and 8 = zero.  A term past the e5m2 range converts to inf / NaN and the tile
+// falls back, as for E4M3.
 
 typedef int xm_v8i __attribute__((ext_vector_type(8)));
 typedef float xm_v16f __attribute__((ext_vector_type(16)));
@@ -61,6 +72,15 @@ constexpr int XBK = 8;                         // K-steps per staged tile
 constexpr int XM_TTK = 16 * 32 + 16;           // tile-table words per K-step: [tx 16][row 16][j 2] + bank shift
 constexpr uint32_t XM_ZERO_WORD = 254u << 23;  // A = 0: cvt scale 2^127 (the code is 0), row 0
 constexpr int XM_CP = BN + 1;  // the 64-column epilogue slices of the other kernels: [64][BN + 1] floats
+
+// Result-grid formats of the matrix-core path: XF 0 = E4M3 (OCP e4m3, bias 7), 1 = E5M2 (OCP e5m2 /
+// bf8, bias 15).
+template <int XF>
+struct XmFmt {
+    static constexpr int M = XF ? 2 : 3;
+    static constexpr int XB = XF ? 15 : 7;  // the OCP format's exponent bias
+};
+__host__ __device__ constexpr int xm_xbias(int Mw) { return Mw == 2 ? 15 : 7; }
 
 // Tile shapes of gemm_f8mx_kernel<NCG, RB, AF32>: 4 waves; NCG column groups of 16 columns x
 // (4 / NCG) row groups of RB 16-row blocks.  NCG = 4 (128 x 64) is the round-2 kernel; the narrow
@@ -102,33 +122,37 @@ struct XmCfg {
 // Exactness / range window shared by the pre-passes (as bias_ok in gemm_fast_kernel)
 __device__ __forceinline__ bool xm_bias_ok(int b) { return b >= -100 && b <= 120; }
 
-// Table word e of layout [pair][m_a]: the bf16 pair V'(m_a, code0), V'(m_a, code1), s_a = +.
-__device__ __forceinline__ uint32_t xm_lut_word(const TablePack &tab, int e) {
-    const int pr = e >> 3, ma = e & 7;
+// Table word e of layout [pair][m_a]: the bf16 pair V'(m_a, code0), V'(m_a, code1), s_a = +, for
+// M mantissa bits (3: E4M3, 2: E5M2; rows / codes >= 2^M are never addressed).
+__device__ __forceinline__ uint32_t xm_lut_word(const TablePack &tab, int e, int M) {
+    const int pr = e >> 3, ma = e & 7, n = 1 << M;
+    const float ulp = M == 3 ? 0.125f : 0.25f;
+    // Q_R's pre-clamp in bf16: any bound in (1.8125, 1.875) (M = 3) / (1.625, 1.75) (M = 2) x
+    // binade rounds like the reference's saturating mantissa (and the subnormal top tie rounding down)
+    const float bound = M == 3 ? 1.8671875f : 1.6875f;
     uint32_t w = 0;
+    if (ma >= n) return 0u;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const int cd = h ? (pr / 9) : (pr % 9);
-        if (cd == 8) continue;  // zero B: +0
-        const float t = (float)tab.raw[ma * 8 + cd];
-        float v = __fmaf_rn(1.0f + 0.125f * ma, 1.0f + 0.125f * cd, -t * 0.125f);  // exact, <= 8 bits
-        // Q_R's pre-clamp in bf16: any bound in (1.8125, 1.875) x binade rounds like the
-        // reference's saturating mantissa (and the subnormal top tie rounding down)
-        v = fminf(v, __uint_as_float(__float_as_uint(v) & 0x7F800000u) * 1.8671875f);
+        if (cd >= n) continue;  // zero B (code 8): +0
+        const float t = (float)tab.raw[ma * n + cd];
+        float v = __fmaf_rn(1.0f + ulp * ma, 1.0f + ulp * cd, -t * ulp);  // exact, <= 2M + 2 bits
+        v = fminf(v, __uint_as_float(__float_as_uint(v) & 0x7F800000u) * bound);
         w |= (__float_as_uint(v) >> 16) << (16 * h);
     }
     return w;
 }
 
-// A element -> word: bits 23-30 the cvt scale exponent se (scale 2^(se-127) = 2^(7-bR-e_a)),
-// bits 3-6 the tile-table row (8 s_a + m_a); zeros XM_ZERO_WORD.  ok = on the (3, bA) grid, inside the
-// exactness window and the scale range.
-__device__ __forceinline__ uint32_t xm_word_a(float x, uint32_t emnA, int bR, bool &ok) {
+// A element -> word: bits 23-30 the cvt scale exponent se (scale 2^(se-127) = 2^(xb-bR-e_a), xb the
+// OCP format's bias: 7 e4m3, 15 e5m2), bits 3-6 the tile-table row (8 s_a + m_a); zeros
+// XM_ZERO_WORD.  ok = on the (M, bA) grid, inside the exactness window and the scale range.
+__device__ __forceinline__ uint32_t xm_word_a(float x, int M, int xb, uint32_t emnA, int bR, bool &ok) {
     float c;
     uint32_t mc;
-    ok = stage_decode(x, 3, emnA, true, c, mc);
+    ok = stage_decode(x, M, emnA, true, c, mc);
     const uint32_t cb = __float_as_uint(c);
-    const int se = 261 - bR - (int)((cb >> 23) & 0xFFu);
+    const int se = 254 + xb - bR - (int)((cb >> 23) & 0xFFu);
     if ((cb & 0x7FFFFFFFu) == 0u) return XM_ZERO_WORD;
     ok = ok && se >= 1 && se <= 254;
     return ((uint32_t)min(max(se, 1), 254) << 23) | (((cb >> 31) * 8u + mc) << XM_ROW_SHIFT);
@@ -221,7 +245,7 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
     auto word = [&](float v, bool &ok) {
         if (p.fqin.mx) v = fq_apply(v, fmx, fbias, p.fqin.M, p.fqin.S);
         return p.wfmt == 3 ? oh_code_a(v, emnA, 6 - bA, bR, ok) : p.wfmt == 2 ? tt16_word_a(v, emnA, bA, ok, win)
-               : p.wfmt ? tt_word_a(v, p.Mw, emnA, ok) : xm_word_a(v, emnA, bR, ok);
+               : p.wfmt ? tt_word_a(v, p.Mw, emnA, ok) : xm_word_a(v, p.Mw, xm_xbias(p.Mw), emnA, bR, ok);
     };
     const uint32_t zw = p.wfmt ? 0u : XM_ZERO_WORD;  // the word of a zero (padding, columns >= K)
     // stores: 32-bit words, or the one-hot path's 16-bit codes (wfmt 3) at the same indices
@@ -335,7 +359,7 @@ __global__ __launch_bounds__(256) void xm_decode_b(const GemmArgs p, int64_t kpa
     const int64_t hq = p.npad / 2, n = kpad * hq;
     uint2 *const bq = const_cast<uint2 *>(p.bqw);
     if (blockIdx.x == 0)  // the table image every GEMM workgroup copies into LDS
-        for (int e = threadIdx.x; e < XM_LUT_WORDS; e += blockDim.x) const_cast<uint32_t *>(p.lutw)[e] = xm_lut_word(p.tab, e);
+        for (int e = threadIdx.x; e < XM_LUT_WORDS; e += blockDim.x) const_cast<uint32_t *>(p.lutw)[e] = xm_lut_word(p.tab, e, p.Mw);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const int64_t k = i / hq, q = i - k * hq;
@@ -348,7 +372,7 @@ __global__ __launch_bounds__(256) void xm_decode_b(const GemmArgs p, int64_t kpa
             mc[h] = 0;
             if (k < p.K && col < p.N) {
                 const int bb = p.bB[col * p.bBs];
-                const bool ok = stage_decode(p.B[k * p.sbk + col * p.sbn], 3, (uint32_t)(128 - bb) << 23, true,
+                const bool ok = stage_decode(p.B[k * p.sbk + col * p.sbn], p.Mw, (uint32_t)(128 - bb) << 23, true,
                                              c[h], mc[h]) && xm_bias_ok(bb);
                 if (!ok) fb_col(p, col);
                 bad |= !ok;
@@ -389,9 +413,10 @@ __global__ __launch_bounds__(256) void xm_decode_b(const GemmArgs p, int64_t kpa
 // checks and the fallback marks included -- instead of by the xm_decode_a pre-pass.  That pass
 // writes and re-reads 8 B per A element through HBM; staging-time decoding costs ~25 VALU
 // operations per element per column tile, the cheaper choice up to a few column tiles (run_gemm).
-template <int NCG, int RB, bool AF32>
+template <int NCG, int RB, bool AF32, int XF>
 __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs p) {
     using Cf = XmCfg<NCG, RB>;
+    constexpr int XM = XmFmt<XF>::M, XB = XmFmt<XF>::XB;
     constexpr int NT = Cf::NT, BMT = Cf::BMT, BNT = Cf::BNT, TTK = Cf::TTK, APR = Cf::APR;
     constexpr int BU = Cf::BU, NBU = Cf::NBU, TXN = Cf::TXN, SR = Cf::SR, CP = Cf::CP;
     __shared__ __attribute__((aligned(16))) typename Cf::Smem smu;
@@ -551,7 +576,7 @@ __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs
                         float v = __uint_as_float(wa[i][r]);
                         if (p.fqin.mx) v = fq_apply(v, fmx, fbias, p.fqin.M, p.fqin.S);
                         bool ok = true;
-                        wa[i][r] = xm_word_a(v, emnA, bR, ok);
+                        wa[i][r] = xm_word_a(v, XM, XB, emnA, bR, ok);
                         if (!ok) {  // the output row this A row feeds (1x1 conv / matrix), as the pre-pass marks it
                             const int64_t m = min(m0 + arow + 64 * i, p.M - 1);
                             fb_rows(p, m, m + 1);
@@ -610,12 +635,18 @@ __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs
 #pragma unroll
                     for (int c = 0; c < 4; ++c) {
                         xm_s2 cv;
-                        asm("v_cvt_scalef32_pk_fp8_bf16 %0, %1, %2" : "=v"(cv) : "v"(v[c].x), "v"(sc));
-                        cv = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(cv, __builtin_bit_cast(xm_b2, v[c].y), sc, true);
+                        if (XF) {
+                            asm("v_cvt_scalef32_pk_bf8_bf16 %0, %1, %2" : "=v"(cv) : "v"(v[c].x), "v"(sc));
+                            cv = __builtin_amdgcn_cvt_scalef32_pk_bf8_bf16(cv, __builtin_bit_cast(xm_b2, v[c].y), sc, true);
+                        } else {
+                            asm("v_cvt_scalef32_pk_fp8_bf16 %0, %1, %2" : "=v"(cv) : "v"(v[c].x), "v"(sc));
+                            cv = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(cv, __builtin_bit_cast(xm_b2, v[c].y), sc, true);
+                        }
                         av[4 * h + c] = __builtin_bit_cast(int, cv);
                     }
                 }
-                dq[b] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, sel, dq[b], 0, 0, 0, 127, 0, 127);
+                // A codes e4m3 (cbsz 0) or bf8 (cbsz 1); the selection operand is e4m3 (blgp 0)
+                dq[b] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, sel, dq[b], XF, 0, 0, 127, 0, 127);
             }
         }
         __syncthreads();
@@ -628,7 +659,7 @@ __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs
 #pragma unroll
     for (int b = 0; b < RB; ++b)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) nan |= __builtin_isnan(dq[b][i]);
+        for (int i = 0; i < 4; ++i) nan |= !__builtin_isfinite(dq[b][i]);
     const bool tnan = __syncthreads_or(nan ? 1 : 0) != 0;
     const bool tbad = AF32 && __syncthreads_or((abad || biasbad) ? 1 : 0) != 0;
     if ((tnan || tbad) && tid == 0) {
@@ -640,7 +671,7 @@ __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs
     // -> tile row 16 (RB wr + b) + 4 (l >> 4) + i, column 16 wc + (l & 15) -> an [SR][BNT] slab in
     // LDS per SR tile rows -> each thread's 4x4 block (64-row sub-slab sub, 4-column block cb),
     // epilogue mapping with consecutive lanes on consecutive pixels
-    const float f8S = __uint_as_float((uint32_t)min(max(134 - bR, 1), 254) << 23);
+    const float f8S = __uint_as_float((uint32_t)min(max(127 + XB - bR, 1), 254) << 23);
     float *ct = smu.ct;
     const int ety = tid & 15, etx = tid >> 4, cb = etx % (BNT / 4), sub = etx / (BNT / 4);
 #pragma unroll
