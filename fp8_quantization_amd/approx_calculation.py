@@ -31,6 +31,7 @@ from .quantization.quantization_manager import QuantizationManager
 from .quantization.base_quantized_classes import QuantizedActivation, QuantizedModule
 from .quantization.hijacker import activations_set
 from .quantization.quantized_folded_bn import BNFusedHijacker
+from .chain import ChainConsumerMixin
 
 # the non-approx products on the fp8 matrix core (gemm_dense.h); FP8A_DENSE=0: torch's fp32 contraction
 DENSE_EXACT = os.environ.get("FP8A_DENSE", "1") != "0"
@@ -104,7 +105,7 @@ class ApproxOpMixin:
         return torch.matmul(x, y)
 
 
-class ApproxConv2dMixin(ApproxOpMixin):
+class ApproxConv2dMixin(ApproxOpMixin, ChainConsumerMixin):
     """run_forward of QCustomBNConv2dTorch (approx_calculation.py:822-917)."""
 
     def im2col(self, input_data, kernel_height, kernel_width, stride, padding, dilation):
@@ -122,11 +123,13 @@ class ApproxConv2dMixin(ApproxOpMixin):
     supports_bn_act_epilogue = True
     supports_input_quant_fusion = True
 
-    def run_forward(self, x, weight, bias, offsets=None, epilogue=None, qin=None, post=None):
+    def run_forward(self, x, weight, bias, offsets=None, epilogue=None, qin=None, post=None, chain=None):
         """qin: the layer's input FPQuantizer when the hijacker fused it (x unquantized; the op
         applies it and its custom_bias is set as its own forward would).  post: ``(residual,
         clamp, lo, hi, output FPQuantizer or None)`` of a residual block's tail (quantized_folded_bn
-        .BNFusedHijacker.forward); the output quantizer's custom_bias is set likewise."""
+        .BNFusedHijacker.forward); the output quantizer's custom_bias is set likewise.  chain: a
+        model_wrap.WordChain -- x's word image from the previous convolution (used with qin) and /
+        or the next convolution to emit one for (fp8a_conv2d_chain, bit-identical results)."""
         x = x.contiguous()
         weight = weight.contiguous()
         if epilogue is not None and (bias is not None or not self.approx_flag):
@@ -142,7 +145,10 @@ class ApproxConv2dMixin(ApproxOpMixin):
                 raise TypeError("'NoneType' object is not subscriptable")
             args = dict(flags=flags, stride=self.stride, padding=self.padding, dilation=self.dilation,
                         groups=self.groups, epilogue=epilogue)
-            if qin is not None or post is not None:
+            ch = chain.request(self, x, qin) if chain is not None and self.groups == 1 else None
+            if ch is not None:
+                args["chain"] = ch
+            if qin is not None or post is not None or ch is not None:
                 qt = lambda q: (q.maxval, q.n_bits, q._mbits_int, q.sign_bits)  # noqa: E731
                 pq = None
                 if post is not None:
@@ -156,6 +162,8 @@ class ApproxConv2dMixin(ApproxOpMixin):
                     qin.custom_bias = ib
                 if pq is not None:
                     pq.custom_bias = ob
+                if ch is not None:
+                    chain.done(ch)
             else:
                 out = approx_conv2d(x.detach(), weight.detach(), E, M, self._default_bias(a_bias, E, x.device),
                                     w_bias, self._default_bias(r_bias, E, x.device), table, **args)

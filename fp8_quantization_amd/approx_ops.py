@@ -433,6 +433,100 @@ def _(x, w, bA, bW, bR, table, E, M, flags, stride, padding, dilation, groups, i
     return x.new_empty((Bn, Cout, Ho, Wo)), one, onei, one.clone(), onei.clone()
 
 
+@torch.library.custom_op("fp8approx::conv2d_chain", mutates_args=("out_image",))
+def _conv2d_chain_op(x: torch.Tensor, w: torch.Tensor, bA: Optional[torch.Tensor], bW: torch.Tensor,
+                     bR: torch.Tensor, table: torch.Tensor, E: int, M: int, flags: int, stride: list[int],
+                     padding: list[int], dilation: list[int], groups: int, in_maxval: Optional[torch.Tensor],
+                     in_nbits: int, in_mbits: int, in_sign_bits: int, res: Optional[torch.Tensor], post_act: int,
+                     post_lo: float, post_hi: float, out_maxval: Optional[torch.Tensor], out_nbits: int,
+                     out_mbits: int, out_sign_bits: int, in_image: Optional[torch.Tensor],
+                     out_image: Optional[torch.Tensor], next_ph: int, next_pw: int,
+                     next_maxval: Optional[torch.Tensor], next_nbits: int, next_mbits: int, next_sign_bits: int,
+                     next_bR: Optional[torch.Tensor], next_Mw: int, bn: Optional[torch.Tensor] = None, act: int = 0,
+                     act_lo: float = 0.0, act_hi: float = 0.0
+                     ) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
+    """fp8a_conv2d_chain: fp8a_conv2d_block that reads its input's word image (in_image) and / or
+    emits the next convolution's (out_image); same results and return values as conv2d_block."""
+    L = _lib.load()
+    x = x.contiguous()
+    w = w.contiguous()
+    Bn, Cin, H, W = x.shape
+    Cout, _, kh, kw = w.shape
+    sh, sw = stride
+    ph, pw = padding
+    dh, dw = dilation
+    Ho = (H + 2 * ph - dh * (kh - 1) - 1) // sh + 1
+    Wo = (W + 2 * pw - dw * (kw - 1) - 1) // sw + 1
+    y = torch.empty((Bn, Cout, Ho, Wo), dtype=torch.float32, device=x.device)
+    ib, iib = torch.empty(1, device=x.device), torch.empty(1, dtype=torch.int32, device=x.device)
+    ob, oib = torch.empty(1, device=x.device), torch.empty(1, dtype=torch.int32, device=x.device)
+    if res is not None:
+        res = res.contiguous()
+        if res.shape != y.shape or res.dtype != torch.float32 or res.device != x.device:
+            raise AssertionError(f"approx_conv2d: residual must be float32 {tuple(y.shape)} on {x.device}")
+    if bn is not None and (bn.shape != (Cout, 2) or bn.dtype != torch.float32 or not bn.is_contiguous()):
+        raise AssertionError(f"approx_conv2d: epilogue parameters must be contiguous float32 [{Cout}, 2]")
+    for img, shp in ((in_image, (Bn, Cin, H, W, ph, pw)), (out_image, (Bn, Cout, Ho, Wo, next_ph, next_pw))):
+        if img is not None and img.numel() < L.fp8a_word_image_bytes(*shp):
+            raise AssertionError("approx_conv2d: word image smaller than fp8a_word_image_bytes")
+    ws = _workspace(x.device, L.fp8a_conv2d_block_workspace_size(Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh,
+                                                                 dw, groups))
+    opt = lambda t: _lib.dev_ptr(t) if t is not None else None  # noqa: E731
+    rc = L.fp8a_conv2d_chain(_lib.dev_ptr(x), _lib.dev_ptr(w), _lib.dev_ptr(y), Bn, Cin, H, W, Cout, kh, kw, sh, sw,
+                             ph, pw, dh, dw, groups, E, M, opt(bA), _lib.dev_ptr(bW), _lib.dev_ptr(bR),
+                             _lib.host_ptr(table), flags, opt(bn), int(act), float(act_lo), float(act_hi),
+                             opt(in_maxval), int(in_nbits), int(in_mbits), int(in_sign_bits), _lib.dev_ptr(ib),
+                             _lib.dev_ptr(iib), opt(res), int(post_act), float(post_lo), float(post_hi),
+                             opt(out_maxval), int(out_nbits), int(out_mbits), int(out_sign_bits), _lib.dev_ptr(ob),
+                             _lib.dev_ptr(oib), opt(in_image), opt(out_image), int(next_ph), int(next_pw),
+                             opt(next_maxval), int(next_nbits), int(next_mbits), int(next_sign_bits), opt(next_bR),
+                             int(next_Mw), _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(x.device))
+    _lib.check(rc, "fp8a_conv2d_chain")
+    return y, ib, iib, ob, oib
+
+
+@_conv2d_chain_op.register_fake
+def _(x, w, bA, bW, bR, table, E, M, flags, stride, padding, dilation, groups, in_maxval, in_nbits, in_mbits,
+      in_sign_bits, res, post_act, post_lo, post_hi, out_maxval, out_nbits, out_mbits, out_sign_bits, in_image,
+      out_image, next_ph, next_pw, next_maxval, next_nbits, next_mbits, next_sign_bits, next_bR, next_Mw, bn=None,
+      act=0, act_lo=0.0, act_hi=0.0):
+    Bn, _, H, W = x.shape
+    Cout, _, kh, kw = w.shape
+    Ho = (H + 2 * padding[0] - dilation[0] * (kh - 1) - 1) // stride[0] + 1
+    Wo = (W + 2 * padding[1] - dilation[1] * (kw - 1) - 1) // stride[1] + 1
+    one = x.new_empty((1,))
+    onei = x.new_empty((1,), dtype=torch.int32)
+    return x.new_empty((Bn, Cout, Ho, Wo)), one, onei, one.clone(), onei.clone()
+
+
+def word_image_bytes(Bn, C, H, W, ph, pw):
+    """fp8a_word_image_bytes: bytes of a convolution input's word image (0: bad arguments)."""
+    return int(_lib.load().fp8a_word_image_bytes(int(Bn), int(C), int(H), int(W), int(ph), int(pw)))
+
+
+def new_word_image(Bn, C, H, W, ph, pw, device):
+    """A freshly initialised word image (fp8a_word_image_init) for a convolution input of shape
+    [Bn, C, H, W] and padding (ph, pw): a 256-byte aligned uint8 device tensor."""
+    n = word_image_bytes(Bn, C, H, W, ph, pw)
+    if n == 0:
+        raise AssertionError("new_word_image: bad shape")
+    buf = torch.empty(n + 256, dtype=torch.uint8, device=device)
+    off = (-buf.data_ptr()) % 256
+    img = buf[off:off + n]
+    rc = _lib.load().fp8a_word_image_init(_lib.dev_ptr(img), int(Bn), int(C), int(H), int(W), int(ph), int(pw),
+                                          _lib.stream_ptr(torch.device(device)))
+    _lib.check(rc, "fp8a_word_image_init")
+    return img
+
+
+def conv2d_wants_image(Cout, kernel, padding, groups, E, M, table, flags):
+    """fp8a_conv2d_wants_image: whether a convolution would read an input word image."""
+    tab = _table_host(table, M, _uses_table(flags))
+    return bool(_lib.load().fp8a_conv2d_wants_image(int(Cout), int(kernel[0]), int(kernel[1]), int(padding[0]),
+                                                    int(padding[1]), int(groups), int(E), int(M),
+                                                    _lib.host_ptr(tab), int(flags) & ~_lib.TB))
+
+
 def _quantizer_args(q):
     """(maxval [1] device tensor, n_bits, mantissa bits, sign bits) of a per-tensor quantizer tuple."""
     mx, nb, mb, sb = q
@@ -443,7 +537,7 @@ def _quantizer_args(q):
 
 
 def approx_conv2d(x, w, E, M, bA, bW, bR, table=None, flags=None, stride=(1, 1), padding=(0, 0), dilation=(1, 1),
-                  groups=1, epilogue=None, qin=None, post=None, **flag_kwargs):
+                  groups=1, epilogue=None, qin=None, post=None, chain=None, **flag_kwargs):
     """approx_v9 convolution, NCHW in / NCHW out (pre-BN), K ordered (c, ky, kx) like the
     reference im2col (approx_calculation.py:724-747); single-output-channel groups get the
     tensor-bias semantics (approx_calculation.py:800-809).  bW: per output channel.
@@ -461,8 +555,14 @@ def approx_conv2d(x, w, E, M, bA, bW, bR, table=None, flags=None, stride=(1, 1),
     None)``: a residual block's tail in the store, y = fq_out(clamp(y + residual))
     (fp8a_conv2d_block).
 
-    With qin or post the result is ``(y, input quantizer bias or None, output quantizer bias or
-    None)`` -- the float biases the quantizers would have set as their custom_bias."""
+    chain: optional ``(in_image or None, out or None)`` -- the word-image hand-off
+    (fp8a_conv2d_chain): in_image is x's word image emitted by the previous convolution (needs
+    qin); out = ``(image, next padding (ph, pw), next input quantizer tuple, next result bias
+    [1] int32 device tensor, next mantissa width)`` emits the next convolution's.  Bit-identical
+    results; x / y are still read / written as fp32.
+
+    With qin, post or chain the result is ``(y, input quantizer bias or None, output quantizer bias
+    or None)`` -- the float biases the quantizers would have set as their custom_bias."""
     if flags is None:
         flags = make_flags(**flag_kwargs)
     flags &= ~_lib.TB
@@ -474,6 +574,30 @@ def approx_conv2d(x, w, E, M, bA, bW, bR, table=None, flags=None, stride=(1, 1),
     if bW_.numel() != w.shape[0]:
         raise AssertionError(f"approx_conv2d: {bW_.numel()} weight biases for {w.shape[0]} output channels")
     ev = _prof_start()
+    if chain is not None:
+        iq = _quantizer_args(qin) if qin is not None else (None, 0, 0, 0)
+        res, pact, plo, phi, oq = post if post is not None else (None, 0, 0.0, 0.0, None)
+        oq = _quantizer_args(oq) if oq is not None else (None, 0, 0, 0)
+        in_img, out = chain
+        if in_img is not None and qin is None:
+            raise AssertionError("approx_conv2d: an input word image needs the fused input quantizer")
+        if out is not None:
+            oimg, (nph, npw), nq, nbR, nM = out
+            nq = _quantizer_args(nq)
+            nbR = _bias_dev(nbR, dev)
+        else:
+            oimg, nph, npw, nq, nbR, nM = None, 0, 0, (None, 0, 0, 0), None, 0
+        y, ib, iib, ob, oib = _conv2d_chain_op(
+            _as_f32(x), _as_f32(w), None if qin is not None else _bias_dev(bA, dev), bW_, _bias_dev(bR, dev), tab,
+            int(E), int(M), int(flags), [int(s) for s in stride], [int(p) for p in padding],
+            [int(d) for d in dilation], int(groups), iq[0].to(dev) if iq[0] is not None else None, iq[1], iq[2],
+            iq[3], res, int(pact), float(plo), float(phi), oq[0].to(dev) if oq[0] is not None else None, oq[1],
+            oq[2], oq[3], in_img, oimg, int(nph), int(npw), nq[0].to(dev) if nq[0] is not None else None, nq[1],
+            nq[2], nq[3], nbR, int(nM), *(epilogue or ()))
+        ib._fp8a_i32 = iib
+        ob._fp8a_i32 = oib
+        _prof_end(ev, y.shape[0] * y.shape[2] * y.shape[3] * w.shape[0] * w.shape[1] * w.shape[2] * w.shape[3])
+        return y, (ib if qin is not None else None), (ob if oq[0] is not None else None)
     if qin is not None or post is not None:
         iq = _quantizer_args(qin) if qin is not None else (None, 0, 0, 0)
         res, pact, plo, phi, oq = post if post is not None else (None, 0, 0.0, 0.0, None)

@@ -1,0 +1,87 @@
+"""The word-image hand-off between consecutive approx convolutions (fp8a_conv2d_chain).
+
+Every convolution on the matrix-core path (csrc/gemm_f8mx.h) reads its input A as one 32-bit word
+per element, which its xm_decode_a pre-pass writes from the fp32 input (after the layer's fused
+input quantizer): the pass reads x back and writes the image, 8 B of HBM traffic per element,
+7.6 % of the ResNet-18 forward (profiles/rocprof_r18_e4m3_r3_breakdown.txt).  In the fixed-range
+eval forward the convolution that PRODUCES x already holds every value in its store, so it
+writes the next convolution's words there (fq_next(y) -> word, bit for bit the pre-pass's), and
+the next launch runs its pre-pass gated: it only writes the input quantizer's bias, or re-decodes
+x when an element left the window.  The reference has no counterpart (its operators materialise
+im2col columns, approx_calculation.py:724-747); the per-layer op order of the reference
+(hijacker.py:77-115, quantized_folded_bn.py:30-83) is unchanged.
+"""
+import os
+
+# FP8A_CHAIN=0 keeps every convolution's own A operand pre-pass
+CHAIN = os.environ.get("FP8A_CHAIN", "1") != "0"
+
+
+class WordChain:
+    """The word-image hand-off (fp8a_conv2d_chain, include/fp8approx.h) for one approx
+    convolution of a fixed-range forward: ``in_image`` is its input's word image, emitted by the
+    convolution that produced the input (used when this layer fuses its input quantizer), and
+    ``next_layer`` the convolution that consumes its output, for which it emits one while storing
+    (when that layer fuses its input quantizer and its launch would read an image).  After the
+    launch, ``emitted`` is the image written for next_layer, or None -- the next layer gets an
+    image only from a launch that wrote it, so a stale buffer is never read.  Results are bit for
+    bit those of the unchained launches: the same words, the fp32 tensors still written."""
+
+    def __init__(self, in_image=None, next_layer=None):
+        self.in_image = in_image
+        self.next_layer = next_layer
+        self.emitted = None
+
+    def request(self, layer, x, qin):
+        """The ``chain`` argument of approx_conv2d for layer's launch on x, or None."""
+        in_img = self.in_image if qin is not None else None
+        out = None
+        nxt = self.next_layer
+        nq = nxt.chain_input_quantizer() if nxt is not None else None
+        if nq is not None and nxt.chain_wants_image():
+            Bn, _, H, W = x.shape
+            kh, kw = layer.kernel_size
+            Ho = (H + 2 * layer.padding[0] - layer.dilation[0] * (kh - 1) - 1) // layer.stride[0] + 1
+            Wo = (W + 2 * layer.padding[1] - layer.dilation[1] * (kw - 1) - 1) // layer.stride[1] + 1
+            E, M, _, _ = nxt._approx_config()
+            img = nxt.chain_image((Bn, layer.out_channels, Ho, Wo), x.device)
+            nbR = nxt._default_bias(nxt.get_res_fp_bias(), E, x.device)
+            out = (img, tuple(nxt.padding), (nq.maxval, nq.n_bits, nq._mbits_int, nq.sign_bits), nbR, M)
+        if in_img is None and out is None:
+            return None
+        return in_img, out
+
+    def done(self, ch):
+        self.emitted = ch[1][0] if ch[1] is not None else None
+
+
+class ChainConsumerMixin:
+    """What WordChain asks of a consumer convolution (mixed into the approx conv operators)."""
+
+    def chain_input_quantizer(self):
+        """The per-tensor input FPQuantizer this layer's next forward fuses into its launch, or None."""
+        from .quantization.quantized_folded_bn import BNFusedHijacker
+        if not CHAIN or not isinstance(self, BNFusedHijacker) or self._fused_epilogue() is None:
+            return None
+        return self._fused_input_quantizer(self._qa())
+
+    def chain_wants_image(self):
+        E, M, table, flags = self._approx_config()
+        key = (E, M, int(flags), tuple(table.reshape(-1).tolist()) if table is not None else None)
+        cached = getattr(self, "_chain_wants", None)
+        if cached is None or cached[0] != key:
+            from .approx_ops import conv2d_wants_image
+            cached = (key, conv2d_wants_image(self.out_channels, self.kernel_size, self.padding, self.groups, E, M,
+                                              table, flags))
+            self._chain_wants = cached
+        return cached[1]
+
+    def chain_image(self, in_shape, device):
+        """This layer's input word image buffer (allocated and initialised once per shape)."""
+        key = (tuple(in_shape), tuple(self.padding), str(device))
+        cached = getattr(self, "_chain_img", None)
+        if cached is None or cached[0] != key:
+            from .approx_ops import new_word_image
+            cached = (key, new_word_image(*in_shape, self.padding[0], self.padding[1], device))
+            self._chain_img = cached
+        return cached[1]

@@ -117,6 +117,25 @@ __device__ __forceinline__ float fq_apply(float v, float mx, float bias, int M, 
     return (k >= -126) ? rintf(xc * p2(-k)) * sc : rintf(xc / sc) * sc;
 }
 
+// Word-image hand-off (round 4, fp8a_conv2d_chain): a convolution's store also writes the NEXT
+// convolution's pre-decoded A operand -- its zero-bordered word image (gemm_f8mx.h: the word of
+// fq_next(y) for every output element y) -- so the next launch skips its xm_decode_a pass (which
+// reads y back and writes the image: 8 B of HBM traffic per element).  Same words as that pass,
+// bit for bit: the same fq_apply / xm_word_a on the same float.  An element outside the
+// matrix-core window sets the image's header word, and the consumer's gated pre-pass then
+// re-decodes its input from y (the fp32 output is always written).
+struct EmitW {
+    uint32_t *w;        // the image's words [Bn][C][awH][awW] (nullptr: no emission)
+    uint32_t *invalid;  // the image's header word
+    int awH, awW, awph, awpw;
+    int Wo;
+    uint32_t hw_mul, hw_shift, wo_mul, wo_shift;  // fastdiv by Ho * Wo and Wo (output index < 2^31)
+    uint32_t hw;
+    FqIn fq;            // the next convolution's input quantizer (per tensor)
+    const int32_t *bR;  // its result bias
+    int Mw;             // its mantissa width (3: e4m3 words, 2: e5m2)
+};
+
 struct GemmArgs {
     const float *A;
     int64_t lda;
@@ -197,6 +216,9 @@ struct GemmArgs {
     int post_act;
     float post_lo, post_hi;
     FqIn post_fq;
+    EmitW em;              // word-image emission for the next convolution (em.w nullptr: off)
+    const uint32_t *gate;  // xm_decode_a: run only if *gate != 0 (the input image arrived invalid)
+    const uint32_t *in_img; // the input's word image (header + words) a previous launch emitted, or nullptr
     TablePack tab;
 };
 
@@ -307,6 +329,66 @@ __device__ __forceinline__ uint32_t fastdiv(uint32_t n, uint32_t mul, uint32_t s
 constexpr int BM = 64, BN = 64, BK = 16, TM = 4, TN = 4, NT = 256;
 constexpr int AP = BM + 4, BP = BN + 4;
 
+__device__ __forceinline__ uint32_t xm_word_a(float x, int M, int xb, uint32_t emnA, int bR, bool &ok);  // gemm_f8mx.h
+__host__ __device__ constexpr int xm_xbias(int Mw);
+
+// Word-image emission (EmitW): one word per final output value at NCHW output index o (< 2^31,
+// the host checks).  The next quantizer's constants sit in the image's header (emit_prep_kernel:
+// [1] maxval, [2] its float bias, [3] 2^(1 - bias) bits, [4] bR), made wave-uniform (SGPRs) once
+// per epilogue: the matrix-core kernel runs at its 80-VGPR budget, and per-thread copies of them
+// (or their recomputation from maxval) in VGPRs made it spill.
+struct EmitCtx {
+    float mx, fb;
+    uint32_t emn;
+    int bR;
+};
+__device__ __forceinline__ EmitCtx emit_ctx(const GemmArgs &p) {
+    EmitCtx e{};
+    if (p.em.w == nullptr) return e;
+    const uint4 h = *reinterpret_cast<const uint4 *>(p.em.invalid);  // header words 0-3 (uniform: SGPRs)
+    e.mx = __uint_as_float(__builtin_amdgcn_readfirstlane(h.y));
+    e.fb = __uint_as_float(__builtin_amdgcn_readfirstlane(h.z));
+    e.emn = __builtin_amdgcn_readfirstlane(h.w);
+    e.bR = __builtin_amdgcn_readfirstlane((int)p.em.invalid[4]);
+    return e;
+}
+__device__ __forceinline__ uint32_t emit_word(const GemmArgs &p, const EmitCtx &e, float v, bool &ok) {
+    return xm_word_a(fq_apply(v, e.mx, e.fb, p.em.fq.M, p.em.fq.S), p.em.Mw, xm_xbias(p.em.Mw), e.emn, e.bR, ok);
+}
+// word index of NCHW output index o
+__device__ __forceinline__ uint32_t emit_index(const GemmArgs &p, uint32_t uo, uint32_t &wo) {
+    const uint32_t plane = fastdiv(uo, p.em.hw_mul, p.em.hw_shift), pix = uo - plane * p.em.hw;
+    const uint32_t ho = fastdiv(pix, p.em.wo_mul, p.em.wo_shift);
+    wo = pix - ho * (uint32_t)p.em.Wo;
+    return (plane * (uint32_t)p.em.awH + ho + (uint32_t)p.em.awph) * (uint32_t)p.em.awW + wo + (uint32_t)p.em.awpw;
+}
+__device__ __forceinline__ void emit1(const GemmArgs &p, const EmitCtx &e, int64_t o, float v) {
+    uint32_t wo;
+    const uint32_t wi = emit_index(p, (uint32_t)o, wo);
+    bool ok = true;
+    p.em.w[wi] = emit_word(p, e, v, ok);
+    if (!ok) atomicOr(p.em.invalid, 1u);
+}
+// four consecutive outputs (o % 4 == 0 in an NCHW plane of hw % 4 == 0): one 16-B store when
+// they sit in one row of the image (Wo % 4 == 0: always; the interior rows start 16-B aligned)
+__device__ __forceinline__ void emit4(const GemmArgs &p, const EmitCtx &e, int64_t o, float4 v) {
+    uint32_t wo;
+    const uint32_t wi = emit_index(p, (uint32_t)o, wo);
+    bool ok0 = true, ok1 = true, ok2 = true, ok3 = true;
+    const uint4 w = make_uint4(emit_word(p, e, v.x, ok0), emit_word(p, e, v.y, ok1), emit_word(p, e, v.z, ok2),
+                               emit_word(p, e, v.w, ok3));
+    if (wo + 3 < (uint32_t)p.em.Wo && (wi & 3u) == 0u) {
+        *reinterpret_cast<uint4 *>(p.em.w + wi) = w;
+    } else {
+        p.em.w[wi] = w.x;
+        uint32_t wo1;
+        p.em.w[emit_index(p, (uint32_t)o + 1, wo1)] = w.y;
+        p.em.w[emit_index(p, (uint32_t)o + 2, wo1)] = w.z;
+        p.em.w[emit_index(p, (uint32_t)o + 3, wo1)] = w.w;
+    }
+    if (!(ok0 && ok1 && ok2 && ok3)) atomicOr(p.em.invalid, 1u);
+}
+
 __device__ __forceinline__ int64_t out_index(const GemmArgs &p, int64_t m, int64_t n) {
     if (!p.nchw) return m * p.ldc + n;
     const int64_t img = m / p.hw, pix = m - img * p.hw;
@@ -339,6 +421,9 @@ __device__ __forceinline__ bool stage_decode(float x, int M, uint32_t emn, bool 
 // Writes one thread's TM x TN outputs (rows m0 + ty*TM + i, columns n0 + tx*TN + j) to the
 // output mapping, or to its split-K partial slice (same layout); applies the fused BN/activation
 // epilogue when unsplit.
+// EMIT = false compiles the word-image emission out (gemm_f8mx_kernel's non-emitting instances:
+// the emission code alone pushed that kernel past its 80-VGPR budget).
+template <bool EMIT = true>
 __device__ __forceinline__ void store_tile(const GemmArgs &p, int64_t split, int64_t m0, int64_t n0, int ty, int tx,
                                            float (&acc)[TM][TN]) {
     const bool partial = p.splits > 1;
@@ -355,8 +440,21 @@ __device__ __forceinline__ void store_tile(const GemmArgs &p, int64_t split, int
     }
     const float pb = partial ? 0.0f : post_bias(p);
     const GemmArgs &q = p;
-    auto fin1 = [&](int64_t o, float v) { return partial ? v : post1(q, o, v, pb); };
-    auto fin4 = [&](int64_t o, float4 v) { return partial ? v : post4(q, o, v, pb); };
+    // word-image emission from each final value (the split-K reduction emits instead)
+    const bool emit = EMIT && !partial && p.em.w != nullptr;
+    const EmitCtx ec = EMIT ? emit_ctx(p) : EmitCtx{};
+    auto fin1 = [&](int64_t o, float v) {
+        if (partial) return v;
+        v = post1(q, o, v, pb);
+        if (emit) emit1(q, ec, o, v);
+        return v;
+    };
+    auto fin4 = [&](int64_t o, float4 v) {
+        if (partial) return v;
+        v = post4(q, o, v, pb);
+        if (emit) emit4(q, ec, o, v);
+        return v;
+    };
     if (!p.nchw) {
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
@@ -785,6 +883,7 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs p) {
     const int64_t MN = p.M * p.N;
     const float pb = post_bias(p);
+    const EmitCtx ec = emit_ctx(p);
     const int S = p.splits + (p.ohd ? 1 : 0);  // (the one-hot path's correction slice follows the partials)
     const bool vec = p.nchw ? ((p.hw & 3) == 0) : ((p.N & 3) == 0 && (p.ldc & 3) == 0);
     const bool aligned = ((((uintptr_t)p.C) & 15) == 0) && ((((uintptr_t)p.part) & 15) == 0) && ((MN & 3) == 0) &&
@@ -819,7 +918,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs p) {
                     acc.w = epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, p.coff + n + 3, acc.w);
                 }
             }
-            *reinterpret_cast<float4 *>(p.C + o) = post4(p, o, acc, pb);
+            const float4 r = post4(p, o, acc, pb);
+            *reinterpret_cast<float4 *>(p.C + o) = r;
+            if (p.em.w) emit4(p, ec, o, r);
         }
         return;
     }
@@ -836,7 +937,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs p) {
             o = m * p.ldc + n;
             ch = p.coff + n;
         }
-        p.C[o] = post1(p, o, epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, ch, acc), pb);
+        const float r = post1(p, o, epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, ch, acc), pb);
+        p.C[o] = r;
+        if (p.em.w) emit1(p, ec, o, r);
     }
 }
 
@@ -878,7 +981,9 @@ __global__ __launch_bounds__(256) void gemm_exact_kernel(const GemmArgs p) {
             }
             s += part;
             const int64_t o = out_index(p, m, n);
-            p.C[o] = post1(p, o, epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, p.coff + n, s), post_bias(p));
+            const float r = post1(p, o, epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, p.coff + n, s), post_bias(p));
+            p.C[o] = r;
+            if (p.em.w) emit1(p, emit_ctx(p), o, r);
         }
         return;
     }
@@ -891,6 +996,7 @@ __global__ __launch_bounds__(256) void gemm_exact_kernel(const GemmArgs p) {
     const int64_t nur = (p.M + 63) >> 6, nuc = (p.N + 63) >> 6;
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_fallback[0], 1ull);
     const float pb = post_bias(p);
+    const EmitCtx ec = emit_ctx(p);
     for (int64_t u = blockIdx.x; u < nur * nuc; u += gridDim.x) {
         const int64_t ur = u / nuc, uc = u - ur * nuc;
         if (!all && !p.urow[ur] && !p.ucol[uc] && !p.utile[u]) continue;  // (block-uniform)
@@ -921,7 +1027,9 @@ __global__ __launch_bounds__(256) void gemm_exact_kernel(const GemmArgs p) {
             const int64_t n = nb + j;
             if (n >= p.N) break;
             const int64_t o = out_index(p, m, n);
-            p.C[o] = post1(p, o, epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, p.coff + n, s[j] + part[j]), pb);
+            const float r = post1(p, o, epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, p.coff + n, s[j] + part[j]), pb);
+            p.C[o] = r;
+            if (p.em.w) emit1(p, ec, o, r);
         }
     }
 }
@@ -1221,8 +1329,16 @@ static void launch_f8mx_t(const GemmArgs &a, hipStream_t s) {
     using Cf = XmCfg<NCG, RB>;
     const int64_t xt = ((a.M + Cf::BMT - 1) / Cf::BMT) * ((a.N + Cf::BNT - 1) / Cf::BNT);
     const dim3 g((unsigned)(xt * a.splits));
-    if (a.af32) gemm_f8mx_kernel<NCG, RB, true, XF><<<g, Cf::NT, 0, s>>>(a);
-    else gemm_f8mx_kernel<NCG, RB, false, XF><<<g, Cf::NT, 0, s>>>(a);
+    // (the emitting instances only where this launch writes the next convolution's word image
+    // from its own store: unsplit, fp8a_conv2d_chain)
+    const bool emit = a.em.w != nullptr && a.splits == 1;
+    if (a.af32) {
+        if (emit) gemm_f8mx_kernel<NCG, RB, true, XF, true><<<g, Cf::NT, 0, s>>>(a);
+        else gemm_f8mx_kernel<NCG, RB, true, XF, false><<<g, Cf::NT, 0, s>>>(a);
+    } else {
+        if (emit) gemm_f8mx_kernel<NCG, RB, false, XF, true><<<g, Cf::NT, 0, s>>>(a);
+        else gemm_f8mx_kernel<NCG, RB, false, XF, false><<<g, Cf::NT, 0, s>>>(a);
+    }
 }
 template <int XF>
 static void launch_f8mx_f(const GemmArgs &a, hipStream_t s) {
@@ -1693,10 +1809,21 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
             for (int i = 0; tt && i < (1 << (2 * a.Mw)); ++i) a.ttf7 |= a.tab.raw[i] < 0;
             a.wfmt = tt ? (tt16_form(a.Mw, a.ttf7, a.K) ? 2 : 1) : 0;
             a.xncg = tt ? 4 : xm_ncg(a.N);
-            a.af32 = !tt && xm_af32(a) ? 1 : 0;
+            // the input's word image from the previous launch (fp8a_conv2d_chain): its words replace
+            // the A pre-pass, which then runs gated (only to write the fused quantizer's bias, or to
+            // re-decode x if the image arrived invalid)
+            const bool use_img = a.in_img != nullptr && !tt && a.conv && a.fqin.mx != nullptr;
+            if (use_img) a.aw = a.in_img + 64;
+            a.af32 = !tt && !use_img && xm_af32(a) ? 1 : 0;
             const int64_t rows = a.conv ? a.M / (a.Ho * a.Wo) : a.M, cols = a_words / std::max<int64_t>(rows, 1);
             const dim3 ga((unsigned)std::min<int64_t>((cols + 255) / 256, 64), (unsigned)std::min<int64_t>(rows, 1024));
-            if (!a.af32) xm_decode_a<<<ga, 256, 0, s>>>(a);
+            if (use_img) {
+                a.gate = a.in_img;
+                xm_decode_a<<<dim3(std::min(ga.x, 8u), std::min(ga.y, 64u)), 256, 0, s>>>(a);
+                a.gate = nullptr;
+            } else if (!a.af32) {
+                xm_decode_a<<<ga, 256, 0, s>>>(a);
+            }
             if (tt) {  // B words [Kpad][Npad] (the same bytes as the E4M3 pair grid) + the static image
                 const unsigned gb = (unsigned)std::min<int64_t>((kpad * npad + 255) / 256, 4096);
                 tt_decode_b<<<gb, 256, 0, s>>>(a, kpad);  // (+ gemm_tt16_kernel's f16 image when wfmt == 2)
@@ -2114,7 +2241,7 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
                        uint32_t flags, const float *bn, int act, float act_lo, float act_hi, void *workspace,
                        size_t workspace_bytes, hipStream_t s, FqIn fq, float *fqb, int32_t *fqi, float *xq,
                        const float *res = nullptr, int post_act = 0, float post_lo = 0.0f, float post_hi = 0.0f,
-                       FqIn post_fq = FqIn{}) {
+                       FqIn post_fq = FqIn{}, const uint32_t *in_img = nullptr, const EmitW &em = EmitW{}) {
     const float2 *ep = reinterpret_cast<const float2 *>(bn);
     if (ep && (((uintptr_t)bn) & 7) != 0) return fail(FP8A_EINVAL, "bn parameters must be 8-byte aligned");
     int rc = check_format(E, Mw);
@@ -2322,6 +2449,10 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
             a.bA = fqi;  // written by the A pre-decode before any kernel reads it
         }
         a.res = res; a.post_act = post_act; a.post_lo = post_lo; a.post_hi = post_hi; a.post_fq = post_fq;
+        if (groups == 1) {  // (fp8a_conv2d_chain only asks for these on ungrouped convolutions)
+            a.in_img = in_img;
+            a.em = em;
+        }
         rc = run_gemm(a, table, workspace, workspace_bytes, s);
         if (rc) return rc;
     }
@@ -2411,6 +2542,132 @@ int fp8a_conv2d_block(const float *x, const float *w, float *y, int64_t Bn, int6
     return conv2d_impl(x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups, E, Mw,
                        fin.mx ? nullptr : bA, bW, bR, table, flags, bn, act, act_lo, act_hi, workspace, rest, s, fin,
                        in_bias_out, in_ibias_out, xq, res, post_act, post_lo, post_hi, fout);
+}
+
+// ----------------------------------------------------------------------------- word-image chain
+// A convolution's input as the zero-bordered word image of gemm_f8mx_kernel (xm_decode_a's
+// layout: [Bn][C][H + 2 ph][W'] with the left border widened for 16-B interior rows), behind a
+// 256-B header whose first word is the "invalid" flag (fp8a_conv2d_chain).
+size_t fp8a_word_image_bytes(int64_t Bn, int64_t C, int64_t H, int64_t W, int ph, int pw) {
+    if (Bn <= 0 || C <= 0 || H <= 0 || W <= 0 || ph < 0 || pw < 0) return 0;
+    const WordImage wi = word_image(H, W, ph, pw);
+    return FLAG_BYTES + align256((size_t)(Bn * C * wi.H * wi.W) * 4);
+}
+
+// The emitting launch's header: [0] valid, [1] the next quantizer's maxval, [2] its float bias,
+// [3] its 2^(1 - bias) bit pattern (the grid's min normal), [4] the next convolution's bR.
+__global__ void emit_prep_kernel(uint32_t *hdr, FqIn fq, const int32_t *bR) {
+    const float mx = *fq.mx, fb = fq_bias(mx, fq.E, fq.M);
+    hdr[0] = 0u;
+    hdr[1] = __float_as_uint(mx);
+    hdr[2] = __float_as_uint(fb);
+    hdr[3] = (uint32_t)(128 - (int)fb) << 23;
+    hdr[4] = (uint32_t)*bR;
+}
+
+__global__ void word_image_fill_kernel(uint32_t *img, int64_t words) {
+    if (blockIdx.x == 0 && threadIdx.x < 64) img[threadIdx.x] = 0u;  // header: valid
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (int64_t)gridDim.x * blockDim.x)
+        img[64 + i] = XM_ZERO_WORD;  // the word of a zero (the border stays so)
+}
+
+int fp8a_word_image_init(void *image, int64_t Bn, int64_t C, int64_t H, int64_t W, int ph, int pw,
+                         fp8a_stream_t stream) {
+    if (image == nullptr || fp8a_word_image_bytes(Bn, C, H, W, ph, pw) == 0) return fail(FP8A_EINVAL, "word image");
+    if (((uintptr_t)image & 255) != 0) return fail(FP8A_EINVAL, "word image must be 256-byte aligned");
+    const WordImage wi = word_image(H, W, ph, pw);
+    const int64_t words = Bn * C * wi.H * wi.W;
+    word_image_fill_kernel<<<(unsigned)std::min<int64_t>((words + 255) / 256, 8192), 256, 0, (hipStream_t)stream>>>(
+        (uint32_t *)image, words);
+    return hip_check("fp8a word image init");
+}
+
+// Whether a convolution would read an in_image (fp8a_conv2d_chain): the matrix-core path with its A
+// pre-pass (not the fp32-staging form of 1x1 convolutions with few column tiles, not the tile-table
+// or VALU kernels), ungrouped, more than one output channel, a fused input quantizer.
+int fp8a_conv2d_wants_image(int64_t Cout, int kh, int kw, int ph, int pw, int groups, int E, int Mw,
+                            const int32_t *table, uint32_t flags) {
+    if (groups != 1 || Cout <= 1 || no_mx() || check_format(E, Mw) != FP8A_OK) return 0;
+    TablePack tp;
+    int mode;
+    if (pack_table(table, Mw, (flags & F_APPROX) != 0, tp, mode) != FP8A_OK) return 0;
+    if (!f8_form(E, Mw, flags & ~F_TB, mode) || g_opt_one_hot) return 0;
+    if (kh == 1 && kw == 1 && ph == 0 && pw == 0) {  // xm_af32: fp32 staging up to af32_maxct column tiles
+        const int64_t bnt = 16 * xm_ncg(Cout), ct = (Cout + bnt - 1) / bnt;
+        if (ct <= g_opt_af32_maxct) return 0;
+    }
+    return 1;
+}
+
+int fp8a_conv2d_chain(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
+                      int64_t Cout, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw, int groups, int E,
+                      int Mw, const int32_t *bA, const int32_t *bW, const int32_t *bR, const int32_t *table,
+                      uint32_t flags, const float *bn, int act, float act_lo, float act_hi, const float *in_maxval,
+                      int in_nbits, int in_mbits, int in_sign_bits, float *in_bias_out, int32_t *in_ibias_out,
+                      const float *res, int post_act, float post_lo, float post_hi, const float *out_maxval,
+                      int out_nbits, int out_mbits, int out_sign_bits, float *out_bias_out, int32_t *out_ibias_out,
+                      const void *in_image, void *out_image, int next_ph, int next_pw, const float *next_maxval,
+                      int next_nbits, int next_mbits, int next_sign_bits, const int32_t *next_bR, int next_Mw,
+                      void *workspace, size_t workspace_bytes, fp8a_stream_t stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if ((in_image && ((uintptr_t)in_image & 255)) || (out_image && ((uintptr_t)out_image & 255)))
+        return fail(FP8A_EINVAL, "word images must be 256-byte aligned");
+    FqIn fin{}, fout{};
+    if (in_maxval) {
+        const int qE = in_nbits - in_sign_bits - in_mbits;
+        if (in_mbits < 1 || qE < 1) return fail(FP8A_EFORMAT, "bad FP8 quantizer format");
+        if (!in_bias_out || !in_ibias_out) return fail(FP8A_EINVAL, "null pointer");
+        fin = FqIn{in_maxval, qE, in_mbits, in_sign_bits};
+    } else if (!bA) {
+        return fail(FP8A_EINVAL, "null pointer");
+    }
+    if (out_maxval) {
+        const int qE = out_nbits - out_sign_bits - out_mbits;
+        if (out_mbits < 1 || qE < 1) return fail(FP8A_EFORMAT, "bad FP8 quantizer format");
+        if (!out_bias_out || !out_ibias_out) return fail(FP8A_EINVAL, "null pointer");
+        fout = FqIn{out_maxval, qE, out_mbits, out_sign_bits};
+        fq_bias_kernel<<<1, 1, 0, s>>>(fout, out_bias_out, out_ibias_out);
+        int rc = hip_check("fp8a output-quantizer bias");
+        if (rc) return rc;
+    }
+    EmitW em{};
+    if (out_image) {
+        const int64_t Ho = (H + 2 * ph - dh * (kh - 1) - 1) / sh + 1, Wo = (W + 2 * pw - dw * (kw - 1) - 1) / sw + 1;
+        const int qE = next_nbits - next_sign_bits - next_mbits;
+        if (!next_maxval || !next_bR || next_mbits < 1 || qE < 1 || !(next_Mw == 2 || next_Mw == 3) || next_ph < 0 ||
+            next_pw < 0)
+            return fail(FP8A_EINVAL, "bad next-convolution parameters for the word image");
+        const WordImage wi = word_image(Ho, Wo, next_ph, next_pw);
+        const bool can = groups == 1 && Cout > 1 && Ho > 0 && Wo > 0 && Bn * Cout * Ho * Wo < (1ll << 31) &&
+                         Bn * Cout * wi.H * wi.W < (1ll << 30);
+        // the header: valid (0) with the next quantizer's constants before this launch emits,
+        // invalid (nonzero) when it cannot emit
+        if (!can && hipMemsetAsync(out_image, 1, sizeof(uint32_t), s) != hipSuccess)
+            return hip_check("fp8a word image header");
+        if (can) {
+            emit_prep_kernel<<<1, 1, 0, s>>>((uint32_t *)out_image, FqIn{next_maxval, qE, next_mbits, next_sign_bits},
+                                             next_bR);
+            em.w = (uint32_t *)out_image + 64;
+            em.invalid = (uint32_t *)out_image;
+            em.awH = (int)wi.H; em.awW = (int)wi.W; em.awph = wi.ph; em.awpw = wi.pw;
+            em.Wo = (int)Wo;
+            em.hw = (uint32_t)(Ho * Wo);
+            fastdiv_params(em.hw, em.hw_mul, em.hw_shift);
+            fastdiv_params((uint32_t)Wo, em.wo_mul, em.wo_shift);
+            em.fq = FqIn{next_maxval, qE, next_mbits, next_sign_bits};
+            em.bR = next_bR;
+            em.Mw = next_Mw;
+        }
+    }
+    const size_t xq_bytes = fin.mx ? align256((size_t)(Bn * Cin * H * W) * sizeof(float)) : 0;
+    if (workspace == nullptr || workspace_bytes < FLAG_BYTES + xq_bytes)
+        return fail(FP8A_EINVAL, "conv2d_chain workspace too small");
+    const size_t rest = (workspace_bytes - xq_bytes) & ~(size_t)255;
+    float *xq = fin.mx ? (float *)((char *)workspace + rest) : nullptr;
+    return conv2d_impl(x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups, E, Mw,
+                       fin.mx ? nullptr : bA, bW, bR, table, flags, bn, act, act_lo, act_hi, workspace, rest, s, fin,
+                       in_bias_out, in_ibias_out, xq, res, post_act, post_lo, post_hi, fout,
+                       (const uint32_t *)in_image, em);
 }
 
 size_t fp8a_matmul_block_workspace_size(int64_t M, int64_t N, int64_t K) {

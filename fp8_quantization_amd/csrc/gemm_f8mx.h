@@ -234,6 +234,9 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
         *p.fq_bias = fbias;
         *p.fq_ibias = bA;
     }
+    // gated (the input's word image was emitted by the previous launch, fp8a_conv2d_chain): the
+    // words are already there unless an element left the window (the image's header word)
+    if (p.gate != nullptr && __hip_atomic_load(p.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
     const uint32_t emnA = (uint32_t)(128 - bA) << 23;
     const bool biasbad = !(xm_bias_ok(bA) && xm_bias_ok(bR));  // every output unit falls back
     bool bad = biasbad, win = true;
@@ -413,7 +416,7 @@ __global__ __launch_bounds__(256) void xm_decode_b(const GemmArgs p, int64_t kpa
 // checks and the fallback marks included -- instead of by the xm_decode_a pre-pass.  That pass
 // writes and re-reads 8 B per A element through HBM; staging-time decoding costs ~25 VALU
 // operations per element per column tile, the cheaper choice up to a few column tiles (run_gemm).
-template <int NCG, int RB, bool AF32, int XF>
+template <int NCG, int RB, bool AF32, int XF, bool EMIT>
 __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs p) {
     using Cf = XmCfg<NCG, RB>;
     constexpr int XM = XmFmt<XF>::M, XB = XmFmt<XF>::XB;
@@ -692,7 +695,7 @@ __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j) acc[i][j] = ct[(64 * sub + ety * TM + i) * CP + cb * TN + j];
-        store_tile(p, split, m0 + SR * h + 64 * sub, n0, ety, cb, acc);
+        store_tile<EMIT>(p, split, m0 + SR * h + 64 * sub, n0, ety, cb, acc);
     }
     FP8A_CLK_END
 }

@@ -24,6 +24,7 @@ from torch import nn
 from torch.nn.modules.conv import _ConvNd
 from torch.nn.modules.pooling import _AdaptiveAvgPoolNd, _AvgPoolNd
 
+from . import chain
 from .approx_calculation import QCustomBNConv2dTorch, QCustomConv2dTorch, QCustomLinearTorch
 from .quantization.base_quantized_classes import (QuantizedActivation, QuantizedModule, _set_layer_approx_calculation,
                                                   _set_layer_estimate_ranges, _set_layer_fix_ranges)
@@ -263,15 +264,18 @@ def quantize_model(model, specials=None, tie_activation_quantizers=False, **quan
 
 # ----------------------------------------------------------------------------------- block tails
 FUSE_BLOCK = os.environ.get("FP8A_FUSE_BLOCK", "1") != "0"
-
-
-def fused_block_tail(block, features, x, residual_fn, clamp):
+def fused_block_tail(block, features, x, residual_fn, clamp, in_image=None, next_layer=None, with_image=False):
     """A residual block's tail fused into its last conv's store (fp8a_conv2d_block):
     quantize_activations(clamp(features(x) + residual)) as one launch for the last conv, when that
     conv runs the fused BN store (BNFusedHijacker.block_epilogue_ok) and the block's activation
     quantizer is a per-tensor FPQuantizer in the fixed-range state (or off).  Returns None when the
     block must run unfused.  residual_fn(x) gives the residual (identity or downsample); clamp is
-    (lo, hi) or None.  Same result bit for bit as the reference's order (add, clamp, quantize)."""
+    (lo, hi) or None.  Same result bit for bit as the reference's order (add, clamp, quantize).
+
+    With CHAIN the block's convolutions hand their outputs to each other as word images
+    (WordChain): in_image is x's image (emitted by the previous block), next_layer the
+    convolution after the block; with_image=True returns (y, the image emitted for next_layer or
+    None)."""
     from .quantization.fp8_quantizer import FPQuantizer
     from .quantization.quantization_manager import Qstates
     from .quantization.quantized_folded_bn import BNFusedHijacker
@@ -288,9 +292,19 @@ def fused_block_tail(block, features, x, residual_fn, clamp):
                 or q.maxval.numel() != 1:
             return None
     residual = residual_fn(x)
-    h = features[:-1](x) if len(features) > 1 else x
     lo, hi = clamp if clamp is not None else (0.0, 0.0)
-    return last(h, post=(residual, int(clamp is not None), lo, hi, q))
+    post = (residual, int(clamp is not None), lo, hi, q)
+    layers = list(features)
+    if not chain.CHAIN or not all(isinstance(m, BNFusedHijacker) for m in layers):
+        h = features[:-1](x) if len(features) > 1 else x
+        y = last(h, post=post)
+        return (y, None) if with_image else y
+    h, img = x, in_image
+    for i, m in enumerate(layers):
+        ch = chain.WordChain(img, layers[i + 1] if i + 1 < len(layers) else next_layer)
+        h = m(h, post=post, chain=ch) if m is last else m(h, chain=ch)
+        img = ch.emitted
+    return (h, img) if with_image else h
 
 
 def fused_linear_tail(block, dense, x, residual, dropout=None):

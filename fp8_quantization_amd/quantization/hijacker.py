@@ -61,7 +61,7 @@ class QuantizationHijacker(QuantizedModule):
             return None
         return q
 
-    def _core(self, x, offsets=None, epilogue=None, post=None):
+    def _core(self, x, offsets=None, epilogue=None, post=None, chain=None):
         """Shared part of QuantizationHijacker.forward and BNFusedHijacker.forward.  epilogue
         (BNFusedHijacker's fused BN + activation) goes to the approx product only; the caller
         guarantees that product is the only one this forward runs."""
@@ -85,6 +85,8 @@ class QuantizationHijacker(QuantizedModule):
                 kw["qin"] = fq  # x is unquantized; the op quantizes it and sets fq.custom_bias
             if post is not None:
                 kw["post"] = post  # a residual block's tail (BNFusedHijacker.forward)
+            if chain is not None:
+                kw["chain"] = chain  # the word-image hand-off (model_wrap.WordChain)
             res = self.run_forward(x, weight, bias, offsets=offsets, **kw)
         self._check_res_flag()
         if res is None:  # fixed ranges, no approx / qamaa product and original_quantize_res off: the

@@ -58,14 +58,16 @@ class BNFusedHijacker(QuantizationHijacker):
         return (self._fused_epilogue() is not None and self.out_channels // self.groups != 1
                 and (self.quantize_input or not self._qa()))
 
-    def forward(self, x, post=None):
+    def forward(self, x, post=None, chain=None):
         """post: ``(residual, clamp, lo, hi, output FPQuantizer or None)`` -- the caller's block
-        tail y = q(clamp(y + residual)) fused into the store (only when block_epilogue_ok())."""
+        tail y = q(clamp(y + residual)) fused into the store (only when block_epilogue_ok()).
+        chain: a model_wrap.WordChain (the word-image hand-off between consecutive convolutions);
+        it only acts in the fused store, and records there whether the next image was emitted."""
         ep = self._fused_epilogue()
         if post is not None and not self.block_epilogue_ok():
             raise AssertionError("block epilogue requested where the fused store does not run")
         if ep is not None:
-            res, qa = self._core(x, epilogue=ep, post=post)
+            res, qa = self._core(x, epilogue=ep, post=post, chain=chain)
             return self._epilogue(res, qa, activation_done=True)
         res, qa = self._core(x)
         res = F.batch_norm(res, self.running_mean, self.running_var, self.gamma, self.beta, self.training,

@@ -183,14 +183,21 @@ class QuantizedBlock(QuantizedActivation):
         self.relu = block.relu
 
     def forward(self, x):
+        return self.forward_chain(x)[0]
+
+    def forward_chain(self, x, in_image=None, next_layer=None):
+        """forward, with the word-image hand-off (chain.WordChain) in the fused state: in_image is
+        x's word image (emitted by the previous block), next_layer the convolution after this
+        block.  Returns (output, the image emitted for next_layer or None)."""
         fused = fused_block_tail(self, self.features, x,
-                                 lambda t: t if self.downsample is None else self.downsample(t), (0.0, float("inf")))
+                                 lambda t: t if self.downsample is None else self.downsample(t), (0.0, float("inf")),
+                                 in_image=in_image, next_layer=next_layer, with_image=True)
         if fused is not None:
             return fused
         residual = x if self.downsample is None else self.downsample(x)
         out = self.features(x)
         out += residual
-        return self.quantize_activations(self.relu(out))
+        return self.quantize_activations(self.relu(out)), None
 
 
 class QuantizedResNet(QuantizedModel):
@@ -213,7 +220,16 @@ class QuantizedResNet(QuantizedModel):
             raise ValueError("Quantization setup '{}' not supported for Resnet".format(quant_setup))
 
     def forward(self, x):
-        return self.fc(self.flattener(self.avgpool(self.features(x))))
+        # the features in order, the blocks handing word images to each other (chain.WordChain)
+        mods = [b for m in self.features for b in (m if isinstance(m, nn.Sequential) else [m])]
+        img = None
+        for i, m in enumerate(mods):
+            if isinstance(m, QuantizedBlock):
+                nxt = mods[i + 1] if i + 1 < len(mods) else None
+                x, img = m.forward_chain(x, img, nxt.features[0] if isinstance(nxt, QuantizedBlock) else None)
+            else:
+                x, img = m(x), None
+        return self.fc(self.flattener(self.avgpool(x)))
 
 
 def resnet18_approx(weights=None, bn_stats_batches=0, device=None, **cfg):

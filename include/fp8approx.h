@@ -265,6 +265,53 @@ int fp8a_conv2d_block(const float *x, const float *w, float *y, int64_t Bn, int6
                       size_t workspace_bytes, fp8a_stream_t stream);
 
 /*
+ * Word-image hand-off between two convolutions (round 4; no reference counterpart: it removes the
+ * A operand pre-pass xm_decode_a that the matrix-core path runs on every convolution's input).
+ * A word image is a convolution's input pre-decoded for the matrix-core kernel -- one 32-bit word
+ * per element in a zero-bordered [Bn][C][H + 2 ph][W'] layout -- behind a 256-byte header whose
+ * first word flags it invalid.  fp8a_word_image_bytes gives its size (0 for bad arguments);
+ * fp8a_word_image_init fills a 256-byte aligned buffer once (header valid, every word that of a
+ * zero: the border keeps it).
+ */
+size_t fp8a_word_image_bytes(int64_t Bn, int64_t C, int64_t H, int64_t W, int ph, int pw);
+int fp8a_word_image_init(void *image, int64_t Bn, int64_t C, int64_t H, int64_t W, int ph, int pw,
+                         fp8a_stream_t stream);
+
+/*
+ * fp8a_conv2d_block with the hand-off (the reference's QuantizedBlock / Sequential chain of
+ * QCustomBNConv2dTorch layers, resnet_quantized_approx.py:11-41, each quantizing its own input,
+ * hijacker.py:81-83):
+ *   in_image: NULL, or THIS convolution's input x as the word image a previous fp8a_conv2d_chain
+ *             call emitted (same Bn, Cin, H, W, ph, pw; needs in_maxval: the words hold
+ *             fq_in(x)).  Where the matrix-core path runs, its words replace the A pre-pass; an
+ *             image flagged invalid (an element outside the path's window) is re-decoded from x,
+ *             which must be the fp32 tensor the emitting call wrote.  Elsewhere it is ignored.
+ *   out_image: NULL, or the NEXT convolution's input image to emit while y is stored: the words
+ *             of next_fq(y) for a next convolution with padding next_ph / next_pw, input quantizer
+ *             next_maxval (per tensor) / next_nbits / next_mbits / next_sign_bits, result bias
+ *             next_bR and mantissa width next_Mw (3: E4M3, 2: E5M2).  y is written as well.
+ *             Where this call cannot emit (groups > 1, Cout == 1) the image is flagged invalid.
+ * Results are bit-identical to the unchained calls.  workspace: fp8a_conv2d_block_workspace_size().
+ */
+/* 1 when a convolution of this shape / format would read an in_image (the matrix-core path with its
+ * A pre-pass: ungrouped, Cout > 1, E4M3 / E5M2 with s2n + qbma and a {0,1} or zero table, not a
+ * 1x1 unpadded convolution staged from fp32), else 0: emitting an image for it would be wasted. */
+int fp8a_conv2d_wants_image(int64_t Cout, int kh, int kw, int ph, int pw, int groups, int E, int Mw,
+                            const int32_t *table, uint32_t flags);
+int fp8a_conv2d_chain(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H,
+                      int64_t W, int64_t Cout, int kh, int kw, int sh, int sw, int ph, int pw, int dh,
+                      int dw, int groups, int E, int Mw, const int32_t *bA, const int32_t *bW,
+                      const int32_t *bR, const int32_t *table, uint32_t flags, const float *bn,
+                      int act, float act_lo, float act_hi, const float *in_maxval, int in_nbits,
+                      int in_mbits, int in_sign_bits, float *in_bias_out, int32_t *in_ibias_out,
+                      const float *res, int post_act, float post_lo, float post_hi,
+                      const float *out_maxval, int out_nbits, int out_mbits, int out_sign_bits,
+                      float *out_bias_out, int32_t *out_ibias_out, const void *in_image,
+                      void *out_image, int next_ph, int next_pw, const float *next_maxval,
+                      int next_nbits, int next_mbits, int next_sign_bits, const int32_t *next_bR,
+                      int next_Mw, void *workspace, size_t workspace_bytes, fp8a_stream_t stream);
+
+/*
  * A linear layer with its neighbours' elementwise work fused (QCustomLinearTorch.run_forward,
  * approx_calculation.py:1007-1023, plus the callers' tails in vit_quantized_approx.py:117-156):
  *   C = fq_out(clamp(bn_act(fq_in(A) @ B) + res, post_lo, post_hi))

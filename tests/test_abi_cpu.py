@@ -91,3 +91,28 @@ def test_bad_extent_maps_to_assertion_error():
     rc = L.fp8a_matmul(None, 2, None, 1, 1, None, 4, 3, 4, 5, 4, 3, None, None, 0, None, None, 0, None, 0, None)
     with pytest.raises(AssertionError):
         _lib.check(rc, "fp8a_matmul")
+
+
+def test_word_image_queries_are_host_only():
+    """fp8a_word_image_bytes / fp8a_conv2d_wants_image (the word-image hand-off,
+    fp8a_conv2d_chain) are host logic: sizes of the zero-bordered image behind its 256-B header,
+    and which convolutions would read one (matrix-core path with its A pre-pass)."""
+    import torch
+    L = _lib.load()
+    # W % 4 == 0: left border widened to 4 words, rows rounded to a multiple of 4
+    assert L.fp8a_word_image_bytes(2, 64, 56, 56, 1, 1) == 256 + _a256(2 * 64 * 58 * 64 * 4)
+    assert L.fp8a_word_image_bytes(1, 3, 7, 7, 1, 1) == 256 + _a256(3 * 9 * 9 * 4)
+    assert L.fp8a_word_image_bytes(0, 3, 7, 7, 1, 1) == 0
+    fl = _lib.APPROX | _lib.S2N | _lib.QBMA
+    z = torch.zeros((8, 8), dtype=torch.int32)
+    z4 = torch.zeros((4, 4), dtype=torch.int32)
+    wants = lambda cout, k, p, g, E, M, t, f=fl: L.fp8a_conv2d_wants_image(  # noqa: E731
+        cout, k, k, p, p, g, E, M, _lib.host_ptr(t), f)
+    assert wants(64, 3, 1, 1, 4, 3, z) == 1          # 3x3: the A pre-pass runs
+    assert wants(64, 3, 1, 1, 5, 2, z4) == 1         # E5M2 too
+    assert wants(64, 1, 0, 1, 4, 3, z) == 0          # 1x1, one column tile: staged from fp32
+    assert wants(1024, 1, 0, 1, 4, 3, z) == 1        # 1x1, 16 column tiles: pre-pass
+    assert wants(64, 3, 1, 2, 4, 3, z) == 0          # grouped
+    assert wants(1, 3, 1, 1, 4, 3, z) == 0           # one output channel: tensor-bias path
+    assert wants(64, 3, 1, 1, 3, 4, torch.zeros((16, 16), dtype=torch.int32)) == 0  # E3M4: tile-table kernel
+    assert wants(64, 3, 1, 1, 4, 3, z, _lib.APPROX | _lib.QBMA) == 0  # no s2n: not the matrix-core form

@@ -1,0 +1,171 @@
+"""The word-image hand-off between consecutive approx convolutions (fp8a_conv2d_chain, round 4).
+
+A producer convolution writes, next to its fp32 output y, the consumer's A operand word image
+(the words of fq_next(y)); the consumer's launch then runs its A pre-pass gated.  Checked:
+  * op level, bit-identical consumer outputs and input-quantizer biases with and without the
+    image: plain producer store, BN + ReLU epilogue, a residual tail with an output quantizer,
+    a split-K producer (the reduction emits), a producer whose gated exact kernel recomputes
+    units (the exact kernel emits), E4M3 and E5M2;
+  * an image flagged invalid is re-decoded from y (same result);
+  * a producer that cannot emit (grouped) flags the image invalid;
+  * model level: ResNet-18 / ResNet-50 logits bit-identical with the hand-off on and off, and the
+    hand-off really ran (fewer full pre-passes: counted through the launch trace of a profiler-free
+    counter, the consumer launches that read an image).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device")
+    from fp8_quantization_amd import _lib
+    _lib.load()
+
+
+def _grid(g, shape, M, lo=-6, hi=3, zero=0.3):
+    e = torch.randint(lo, hi, shape, generator=g).float()
+    m = torch.randint(0, 2 ** M, shape, generator=g).float()
+    v = torch.ldexp(1.0 + m / 2 ** M, e.int()) * (torch.randint(0, 2, shape, generator=g).float() * 2 - 1)
+    v[torch.rand(shape, generator=g) < zero] = 0.0
+    return v
+
+
+def _bits(t):
+    return t.detach().cpu().contiguous().view(torch.int32)
+
+
+def _run_pair(E, M, cin, cmid, cout, hw, Bn, k1, k2, p1, p2, epilogue, post, seed, bad_w=False, fmt_table=None):
+    """producer conv1 (x -> y) and consumer conv2 (y -> z, fused input quantizer), unchained and
+    chained; returns (z, z_chained, consumer input bias pair)."""
+    from fp8_quantization_amd.approx_ops import approx_conv2d, make_flags, new_word_image, bn_act_epilogue
+    from fp8_quantization_amd.error_tables import get_error_table_NN
+    g = torch.Generator().manual_seed(seed)
+    tab = fmt_table if fmt_table is not None else get_error_table_NN(E, M, False, 3, zero_table_ext=(E, M) == (5, 2))
+    fl = make_flags(True, True, True)
+    b = 2 ** (E - 1)
+    x = _grid(g, (Bn, cin, hw, hw), M).to(DEV)
+    w1 = _grid(g, (cmid, cin, k1, k1), M, -8, 0, 0.0).to(DEV)
+    w2 = _grid(g, (cout, cmid, k2, k2), M, -8, 0, 0.0).to(DEV)
+    if bad_w:  # off-grid weights: the producer's gated exact kernel recomputes their column units
+        w1[3, 0, 0, 0] = 0.3333
+    bA, bR1, bR2 = b + 2, b + 1, b
+    bW1 = torch.full((cmid,), b + 6, dtype=torch.int32, device=DEV)
+    bW2 = torch.full((cout,), b + 6, dtype=torch.int32, device=DEV)
+    ep = None
+    if epilogue:
+        gam = torch.rand(cmid, generator=g) + 0.5
+        ep = bn_act_epilogue(torch.randn(cmid, generator=g) * 0.1, torch.rand(cmid, generator=g) + 0.5, gam,
+                             torch.randn(cmid, generator=g) * 0.1, 1e-5, torch.nn.ReLU())
+        ep = (ep[0].to(DEV),) + tuple(ep[1:])
+    mx_out = torch.tensor([6.0], device=DEV)
+    pst = None
+    if post:
+        res = _grid(g, (Bn, cmid, hw, hw), M).to(DEV)
+        pst = (res, 1, 0.0, float("inf"), (mx_out, 8, M, 1))
+    mx2 = torch.tensor([5.5], device=DEV)
+    qin2 = (mx2, 8, M, 1)
+    bR2t = torch.tensor([bR2], dtype=torch.int32, device=DEV)
+    args1 = dict(flags=fl, padding=(p1, p1), epilogue=ep)
+    args2 = dict(flags=fl, padding=(p2, p2))
+
+    def produce(chain=None):
+        kw = dict(args1)
+        if pst is not None:
+            kw["post"] = pst
+        if chain is not None or pst is not None:
+            out = approx_conv2d(x, w1, E, M, bA, bW1, bR1, tab, chain=chain, **kw)
+            return out[0]
+        return approx_conv2d(x, w1, E, M, bA, bW1, bR1, tab, **kw)
+
+    y = produce()
+    z, ib, _ = approx_conv2d(y, w2, E, M, None, bW2, bR2t, tab, qin=qin2, **args2)
+    img = new_word_image(Bn, cmid, hw, hw, p2, p2, DEV)
+    y2 = produce(chain=(None, (img, (p2, p2), qin2, bR2t, M)))
+    assert torch.equal(_bits(y), _bits(y2)), "producer output changed by the emission"
+    z2, ib2, _ = approx_conv2d(y2, w2, E, M, None, bW2, bR2t, tab, qin=qin2, chain=(img, None), **args2)
+    torch.cuda.synchronize()
+    header = int(img[:4].view(torch.int32).item())
+    return z, z2, (ib, ib2), header, (y2, w2, bW2, bR2t, qin2, args2, img, tab)
+
+
+@pytest.mark.parametrize("E,M", [(4, 3), (5, 2)])
+@pytest.mark.parametrize("case", ["plain", "bn_relu", "tail", "splitk", "fallback"])
+def test_chain_bit_identical(E, M, case):
+    from fp8_quantization_amd import _lib
+    kw = dict(cin=16, cmid=64, cout=64, hw=14, Bn=3, k1=3, k2=3, p1=1, p2=1, epilogue=False, post=False, seed=7)
+    if case == "bn_relu":
+        kw.update(epilogue=True)
+    elif case == "tail":
+        kw.update(epilogue=True, post=True)
+    elif case == "splitk":  # long K, few output tiles: split-K (the reduction kernel stores y)
+        kw.update(cin=512, cmid=128, cout=64, hw=7, Bn=2, seed=8)
+    elif case == "fallback":
+        kw.update(bad_w=True, seed=9)
+    _lib.fallback_stats(reset=True)
+    z, z2, (ib, ib2), header, _ = _run_pair(E, M, **kw)
+    assert header == 0, "the emitted image was flagged invalid"
+    assert torch.equal(_bits(z), _bits(z2)), "consumer output differs with the word image"
+    assert torch.equal(ib, ib2)
+    if case == "fallback":
+        assert _lib.fallback_stats()["exact_launches"] >= 1
+
+
+def test_invalid_image_is_redecoded():
+    from fp8_quantization_amd.approx_ops import approx_conv2d
+    z, _, _, _, (y2, w2, bW2, bR2t, qin2, args2, img, tab) = _run_pair(
+        4, 3, cin=16, cmid=64, cout=64, hw=14, Bn=2, k1=3, k2=3, p1=1, p2=1, epilogue=True, post=False, seed=11)
+    img[4:].zero_()  # garbage words ...
+    img[:4].view(torch.int32).fill_(1)  # ... flagged invalid: the gated pre-pass re-decodes y
+    z3, _, _ = approx_conv2d(y2, w2, 4, 3, None, bW2, bR2t, tab, qin=qin2, chain=(img, None), **args2)
+    assert torch.equal(_bits(z), _bits(z3))
+
+
+def test_grouped_producer_flags_invalid():
+    from fp8_quantization_amd.approx_ops import approx_conv2d, make_flags, new_word_image
+    from fp8_quantization_amd.error_tables import get_error_table_NN
+    g = torch.Generator().manual_seed(3)
+    x = _grid(g, (2, 8, 10, 10), 3).to(DEV)
+    w = _grid(g, (8, 4, 3, 3), 3, -8, 0, 0.0).to(DEV)
+    img = new_word_image(2, 8, 10, 10, 1, 1, DEV)
+    tab = get_error_table_NN(4, 3, False, 3)
+    approx_conv2d(x, w, 4, 3, 10, torch.full((8,), 14, dtype=torch.int32, device=DEV), 9, tab,
+                  flags=make_flags(True, True, True), padding=(1, 1), groups=2,
+                  chain=(None, (img, (1, 1), (torch.tensor([4.0], device=DEV), 8, 3, 1),
+                                torch.tensor([8], dtype=torch.int32, device=DEV), 3)))
+    torch.cuda.synchronize()
+    assert int(img[:4].view(torch.int32).item()) != 0
+
+
+@pytest.mark.parametrize("arch,fmt", [("resnet18", (4, 3)), ("resnet50", (4, 3)), ("resnet18", (5, 2))])
+def test_model_logits_identical_with_chain(arch, fmt, monkeypatch):
+    from fp8_quantization_amd import chain, resnet_workload as rw
+    E, M = fmt
+    torch.manual_seed(1)
+    m = getattr(rw, arch + "_approx")(bn_stats_batches=2, device=DEV, expo_width=E, mant_width=M).to(DEV).eval()
+    g = torch.Generator().manual_seed(2)
+    m.quantized()
+    m.estimate_ranges()
+    with torch.no_grad():
+        m(torch.randn((4, 3, 64, 64), generator=g).to(DEV))
+    m.fix_ranges()
+    x = torch.randn((3, 3, 64, 64), generator=g).to(DEV)
+    emitted = []
+    orig_done = chain.WordChain.done
+
+    def done(self, ch):
+        orig_done(self, ch)
+        emitted.append(self.emitted is not None)
+    monkeypatch.setattr(chain.WordChain, "done", done)
+    with torch.no_grad():
+        on = m(x)
+    assert sum(emitted) >= (7 if arch == "resnet18" else 10), emitted  # the hand-off ran
+    monkeypatch.setattr(chain, "CHAIN", False)
+    with torch.no_grad():
+        off = m(x)
+    assert torch.equal(_bits(on), _bits(off)), "logits differ with the word-image hand-off"
