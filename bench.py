@@ -366,7 +366,7 @@ def run(args, dev, rank=0, world=1):
             gbs = op_bytes / (op_ms / 1e3) / 1e9 if op_ms > 0 else None
             res["roofline"] = {
                 "bound": "hbm",
-                "kernel": "dn_gemm (csrc/gemm_dense.h: the exact product on the block-scaled fp8 matrix core, "
+                "kernel": "dn_gemm_bf16 (csrc/gemm_dense.h: the exact product on the bf16 matrix core, "
                           "implicit-GEMM conv / matmul; groups = 1 -- the depthwise convs stay torch's fp32 "
                           "contraction); timed per op with its operand packing and gated fp32 units",
                 "achieved": gbs,

@@ -91,15 +91,25 @@ class ApproxOpMixin:
             return approx_matmul(x, y, E, M, x_bias, y_bias, res_bias, table, flags=flags | tb)
         return self._exact_product(x, y, M)
 
-    @staticmethod
-    def _exact_product(x, y, M):
-        """The non-approx ``x @ y`` (approx_calculation.py:797, 811): on the GPU the block-scaled
-        fp8 matrix-core product for FP8-grid operands (E4M3 / E5M2), else the fp32 contraction
-        (also with FP8A_DENSE=0: A/B measurements)."""
-        fmt = dense_format(M) if DENSE_EXACT else None
+    def _exact_product(self, x, y, M):
+        """The non-approx ``x @ y`` (approx_calculation.py:797, 811): on the GPU the matrix-core
+        product (dense_format: the bf16 form, exact for every FP8 / E3M4 / E2M5 grid value) when
+        both operands went through this layer's FP8 quantizers, else the fp32 contraction (also
+        with FP8A_DENSE=0: A/B measurements).  Unquantized operands would mark every 64 x 64 unit
+        of the matrix-core launch for its fp32 recompute (dn_fix), far slower than torch's."""
+        fmt = dense_format(M) if DENSE_EXACT and self._operands_quantized() else None
         if x.is_cuda and fmt is not None:
             return dense_matmul(x, y, fmt)
         return x @ y
+
+    def _operands_quantized(self):
+        """Weights and activations both FP8-quantized in this forward (quantization on for both;
+        the hijacker quantizes the input, or the previous layer's output quantizer did)."""
+        if hasattr(self, "_qw") and hasattr(self, "_qa"):
+            return bool(self._qw() and self._qa())
+        # (the reference's own QuantizedModule, bind_operator_classes: its state buffers)
+        qw, qa = getattr(self, "_quant_w", None), getattr(self, "_quant_a", None)
+        return qw is not None and qa is not None and bool(qw.reshape(-1)[0]) and bool(qa.reshape(-1)[0])
 
     def multiply(self, x, y):
         return torch.matmul(x, y)
@@ -171,7 +181,7 @@ class ApproxConv2dMixin(ApproxOpMixin, ChainConsumerMixin):
             out = qamaa_conv2d(x.detach(), weight.detach(), *self._qamaa_params(), stride=self.stride,
                                padding=self.padding, dilation=self.dilation, groups=self.groups)
         else:  # exact product (also qamaa's single-column groups, approx_calculation.py:810-811)
-            fmt = dense_format(M) if DENSE_EXACT else None
+            fmt = dense_format(M) if DENSE_EXACT and self._operands_quantized() else None
             if x.is_cuda and fmt is not None and self.groups == 1:
                 out = dense_conv2d(x.detach(), weight.detach(), fmt, self.stride, self.padding, self.dilation)
             else:  # grouped (depthwise: one-column products) / wide-mantissa formats: the fp32 contraction

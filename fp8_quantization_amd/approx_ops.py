@@ -755,9 +755,11 @@ def _(A, B, fmt):
 
 
 def dense_matmul(A, B, fmt):
-    """A [M, K] @ B [K, N] (fp32 values on an FP8 grid, any strides) on the block-scaled fp8
-    matrix core: the reference's exact branch ``x @ y`` (approx_calculation.py:797, 811), equal to
-    the fp32 product up to summation order (off-grid values: their units in fp32)."""
+    """A [M, K] @ B [K, N] (fp32 values on an FP8 grid, any strides) on the matrix core: the
+    reference's exact branch ``x @ y`` (approx_calculation.py:797, 811), equal to the fp32 product
+    up to summation order (off-grid values: their units in fp32).  fmt: dense_format() -- the bf16
+    form (dn_gemm_bf16, v_mfma_f32_16x16x32_bf16) by default, the block-scaled fp8 form
+    (v_mfma_scale_f32_16x16x128_f8f6f4) with FP8A_DENSE_FMT=fp8."""
     if A.dim() != 2 or B.dim() != 2 or A.shape[1] != B.shape[0]:
         raise AssertionError(f"dense_matmul: shape mismatch {tuple(A.shape)} @ {tuple(B.shape)}")
     A, B = _as_f32(A), _as_f32(B)
@@ -794,8 +796,9 @@ def _(x, w, fmt, stride, padding, dilation):
 
 
 def dense_conv2d(x, w, fmt, stride=(1, 1), padding=(0, 0), dilation=(1, 1)):
-    """Exact-product convolution (groups = 1) on the block-scaled fp8 matrix core: the reference's
-    im2col + ``x @ y`` (approx_calculation.py:811) without the im2col image."""
+    """Exact-product convolution (groups = 1) on the matrix core (the bf16 form by default, the
+    block-scaled fp8 form with FP8A_DENSE_FMT=fp8; see dense_matmul): the reference's im2col +
+    ``x @ y`` (approx_calculation.py:811) without the im2col image."""
     if x.dim() != 4 or w.dim() != 4 or x.shape[1] != w.shape[1]:
         raise AssertionError(f"dense_conv2d: shape mismatch {tuple(x.shape)} * {tuple(w.shape)}")
     x = _as_f32(x).contiguous()

@@ -204,6 +204,10 @@ struct GemmArgs {
     float *ohd;
     int ohstats;  // count into g_ohstat (diagnostics)
     const uint32_t *lutw;  // the LDS table image (XM_LUT_WORDS words), written by xm_decode_b
+    // E5M2 (gemm_f8mx_kernel XF = 1): per (K-step, 16-column group) the nonzero B elements' exponent
+    // range, (max e_b + 128) | (min e_b + 128) << 8 ([kpad][npad / 16]; 0xFF00 when all are zero)
+    const uint16_t *ebr;
+    int xm_vmin;  // the smallest binade of the table value V' (0: V' >= 1, -1 with a {0,1} table)
     int64_t npad;
     // fused input quantization (fp8a_conv2d_qin): A = fq(X); the quantizer's bias is written to
     // fq_bias / fq_ibias by the A pre-decode, and bA points at fq_ibias
@@ -332,6 +336,11 @@ constexpr int AP = BM + 4, BP = BN + 4;
 __device__ __forceinline__ uint32_t xm_word_a(float x, int M, int xb, uint32_t emnA, int bR, bool &ok);  // gemm_f8mx.h
 __host__ __device__ constexpr int xm_xbias(int Mw);
 
+// A = 0 as an A word of the matrix-core path (gemm_f8mx.h): cvt scale 2^126 (the code is 0), row 0.
+// Nonzero words keep se <= 252, so a zero word is the one with se = 253, and the E5M2 halved form's
+// se + 1 (254: 2^127) still flushes it to 0.
+constexpr uint32_t XM_ZERO_WORD = 253u << 23;
+
 // Word-image emission (EmitW): one word per final output value at NCHW output index o (< 2^31,
 // the host checks).  The next quantizer's constants sit in the image's header (emit_prep_kernel:
 // [1] maxval, [2] its float bias, [3] 2^(1 - bias) bits, [4] bR), made wave-uniform (SGPRs) once
@@ -362,21 +371,35 @@ __device__ __forceinline__ uint32_t emit_index(const GemmArgs &p, uint32_t uo, u
     wo = pix - ho * (uint32_t)p.em.Wo;
     return (plane * (uint32_t)p.em.awH + ho + (uint32_t)p.em.awph) * (uint32_t)p.em.awW + wo + (uint32_t)p.em.awpw;
 }
-__device__ __forceinline__ void emit1(const GemmArgs &p, const EmitCtx &e, int64_t o, float v) {
+// Max of v over the wave, then one atomicMax into *dst (v >= 0; 0 records nothing).  Every lane
+// of the wave must call it.
+__device__ __forceinline__ void wave_max_atomic(uint32_t *dst, uint32_t v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off));
+    if ((threadIdx.x & 63) == 0 && v != 0u) atomicMax(dst, v);
+}
+// 255 - the scale exponent of a nonzero word (the E5M2 halved-block decision reads the largest,
+// gemm_f8mx.h xm_needs_halving; the header's word 5 collects it for the consumer)
+__device__ __forceinline__ uint32_t word_sehi(uint32_t w) { return w == XM_ZERO_WORD ? 0u : 255u - (w >> 23); }
+
+__device__ __forceinline__ void emit1(const GemmArgs &p, const EmitCtx &e, int64_t o, float v, uint32_t &sehi) {
     uint32_t wo;
     const uint32_t wi = emit_index(p, (uint32_t)o, wo);
     bool ok = true;
-    p.em.w[wi] = emit_word(p, e, v, ok);
+    const uint32_t w = emit_word(p, e, v, ok);
+    p.em.w[wi] = w;
+    sehi = max(sehi, word_sehi(w));
     if (!ok) atomicOr(p.em.invalid, 1u);
 }
 // four consecutive outputs (o % 4 == 0 in an NCHW plane of hw % 4 == 0): one 16-B store when
 // they sit in one row of the image (Wo % 4 == 0: always; the interior rows start 16-B aligned)
-__device__ __forceinline__ void emit4(const GemmArgs &p, const EmitCtx &e, int64_t o, float4 v) {
+__device__ __forceinline__ void emit4(const GemmArgs &p, const EmitCtx &e, int64_t o, float4 v, uint32_t &sehi) {
     uint32_t wo;
     const uint32_t wi = emit_index(p, (uint32_t)o, wo);
     bool ok0 = true, ok1 = true, ok2 = true, ok3 = true;
     const uint4 w = make_uint4(emit_word(p, e, v.x, ok0), emit_word(p, e, v.y, ok1), emit_word(p, e, v.z, ok2),
                                emit_word(p, e, v.w, ok3));
+    sehi = max(max(sehi, max(word_sehi(w.x), word_sehi(w.y))), max(word_sehi(w.z), word_sehi(w.w)));
     if (wo + 3 < (uint32_t)p.em.Wo && (wi & 3u) == 0u) {
         *reinterpret_cast<uint4 *>(p.em.w + wi) = w;
     } else {
@@ -443,16 +466,17 @@ __device__ __forceinline__ void store_tile(const GemmArgs &p, int64_t split, int
     // word-image emission from each final value (the split-K reduction emits instead)
     const bool emit = EMIT && !partial && p.em.w != nullptr;
     const EmitCtx ec = EMIT ? emit_ctx(p) : EmitCtx{};
+    uint32_t sehi = 0;
     auto fin1 = [&](int64_t o, float v) {
         if (partial) return v;
         v = post1(q, o, v, pb);
-        if (emit) emit1(q, ec, o, v);
+        if (emit) emit1(q, ec, o, v, sehi);
         return v;
     };
     auto fin4 = [&](int64_t o, float4 v) {
         if (partial) return v;
         v = post4(q, o, v, pb);
-        if (emit) emit4(q, ec, o, v);
+        if (emit) emit4(q, ec, o, v, sehi);
         return v;
     };
     if (!p.nchw) {
@@ -498,6 +522,7 @@ __device__ __forceinline__ void store_tile(const GemmArgs &p, int64_t split, int
             }
         }
     }
+    if (emit) wave_max_atomic(p.em.invalid + 5, sehi);
 }
 
 template <bool S2N, bool QBMA, bool GCLIP, int TMODE>
@@ -884,6 +909,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs p) {
     const int64_t MN = p.M * p.N;
     const float pb = post_bias(p);
     const EmitCtx ec = emit_ctx(p);
+    uint32_t sehi = 0;
     const int S = p.splits + (p.ohd ? 1 : 0);  // (the one-hot path's correction slice follows the partials)
     const bool vec = p.nchw ? ((p.hw & 3) == 0) : ((p.N & 3) == 0 && (p.ldc & 3) == 0);
     const bool aligned = ((((uintptr_t)p.C) & 15) == 0) && ((((uintptr_t)p.part) & 15) == 0) && ((MN & 3) == 0) &&
@@ -920,8 +946,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs p) {
             }
             const float4 r = post4(p, o, acc, pb);
             *reinterpret_cast<float4 *>(p.C + o) = r;
-            if (p.em.w) emit4(p, ec, o, r);
+            if (p.em.w) emit4(p, ec, o, r, sehi);
         }
+        if (p.em.w) wave_max_atomic(p.em.invalid + 5, sehi);
         return;
     }
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < MN; q += stride) {
@@ -939,8 +966,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs p) {
         }
         const float r = post1(p, o, epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, ch, acc), pb);
         p.C[o] = r;
-        if (p.em.w) emit1(p, ec, o, r);
+        if (p.em.w) emit1(p, ec, o, r, sehi);
     }
+    if (p.em.w) wave_max_atomic(p.em.invalid + 5, sehi);
 }
 
 // A(m, k) for the exact kernels: matrix or implicit im2col (through the fused input quantizer
@@ -983,7 +1011,11 @@ __global__ __launch_bounds__(256) void gemm_exact_kernel(const GemmArgs p) {
             const int64_t o = out_index(p, m, n);
             const float r = post1(p, o, epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, p.coff + n, s), post_bias(p));
             p.C[o] = r;
-            if (p.em.w) emit1(p, emit_ctx(p), o, r);
+            if (p.em.w) {
+                uint32_t sh = 0;
+                emit1(p, emit_ctx(p), o, r, sh);
+                if (sh) atomicMax(p.em.invalid + 5, sh);
+            }
         }
         return;
     }
@@ -1029,7 +1061,11 @@ __global__ __launch_bounds__(256) void gemm_exact_kernel(const GemmArgs p) {
             const int64_t o = out_index(p, m, n);
             const float r = post1(p, o, epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, p.coff + n, s[j] + part[j]), pb);
             p.C[o] = r;
-            if (p.em.w) emit1(p, ec, o, r);
+            if (p.em.w) {
+                uint32_t sh = 0;
+                emit1(p, ec, o, r, sh);
+                if (sh) atomicMax(p.em.invalid + 5, sh);
+            }
         }
     }
 }
@@ -1342,14 +1378,25 @@ static void launch_f8mx_t(const GemmArgs &a, hipStream_t s) {
 }
 template <int XF>
 static void launch_f8mx_f(const GemmArgs &a, hipStream_t s) {
-    if (a.xncg == 1) launch_f8mx_t<1, 4, XF>(a, s);
-    else if (a.xncg == 2) launch_f8mx_t<2, 4, XF>(a, s);
-    else launch_f8mx_t<4, 8, XF>(a, s);
+    if (a.xncg == 1) {
+        launch_f8mx_t<1, 4, XF>(a, s);
+    } else if constexpr (XF == 2) {
+        launch_f8mx_t<2, 4, XF>(a, s);  // (the halved-block form: at most 32 columns, gemm_f8mx.h)
+    } else {
+        if (a.xncg == 2) launch_f8mx_t<2, 4, XF>(a, s);
+        else launch_f8mx_t<4, 8, XF>(a, s);
+    }
 }
-// E4M3 (XF 0) or E5M2 (XF 1, mant_width 2) result grid
+// E4M3 (XF 0) or E5M2 (mant_width 2) result grid; E5M2 launches both its kernels, the plain one
+// (XF 1) and the halved-block one (XF 2), and the one the launch's operands do not call for exits
+// at once (xm_needs_halving, gemm_f8mx.h)
 static void launch_f8mx(const GemmArgs &a, hipStream_t s) {
-    if (a.Mw == 2) launch_f8mx_f<1>(a, s);
-    else launch_f8mx_f<0>(a, s);
+    if (a.Mw == 2) {
+        launch_f8mx_f<1>(a, s);
+        launch_f8mx_f<2>(a, s);
+    } else {
+        launch_f8mx_f<0>(a, s);
+    }
 }
 
 // gemm_f8mx_kernel's tile width: the fewest padded columns, ties to the wider tile (N = 16 -> 16,
@@ -1539,7 +1586,9 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // (a_words of them) + B column pairs [Kpad][Npad / 2] of 8 bytes.
 static size_t xm_operand_bytes(int64_t N, int64_t K, int64_t a_words) {
     const int64_t kpad = (K + BK - 1) / BK * BK, npad = (N + BN - 1) / BN * BN;
-    return align256((size_t)a_words * 4) + align256((size_t)(kpad * npad / 2) * 8) + 16384;  // + table image
+    // + table image + the E5M2 B exponent ranges
+    return align256((size_t)a_words * 4) + align256((size_t)(kpad * npad / 2) * 8) + 16384 +
+           align256((size_t)(kpad * npad / 16) * 2);
 }
 
 // The per-unit fallback marks after the flag word: urow [nur], ucol [nuc], utile [nur * nuc] bytes.
@@ -1804,6 +1853,8 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
             a.awld = kpad;
             a.bqw = (const uint2 *)(base + align256((size_t)a_words * 4));
             a.lutw = (const uint32_t *)(base + align256((size_t)a_words * 4) + align256((size_t)(kpad * npad / 2) * 8));
+            a.ebr = (const uint16_t *)((const char *)a.lutw + 16384);
+            a.xm_vmin = mode == TM_NONE ? 0 : -1;
             a.npad = npad;
             a.ttf7 = 0;
             for (int i = 0; tt && i < (1 << (2 * a.Mw)); ++i) a.ttf7 |= a.tab.raw[i] < 0;
@@ -2563,6 +2614,7 @@ __global__ void emit_prep_kernel(uint32_t *hdr, FqIn fq, const int32_t *bR) {
     hdr[2] = __float_as_uint(fb);
     hdr[3] = (uint32_t)(128 - (int)fb) << 23;
     hdr[4] = (uint32_t)*bR;
+    hdr[5] = 0u;  // 255 - the smallest scale exponent of the emitted nonzero words (wave_max_atomic)
 }
 
 __global__ void word_image_fill_kernel(uint32_t *img, int64_t words) {

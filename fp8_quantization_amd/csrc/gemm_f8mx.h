@@ -70,16 +70,29 @@ constexpr int XM_LUT_WORDS = XM_NPAIR * 8;  // [pair][m_a] u32 (s_a = +), 2.5 Ki
 constexpr uint32_t XM_ROW_SHIFT = 3, XM_ROW_MASK = 0x78u;  // A word bits 3-6: row * 8 = byte offset in a column block
 constexpr int XBK = 8;                         // K-steps per staged tile
 constexpr int XM_TTK = 16 * 32 + 16;           // tile-table words per K-step: [tx 16][row 16][j 2] + bank shift
-constexpr uint32_t XM_ZERO_WORD = 254u << 23;  // A = 0: cvt scale 2^127 (the code is 0), row 0
+// (XM_ZERO_WORD, the word of A = 0: fp8approx.hip, next to the word-image emission)
 constexpr int XM_CP = BN + 1;  // the 64-column epilogue slices of the other kernels: [64][BN + 1] floats
 
 // Result-grid formats of the matrix-core path: XF 0 = E4M3 (OCP e4m3, bias 7), 1 = E5M2 (OCP e5m2 /
-// bf8, bias 15).
+// bf8, bias 15), 2 = E5M2 with the halved-block form for the grid's top binade (below).
 template <int XF>
 struct XmFmt {
     static constexpr int M = XF ? 2 : 3;
     static constexpr int XB = XF ? 15 : 7;  // the OCP format's exponent bias
 };
+// E5M2: the launch needs the halved-block form when its largest A element times its largest B
+// element can reach the result grid's top binade 31 - bR: e_a + e_b + 1 >= 31 - bR, i.e. the
+// smallest A scale exponent se <= 112 + max e_b.  The pre-passes record both extremes in the
+// workspace head (xm_decode_a: 255 - min se, xm_decode_b: max e_b + 128; 0 = none); without the A
+// pre-pass (fp32 staging) the A grid's top binade (plus the one the quantizer's rounding can add)
+// stands in.  Both E5M2 kernels are launched; the one that does not apply exits at once.
+__device__ __forceinline__ bool xm_needs_halving(const GemmArgs &p, bool af32, int bA, int bR) {
+    const uint32_t a = __hip_atomic_load(p.flag + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t b = __hip_atomic_load(p.flag + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (b == 0u) return false;  // every B element is zero
+    const int se_min = af32 ? 110 + bA - bR : (a == 0u ? 1000 : 255 - (int)a);
+    return se_min <= 112 + (int)b - 128;
+}
 __host__ __device__ constexpr int xm_xbias(int Mw) { return Mw == 2 ? 15 : 7; }
 
 // Tile shapes of gemm_f8mx_kernel<NCG, RB, AF32>: 4 waves; NCG column groups of 16 columns x
@@ -154,8 +167,8 @@ __device__ __forceinline__ uint32_t xm_word_a(float x, int M, int xb, uint32_t e
     const uint32_t cb = __float_as_uint(c);
     const int se = 254 + xb - bR - (int)((cb >> 23) & 0xFFu);
     if ((cb & 0x7FFFFFFFu) == 0u) return XM_ZERO_WORD;
-    ok = ok && se >= 1 && se <= 254;
-    return ((uint32_t)min(max(se, 1), 254) << 23) | (((cb >> 31) * 8u + mc) << XM_ROW_SHIFT);
+    ok = ok && se >= 1 && se <= 252;
+    return ((uint32_t)min(max(se, 1), 252) << 23) | (((cb >> 31) * 8u + mc) << XM_ROW_SHIFT);
 }
 
 constexpr int TT_RS = 68;  // floats per m_a row of a K-step's table (64 columns + 4: conflict-free
@@ -220,6 +233,11 @@ __device__ __forceinline__ uint32_t oh_code_a(float x, uint32_t emnA, int sA, in
     return ((cb >> 31) << 7) | ((uint32_t)min(max(e, 1), 30) << 2) | (mc << 11);
 }
 
+// xm_decode_a's record for xm_needs_halving: 255 - (the smallest se of its nonzero E5M2 words)
+__device__ __forceinline__ void xm_record_se(const GemmArgs &p, uint32_t sehi) {
+    if (p.Mw == 2 && p.wfmt == 0) wave_max_atomic(p.flag + 1, sehi);
+}
+
 // A pre-pass, one (image | row) per blockIdx.y step.  conv: the group's channel slice of x
 // [Bn][Cin][H][W] (channels cbase..cbase+aw_c) -> words [Bn][aw_c][awH][awW], x at (awph, awpw)
 // inside a border of zero words (the padding the convolution reads, so the wave-independent
@@ -236,7 +254,12 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
     }
     // gated (the input's word image was emitted by the previous launch, fp8a_conv2d_chain): the
     // words are already there unless an element left the window (the image's header word)
-    if (p.gate != nullptr && __hip_atomic_load(p.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
+    if (p.gate != nullptr && __hip_atomic_load(p.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+        // (the emitting launch recorded its words' smallest scale exponent in the image header)
+        if (p.Mw == 2 && p.wfmt == 0 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+            atomicMax(p.flag + 1, p.gate[5]);
+        return;
+    }
     const uint32_t emnA = (uint32_t)(128 - bA) << 23;
     const bool biasbad = !(xm_bias_ok(bA) && xm_bias_ok(bR));  // every output unit falls back
     bool bad = biasbad, win = true;
@@ -245,10 +268,15 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
     uint32_t *const out = const_cast<uint32_t *>(p.aw);
     const int64_t hw = p.H * p.W;
     const int64_t rows = p.conv ? p.M / (p.Ho * p.Wo) : p.M, cols = p.conv ? p.aw_c * p.awH * p.awW : p.awld;
+    uint32_t sehi = 0;  // 255 - the smallest se of this thread's nonzero E5M2 words (xm_record_se)
     auto word = [&](float v, bool &ok) {
         if (p.fqin.mx) v = fq_apply(v, fmx, fbias, p.fqin.M, p.fqin.S);
-        return p.wfmt == 3 ? oh_code_a(v, emnA, 6 - bA, bR, ok) : p.wfmt == 2 ? tt16_word_a(v, emnA, bA, ok, win)
-               : p.wfmt ? tt_word_a(v, p.Mw, emnA, ok) : xm_word_a(v, p.Mw, xm_xbias(p.Mw), emnA, bR, ok);
+        if (p.wfmt == 3) return oh_code_a(v, emnA, 6 - bA, bR, ok);
+        if (p.wfmt == 2) return tt16_word_a(v, emnA, bA, ok, win);
+        if (p.wfmt) return tt_word_a(v, p.Mw, emnA, ok);
+        const uint32_t w = xm_word_a(v, p.Mw, xm_xbias(p.Mw), emnA, bR, ok);
+        sehi = max(sehi, word_sehi(w));
+        return w;
     };
     const uint32_t zw = p.wfmt ? 0u : XM_ZERO_WORD;  // the word of a zero (padding, columns >= K)
     // stores: 32-bit words, or the one-hot path's 16-bit codes (wfmt 3) at the same indices
@@ -311,6 +339,7 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
         }
         if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, fb_bits(p, biasbad));
         if (__syncthreads_or(win ? 0 : 1) && threadIdx.x == 0) atomicOr(p.flag, 4u);  // gemm_tt16_kernel's window (A)
+        xm_record_se(p, sehi);
         return;
     }
     // 16-B form: every row start 16-B aligned and the valid columns a multiple of 4 (all the
@@ -349,6 +378,7 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
     }
     if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, fb_bits(p, biasbad));
     if (__syncthreads_or(win ? 0 : 1) && threadIdx.x == 0) atomicOr(p.flag, 4u);  // gemm_tt16_kernel's window (A)
+    xm_record_se(p, sehi);
 }
 
 // B pre-pass: per (k, pair Q) of the padded [Kpad][npad / 2] pair grid, the addend pair
@@ -394,6 +424,29 @@ __global__ __launch_bounds__(256) void xm_decode_b(const GemmArgs p, int64_t kpa
             }
         }
         bq[i] = make_uint2(add, (code[0] + 9u * code[1]) * 32u);
+    }
+    if (p.Mw == 2 && p.ebr != nullptr) {  // E5M2: each (K-step, 16-column group)'s exponent range
+        const int64_t ng = p.npad / 16;
+        uint32_t bmax = 0;
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < kpad * ng; i += stride) {
+            const int64_t k = i / ng, g = i - k * ng;
+            int emax = -128, emin = 127;
+            for (int j = 0; j < 16 && k < p.K; ++j) {
+                const int64_t col = 16 * g + j;
+                if (col >= p.N) break;
+                float c;
+                uint32_t mc;
+                stage_decode(p.B[k * p.sbk + col * p.sbn], p.Mw, (uint32_t)(128 - p.bB[col * p.bBs]) << 23, true, c, mc);
+                const uint32_t cb = __float_as_uint(c);
+                if ((cb & 0x7FFFFFFFu) == 0u) continue;
+                const int e = (int)((cb >> 23) & 0xFFu) - 127;
+                emax = max(emax, e);
+                emin = min(emin, e);
+            }
+            const_cast<uint16_t *>(p.ebr)[i] = (uint16_t)((emax + 128) | ((emin + 128) << 8));
+            bmax = max(bmax, (uint32_t)(emax + 128));
+        }
+        wave_max_atomic(p.flag + 2, bmax);  // for xm_needs_halving
     }
     if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, fb_bits(p, biasbad));
 }
@@ -451,6 +504,7 @@ __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs
         biasbad = !(xm_bias_ok(bA) && xm_bias_ok(bR));  // every output unit falls back
     }
     const uint32_t emnA = (uint32_t)(128 - bA) << 23;
+    if (XF && xm_needs_halving(p, AF32, AF32 ? bA : 0, bR) != (XF == 2)) return;  // (the other E5M2 kernel's launch)
 
     // table: copied from the launch's pre-computed image (xm_decode_b), 16-B per thread and step
     for (int e = 4 * tid; e < XM_LUT_WORDS; e += 4 * NT)
@@ -616,10 +670,52 @@ __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs
             const int r16 = lane & 15, g = lane >> 4;
             const uint32_t base = wvo + (uint32_t)(2 * g) * (uint32_t)(TTK * 4);  // multiple of 128 B
             const char *tt0 = reinterpret_cast<const char *>(&sm.tt[0][0]);
+            // E5M2: the result grid has one normal binade more than e5m2 (31 - bR, the OCP top
+            // exponent being inf / NaN).  An A element whose products can reach it (se <= thi:
+            // e_a + max e_b + 1 >= 31 - bR over its 16 columns) is converted one binade down (scale
+            // exponent + 1, codes halved) and its MX block (the two A elements of lanes g, g ^ 1 at
+            // the same h) scaled by 2 -- allowed when both elements' products stay at or above the
+            // grid's second normal binade (se <= tok: e_a + min e_b + min binade(V') >= 2 - bR, a
+            // zero element always), so the halved codes round exactly as the unhalved ones; else the
+            // element stays unhalved, converts to inf and its tile falls back (as beyond the range).
+            // thi / tok: the (K-step 2 g + h, this wave's 16 columns) thresholds on se, packed as
+            // bytes (thi0, thi1, tok0, tok1).  (Branching around this per tile -- on whether any A
+            // element of the launch could need it -- made the register allocator spill 50-250
+            // VGPRs; as its own instance (XF = 2, launches where xm_needs_halving), on the
+            // 128 x 32 / 256 x 16 tiles, whose 60-70 VGPRs leave room for it: launch_f8mx.)
+            uint32_t thr = 0u;
+            if (XF == 2) {
+                const int64_t ng = p.npad / 16, e0 = (int64_t)(k0 + 2 * g) * ng + (n0 / 16 + wc);
+                const uint32_t r0 = p.ebr[e0], r1 = p.ebr[e0 + ng];
+                const uint32_t thi0 = (uint32_t)max(112 + (int)(r0 & 0xFFu) - 128, 0);
+                const uint32_t thi1 = (uint32_t)max(112 + (int)(r1 & 0xFFu) - 128, 0);
+                const uint32_t tok0 = (uint32_t)min(max(140 + (int)(r0 >> 8) - 128 + p.xm_vmin, 0), 252);
+                const uint32_t tok1 = (uint32_t)min(max(140 + (int)(r1 >> 8) - 128 + p.xm_vmin, 0), 252);
+                thr = thi0 | (thi1 << 8) | (tok0 << 16) | (tok1 << 24);
+            }
 #pragma unroll
             for (int b = 0; b < RB; ++b) {
                 const uint2 aw2 = *reinterpret_cast<const uint2 *>(&sm.aw[g][2 * (16 * (RB * wr + b) + r16)]);
-                const uint32_t awh[2] = {aw2.x, aw2.y};
+                uint32_t awh[2] = {aw2.x, aw2.y};
+                int sca = 127;  // this lane group's MX block scale (E8M0)
+                if (XF == 2) {
+                    // per element: need (se <= thi) and allow (se <= tok, or a zero: se 253), as
+                    // sign bits of differences (se, thresholds < 256)
+                    const uint32_t se0 = awh[0] >> 23, se1 = awh[1] >> 23;
+                    const uint32_t n0b = (se0 - (thr & 0xFFu) - 1u) >> 31, n1b = (se1 - ((thr >> 8) & 0xFFu) - 1u) >> 31;
+                    const uint32_t o0b = ((se0 - ((thr >> 16) & 0xFFu) - 1u) >> 31) | ((252u - se0) >> 31);
+                    const uint32_t o1b = ((se1 - (thr >> 24) - 1u) >> 31) | ((252u - se1) >> 31);
+                    const uint32_t bits = n0b | (n1b << 1) | (o0b << 2) | (o1b << 3);
+                    const auto sw16 = __builtin_amdgcn_permlane16_swap(bits, bits, false, false);
+                    const uint32_t pb = (g & 1) ? sw16[0] : sw16[1];  // lane ^ 16: the block partner
+                    const uint32_t halve = (bits | pb) & ((bits & pb) >> 2) & 3u;
+                    awh[0] += (halve & 1u) << 23;
+                    awh[1] += (halve >> 1) << 23;
+                    // block g's scale: blocks 0 / 2 (h = 0 / 1 of lane groups 0, 1), 1 / 3 (lane groups 2, 3)
+                    const auto sw32 = __builtin_amdgcn_permlane32_swap(halve, halve, false, false);
+                    const uint32_t ph = (g >= 2) ? sw32[0] : sw32[1];  // lane ^ 32
+                    sca = 127 + (int)(((g == 1 || g == 2) ? ph : halve) >> (g >> 1) & 1u);
+                }
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     uint32_t a;
@@ -649,7 +745,7 @@ __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs
                     }
                 }
                 // A codes e4m3 (cbsz 0) or bf8 (cbsz 1); the selection operand is e4m3 (blgp 0)
-                dq[b] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, sel, dq[b], XF, 0, 0, 127, 0, 127);
+                dq[b] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, sel, dq[b], XF ? 1 : 0, 0, 0, sca, 0, 127);
             }
         }
         __syncthreads();

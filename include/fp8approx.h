@@ -103,10 +103,12 @@ int fp8a_debug_stats(uint64_t *out, int reset);
 /*
  * The exact (non-approx) product on the matrix core -- the reference's `x @ y` of FP8-quantized
  * operands (approx_calculation.py:797, 811: QuantizationHijacker with approx_flag off, BASELINE
- * config 1; the im2col form for convs).  Operands are fp32 values; per (row, 32-k block) they are
- * converted to OCP fp8 with a power-of-two block scale (fmt FP8A_DENSE_E4M3: e4m3, for E4M3-grid
- * values; FP8A_DENSE_E5M2: e5m2, for E5M2 / narrower grids) and multiplied exactly by the
- * block-scaled MFMA with fp32 accumulation.  Values that are not exact in the block's fp8 format
+ * config 1; the im2col form for convs).  Operands are fp32 values.  fmt FP8A_DENSE_BF16 (what the
+ * Python operators use by default): truncated to bf16 -- exact for every value with <= 8
+ * significant bits, i.e. every FP8 / E3M4 / E2M5 grid value at any exponent -- and multiplied by
+ * v_mfma_f32_16x16x32_bf16.  fmt FP8A_DENSE_E4M3 / _E5M2 (opt-in): per (row, 32-k block)
+ * converted to OCP e4m3 / e5m2 with a power-of-two block scale and multiplied by the block-scaled
+ * MFMA.  Both accumulate in fp32.  Values that are not exact in the operand format
  * (off-grid, too far below the block's largest, inf / NaN) send their 64-row / 64-column output
  * units to an fp32 FMA recompute, so ANY finite or non-finite input gives the fp32 product up to
  * summation order.  fp8a_dense_matmul: A element (m, k) at A[m * sam + k * sak], B element (k, n)

@@ -130,3 +130,53 @@ def test_sums_within_bar(shape):
     assert paths["f8mx"] == 1, paths
     ref, S = orc.matmul(A, B, E, M, bA, bB, bR, tab, fl, with_abs=True)
     assert np.all(np.abs(C.astype(np.float64) - ref) <= gio.sum_tolerance(S))
+
+
+def _codes_from(bias, min_field):
+    """The E5M2 values of the given bias whose exponent field is >= min_field (both signs)."""
+    e = np.repeat(np.arange(min_field, 32), 4)
+    m = np.tile(np.arange(4), 32 - min_field)
+    v = np.ldexp(1.0 + m / 4.0, e - bias)
+    return np.concatenate([v, -v]).astype(np.float32)
+
+
+def test_top_binade_terms_without_fallback():
+    """The E5M2 result grid's top binade 31 - bR (e5m2's exponent 31 is inf / NaN): an A element
+    whose products reach it is converted one binade down and its MX block scaled by 2 -- bit-exact
+    terms with NO fallback, as long as its products stay at or above the grid's second binade
+    (here: every A code against B codes of exponent field >= 16, bA + bB - bR = 32)."""
+    bA, bB, bR = 20, 20, 8
+    A = _all_codes(bA).reshape(-1, 1)
+    B = _codes_from(bB, 16).reshape(1, -1)
+    tab = _table("zero")
+    fl = orc.flags_of(approx=True, s2n=True, qbma=True)
+    ref = orc.terms(A, B, E, M, bA, bB, bR, tab, fl)[:, 0, :]
+    assert np.abs(ref).max() >= 2.0 ** (31 - bR), "the case must reach the top binade"
+    C, flag, paths = _matmul_raw(A, B, bA, bB, bR, tab, fl)
+    _terms_equal(C, ref)
+    assert paths["f8mx"] == 1 and flag == 0, flag
+
+
+@pytest.mark.parametrize("mixed", [False, True])
+def test_top_binade_sums(mixed):
+    """Sums with top-binade products: moderate A (halvable everywhere: no fallback) or A mixing
+    very large and tiny values in one MX block (those tiles fall back): within the bar either way."""
+    rng = np.random.default_rng(11 + mixed)
+    bA, bB, bR = 20, 20, 8
+    Mr, K, N = 256, 96, 48
+    ea = rng.integers(25, 32, size=(Mr, K)) if not mixed else np.where(rng.random((Mr, K)) < 0.5,
+                                                                        rng.integers(28, 32, size=(Mr, K)),
+                                                                        rng.integers(0, 4, size=(Mr, K)))
+    A = np.where(ea == 0, np.ldexp(rng.integers(0, 4, size=(Mr, K)) / 4.0, 1 - bA),
+                 np.ldexp(1.0 + rng.integers(0, 4, size=(Mr, K)) / 4.0, ea - bA))
+    A = (A * rng.choice([-1.0, 1.0], size=(Mr, K))).astype(np.float32)
+    B = (np.ldexp(1.0 + rng.integers(0, 4, size=(K, N)) / 4.0, rng.integers(16, 32, size=(K, N)) - bB)
+         * rng.choice([-1.0, 1.0], size=(K, N))).astype(np.float32)
+    tab = _table("zero")
+    fl = orc.flags_of(approx=True, s2n=True, qbma=True)
+    C, flag, paths = _matmul_raw(A, B, bA, bB, bR, tab, fl)
+    assert paths["f8mx"] == 1
+    if not mixed:
+        assert flag == 0, flag
+    ref, S = orc.matmul(A, B, E, M, bA, bB, bR, tab, fl, with_abs=True)
+    assert np.all(np.abs(C.astype(np.float64) - ref) <= gio.sum_tolerance(S))

@@ -4,7 +4,7 @@ state, goes through estimate -> fix -> approx on the GPU.  Cases: E4M3 approx_v9
 approx_flag off (BASELINE config 1: the reference's canonical --no-approx_flag
 --original-quantize-res run, exact product + quantizers); E5M2 approx_v9 with the opt-in zero
 table (BASELINE config 3's format; the reference was given the same zero table).  In the
-no-approx case the exact products (groups = 1) run on the block-scaled fp8 matrix core
+no-approx case the exact products (groups = 1) run on the bf16 matrix core (dn_gemm_bf16)
 (csrc/gemm_dense.h), the depthwise ones as the fp32 contraction.
 
 Bars: every approx layer's bA / per-channel bB / bR identical (calibration reproduced through
