@@ -152,7 +152,7 @@ def pmc_files():
                   key=lambda n: (n[5:7], n), reverse=True)
 
 
-def pmc_traffic(kernel, arch, E, M, batch):
+def pmc_traffic(kernel, arch, E, M, batch, strict=False):
     """Per-launch HBM bytes of the approx GEMM kernel from a committed rocprofv3 PMC summary
     (profiles/pmc_r<round>*.json, tools/prof_summary.py) recorded for this same kernel, workload,
     format and batch (summaries without a batch field were taken at 256); None when no such
@@ -168,8 +168,8 @@ def pmc_traffic(kernel, arch, E, M, batch):
             found.setdefault(j.get("kernel"), j.get("bytes_per_launch"))
     # the named kernel's summary, else the one recorded for this workload (E3M4 on MobileNetV2:
     # its short-K layers run gemm_tt_kernel<4>, which dominates there)
-    if kernel in found:
-        return found[kernel]
+    if kernel in found or strict:
+        return found.get(kernel)
     return next(iter(found.values()), None)
 
 
@@ -367,13 +367,14 @@ def run(args, dev, rank=0, world=1):
             res["roofline"] = {
                 "bound": "hbm",
                 "kernel": "dn_gemm_bf16 (csrc/gemm_dense.h: the exact product on the bf16 matrix core, "
-                          "implicit-GEMM conv / matmul; groups = 1 -- the depthwise convs stay torch's fp32 "
-                          "contraction); timed per op with its operand packing and gated fp32 units",
+                          "implicit-GEMM conv / matmul, groups = 1) and dn_group_conv (the depthwise convs, fp32 "
+                          "FMAs); timed per op with its operand packing and gated fp32 units",
                 "achieved": gbs,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": gbs / HBM_PEAK_GBS if gbs else None,
-                "traffic": None,
+                "traffic": pmc_traffic("dn_gemm_bf16", args.arch, args.expo_width, args.mant_width, args.batch,
+                                       strict=True),
                 "algorithmic": f"fp32 operands read once + fp32 output written once: {op_bytes / launches:.4g} B per "
                                f"launch avg over {launches} launches, {avg_s * 1e3:.3f} ms avg launch (HIP events); "
                                f"{2.0 * op_macs / (op_ms / 1e3) / 1e12 if op_ms > 0 else 0:.1f} TFLOP/s of exact "

@@ -23,7 +23,7 @@ from torch import nn
 
 from . import _lib
 from .approx_ops import (_res_quant_params, approx_conv2d, approx_matmul, approx_matmul_block, bias_epilogue,
-                         dense_conv2d, dense_format, dense_matmul, make_flags, make_flags_v5, qamaa_conv2d,
+                         dense_conv2d, dense_format, dense_matmul, grouped_conv2d, make_flags, make_flags_v5, qamaa_conv2d,
                          qamaa_matmul)
 from .error_tables import get_comp_table_NN_v5, get_error_table_NN
 from .quantization.hijacker import QuantizationHijacker
@@ -181,23 +181,35 @@ class ApproxConv2dMixin(ApproxOpMixin, ChainConsumerMixin):
             out = qamaa_conv2d(x.detach(), weight.detach(), *self._qamaa_params(), stride=self.stride,
                                padding=self.padding, dilation=self.dilation, groups=self.groups)
         else:  # exact product (also qamaa's single-column groups, approx_calculation.py:810-811)
-            fmt = dense_format(M) if DENSE_EXACT and self._operands_quantized() else None
-            if x.is_cuda and fmt is not None and self.groups == 1:
-                out = dense_conv2d(x.detach(), weight.detach(), fmt, self.stride, self.padding, self.dilation)
-            else:  # grouped (depthwise: one-column products) / wide-mantissa formats: the fp32 contraction
-                out = F.conv2d(x.detach(), weight.detach(), None, self.stride, self.padding, self.dilation,
-                               self.groups)
+            out = exact_conv2d(self, x.detach(), weight.detach(), M)
         if bias is not None:
             out += bias.view(1, -1, 1, 1)
         return out
 
 
+def exact_conv2d(mod, x, w, M):
+    """The exact convolution product of ``mod`` (a conv hijacker) on CUDA tensors: grouped /
+    depthwise convs on fp8a_grouped_conv2d (the reference's per-group ``x @ y[:, i]``,
+    approx_calculation.py:797 / 686-711: fp32 FMAs, any input), groups = 1 on the matrix core
+    (dense_conv2d, :811) when both operands went through FP8 quantizers (else the fp32 contraction:
+    the bf16 form would send every unit to its fp32 recompute).  CPU tensors, FP8A_DENSE=0 (A/B
+    measurements) and wide-mantissa formats: F.conv2d."""
+    if x.is_cuda and DENSE_EXACT:
+        if mod.groups > 1:
+            return grouped_conv2d(x, w, mod.groups, mod.stride, mod.padding, mod.dilation)
+        fmt = dense_format(M) if ApproxOpMixin._operands_quantized(mod) else None
+        if fmt is not None:
+            return dense_conv2d(x, w, fmt, mod.stride, mod.padding, mod.dilation)
+    return F.conv2d(x, w, None, mod.stride, mod.padding, mod.dilation, mod.groups)
+
+
 class ExactConv2dMixin:
-    """run_forward of QCustomConv2dTorch: exact fp32 product (approx_calculation.py:660-719)."""
+    """run_forward of QCustomConv2dTorch: exact fp32 product (approx_calculation.py:660-719), on
+    the HIP kernels for CUDA tensors (exact_conv2d)."""
 
     def run_forward(self, x, weight, bias, offsets=None):
-        out = F.conv2d(x.contiguous().detach(), weight.contiguous().detach(), None, self.stride, self.padding,
-                       self.dilation, self.groups)
+        params = getattr(self, "custom_approx_params", None) or {}
+        out = exact_conv2d(self, x.contiguous().detach(), weight.contiguous().detach(), params.get("mant_width", 3))
         if bias is not None:
             out += bias.view(1, -1, 1, 1)
         return out

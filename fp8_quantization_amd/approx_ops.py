@@ -24,7 +24,7 @@ from .error_tables import get_error_table_NN  # noqa: F401  (re-exported, v9:555
 __all__ = ["custom_matmul_vectorize", "approx_matmul", "approx_matmul_block", "approx_terms", "approx_conv2d", "qamaa_matmul", "qamaa_conv2d",
            "quant_to_fp_any_vectorize_torch", "float_to_fpany_absint_torch", "get_error_table_NN",
            "make_flags", "make_flags_v5", "fp8_fake_quantize", "bn_act_epilogue", "dense_format", "dense_matmul",
-           "dense_conv2d"]
+           "dense_conv2d", "grouped_conv2d"]
 
 
 def make_flags(with_approx=True, with_s2nn2s_opt=False, quant_btw_mult_accu=True, golden_clip_OF=False,
@@ -808,6 +808,46 @@ def dense_conv2d(x, w, fmt, stride=(1, 1), padding=(0, 0), dilation=(1, 1)):
                          [int(v) for v in dilation])
     _prof_end(ev, y.shape[0] * y.shape[2] * y.shape[3] * w.shape[0] * w.shape[1] * w.shape[2] * w.shape[3],
               4 * (x.numel() + w.numel() + y.numel()))
+    return y
+
+
+@torch.library.custom_op("fp8approx::grouped_conv2d", mutates_args=())
+def _grouped_conv2d_op(x: torch.Tensor, w: torch.Tensor, groups: int, stride: list[int], padding: list[int],
+                       dilation: list[int]) -> torch.Tensor:
+    L = _lib.load()
+    Bn, Cin, H, W = x.shape
+    Cout, _, kh, kw = w.shape
+    Ho = (H + 2 * padding[0] - dilation[0] * (kh - 1) - 1) // stride[0] + 1
+    Wo = (W + 2 * padding[1] - dilation[1] * (kw - 1) - 1) // stride[1] + 1
+    y = torch.empty((Bn, Cout, Ho, Wo), dtype=torch.float32, device=x.device)
+    rc = L.fp8a_grouped_conv2d(_lib.dev_ptr(x), _lib.dev_ptr(w), _lib.dev_ptr(y), Bn, Cin, H, W, Cout, int(groups),
+                               kh, kw, stride[0], stride[1], padding[0], padding[1], dilation[0], dilation[1],
+                               _lib.stream_ptr(x.device))
+    _lib.check(rc, "fp8a_grouped_conv2d")
+    return y
+
+
+@_grouped_conv2d_op.register_fake
+def _(x, w, groups, stride, padding, dilation):
+    Bn, _, H, W = x.shape
+    Cout, _, kh, kw = w.shape
+    Ho = (H + 2 * padding[0] - dilation[0] * (kh - 1) - 1) // stride[0] + 1
+    Wo = (W + 2 * padding[1] - dilation[1] * (kw - 1) - 1) // stride[1] + 1
+    return x.new_empty((Bn, Cout, Ho, Wo), dtype=torch.float32)
+
+
+def grouped_conv2d(x, w, groups, stride=(1, 1), padding=(0, 0), dilation=(1, 1)):
+    """Exact-product grouped / depthwise convolution on the HIP kernel fp8a_grouped_conv2d: the
+    reference's per-group im2col + ``x @ w^T`` (QCustomConv2dTorch, approx_calculation.py:686-711;
+    the exact branch's ``x @ y[:, i]``, :797) -- fp32 FMAs in im2col k order, any fp32 input."""
+    if x.dim() != 4 or w.dim() != 4 or x.shape[1] != w.shape[1] * groups or w.shape[0] % groups:
+        raise AssertionError(f"grouped_conv2d: shape mismatch {tuple(x.shape)} * {tuple(w.shape)} / {groups}")
+    x = _as_f32(x).contiguous()
+    w = _as_f32(w).contiguous()
+    ev = _prof_start()
+    y = _grouped_conv2d_op(x, w, int(groups), [int(v) for v in stride], [int(v) for v in padding],
+                           [int(v) for v in dilation])
+    _prof_end(ev, y.numel() * w.shape[1] * w.shape[2] * w.shape[3], 4 * (x.numel() + w.numel() + y.numel()))
     return y
 
 

@@ -230,6 +230,12 @@ struct GemmArgs {
 // unit does (a bias outside the exactness window, or no unit marks in the workspace).  (Bits
 // 1-4 belong to gemm_tt16_kernel's f16 window, gemm_tt16.h.)
 constexpr uint32_t FB_ANY = 1u, FB_ALL = 32u;
+// FB_HALF: an E5M2 tile of gemm_f8mx_kernel's plain form met the result grid's top binade and
+// asks the halved-block form (XF = 2) to recompute it; its unit marks carry UT_HALF.  Unit mark
+// bits: UT_EXACT = recompute in the exact kernel, UT_HALF = recompute in the halved-block form
+// (kept set by a halved-block tile that fails, so the tiles sharing the unit still see it).
+constexpr uint32_t FB_HALF = 64u;
+constexpr uint8_t UT_EXACT = 1u, UT_HALF = 2u;
 
 // Fallback flag value of a block that found a bad operand: FB_ANY once the unit marks are
 // written, FB_ALL too without them (or when `all`).
@@ -278,10 +284,11 @@ __device__ __forceinline__ void fb_rows(const GemmArgs &p, int64_t m_lo, int64_t
 __device__ __forceinline__ void fb_col(const GemmArgs &p, int64_t n) {
     if (p.ucol != nullptr) p.ucol[n >> 6] = 1;
 }
-__device__ __forceinline__ void fb_tile(const GemmArgs &p, int64_t m0, int64_t rows, int64_t n0) {
+__device__ __forceinline__ void fb_tile(const GemmArgs &p, int64_t m0, int64_t rows, int64_t n0,
+                                        uint8_t mark = UT_EXACT) {
     if (p.utile == nullptr) return;
     const int64_t hi = min(m0 + rows, p.M);
-    for (int64_t u = m0 >> 6; u <= (hi - 1) >> 6; ++u) p.utile[u * p.nuc + (n0 >> 6)] = 1;
+    for (int64_t u = m0 >> 6; u <= (hi - 1) >> 6; ++u) p.utile[u * p.nuc + (n0 >> 6)] = mark;
 }
 
 // The block-output epilogue on one value / four values of the output at index o; pb = the post
@@ -1031,7 +1038,7 @@ __global__ __launch_bounds__(256) void gemm_exact_kernel(const GemmArgs p) {
     const EmitCtx ec = emit_ctx(p);
     for (int64_t u = blockIdx.x; u < nur * nuc; u += gridDim.x) {
         const int64_t ur = u / nuc, uc = u - ur * nuc;
-        if (!all && !p.urow[ur] && !p.ucol[uc] && !p.utile[u]) continue;  // (block-uniform)
+        if (!all && !p.urow[ur] && !p.ucol[uc] && !(p.utile[u] & UT_EXACT)) continue;  // (block-uniform)
         if (threadIdx.x == 0) atomicAdd(&g_fallback[1], 1ull);
         const int64_t m = 64 * ur + (threadIdx.x & 63), nb = 64 * uc + 16 * (threadIdx.x >> 6);
         if (m >= p.M) continue;
@@ -1388,8 +1395,8 @@ static void launch_f8mx_f(const GemmArgs &a, hipStream_t s) {
     }
 }
 // E4M3 (XF 0) or E5M2 (mant_width 2) result grid; E5M2 launches both its kernels, the plain one
-// (XF 1) and the halved-block one (XF 2), and the one the launch's operands do not call for exits
-// at once (xm_needs_halving, gemm_f8mx.h)
+// (XF 1) over every tile and the halved-block one (XF 2), which recomputes only the tiles the plain
+// one marked UT_HALF (the top binade, gemm_f8mx.h) and exits at once without FB_HALF
 static void launch_f8mx(const GemmArgs &a, hipStream_t s) {
     if (a.Mw == 2) {
         launch_f8mx_f<1>(a, s);
@@ -2006,6 +2013,17 @@ static DenseArgs dense_args() {
 
 using namespace fp8a;
 
+template <typename I>
+static void launch_group_conv(const GcArgs &a, hipStream_t s) {
+    const unsigned g = (unsigned)std::min<int64_t>((a.total + 255) / 256, 65536);
+    const bool d1 = a.dw == 1;
+    if (d1 && a.kw == 3 && a.sw == 1) dn_group_conv<I, 3, 1><<<g, 256, 0, s>>>(a);
+    else if (d1 && a.kw == 3 && a.sw == 2) dn_group_conv<I, 3, 2><<<g, 256, 0, s>>>(a);
+    else if (d1 && a.kw == 5 && a.sw == 1) dn_group_conv<I, 5, 1><<<g, 256, 0, s>>>(a);
+    else if (d1 && a.kw == 5 && a.sw == 2) dn_group_conv<I, 5, 2><<<g, 256, 0, s>>>(a);
+    else dn_group_conv<I, 0, 1><<<g, 256, 0, s>>>(a);
+}
+
 extern "C" {
 
 const char *fp8a_version(void) { return "fp8approx gfx950 r1"; }
@@ -2115,6 +2133,29 @@ int fp8a_dense_conv2d(const float *x, const float *w, float *y, int64_t Bn, int6
     a.sbk = 1; a.sbn = a.K;  // w [Cout][Cin][kh][kw]: B(k, n) = w[n * K + k]
     a.ldc = Cout; a.fmt = fmt;
     return run_dense(a, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int fp8a_grouped_conv2d(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
+                        int64_t Cout, int groups, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw,
+                        fp8a_stream_t stream) {
+    if (kh < 1 || kw < 1 || sh < 1 || sw < 1 || dh < 1 || dw < 1 || ph < 0 || pw < 0 || Bn < 0 || Cin < 0 || Cout < 0)
+        return fail(FP8A_EINVAL, "bad convolution geometry");
+    if (groups < 1 || Cin % groups != 0 || Cout % groups != 0) return fail(FP8A_EINVAL, "channels not divisible by groups");
+    const int64_t Ho = (H + 2 * ph - dh * (kh - 1) - 1) / sh + 1;
+    const int64_t Wo = (W + 2 * pw - dw * (kw - 1) - 1) / sw + 1;
+    if (Ho <= 0 || Wo <= 0) return fail(FP8A_EINVAL, "empty convolution output");
+    GcArgs a{};
+    a.x = x; a.w = w; a.y = y;
+    a.Cin = Cin; a.H = H; a.W = W; a.Cout = Cout; a.Ho = Ho; a.Wo = Wo;
+    a.total = Bn * Cout * Ho * ((Wo + GC_OW - 1) / GC_OW);
+    a.cig = (int)(Cin / groups); a.cog = (int)(Cout / groups);
+    a.kh = kh; a.kw = kw; a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw; a.dh = dh; a.dw = dw;
+    if (a.total == 0) return FP8A_OK;
+    if (!x || !w || !y) return fail(FP8A_EINVAL, "null pointer");
+    if (a.total + 65536ll * 256 < (1ll << 31)) launch_group_conv<uint32_t>(a, (hipStream_t)stream);
+    else launch_group_conv<int64_t>(a, (hipStream_t)stream);
+    ++g_paths[PATH_DENSE];
+    return hip_check("fp8a grouped conv launch");
 }
 
 int fp8a_clock_stats(uint64_t *out, int reset) {

@@ -510,3 +510,72 @@ __global__ __launch_bounds__(256) void dn_fix(const DenseArgs p) {
         }
     }
 }
+
+// The exact grouped / depthwise convolution: QCustomConv2dTorch's per-group im2col + x @ w^T
+// (approx_calculation.py:686-711) and the exact branch of QCustomBNConv2dTorch for groups > 1
+// (x @ y[:, i], :797 -- MobileNetV2's depthwise layers, BASELINE config 1).  One output = fp32
+// FMAs in the im2col k order (input channel, ky, kx) with the padding read as zeros (0 * w keeps a
+// non-finite weight's NaN, as the im2col product does); any fp32 input.  Thread = (image, output
+// channel, output row, GC_OW consecutive output columns), the input row segment the GC_OW outputs
+// share loaded once per (channel, ky) when the window's width and stride are compile-time (KW > 0;
+// KW = 0: the general loop).  HBM-bound: x is read about once (the row overlap of neighbouring
+// threads hits L2), y written once -- (x + y + w) bytes per launch.
+struct GcArgs {
+    const float *x, *w;
+    float *y;
+    int64_t Cin, H, W, Cout, Ho, Wo, total;  // total = Bn Cout Ho ceil(Wo / GC_OW)
+    int cig, cog, kh, kw, sh, sw, ph, pw, dh, dw;
+};
+constexpr int GC_OW = 4;
+
+template <typename I, int KW, int SW>
+__global__ __launch_bounds__(256) void dn_group_conv(const GcArgs p) {
+    constexpr int SEG = KW > 0 ? (GC_OW - 1) * SW + KW : 1;
+    const I wq = (I)((p.Wo + GC_OW - 1) / GC_OW), Ho = (I)p.Ho, Cout = (I)p.Cout;
+    const int kh = p.kh, kw = KW > 0 ? KW : p.kw, sw = KW > 0 ? SW : p.sw;
+    for (I t = (I)blockIdx.x * 256 + (I)threadIdx.x; t < (I)p.total; t += (I)gridDim.x * 256) {
+        const I q = t % wq, r = t / wq, ho = r % Ho, plane = r / Ho;  // plane = image Cout + co
+        const I co = plane % Cout, n = plane / Cout, c0 = (co / (I)p.cog) * (I)p.cig;
+        const int64_t wo0 = (int64_t)q * GC_OW, wi0 = wo0 * sw - p.pw;
+        float acc[GC_OW];
+#pragma unroll
+        for (int j = 0; j < GC_OW; ++j) acc[j] = 0.0f;
+        const float *wp = p.w + (int64_t)co * p.cig * kh * kw;
+        for (int ci = 0; ci < p.cig; ++ci) {
+            const float *xp = p.x + ((int64_t)n * p.Cin + c0 + ci) * p.H * p.W;
+            for (int ky = 0; ky < kh; ++ky) {
+                const int64_t hi = (int64_t)ho * p.sh - p.ph + (int64_t)ky * p.dh;
+                const bool hok = hi >= 0 && hi < p.H;
+                const float *xr = xp + (hok ? hi : 0) * p.W;
+                const float *wr = wp + (ci * kh + ky) * kw;
+                if constexpr (KW > 0) {  // dilation 1 (dn_group_conv launch)
+                    float seg[SEG];
+#pragma unroll
+                    for (int s = 0; s < SEG; ++s) {
+                        const int64_t wi = wi0 + s;
+                        seg[s] = (hok && wi >= 0 && wi < p.W) ? xr[wi] : 0.0f;
+                    }
+#pragma unroll
+                    for (int kx = 0; kx < KW; ++kx) {
+                        const float wv = wr[kx];
+#pragma unroll
+                        for (int j = 0; j < GC_OW; ++j) acc[j] = __fmaf_rn(seg[j * SW + kx], wv, acc[j]);
+                    }
+                } else {
+                    for (int kx = 0; kx < kw; ++kx) {
+                        const float wv = wr[kx];
+#pragma unroll
+                        for (int j = 0; j < GC_OW; ++j) {
+                            const int64_t wi = wi0 + (int64_t)j * sw + (int64_t)kx * p.dw;
+                            acc[j] = __fmaf_rn((hok && wi >= 0 && wi < p.W) ? xr[wi] : 0.0f, wv, acc[j]);
+                        }
+                    }
+                }
+            }
+        }
+        float *yp = p.y + ((int64_t)plane * p.Ho + ho) * p.Wo;
+#pragma unroll
+        for (int j = 0; j < GC_OW; ++j)
+            if (wo0 + j < p.Wo) yp[wo0 + j] = acc[j];
+    }
+}

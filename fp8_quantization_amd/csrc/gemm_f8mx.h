@@ -85,13 +85,26 @@ struct XmFmt {
 // smallest A scale exponent se <= 112 + max e_b.  The pre-passes record both extremes in the
 // workspace head (xm_decode_a: 255 - min se, xm_decode_b: max e_b + 128; 0 = none); without the A
 // pre-pass (fp32 staging) the A grid's top binade (plus the one the quantizer's rounding can add)
-// stands in.  Both E5M2 kernels are launched; the one that does not apply exits at once.
+// stands in.  The plain form runs every tile; a tile of it that met a NaN (a term past the e5m2
+// range) goes to the halved-block form when the extremes allow the top binade (UT_HALF), else
+// straight to the exact kernel.
 __device__ __forceinline__ bool xm_needs_halving(const GemmArgs &p, bool af32, int bA, int bR) {
     const uint32_t a = __hip_atomic_load(p.flag + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t b = __hip_atomic_load(p.flag + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (b == 0u) return false;  // every B element is zero
     const int se_min = af32 ? 110 + bA - bR : (a == 0u ? 1000 : 255 - (int)a);
     return se_min <= 112 + (int)b - 128;
+}
+// The halved-block form's tile gate: the plain form raised FB_HALF and marked a unit of this tile
+// UT_HALF (every tile without the unit marks)
+__device__ __forceinline__ bool xm_half_gate(const GemmArgs &p, int64_t m0, int rows, int64_t n0, int cols) {
+    if ((__hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & FB_HALF) == 0u) return false;
+    if (p.utile == nullptr) return true;
+    const int64_t r1 = (min(m0 + rows, p.M) - 1) >> 6, c1 = (min(n0 + cols, p.N) - 1) >> 6;
+    bool any = false;
+    for (int64_t r = m0 >> 6; r <= r1; ++r)
+        for (int64_t c = n0 >> 6; c <= c1; ++c) any |= (p.utile[r * p.nuc + c] & UT_HALF) != 0;
+    return any;
 }
 __host__ __device__ constexpr int xm_xbias(int Mw) { return Mw == 2 ? 15 : 7; }
 
@@ -487,6 +500,7 @@ __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs
     const int64_t bid = (int64_t)blockIdx.x % tiles, split = (int64_t)blockIdx.x / tiles;
     const int64_t m0 = (bid % num_mt) * BMT;
     const int64_t n0 = (bid / num_mt) * BNT;
+    if (XF == 2 && !xm_half_gate(p, m0, BMT, n0, BNT)) return;  // (a tile the plain form completed)
     const int kbeg = (int)(split * p.kchunk), kend = (int)min(p.K, (int64_t)kbeg + p.kchunk), K32 = (int)p.K;
     const int bR = *p.bR;
     // AF32: the A operand's bias (the fused input quantizer's, written once for the gated kernels)
@@ -504,7 +518,6 @@ __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs
         biasbad = !(xm_bias_ok(bA) && xm_bias_ok(bR));  // every output unit falls back
     }
     const uint32_t emnA = (uint32_t)(128 - bA) << 23;
-    if (XF && xm_needs_halving(p, AF32, AF32 ? bA : 0, bR) != (XF == 2)) return;  // (the other E5M2 kernel's launch)
 
     // table: copied from the launch's pre-computed image (xm_decode_b), 16-B per thread and step
     for (int e = 4 * tid; e < XM_LUT_WORDS; e += 4 * NT)
@@ -681,8 +694,8 @@ __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs
             // thi / tok: the (K-step 2 g + h, this wave's 16 columns) thresholds on se, packed as
             // bytes (thi0, thi1, tok0, tok1).  (Branching around this per tile -- on whether any A
             // element of the launch could need it -- made the register allocator spill 50-250
-            // VGPRs; as its own instance (XF = 2, launches where xm_needs_halving), on the
-            // 128 x 32 / 256 x 16 tiles, whose 60-70 VGPRs leave room for it: launch_f8mx.)
+            // VGPRs; as its own instance (XF = 2, the tiles the plain form marked UT_HALF), on
+            // the 128 x 32 / 256 x 16 tiles, whose 60-70 VGPRs leave room for it: launch_f8mx.)
             uint32_t thr = 0u;
             if (XF == 2) {
                 const int64_t ng = p.npad / 16, e0 = (int64_t)(k0 + 2 * g) * ng + (n0 / 16 + wc);
@@ -762,8 +775,16 @@ __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs
     const bool tnan = __syncthreads_or(nan ? 1 : 0) != 0;
     const bool tbad = AF32 && __syncthreads_or((abad || biasbad) ? 1 : 0) != 0;
     if ((tnan || tbad) && tid == 0) {
-        if (tnan) fb_tile(p, m0, BMT, n0);
-        atomicOr(p.flag, fb_bits(p, biasbad));
+        // E5M2: a NaN of the plain form where the launch's extremes reach the top binade goes to
+        // the halved-block form first (its own NaN -- beyond the range -- to the exact kernel)
+        if (XF == 1 && tnan && xm_needs_halving(p, AF32, AF32 ? bA : 0, bR)) {
+            fb_tile(p, m0, BMT, n0, UT_HALF);
+            atomicOr(p.flag, FB_HALF);
+            if (tbad) atomicOr(p.flag, fb_bits(p, biasbad));
+        } else {
+            if (tnan) fb_tile(p, m0, BMT, n0, XF == 2 ? (uint8_t)(UT_EXACT | UT_HALF) : UT_EXACT);
+            atomicOr(p.flag, fb_bits(p, biasbad));
+        }
     }
 
     // D (units of 2^(7-bR)) of row block b: lane l holds rows 4 (l >> 4) .. + 3, column l & 15

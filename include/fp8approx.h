@@ -127,6 +127,13 @@ size_t fp8a_dense_conv2d_workspace_size(int64_t Bn, int64_t Cin, int64_t H, int6
 int fp8a_dense_conv2d(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
                       int64_t Cout, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw, int fmt,
                       void *workspace, size_t workspace_bytes, fp8a_stream_t stream);
+/* The exact grouped / depthwise convolution (QCustomConv2dTorch's per-group im2col + x @ w^T,
+ * approx_calculation.py:686-711; the exact branch's x @ y[:, i] for groups > 1, :797): NCHW x,
+ * w [Cout][Cin / groups][kh][kw], NCHW y, fp32 FMAs in the im2col k order (channel, ky, kx), the
+ * padding as zeros.  Any fp32 input; no workspace.  Counted as a dense launch (fp8a_path_stats). */
+int fp8a_grouped_conv2d(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
+                        int64_t Cout, int groups, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw,
+                        fp8a_stream_t stream);
 /* Dense-path counters since load / the last reset (out[2]): [0] launches with units recomputed in
  * fp32, [1] 64 x 64 units recomputed.  Synchronises the device. */
 int fp8a_dense_stats(uint64_t *out, int reset);

@@ -1,0 +1,110 @@
+"""fp8a_grouped_conv2d -- the exact grouped / depthwise convolution (QCustomConv2dTorch's per-group
+im2col + x @ w^T, approx_calculation.py:686-711; the exact branch's x @ y[:, i] for groups > 1,
+:797; BASELINE config 1's depthwise layers) against the same im2col product in float64.
+
+Bar: |y - ref| <= 1e-5 * sum |x w| per output (fp32 FMAs in im2col k order vs an exact sum); the
+padding is read as zeros, so a non-finite weight gives NaN exactly where the im2col product does."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def im2col_ref(x, w, groups, stride, padding, dilation):
+    """The reference's per-group im2col product in float64 (approx_calculation.py:686-711)."""
+    Bn, Cin, H, W = x.shape
+    Cout, cig, kh, kw = w.shape
+    Ho = (H + 2 * padding[0] - dilation[0] * (kh - 1) - 1) // stride[0] + 1
+    Wo = (W + 2 * padding[1] - dilation[1] * (kw - 1) - 1) // stride[1] + 1
+    col = F.unfold(x.double(), (kh, kw), dilation=dilation, padding=padding, stride=stride)  # [Bn, Cin kh kw, L]
+    col = col.transpose(1, 2).reshape(Bn * Ho * Wo, Cin * kh * kw)
+    wc = w.double().reshape(Cout, -1)
+    cog, kg = Cout // groups, cig * kh * kw
+    out, mag = [], []
+    for g in range(groups):
+        a = col[:, g * kg:(g + 1) * kg]
+        b = wc[g * cog:(g + 1) * cog].T
+        out.append(a @ b)
+        mag.append(a.abs() @ b.abs())
+    to_nchw = lambda t: torch.cat(t, 1).reshape(Bn, Ho, Wo, Cout).permute(0, 3, 1, 2)  # noqa: E731
+    return to_nchw(out), to_nchw(mag)
+
+
+CASES = [  # (Bn, Cin, H, W, Cout, groups, k, stride, padding, dilation)
+    (2, 32, 14, 14, 32, 32, 3, 1, 1, 1),    # MobileNetV2 depthwise, stride 1
+    (2, 24, 15, 13, 24, 24, 3, 2, 1, 1),    # stride 2, odd sizes (Wo not a multiple of 4)
+    (1, 16, 9, 11, 16, 16, 5, 2, 2, 1),     # 5x5
+    (1, 16, 10, 10, 32, 16, 3, 1, 1, 1),    # depth multiplier 2
+    (2, 6, 12, 12, 8, 2, 3, 1, 2, 2),       # groups of 3 input channels, dilation 2 (general loop)
+    (1, 8, 7, 7, 8, 4, 1, 1, 0, 1),         # 1x1 grouped
+    (1, 4, 20, 20, 4, 4, 7, 3, 3, 1),       # 7x7 stride 3 (general loop)
+    (3, 1, 5, 6, 2, 1, 3, 1, 1, 1),         # groups 1
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c)))
+def test_grouped_conv_matches_im2col(case):
+    from fp8_quantization_amd.approx_ops import grouped_conv2d
+    Bn, Cin, H, W, Cout, groups, k, s, p, d = case
+    g = torch.Generator().manual_seed(sum(case))
+    x = torch.randn(Bn, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin // groups, k, k, generator=g)
+    y = grouped_conv2d(x.to(DEV), w.to(DEV), groups, (s, s), (p, p), (d, d)).cpu().double()
+    ref, mag = im2col_ref(x, w, groups, (s, s), (p, p), (d, d))
+    assert y.shape == ref.shape
+    assert torch.all((y - ref).abs() <= 1e-5 * mag + 1e-30)
+
+
+def test_grouped_conv_fp8_values_exact_order():
+    """FP8 (E4M3) operands on a depthwise 3x3: fp32 FMAs in k order equal the fp32 im2col sum in
+    the same order to the bit (each product is exact in fp32)."""
+    from fp8_quantization_amd.approx_ops import grouped_conv2d
+    g = torch.Generator().manual_seed(7)
+    q = lambda t: t.to(torch.float8_e4m3fn).float()  # noqa: E731
+    x, w = q(torch.randn(2, 8, 9, 9, generator=g) * 4), q(torch.randn(8, 1, 3, 3, generator=g))
+    y = grouped_conv2d(x.to(DEV), w.to(DEV), 8, (1, 1), (1, 1), (1, 1)).cpu()
+    col = F.unfold(x, (3, 3), padding=1).reshape(2, 8, 9, 81)  # [Bn, C, k, L]
+    acc = torch.zeros(2, 8, 81)
+    for kk in range(9):  # fp32, k order
+        acc = acc + col[:, :, kk, :] * w.reshape(8, 9)[None, :, kk, None]
+    assert torch.equal(y.reshape(2, 8, 81), acc)
+
+
+def test_grouped_conv_nonfinite_weight_like_im2col():
+    from fp8_quantization_amd.approx_ops import grouped_conv2d
+    x = torch.rand(1, 4, 6, 6) + 0.5
+    w = torch.rand(4, 1, 3, 3)
+    w[1, 0, 0, 0] = float("inf")
+    y = grouped_conv2d(x.to(DEV), w.to(DEV), 4, (1, 1), (1, 1), (1, 1)).cpu()
+    ref, _ = im2col_ref(x, w, 4, (1, 1), (1, 1), (1, 1))
+    assert torch.equal(torch.isnan(y), torch.isnan(ref))  # 0 (padding) * inf in the top row / left column
+    assert torch.isnan(y[0, 1, 0, :]).all() and torch.isinf(y[0, 1, 1:, 1:]).all()
+
+
+def test_grouped_conv_empty_batch_and_errors():
+    from fp8_quantization_amd.approx_ops import grouped_conv2d
+    y = grouped_conv2d(torch.zeros(0, 4, 5, 5, device=DEV), torch.ones(4, 1, 3, 3, device=DEV), 4, (1, 1), (1, 1))
+    assert y.shape == (0, 4, 5, 5)
+    with pytest.raises(AssertionError):
+        grouped_conv2d(torch.zeros(1, 6, 5, 5, device=DEV), torch.ones(4, 1, 3, 3, device=DEV), 4)
+
+
+def test_exact_conv_module_routes_to_hip():
+    """QCustomConv2dTorch with groups > 1 runs fp8a_grouped_conv2d (a dense-path launch), never
+    torch's convolution (the no-approx QCustomBNConv2dTorch depthwise layers: test_gpu_model.py)."""
+    from fp8_quantization_amd import _lib
+    from fp8_quantization_amd.approx_calculation import QCustomConv2dTorch
+    m = QCustomConv2dTorch(8, 8, 3, padding=1, groups=8, bias=True).to(DEV).eval()
+    x = torch.randn(2, 8, 10, 10, device=DEV)
+    _lib.path_stats(reset=True)
+    orig = F.conv2d
+    try:
+        F.conv2d = lambda *a, **k: (_ for _ in ()).throw(AssertionError("torch convolution"))
+        y = m.run_forward(x, m.weight, m.bias)
+    finally:
+        F.conv2d = orig
+    assert _lib.path_stats(reset=True)["dense"] == 1
+    ref = orig(x.cpu().double(), m.weight.detach().cpu().double(), m.bias.detach().cpu().double(), 1, 1, 1, 8)
+    assert torch.allclose(y.cpu().double(), ref, atol=1e-5, rtol=1e-5)

@@ -5,7 +5,8 @@ approx_flag off (BASELINE config 1: the reference's canonical --no-approx_flag
 --original-quantize-res run, exact product + quantizers); E5M2 approx_v9 with the opt-in zero
 table (BASELINE config 3's format; the reference was given the same zero table).  In the
 no-approx case the exact products (groups = 1) run on the bf16 matrix core (dn_gemm_bf16)
-(csrc/gemm_dense.h), the depthwise ones as the fp32 contraction.
+(csrc/gemm_dense.h), the depthwise ones on fp8a_grouped_conv2d: no torch / MIOpen convolution
+runs in that forward.
 
 Bars: every approx layer's bA / per-channel bB / bR identical (calibration reproduced through
 the whole network); logits within a summation-order tolerance; top-1 identical."""
@@ -20,7 +21,7 @@ DEV = "cuda:0"
 
 
 @pytest.mark.parametrize("case", gio.meta()["g8"], ids=lambda c: c["name"])
-def test_mobilenet_v2_model_level(case):
+def test_mobilenet_v2_model_level(case, monkeypatch):
     from fp8_quantization_amd.approx_calculation import QCustomBNConv2dTorch, QCustomLinearTorch
     from fp8_quantization_amd.mobilenet_workload import mobilenet_v2_approx
     g = gio.load("g8_mbv2.npz")
@@ -39,8 +40,13 @@ def test_mobilenet_v2_model_level(case):
     m.fix_ranges()
     from fp8_quantization_amd import _lib
     _lib.path_stats(reset=True)
+    if not case["run_method"]["approx_flag"]:  # config 1: every product on the HIP kernels
+        def no_torch_conv(*a, **k):
+            raise AssertionError("torch convolution in the config-1 forward")
+        monkeypatch.setattr(torch.nn.functional, "conv2d", no_torch_conv)
     with torch.no_grad():
         logits = m(torch.from_numpy(g[f"{name}__x_ev"]).to(DEV)).cpu().numpy()
+    monkeypatch.undo()
     paths = _lib.path_stats(reset=True)
     if not case["run_method"]["approx_flag"]:  # config 1: the exact products on the fp8 matrix core
         assert paths["dense"] > 0 and paths["f8mx"] == 0, paths
