@@ -194,7 +194,8 @@ def test_conv_on_grid(geo, fmt):
 
 def test_module_exact_branch_runs_dense():
     """QCustomBNConv2dTorch / QCustomLinearTorch with approx_flag off route their exact product
-    through the dense path (E4M3), matching F.conv2d / x @ y."""
+    through the dense path once their operands are FP8-quantized (state flags on), matching
+    F.conv2d / x @ y; with quantization off the product stays torch's fp32 contraction."""
     from fp8_quantization_amd import _lib
     from fp8_quantization_amd.approx_calculation import QCustomBNConv2dTorch, QCustomLinearTorch
     from fp8_quantization_amd.resnet_workload import approx_qparams
@@ -210,6 +211,12 @@ def test_module_exact_branch_runs_dense():
     _lib.path_stats(reset=True)
     with torch.no_grad():
         w = conv.weight.detach()
+        conv.run_forward(x, w, None)
+        lin.run_forward(z, lin.weight.detach(), lin.bias.detach())
+    assert _lib.path_stats(reset=True)["dense"] == 0  # quantization off: torch's contraction
+    for m in (conv, lin):
+        m.quantized()
+    with torch.no_grad():
         y = conv.run_forward(x, w, None)
         yl = lin.run_forward(z, lin.weight.detach(), lin.bias.detach())
     assert _lib.path_stats(reset=True)["dense"] == 2

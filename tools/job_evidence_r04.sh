@@ -1,0 +1,27 @@
+#!/bin/bash
+# Round 4 evidence: per configuration a kernel trace + FETCH / WRITE PMC
+# passes (tools/profile_config.sh), the PMC summary placed under profiles/ as pmc_r04_<tag>.json so
+# the bench line that follows carries its traffic, and the per-kernel breakdown.
+# Usage: bash tools/job_evidence_r04.sh [tag ...]   (default: every configuration below)
+set -o pipefail
+OUT=gpurun_out/ev4; mkdir -p $OUT
+declare -A SPEC=(
+  [c1_mbv2_noapprox]="dn_gemm_bf16 mobilenet_v2 4 3 512 --no-approx"
+  [c3_mbv2_e5m2_v5]="gemm_fast_kernel mobilenet_v2 5 2 512 --v5-ofuf"
+  [c3_mbv2_e5m2_v9]="gemm_f8mx_kernel mobilenet_v2 5 2 512"
+  [c4_vit_b16]="gemm_f8mx_kernel vit_b16 4 3 64"
+  [c5_r50_e5m2]="gemm_f8mx_kernel resnet50 5 2 512"
+)
+TAGS="$*"; [ -n "$TAGS" ] || TAGS="c1_mbv2_noapprox c3_mbv2_e5m2_v5 c3_mbv2_e5m2_v9 c4_vit_b16 c5_r50_e5m2"
+for t in $TAGS; do
+  set -- ${SPEC[$t]}
+  K=$1; ARCH=$2; E=$3; M=$4; B=$5; shift 5; EXTRA="$*"
+  bash tools/profile_config.sh ev4_$t $K $ARCH $E $M $B $EXTRA > $OUT/$t.prof.log 2>&1 || { tail -5 $OUT/$t.prof.log; exit 1; }
+  cp gpurun_out/ev4_$t/pmc.json profiles/pmc_r04_$t.json && cp gpurun_out/ev4_$t/pmc.json $OUT/pmc_r04_$t.json
+  python tools/trace_breakdown.py $(ls gpurun_out/ev4_$t/trace/*kernel_trace.csv) --forwards 5:3 \
+      --out $OUT/breakdown_$t.txt > /dev/null || exit 1
+  sed -n 2,8p $OUT/breakdown_$t.txt
+  timeout -k 10 300 python bench.py --arch $ARCH --expo-width $E --mant-width $M --batch $B $EXTRA > $OUT/bench_r04_$t.json \
+      2> $OUT/bench_r04_$t.err || { tail -3 $OUT/bench_r04_$t.err; exit 1; }
+  python -c "import json; d=json.load(open('$OUT/bench_r04_$t.json')); r=d.get('roofline') or {}; print('$t', round(d['value'],1), r.get('frac'), r.get('traffic'))"
+done

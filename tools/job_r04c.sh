@@ -4,9 +4,11 @@
 set -o pipefail
 OUT=gpurun_out/r04c; mkdir -p $OUT
 R=$(pwd)
-timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_grouped_conv.py \
-    tests/test_gpu_model.py tests/test_gpu_f8_e5m2.py tests/test_gpu_f8.py tests/test_gpu_mbv2_layers.py \
-    tests/test_gpu_model_formats.py tests/test_gpu_dense.py > $OUT/tests.log 2>&1
+timeout -k 5 60 ./tools/bin_mfma_bf16_denorm > $OUT/bf16_denorm.txt 2>&1 || exit $?
+cat $OUT/bf16_denorm.txt
+TESTS=${TESTS:-"tests/test_gpu_grouped_conv.py tests/test_gpu_model.py tests/test_gpu_f8_e5m2.py tests/test_gpu_f8.py
+    tests/test_gpu_mbv2_layers.py tests/test_gpu_model_formats.py tests/test_gpu_dense.py"}
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread $TESTS > $OUT/tests.log 2>&1
 rc=$?; tail -5 $OUT/tests.log; [ $rc -eq 0 ] || exit $rc
 for spec in "r50_e5m2:--arch resnet50 --expo-width 5 --mant-width 2" "mb_e5m2:--arch mobilenet_v2 --expo-width 5 --mant-width 2" \
             "c1_mb_noapprox:--arch mobilenet_v2 --no-approx"; do
