@@ -35,7 +35,8 @@ struct TbxArgs {
 // With fused input quantization (fq.mx set) the values are fq(x) and the quantizer's bias is
 // written to fq_bias / fq_ibias (the kernels' bA).
 __global__ __launch_bounds__(256) void tbx_decode_a(const float *x, int64_t n, uint32_t *out, uint32_t *gate,
-                                                    FqIn fq, float *fq_bias_out, int32_t *fq_ibias_out) {
+                                                    FqIn fq, float *fq_bias_out, int32_t *fq_ibias_out, int M = 3) {
+    const uint32_t lowm = (1u << (23 - M)) - 1u, mmask = (1u << M) - 1u;  // below the grid's mantissa / its bits
     bool bad = false;
     const float fmx = fq.mx ? *fq.mx : 0.0f, fbias = fq.mx ? fq_bias(fmx, fq.E, fq.M) : 0.0f;
     if (fq.mx && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -45,8 +46,8 @@ __global__ __launch_bounds__(256) void tbx_decode_a(const float *x, int64_t n, u
     auto word = [&](float v) {
         if (fq.mx) v = fq_apply(v, fmx, fbias, fq.M, fq.S);
         const uint32_t u = __float_as_uint(v), ua = u & 0x7FFFFFFFu;
-        bad |= (ua != 0u) && ((ua & 0xFFFFFu) != 0u || ua < 0x20800000u || ua > 0x58800000u);
-        return ua == 0u ? 0u : ((u & 0xFF800000u) | (((ua >> 20) & 7u) << 6));
+        bad |= (ua != 0u) && ((ua & lowm) != 0u || ua < 0x20800000u || ua > 0x58800000u);
+        return ua == 0u ? 0u : ((u & 0xFF800000u) | (((ua >> (23 - M)) & mmask) << 6));
     };
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     int64_t i0 = 0;
@@ -61,25 +62,31 @@ __global__ __launch_bounds__(256) void tbx_decode_a(const float *x, int64_t n, u
     if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(gate, 1u);
 }
 
-template <int SW>
+// M = 3 (E4M3) or 2 (E5M2, the same derivation with M-bit mantissas: L = QMc(sig_a sig_b - T / 2^M),
+// saturating at 2 - 2^-M; F7 for u <= 1 + 2^-(M+1) or u in [2, 2 + 2^-M]); the table keeps the
+// 8 x 8 layout (entry m_a * 8 + m_b) for both.
+template <int SW, int M>
 __global__ __launch_bounds__(256) void conv_tbx_kernel(const uint32_t *aw, const float *w, float *y, TbxArgs t,
                                                        const int32_t *bA, const int32_t *bW, const int32_t *bR,
                                                        TablePack tab, uint32_t *gate, const float2 *ep, int ep_act,
                                                        float ep_lo, float ep_hi) {
     constexpr int KW = 3, NCOL = (TBX_TW - 1) * SW + KW;
+    constexpr float ULP = 1.0f / (1 << M);                            // 2^-M
+    constexpr uint32_t LOWM = (1u << (23 - M)) - 1u, MMASK = (1u << M) - 1u;
     __shared__ float2 sL[64];
     const int a_b = *bA, r_b = *bR;
     bool bad = !(a_b >= 2 && a_b <= 120 && r_b >= 2 && r_b <= 120);
     if (threadIdx.x < 64) {
         const int ma = threadIdx.x >> 3, mb = threadIdx.x & 7;
-        const float u = (1.0f + 0.125f * ma) * (1.0f + 0.125f * mb);  // exact
-        const float v = __fmaf_rn(1.0f + 0.125f * ma, 1.0f + 0.125f * mb, -0.125f * (float)tab.raw[ma * 8 + mb]);
+        const int tv = (ma < (1 << M) && mb < (1 << M)) ? tab.raw[(ma << M) | mb] : 0;
+        const float u = (1.0f + ULP * ma) * (1.0f + ULP * mb);  // exact
+        const float v = __fmaf_rn(1.0f + ULP * ma, 1.0f + ULP * mb, -ULP * (float)tv);
         const float pe = __uint_as_float(__float_as_uint(v) & 0x7F800000u);
-        const float xs = fminf(v, pe * (1.875f - p2(-22))), cc = pe * 1048576.0f * 1.5f;
-        const float L = (xs + cc) - cc;  // Q3c(V'): RNE at V's binade after the saturating clamp
+        const float xs = fminf(v, pe * (2.0f - ULP - p2(-22))), cc = pe * (float)(1 << (23 - M)) * 1.5f;
+        const float L = (xs + cc) - cc;  // QMc(V'): RNE at V's binade after the saturating clamp
         uint32_t f7 = 0xFFFFFFFFu;       // never equal to a product of binades
-        if (u <= 1.0625f) f7 = 0x80000000u | ((uint32_t)(127 - r_b) << 23);
-        else if (u >= 2.0f && u <= 2.125f) f7 = 0x80000000u | ((uint32_t)(126 - r_b) << 23);
+        if (u <= 1.0f + 0.5f * ULP) f7 = 0x80000000u | ((uint32_t)(127 - r_b) << 23);
+        else if (u >= 2.0f && u <= 2.0f + ULP) f7 = 0x80000000u | ((uint32_t)(126 - r_b) << 23);
         sL[threadIdx.x] = make_float2(L, __uint_as_float(f7));
     }
     __syncthreads();
@@ -112,9 +119,9 @@ __global__ __launch_bounds__(256) void conv_tbx_kernel(const uint32_t *aw, const
 #pragma unroll
                 for (int kx = 0; kx < KW; ++kx) {
                     const uint32_t bw = __float_as_uint(wk[ky * KW + kx]), bwa = bw & 0x7FFFFFFFu;
-                    bad |= (bwa != 0u) && ((bwa & 0xFFFFFu) != 0u || bwa < 0x20800000u || bwa > 0x58800000u);
+                    bad |= (bwa != 0u) && ((bwa & LOWM) != 0u || bwa < 0x20800000u || bwa > 0x58800000u);
                     const float cB = __uint_as_float(bw & 0xFF800000u);
-                    const uint32_t mb8 = ((bwa >> 20) & 7u) << 3;
+                    const uint32_t mb8 = ((bwa >> (23 - M)) & MMASK) << 3;
 #pragma unroll
                     for (int q = 0; q < TBX_TW; ++q) {
                         const uint32_t wa = col[q * SW + kx];

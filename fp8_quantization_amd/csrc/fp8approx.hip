@@ -378,12 +378,15 @@ __device__ __forceinline__ uint32_t emit_index(const GemmArgs &p, uint32_t uo, u
     wo = pix - ho * (uint32_t)p.em.Wo;
     return (plane * (uint32_t)p.em.awH + ho + (uint32_t)p.em.awph) * (uint32_t)p.em.awW + wo + (uint32_t)p.em.awpw;
 }
-// Max of v over the wave, then one atomicMax into *dst (v >= 0; 0 records nothing).  Every lane
+// Max of v over the wave, then one atomicMax into *dst (v >= 0; 0 records nothing) unless *dst
+// already holds at least v -- every wave of a launch records into the same word, and the read
+// first keeps the atomics (serialised on one L2 line) to the few waves that raise it.  Every lane
 // of the wave must call it.
 __device__ __forceinline__ void wave_max_atomic(uint32_t *dst, uint32_t v) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off));
-    if ((threadIdx.x & 63) == 0 && v != 0u) atomicMax(dst, v);
+    if ((threadIdx.x & 63) == 0 && v != 0u && v > __hip_atomic_load(dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMax(dst, v);
 }
 // 255 - the scale exponent of a nonzero word (the E5M2 halved-block decision reads the largest,
 // gemm_f8mx.h xm_needs_halving; the header's word 5 collects it for the consumer)
@@ -2372,7 +2375,8 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
         // E4M3 table form (conv_tbx.h): {0,1} / zero table, qbma, 3-wide kernel rows, stride 1 or 2
         const int64_t nwg = (Wo + TBX_TW - 1) / TBX_TW, items = Bn * Cout * Ho * nwg;
         static const bool no_tbx = getenv("FP8A_NO_TBX") != nullptr;
-        const bool tbx_ok = fast_ok && !no_tbx && E == 4 && Mw == 3 && (mode == TM_NONE || mode == TM_W1U) &&
+        const bool tbx_ok = fast_ok && !no_tbx && ((E == 4 && Mw == 3) || (E == 5 && Mw == 2)) &&
+                            (mode == TM_NONE || mode == TM_W1U) &&
                             (flags & F_QBMA) && kw == 3 && dw == 1 && sh == sw && (sw == 1 || sw == 2) &&
                             items < (1ll << 31) && Ho * Wo < (1ll << 31) &&
                             workspace_bytes >= FLAG_BYTES + (size_t)(Bn * Cin * H * W) * 4;
@@ -2446,7 +2450,7 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
             if (hipMemsetAsync(gate, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a gate reset");
             const int64_t nx = Bn * Cin * H * W;
             tbx_decode_a<<<(unsigned)std::min<int64_t>((nx + 255) / 256, 8192), 256, 0, s>>>(x, nx, aw, gate, fq, fqb,
-                                                                                                fqi);
+                                                                                                fqi, Mw);
             if (fq.mx) bA = fqi;
             TbxArgs ta;
             ta.Cin = Cin; ta.H = H; ta.W = W; ta.Cout = Cout; ta.Ho = Ho; ta.Wo = Wo;
@@ -2454,11 +2458,14 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
             ta.nwg = (uint32_t)nwg;
             ta.items = (uint32_t)items;
             const unsigned gb = (unsigned)std::min<int64_t>((items + 255) / 256, 8 * 1024);
-            if (sw == 1)
-                conv_tbx_kernel<1><<<gb, 256, 0, s>>>(aw, w, y, ta, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi);
-            else
-                conv_tbx_kernel<2><<<gb, 256, 0, s>>>(aw, w, y, ta, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi);
-            rc = hip_check("fp8a_conv2d (tensor-bias groups, E4M3 table form)");
+            if (Mw == 2) {
+                if (sw == 1) conv_tbx_kernel<1, 2><<<gb, 256, 0, s>>>(aw, w, y, ta, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi);
+                else conv_tbx_kernel<2, 2><<<gb, 256, 0, s>>>(aw, w, y, ta, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi);
+            } else {
+                if (sw == 1) conv_tbx_kernel<1, 3><<<gb, 256, 0, s>>>(aw, w, y, ta, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi);
+                else conv_tbx_kernel<2, 3><<<gb, 256, 0, s>>>(aw, w, y, ta, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi);
+            }
+            rc = hip_check("fp8a_conv2d (tensor-bias groups, E4M3 / E5M2 table form)");
             if (rc) return rc;
         } else if (fast_ok) {
             gate = (uint32_t *)workspace;

@@ -9,7 +9,9 @@ times the operands' binades plus the expo-0-binade and F7 fix-ups.  Checked here
     band included: biases put products near 2^-bR);
   * sums of realistic MobileNetV2-like depthwise layers (stride 1 and 2, 3x3) within the bar;
   * an off-grid input raises the gate and the exact kernel's result is returned.
-The launch's gate word is read back: 0 proves the table form produced the result.
+The launch's gate word is read back: 0 proves the table form produced the result.  E5M2 (round 4:
+the same form with 2-bit mantissas; the zero table of zero_table_ext and a {0,1} table): every code
+pair and layer sums likewise.
 """
 import numpy as np
 import pytest
@@ -38,7 +40,7 @@ def _codes(bias):
     return np.concatenate([v, -v]).astype(np.float32)
 
 
-def _dw_raw(x, w, bA, bW, bR, table, flags, stride, pad):
+def _dw_raw(x, w, bA, bW, bR, table, flags, stride, pad, fmt=(E, M)):
     """fp8a_conv2d on a depthwise layer with a caller-owned workspace: (y, gate word)."""
     from fp8_quantization_amd import _lib
     L = _lib.load()
@@ -56,7 +58,7 @@ def _dw_raw(x, w, bA, bW, bR, table, flags, stride, pad):
     tR = torch.tensor([bR], dtype=torch.int32, device=DEV)
     tab = torch.as_tensor(np.ascontiguousarray(table, np.int32))
     rc = L.fp8a_conv2d(_lib.dev_ptr(xt), _lib.dev_ptr(wt), _lib.dev_ptr(y), Bn, C, H, W, C, kh, kw, stride, stride,
-                       pad, pad, 1, 1, C, E, M, _lib.dev_ptr(tA), _lib.dev_ptr(tW), _lib.dev_ptr(tR),
+                       pad, pad, 1, 1, C, fmt[0], fmt[1], _lib.dev_ptr(tA), _lib.dev_ptr(tW), _lib.dev_ptr(tR),
                        _lib.host_ptr(tab), flags, _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(DEV))
     _lib.check(rc, "fp8a_conv2d")
     torch.cuda.synchronize()
@@ -142,6 +144,68 @@ def test_off_grid_input_falls_back():
     cols = torch.nn.functional.unfold(torch.from_numpy(x), (3, 3), padding=1).transpose(1, 2).reshape(-1, 72).numpy()
     for c in range(8):
         ref, S = orc.matmul(cols[:, c * 9:(c + 1) * 9], w[c].reshape(9, 1), E, M, bA, bW[c:c + 1], bR, tab,
+                            FL | orc.TB, with_abs=True)
+        got = y[:, c].reshape(-1, 1).astype(np.float64)
+        assert np.all(np.abs(got - ref) <= gio.sum_tolerance(S.astype(np.float64))), f"channel {c}"
+
+
+# ---------------------------------------------------------------------------------------- E5M2
+def _codes_e5m2(bias):
+    e = np.repeat(np.arange(32), 4)
+    m = np.tile(np.arange(4), 32)
+    v = np.where(e == 0, np.ldexp(m / 4.0, 1 - bias), np.ldexp(1.0 + m / 4.0, e - bias))
+    return np.concatenate([v, -v]).astype(np.float32)
+
+
+def _table_e5m2(kind):
+    if kind == "zero":
+        return gio.load("g2_matmul.npz")["E5M2_table_zero"]
+    return np.array([[0, 1, 0, 1], [1, 0, 1, 0], [0, 0, 1, 1], [1, 1, 0, 0]], np.int32)
+
+
+@pytest.mark.parametrize("table", ["zero", "w1"])
+@pytest.mark.parametrize("biases", [(20, 20, 9), (16, 24, 12), (12, 12, 2), (28, 28, 40), (24, 20, 30)])
+@pytest.mark.parametrize("stride", [1, 2])
+def test_e5m2_every_code_pair_bitexact(biases, table, stride):
+    bA, bW_, bR = biases
+    a, b = _codes_e5m2(bA), _codes_e5m2(bW_)
+    C = 256
+    if stride == 1:
+        x = np.broadcast_to(a.reshape(1, 1, 16, 16), (1, C, 16, 16)).copy()
+    else:
+        x = np.zeros((1, C, 32, 32), np.float32)
+        x[:, :, 0::2, 0::2] = a.reshape(1, 1, 16, 16)
+    w = np.zeros((C, 1, 3, 3), np.float32)
+    w[:, 0, 1, 1] = b
+    bW = np.full(C, bW_, np.int32)
+    tab = _table_e5m2(table)
+    y, gate = _dw_raw(x, w, bA, bW, bR, tab, FL, stride, 1, fmt=(5, 2))
+    ref = orc.terms(a.reshape(-1, 1), b.reshape(1, -1), 5, 2, bA, bW, bR, tab, FL | orc.TB)[:, 0, :]
+    assert gate == 0, "gate raised: the table form did not produce these terms"
+    got = y[0].reshape(C, 256).T
+    _terms_equal(got, ref, f"E5M2 biases {biases} {table} stride {stride}")
+
+
+@pytest.mark.parametrize("cfg", [dict(C=32, hw=28, s=1), dict(C=24, hw=29, s=2), dict(C=16, hw=14, s=2)])
+def test_e5m2_depthwise_layer_sums(cfg):
+    rng = np.random.default_rng(cfg["C"] * 7 + cfg["hw"])
+    bA, bR = 18, 16
+    C, hw, s = cfg["C"], cfg["hw"], cfg["s"]
+    expo = rng.integers(6, 32, size=(3, C, hw, hw))
+    x = np.ldexp(1.0 + rng.integers(0, 4, size=expo.shape) / 4.0, expo - bA) * rng.choice([-1.0, 1.0], size=expo.shape)
+    x[rng.random(x.shape) < 0.4] = 0.0
+    x = x.astype(np.float32)
+    bW = rng.integers(20, 24, size=C).astype(np.int32)
+    we = rng.integers(6, 32, size=(C, 1, 3, 3))
+    w = (np.ldexp(1.0 + rng.integers(0, 4, size=we.shape) / 4.0, we - bW[:, None, None, None])
+         * rng.choice([-1.0, 1.0], size=we.shape)).astype(np.float32)
+    tab = _table_e5m2("zero")
+    y, gate = _dw_raw(x, w, bA, bW, bR, tab, FL, s, 1, fmt=(5, 2))
+    assert gate == 0
+    cols = torch.nn.functional.unfold(torch.from_numpy(x), (3, 3), padding=1, stride=s)
+    cols = cols.transpose(1, 2).reshape(-1, C * 9).numpy()
+    for c in range(C):
+        ref, S = orc.matmul(cols[:, c * 9:(c + 1) * 9], w[c].reshape(9, 1), 5, 2, bA, bW[c:c + 1], bR, tab,
                             FL | orc.TB, with_abs=True)
         got = y[:, c].reshape(-1, 1).astype(np.float64)
         assert np.all(np.abs(got - ref) <= gio.sum_tolerance(S.astype(np.float64))), f"channel {c}"
