@@ -140,7 +140,7 @@ def fallback_stats(reset=False):
     return dict(exact_launches=int(out[0]), exact_units=int(out[1]), f32_reruns=int(out[2]), tb_launches=int(out[3]))
 
 
-PATHS = ("one_hot", "f8mx", "tt", "tt16", "fast", "exact", "dense", "reserved7")
+PATHS = ("one_hot", "f8mx", "tt", "tt16", "fast", "exact", "dense", "v5mx")
 
 
 def path_stats(reset=False):

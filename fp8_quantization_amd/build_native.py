@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "fp8approx.hip")
 DEPS = [SRC, os.path.join(HERE, "csrc", "fp8approx_device.h"), os.path.join(HERE, "csrc", "gemm_f8mx.h"), os.path.join(HERE, "csrc", "conv_tbx.h"), os.path.join(HERE, "csrc", "gemm_tt.h"), os.path.join(HERE, "csrc", "gemm_tt16.h"), os.path.join(HERE, "csrc", "gemm_oh.h"),
-        os.path.join(HERE, "csrc", "gemm_dense.h"),
+        os.path.join(HERE, "csrc", "gemm_dense.h"), os.path.join(HERE, "csrc", "gemm_v5mx.h"),
         os.path.join(ROOT, "include", "fp8approx.h")]
 OUT_DIR = os.path.join(HERE, "lib")
 OUT = os.path.join(OUT_DIR, "libfp8approx.so")

@@ -428,3 +428,108 @@ __global__ __launch_bounds__(256) void conv_dwg_kernel(const float *x, const flo
     }
     if (__syncthreads_or(bad ? 1 : 0) && tid == 0) atomicOr(gate, 1u);
 }
+
+// ---------------------------------------------------------------------------------------------
+// conv_v5dw_kernel: the v5 integer-adder model's depthwise convolutions (BASELINE config 3 with
+// approx_version 5, MobileNetV2 E5M2) -- the terms of exact_term_v5 (fp8approx_device.h; the
+// reference's approx_mult_new, approx_matmul_whole_v5.py:155-182) in conv_tbx_kernel's layout.
+// v5 decodes every operand exactly (clip_OF), so the A pre-pass (v5dw_decode_a) turns each input
+// into a word and never gates; the weights' words come from v5dw_decode_b.  Per term:
+//   r = c_a + c_b' + T[m_a][m_b]    (c_b' = B code - (bA + bB - bR) << M, a byte of the tap's row)
+//   r = v5_ofuf(r)                   (adder wrap / OF / UF switches)
+//   value: r in [0, 2^M): the subnormal band, r 2^(1-bR-M) (float(r) times a power of two);
+//          else the normal binade (r >> M) - bR with mantissa r & (2^M - 1), whose float bits
+//          are linear in r: (r << (23 - M)) + ((127 - bR) << 23) (also for r < 0 without the wrap)
+//   signed with sign(a) sign(b), summed in k order (one channel, 3 taps x kh rows <= 16 terms, so
+//   the chunked sum of conv_tb_direct_kernel<false> is the plain sequential sum).
+// E5M2 with the adder wrap on (sim_hw_add_OFUF: r in [0, 2^(E+M)) after v5_ofuf, whatever the
+// OF / UF switches) only -- 4 table bytes per tap row.  A result bias whose binades leave the
+// normal float range raises the gate and conv_tb_direct_kernel<false> recomputes the launch.
+//
+// A word: sign(a) << 31 | (m_a * 8) << 16 | c_a (c_a < 2^7); the zero word (0) is the code of +0,
+// which is also what the reference's im2col padding decodes to.
+__global__ __launch_bounds__(256) void v5dw_decode_a(const float *x, int64_t n, uint32_t *out, int E, int M,
+                                                     const int32_t *bA) {
+    const DFmt f = dfmt(E, M, *bA, false);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float v = x[i];
+        int e, m;
+        exact_dec(v, f, true, e, m);
+        out[i] = (v < 0.0f ? 0x80000000u : 0u) | ((uint32_t)(m * 8) << 16) | (uint32_t)(e * (1 << M) + m);
+    }
+}
+
+// B words per (channel, tap): x = (c_b' << 1) | sign(b), y = the tap's table row T[m_a][m_b]
+// for m_a = 0..3 as signed bytes.
+__global__ __launch_bounds__(256) void v5dw_decode_b(const float *w, int64_t n, int taps, uint2 *out, int E, int M,
+                                                     const int32_t *bA, const int32_t *bW, const int32_t *bR,
+                                                     TablePack tab) {
+    const int a_b = *bA, r_b = *bR;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t co = i / taps;
+        const int b_b = bW[co];
+        const float v = w[i];
+        int e, m;
+        exact_dec(v, dfmt(E, M, b_b, false), true, e, m);
+        const int32_t cb = (e - (a_b + b_b - r_b)) * (1 << M) + m;
+        uint32_t row = 0;
+        for (int ma = 0; ma < 4; ++ma) row |= ((uint32_t)(uint8_t)tab.raw[(ma << M) | m]) << (8 * ma);
+        out[i] = make_uint2(((uint32_t)cb << 1) | (v < 0.0f ? 1u : 0u), row);
+    }
+}
+
+template <int SW>
+__global__ __launch_bounds__(256) void conv_v5dw_kernel(const uint32_t *aw, const uint2 *bw, float *y, TbxArgs t,
+                                                        const int32_t *bR, uint32_t flags, int E, uint32_t *gate,
+                                                        const float2 *ep,
+                                                        int ep_act, float ep_lo, float ep_hi) {
+    constexpr int KW = 3, NCOL = (TBX_TW - 1) * SW + KW, M = 2;
+    const int r_b = *bR;
+    const int32_t maxi = ((1 << E) << M) - 1;
+    bool bad = !(r_b >= -90 && r_b <= 120);
+    const uint32_t lin0 = (uint32_t)(127 - r_b) << 23;          // float bits of r = 0 on the normal line
+    const float csub = __uint_as_float((uint32_t)(126 - r_b) << 23);  // 2^(1 - bR - M), M = 2
+    const int64_t HW = t.H * t.W;
+    for (uint32_t item = blockIdx.x * blockDim.x + threadIdx.x; item < t.items; item += gridDim.x * blockDim.x) {
+        const uint32_t wg = item % t.nwg, r1 = item / t.nwg;
+        const uint32_t ho = r1 % (uint32_t)t.Ho, r2 = r1 / (uint32_t)t.Ho;
+        const uint32_t co = r2 % (uint32_t)t.Cout, img = r2 / (uint32_t)t.Cout;
+        const int wo0 = (int)wg * TBX_TW, wi0 = wo0 * SW - t.pw;
+        float acc[TBX_TW] = {0.0f, 0.0f, 0.0f, 0.0f};
+        const uint32_t *plane = aw + ((int64_t)img * t.Cin + (int64_t)co) * HW;
+        const uint2 *wk = bw + (int64_t)co * t.kh * KW;
+        for (int ky = 0; ky < t.kh; ++ky) {
+            const int hi = (int)ho * SW - t.ph + ky * t.dh;
+            const bool rowok = (uint32_t)hi < (uint32_t)t.H;
+            const uint32_t *row = plane + (int64_t)hi * t.W;
+            uint32_t col[NCOL];
+#pragma unroll
+            for (int j = 0; j < NCOL; ++j) {
+                const int wi = wi0 + j;
+                col[j] = (rowok && (uint32_t)wi < (uint32_t)t.W) ? row[wi] : 0u;
+            }
+#pragma unroll
+            for (int kx = 0; kx < KW; ++kx) {
+                const uint2 b = wk[ky * KW + kx];
+                const int32_t cb = (int32_t)b.x >> 1;
+                const uint32_t sb = b.x << 31;
+#pragma unroll
+                for (int q = 0; q < TBX_TW; ++q) {
+                    const uint32_t wa = col[q * SW + kx];
+                    const int32_t tv = __builtin_amdgcn_sbfe((int32_t)b.y, (wa >> 16) & 31u, 8);  // T[m_a][m_b]
+                    int32_t r = (int32_t)(wa & 0xFFu) + cb + tv;
+                    r = v5_ofuf(r, maxi, M, flags);
+                    const float vn = __uint_as_float(((uint32_t)r << (23 - M)) + lin0);
+                    const float vs = (float)r * csub;
+                    const float v = ((uint32_t)r < (1u << M)) ? vs : vn;
+                    acc[q] += __uint_as_float(__float_as_uint(v) ^ ((wa & 0x80000000u) ^ sb));
+                }
+            }
+        }
+        float *yr = y + (((int64_t)img * t.Cout + co) * t.Ho + ho) * t.Wo;
+#pragma unroll
+        for (int q = 0; q < TBX_TW; ++q)
+            if (wo0 + q < t.Wo) yr[wo0 + q] = epi(ep, ep_act, ep_lo, ep_hi, co, acc[q]);
+    }
+    if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(gate, 1u);
+}

@@ -908,6 +908,7 @@ __global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
 }
 
 #include "gemm_f8mx.h"
+#include "gemm_v5mx.h"
 #include "gemm_tt.h"
 #include "gemm_tt16.h"
 #include "gemm_oh.h"
@@ -1432,6 +1433,15 @@ static void launch_fast(int mode, const GemmArgs &a, hipStream_t s) {
     const int64_t tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
     dim3 grid((unsigned)(tiles * a.splits));
     if (mode == TM_V5) {  // the v5 model has no s2n / qbma / golden-clip variants
+        if (a.aw && a.wfmt == 4) {  // the matrix-core form (gemm_v5mx.h), per OF / UF switch pair
+            const dim3 gv((unsigned)(((a.M + V5_BMT - 1) / V5_BMT) * ((a.N + V5_BNT - 1) / V5_BNT) * a.splits));
+            const bool uf = a.flags & F_UF, of = a.flags & F_OF;
+            if (uf && of) gemm_v5mx_kernel<true, true><<<gv, 256, 0, s>>>(a);
+            else if (uf) gemm_v5mx_kernel<true, false><<<gv, 256, 0, s>>>(a);
+            else if (of) gemm_v5mx_kernel<false, true><<<gv, 256, 0, s>>>(a);
+            else gemm_v5mx_kernel<false, false><<<gv, 256, 0, s>>>(a);
+            return;
+        }
         gemm_fast_kernel<false, false, false, TM_V5><<<grid, NT, 0, s>>>(a);
         return;
     }
@@ -1483,7 +1493,7 @@ constexpr size_t FLAG_BYTES = 256;  // workspace prefix holding the off-grid fla
 
 // Launch paths taken by run_gemm since load (fp8a_path_stats): host-side counters.
 enum { PATH_OH = 0, PATH_F8MX = 1, PATH_TT = 2, PATH_TT16 = 3, PATH_FAST = 4, PATH_EXACT = 5, PATH_DENSE = 6,
-       PATH_N = 8 };
+       PATH_V5MX = 7, PATH_N = 8 };
 static std::atomic<uint64_t> g_paths[PATH_N];
 // Options (fp8a_set_option): "one_hot" -- the E4M3 one-hot path (gemm_oh.h), default off: its
 // dense GEMM beats gemm_f8mx_kernel by 1.6x, but the 1.1% candidate pairs of the benchmark network
@@ -1594,11 +1604,13 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // Bytes of the pre-decoded operands of the matrix-core E4M3 kernel (gemm_f8mx.h): A words
 // (a_words of them) + B column pairs [Kpad][Npad / 2] of 8 bytes.
+// The B image: the E4M3 / E5M2 column pairs ([kpad][npad / 2] uint2) or the v5 form's four table
+// words per column ([kpad][npad] uint2, gemm_v5mx.h) -- sized for the larger.
+static size_t xm_b_bytes(int64_t kpad, int64_t npad) { return align256((size_t)(kpad * npad) * 8); }
 static size_t xm_operand_bytes(int64_t N, int64_t K, int64_t a_words) {
     const int64_t kpad = (K + BK - 1) / BK * BK, npad = (N + BN - 1) / BN * BN;
     // + table image + the E5M2 B exponent ranges
-    return align256((size_t)a_words * 4) + align256((size_t)(kpad * npad / 2) * 8) + 16384 +
-           align256((size_t)(kpad * npad / 16) * 2);
+    return align256((size_t)a_words * 4) + xm_b_bytes(kpad, npad) + 16384 + align256((size_t)(kpad * npad / 16) * 2);
 }
 
 // The per-unit fallback marks after the flag word: urow [nur], ucol [nuc], utile [nur * nuc] bytes.
@@ -1849,7 +1861,11 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     // operands in the workspace (else gemm_fast_kernel runs); FP8A_NO_MX=1 forces the latter
     a.aw = nullptr;
     const bool tt = mode != TM_F8 && tt_form(a.Mw, a.flags, a.tab);
-    if ((mode == TM_F8 || tt) && !no_mx()) {
+    // v5 (E5M2, adder wrap on): the matrix-core form of gemm_v5mx.h; FP8A_NO_V5MX=1 keeps
+    // gemm_fast_kernel<TM_V5> (A/B runs)
+    static const bool no_v5mx = getenv("FP8A_NO_V5MX") != nullptr;
+    const bool v5mx = mode == TM_V5 && a.Mw == 2 && (a.flags & F_OFUF) && !no_v5mx;
+    if ((mode == TM_F8 || tt || v5mx) && !no_mx()) {
         const int64_t kpad = kt * BK, npad = (a.N + BN - 1) / BN * BN;
         const size_t off = head + (a.splits > 1 ? splitk_bytes(a.M, a.N, a.K) : 0);
         // gemm_f8mx_kernel reads its operands with 32-bit byte offsets
@@ -1862,20 +1878,20 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
             a.aw = (const uint32_t *)base;
             a.awld = kpad;
             a.bqw = (const uint2 *)(base + align256((size_t)a_words * 4));
-            a.lutw = (const uint32_t *)(base + align256((size_t)a_words * 4) + align256((size_t)(kpad * npad / 2) * 8));
+            a.lutw = (const uint32_t *)(base + align256((size_t)a_words * 4) + xm_b_bytes(kpad, npad));
             a.ebr = (const uint16_t *)((const char *)a.lutw + 16384);
             a.xm_vmin = mode == TM_NONE ? 0 : -1;
             a.npad = npad;
             a.ttf7 = 0;
             for (int i = 0; tt && i < (1 << (2 * a.Mw)); ++i) a.ttf7 |= a.tab.raw[i] < 0;
-            a.wfmt = tt ? (tt16_form(a.Mw, a.ttf7, a.K) ? 2 : 1) : 0;
+            a.wfmt = v5mx ? 4 : tt ? (tt16_form(a.Mw, a.ttf7, a.K) ? 2 : 1) : 0;
             a.xncg = tt ? 4 : xm_ncg(a.N);
             // the input's word image from the previous launch (fp8a_conv2d_chain): its words replace
             // the A pre-pass, which then runs gated (only to write the fused quantizer's bias, or to
             // re-decode x if the image arrived invalid)
-            const bool use_img = a.in_img != nullptr && !tt && a.conv && a.fqin.mx != nullptr;
+            const bool use_img = a.in_img != nullptr && !tt && !v5mx && a.conv && a.fqin.mx != nullptr;
             if (use_img) a.aw = a.in_img + 64;
-            a.af32 = !tt && !use_img && xm_af32(a) ? 1 : 0;
+            a.af32 = !tt && !v5mx && !use_img && xm_af32(a) ? 1 : 0;
             const int64_t rows = a.conv ? a.M / (a.Ho * a.Wo) : a.M, cols = a_words / std::max<int64_t>(rows, 1);
             const dim3 ga((unsigned)std::min<int64_t>((cols + 255) / 256, 64), (unsigned)std::min<int64_t>(rows, 1024));
             if (use_img) {
@@ -1885,7 +1901,10 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
             } else if (!a.af32) {
                 xm_decode_a<<<ga, 256, 0, s>>>(a);
             }
-            if (tt) {  // B words [Kpad][Npad] (the same bytes as the E4M3 pair grid) + the static image
+            if (v5mx) {  // the four table words per (k, n), [Kpad][Npad]
+                const unsigned gb = (unsigned)std::min<int64_t>((kpad * npad + 255) / 256, 4096);
+                v5mx_decode_b<<<gb, 256, 0, s>>>(a, kpad);
+            } else if (tt) {  // B words [Kpad][Npad] (the same bytes as the E4M3 pair grid) + the static image
                 const unsigned gb = (unsigned)std::min<int64_t>((kpad * npad + 255) / 256, 4096);
                 tt_decode_b<<<gb, 256, 0, s>>>(a, kpad);  // (+ gemm_tt16_kernel's f16 image when wfmt == 2)
             } else {
@@ -1899,7 +1918,7 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     if (a.fqin.mx && !a.aw)  // the caller (conv2d_impl) only fuses where the pre-decode runs
         return fail(FP8A_EINVAL, "internal: fused input quantization without the matrix-core path");
     if (mode == TM_F8 && a.Mw != 3 && !a.aw) mode = mode0;  // (gemm_fast_kernel's TM_F8 form is E4M3 only)
-    ++g_paths[!a.aw ? PATH_FAST : a.wfmt == 0 ? PATH_F8MX : a.wfmt == 1 ? PATH_TT : PATH_TT16];
+    ++g_paths[!a.aw ? PATH_FAST : a.wfmt == 0 ? PATH_F8MX : a.wfmt == 1 ? PATH_TT : a.wfmt == 4 ? PATH_V5MX : PATH_TT16];
     launch_fast(mode, a, s);
     rc = hip_check("fp8a fast gemm launch");
     if (rc) return rc;
@@ -2275,7 +2294,8 @@ size_t fp8a_conv2d_workspace_size(int64_t Bn, int64_t Cin, int64_t H, int64_t W,
     // implicit GEMM (no im2col image): the off-grid flag word + split-K partials of one group
     const int64_t Mrows = Bn * Ho * Wo, cog = Cout / groups, Kg = (Cin / groups) * kh * kw;
     if (Mrows <= 0 || Kg <= 0) return FLAG_BYTES;
-    if (cog == 1) return FLAG_BYTES + (size_t)(Bn * Cin * H * W) * 4;  // tensor-bias kernels: A words
+    // tensor-bias kernels: A words (+ the v5 depthwise form's B words)
+    if (cog == 1) return FLAG_BYTES + align256((size_t)(Bn * Cin * H * W) * 4) + (size_t)(Cout * kh * kw) * 8;
     // A words: the zero-bordered word image of gemm_f8mx_kernel (xm_a_words)
     const WordImage wi = word_image(H, W, ph, pw);
     return gemm_workspace_bytes(Mrows, cog, Kg, Bn * (Cin / groups) * wi.H * wi.W);
@@ -2521,10 +2541,43 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
         rc = pack_table(table, Mw, true, tp, mode);
         if (rc) return rc;
         const int64_t total = Bn * Cout * Ho * Wo;
-        ++g_paths[PATH_EXACT];
+        // the word form (conv_v5dw_kernel, conv_tbx.h): E5M2 with the adder wrap, depthwise 3-wide
+        // rows, stride 1 / 2; the literal kernel behind it runs only if its gate is raised
+        const int64_t nx = Bn * Cin * H * W, nwg = (Wo + TBX_TW - 1) / TBX_TW, items = Bn * Cout * Ho * nwg;
+        const size_t awb = align256((size_t)nx * 4);
+        static const bool no_v5dw = getenv("FP8A_NO_V5DW") != nullptr;
+        const bool v5dw_ok = !no_v5dw && Mw == 2 && (flags & F_OFUF) && cig == 1 && kw == 3 && kh <= 5 && dw == 1 &&
+                             sh == sw && (sw == 1 || sw == 2) && items < (1ll << 31) && Ho * Wo < (1ll << 31) &&
+                             workspace != nullptr && workspace_bytes >= FLAG_BYTES + awb + (size_t)(Cout * kh * kw) * 8;
+        uint32_t *gate = nullptr;
+        if (v5dw_ok) {
+            gate = (uint32_t *)workspace;
+            uint32_t *aw = (uint32_t *)((char *)workspace + FLAG_BYTES);
+            uint2 *bwd = (uint2 *)((char *)workspace + FLAG_BYTES + awb);
+            if (hipMemsetAsync(gate, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a gate reset");
+            v5dw_decode_a<<<(unsigned)std::min<int64_t>((nx + 255) / 256, 8192), 256, 0, s>>>(x, nx, aw, E, Mw, bA);
+            const int64_t nb = Cout * kh * kw;
+            v5dw_decode_b<<<(unsigned)std::min<int64_t>((nb + 255) / 256, 1024), 256, 0, s>>>(w, nb, kh * kw, bwd, E, Mw,
+                                                                                               bA, bW, bR, tp);
+            TbxArgs ta;
+            ta.Cin = Cin; ta.H = H; ta.W = W; ta.Cout = Cout; ta.Ho = Ho; ta.Wo = Wo;
+            ta.kh = kh; ta.ph = ph; ta.pw = pw; ta.dh = dh; ta.cpg = 1;
+            ta.nwg = (uint32_t)nwg;
+            ta.items = (uint32_t)items;
+            const unsigned gb = (unsigned)std::min<int64_t>((items + 255) / 256, 8 * 1024);
+            if (sw == 1)
+                conv_v5dw_kernel<1><<<gb, 256, 0, s>>>(aw, bwd, y, ta, bR, flags, E, gate, ep, act, act_lo, act_hi);
+            else
+                conv_v5dw_kernel<2><<<gb, 256, 0, s>>>(aw, bwd, y, ta, bR, flags, E, gate, ep, act, act_lo, act_hi);
+            rc = hip_check("fp8a_conv2d (v5 depthwise, word form)");
+            if (rc) return rc;
+            ++g_paths[PATH_FAST];
+        } else {
+            ++g_paths[PATH_EXACT];
+        }
         conv_tb_direct_kernel<false><<<(unsigned)std::min<int64_t>((total + 255) / 256, 16384), 256, 0, s>>>(
             x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups, Ho, Wo, E, Mw, bA, bW, bR, tp, flags,
-            nullptr, ep, act, act_lo, act_hi, FqIn{});
+            gate, ep, act, act_lo, act_hi, FqIn{});
         return hip_check("fp8a_conv2d (v5 depthwise, direct)");
     }
     for (int g = 0; g < groups; ++g) {

@@ -246,6 +246,14 @@ __device__ __forceinline__ uint32_t oh_code_a(float x, uint32_t emnA, int sA, in
     return ((cb >> 31) << 7) | ((uint32_t)min(max(e, 1), 30) << 2) | (mc << 11);
 }
 
+// A word of the v5 matrix-core form (xm_decode_a, wfmt 4; gemm_v5mx.h): (sign << 15 | code << 5) in both halves
+__device__ __forceinline__ uint32_t v5_word_a(float v, const DFmt &f) {
+    int e, m;
+    exact_dec(v, f, true, e, m);
+    const uint32_t h = (v < 0.0f ? 0x8000u : 0u) | ((uint32_t)(e * (1 << f.M) + m) << 5);
+    return h * 0x10001u;
+}
+
 // xm_decode_a's record for xm_needs_halving: 255 - (the smallest se of its nonzero E5M2 words)
 __device__ __forceinline__ void xm_record_se(const GemmArgs &p, uint32_t sehi) {
     if (p.Mw == 2 && p.wfmt == 0) wave_max_atomic(p.flag + 1, sehi);
@@ -282,8 +290,10 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
     const int64_t hw = p.H * p.W;
     const int64_t rows = p.conv ? p.M / (p.Ho * p.Wo) : p.M, cols = p.conv ? p.aw_c * p.awH * p.awW : p.awld;
     uint32_t sehi = 0;  // 255 - the smallest se of this thread's nonzero E5M2 words (xm_record_se)
+    const DFmt fv5 = dfmt(p.E, p.Mw, bA, false);  // (wfmt 4: the v5 decode, clip_OF)
     auto word = [&](float v, bool &ok) {
         if (p.fqin.mx) v = fq_apply(v, fmx, fbias, p.fqin.M, p.fqin.S);
+        if (p.wfmt == 4) return v5_word_a(v, fv5);
         if (p.wfmt == 3) return oh_code_a(v, emnA, 6 - bA, bR, ok);
         if (p.wfmt == 2) return tt16_word_a(v, emnA, bA, ok, win);
         if (p.wfmt) return tt_word_a(v, p.Mw, emnA, ok);

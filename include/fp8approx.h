@@ -70,7 +70,7 @@ int fp8a_fallback_stats(uint64_t *out, int reset);
  *   [0] E4M3 one-hot dense matrix-core GEMM + candidate correction (gemm_oh.h),
  *   [1] E4M3 per-pair matrix-core kernel (gemm_f8mx.h), [2] gemm_tt_kernel (E3M4 / E2M5),
  *   [3] gemm_tt16_kernel (E3M4), [4] gemm_fast_kernel (VALU tiled), [5] the exact kernel alone
- *   (tensor-bias products), [6] the dense exact product (fp8a_dense_*), [7] reserved.  reset != 0 zeroes them after reading.
+ *   (tensor-bias products), [6] the dense exact product (fp8a_dense_*), [7] the v5 matrix-core form (gemm_v5mx.h).  reset != 0 zeroes them after reading.
  */
 int fp8a_path_stats(uint64_t *out, int reset);
 

@@ -61,20 +61,21 @@ def test_workspace_queries_are_host_only():
     Mr, N, K = 3211264, 64, 147
     kpad, npad = (K + 15) // 16 * 16, (N + 63) // 64 * 64
     assert L.fp8a_matmul_workspace_size_mnk(Mr, N, K) == flag + _units(Mr, N) + max(
-        _a256(Mr * kpad * 4) + _a256(kpad * npad // 2 * 8) + 16384, _oh(Mr, N, K))
+        _a256(Mr * kpad * 4) + _a256(kpad * npad * 8) + 16384 + _a256(kpad * npad // 16 * 2), _oh(Mr, N, K))
     Mr, N, K = 12544, 512, 4608
     assert L.fp8a_matmul_workspace_size_mnk(Mr, N, K) > flag + _a256(Mr * K * 4) + _a256(K * N // 2 * 8)  # split
     # depthwise (single output channel per group): the tensor-bias kernels need the flag word and
-    # the E4M3 table form's input words (the v5 mode takes the GEMM path, unsplit, no pre-decode)
-    assert L.fp8a_conv2d_workspace_size(2, 8, 6, 6, 8, 3, 3, 1, 1, 1, 1, 1, 1, 8) == flag + 2 * 8 * 6 * 6 * 4
+    # the table forms' input words, + the v5 word form's (channel, tap) words
+    assert L.fp8a_conv2d_workspace_size(2, 8, 6, 6, 8, 3, 3, 1, 1, 1, 1, 1, 1, 8) == flag + _a256(2 * 8 * 6 * 6 * 4) + 8 * 9 * 8
     # implicit-GEMM conv: no im2col image; the A words of one group's input slice in a zero
     # border (ph rows above / below; W % 4 == 0: a 4-word left margin and rows rounded up to 4
-    # words, here 8 + 4 + 1 -> 16), + B column pairs + the table image (unsplit here)
+    # words, here 8 + 4 + 1 -> 16), + the B image (sized for the v5 form's 8 B per (k, n)) + the
+    # table image + the E5M2 exponent ranges (unsplit here)
     n2 = L.fp8a_conv2d_workspace_size(2, 3, 8, 8, 4, 3, 3, 1, 1, 1, 1, 1, 1, 1)
-    assert n2 == flag + _units(2 * 8 * 8, 4) + max(_a256(2 * 3 * 10 * 16 * 4) + _a256(32 * 64 // 2 * 8) + 16384,
+    assert n2 == flag + _units(2 * 8 * 8, 4) + max(_a256(2 * 3 * 10 * 16 * 4) + _a256(32 * 64 * 8) + 16384 + 256,
                                                    _oh(2 * 8 * 8, 4, 27, 2 * 3 * 10 * 16))
     n3 = L.fp8a_conv2d_workspace_size(2, 3, 7, 7, 4, 3, 3, 1, 1, 1, 1, 1, 1, 1)  # W % 4 != 0: 9 x 9
-    assert n3 == flag + _units(2 * 7 * 7, 4) + max(_a256(2 * 3 * 9 * 9 * 4) + _a256(32 * 64 // 2 * 8) + 16384,
+    assert n3 == flag + _units(2 * 7 * 7, 4) + max(_a256(2 * 3 * 9 * 9 * 4) + _a256(32 * 64 * 8) + 16384 + 256,
                                                    _oh(2 * 7 * 7, 4, 27, 2 * 3 * 9 * 9))
     assert L.fp8a_conv2d_workspace_size(256, 3, 224, 224, 4, 7, 7, 2, 2, 3, 3, 1, 1, 1) >= flag + 256 * 3 * 230 * 230 * 4
 

@@ -111,3 +111,146 @@ def test_v5_operator_opt_in():
                                m.get_res_fp_bias(), get_comp_table_NN(3, 4, True, 3), sim_hw_add_OFUF=True,
                                with_UF_opt=True, padding=(1, 1))
     assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+@pytest.mark.parametrize("sw", [dict(sim_hw_add_OFUF=True), dict(sim_hw_add_OFUF=True, with_OF_opt=True, with_UF_opt=True),
+                                dict(sim_hw_add_OFUF=True, with_UF_opt=True)], ids=["wrap", "wrap_of_uf", "wrap_uf"])
+def test_v5_depthwise_e5m2_word_form(stride, sw):
+    """MobileNetV2-like E5M2 depthwise layers in v5 mode with the adder wrap (BASELINE config 3's
+    switches) run the word form conv_v5dw_kernel (a "fast" launch, no literal recompute); every
+    output equals the oracle's sum of its 9 v5 terms within the bar, and single-tap outputs (the
+    other 8 terms of a zero weight row pinned separately) are bit-exact terms."""
+    from fp8_quantization_amd import _lib
+    from fp8_quantization_amd.approx_v5 import approx_conv2d_v5
+    rng = np.random.default_rng(stride * 10 + len(sw))
+    E, M, bA, bR = 5, 2, 16, 12
+    C, hw = 24, 15
+    x = np.ldexp(1.0 + rng.integers(0, 4, size=(2, C, hw, hw)) / 4.0, rng.integers(-14, 16, size=(2, C, hw, hw)))
+    x[rng.random(x.shape) < 0.4] = 0.0
+    x = (x * rng.choice([-1.0, 1.0], size=x.shape)).astype(np.float32)
+    w = np.ldexp(1.0 + rng.integers(0, 4, size=(C, 1, 3, 3)) / 4.0, rng.integers(-12, 11, size=(C, 1, 3, 3)))
+    w = (w * rng.choice([-1.0, 1.0], size=w.shape)).astype(np.float32)
+    bW = rng.integers(14, 20, size=C).astype(np.int32)
+    tab = torch.zeros(4, 4, dtype=torch.int32)  # the E5M2 zero table (zero_table_ext)
+    _lib.path_stats(reset=True)
+    _lib.fallback_stats(reset=True)
+    y = approx_conv2d_v5(t(x), t(w), E, M, bA, t(bW, torch.int32), bR, tab, stride=(stride, stride), padding=(1, 1),
+                         groups=C, **sw).cpu().numpy()
+    paths = _lib.path_stats(reset=True)
+    assert paths["fast"] == 1 and paths["exact"] == 0, paths
+    assert _lib.fallback_stats(reset=True)["tb_launches"] == 0
+    cols = torch.nn.functional.unfold(torch.from_numpy(x), (3, 3), padding=1, stride=stride).transpose(1, 2)
+    cols = cols.reshape(-1, C * 9).numpy()
+    fl = orc.flags_v5(True, sw.get("with_OF_opt", False), sw.get("with_UF_opt", False))
+    for c in range(C):
+        ref, S = orc.matmul(cols[:, c * 9:(c + 1) * 9], w[c].reshape(9, 1), E, M, bA, bW[c:c + 1], bR, tab.numpy(), fl,
+                            with_abs=True)
+        got = y[:, c].reshape(-1, 1).astype(np.float64)
+        assert np.all(np.abs(got - ref) <= gio.sum_tolerance(S)), f"channel {c}"
+        tm = orc.terms(cols[:, c * 9:(c + 1) * 9], w[c].reshape(9, 1), E, M, bA, bW[c:c + 1], bR, tab.numpy(), fl)
+        seq = np.zeros(tm.shape[0], np.float32)
+        for k in range(9):
+            seq = (seq + tm[:, k, 0].astype(np.float32)).astype(np.float32)
+        assert same_bits(y[:, c].reshape(-1), seq).all(), f"channel {c}: not the literal k-order sum"
+
+
+def _e5m2_codes(bias):
+    e = np.repeat(np.arange(32), 4)
+    m = np.tile(np.arange(4), 32)
+    v = np.where(e == 0, np.ldexp(m / 4.0, 1 - bias), np.ldexp(1.0 + m / 4.0, e - bias))
+    return np.concatenate([v, -v]).astype(np.float32)
+
+
+def _v5_e5m2_tables():
+    from fp8_quantization_amd.approx_v5 import get_comp_table_NN
+    tabs = {"zero": np.zeros((4, 4), np.int32)}
+    try:
+        tabs["v5comp"] = np.asarray(get_comp_table_NN(5, 2, True, 3), np.int32).reshape(4, 4)
+    except Exception:  # (no v5 table for this format)
+        pass
+    tabs["signed"] = np.array([[0, -1, 2, 0], [1, 0, -2, 1], [0, 3, 0, -1], [-3, 1, 1, 0]], np.int32)
+    return tabs
+
+
+SWITCHES = [dict(sim_hw_add_OFUF=True), dict(sim_hw_add_OFUF=True, with_UF_opt=True),
+            dict(sim_hw_add_OFUF=True, with_OF_opt=True), dict(sim_hw_add_OFUF=True, with_OF_opt=True, with_UF_opt=True)]
+SW_IDS = ["wrap", "wrap_uf", "wrap_of", "wrap_of_uf"]
+
+
+@pytest.mark.parametrize("sw", SWITCHES, ids=SW_IDS)
+@pytest.mark.parametrize("biases", [(16, 16, 12), (12, 20, 30), (20, 10, 2), (8, 8, -20)])
+@pytest.mark.parametrize("table", ["zero", "signed", "v5comp"])
+def test_v5mx_every_code_pair_bitexact(sw, biases, table):
+    """gemm_v5mx_kernel (E5M2, the adder wrap on): every one of the 256 x 256 code pairs as a
+    K = 1 product equals the oracle's v5 term bit for bit, for each OF / UF switch pair (the
+    ragged last K-tile masks the seven padded K-steps)."""
+    from fp8_quantization_amd import _lib
+    from fp8_quantization_amd.approx_v5 import approx_matmul_v5
+    tabs = _v5_e5m2_tables()
+    if table not in tabs:
+        pytest.skip("no v5 E5M2 compensation table")
+    tab = tabs[table]
+    bA, bB, bR = biases
+    A = _e5m2_codes(bA).reshape(-1, 1)
+    B = _e5m2_codes(bB).reshape(1, -1)
+    _lib.path_stats(reset=True)
+    C = approx_matmul_v5(t(A), t(B), 5, 2, bA, bB, bR, torch.as_tensor(tab), **sw).cpu().numpy()
+    paths = _lib.path_stats(reset=True)
+    assert paths["v5mx"] == 1, paths
+    fl = orc.flags_v5(True, sw.get("with_OF_opt", False), sw.get("with_UF_opt", False))
+    ref = orc.terms(A, B, 5, 2, bA, bB, bR, tab, fl)[:, 0, :]
+    ok = same_bits(C, ref)
+    assert ok.all(), f"{np.count_nonzero(~ok)} terms differ; first {np.argwhere(~ok)[0]}"
+
+
+@pytest.mark.parametrize("sw", SWITCHES, ids=SW_IDS)
+@pytest.mark.parametrize("shape", [(300, 200, 72), (64, 37, 16), (1000, 960, 32)])
+def test_v5mx_sums_within_bar(sw, shape):
+    from fp8_quantization_amd import _lib
+    from fp8_quantization_amd.approx_v5 import approx_matmul_v5
+    Mr, K, N = shape
+    rng = np.random.default_rng(Mr + K + N + len(sw))
+    bA, bR = 16, 14
+    A = np.ldexp(1.0 + rng.integers(0, 4, size=(Mr, K)) / 4.0, rng.integers(-16, 16, size=(Mr, K)))
+    A[rng.random(A.shape) < 0.3] = 0.0
+    A = (A * rng.choice([-1.0, 1.0], size=A.shape)).astype(np.float32)
+    B = (np.ldexp(1.0 + rng.integers(0, 4, size=(K, N)) / 4.0, rng.integers(-14, 8, size=(K, N)))
+         * rng.choice([-1.0, 1.0], size=(K, N))).astype(np.float32)
+    bB = rng.integers(14, 19, size=N).astype(np.int32)
+    tab = _v5_e5m2_tables()["signed"]
+    _lib.path_stats(reset=True)
+    C = approx_matmul_v5(t(A), t(B), 5, 2, bA, t(bB, torch.int32), bR, torch.as_tensor(tab), **sw).cpu().numpy()
+    assert _lib.path_stats(reset=True)["v5mx"] == 1
+    fl = orc.flags_v5(True, sw.get("with_OF_opt", False), sw.get("with_UF_opt", False))
+    ref, S = orc.matmul(A, B, 5, 2, bA, bB, bR, tab, fl, with_abs=True)
+    assert np.all(np.abs(C.astype(np.float64) - ref) <= gio.sum_tolerance(S))
+
+
+@pytest.mark.parametrize("k,pad,stride", [(3, 1, 1), (3, 1, 2), (1, 0, 1)])
+def test_v5mx_conv2d_e5m2(k, pad, stride):
+    """The implicit-GEMM conv on gemm_v5mx_kernel: the zero border of the word image gives the
+    padded positions the v5 term of a zero operand, as the reference's im2col does."""
+    from fp8_quantization_amd import _lib
+    from fp8_quantization_amd.approx_v5 import approx_conv2d_v5
+    rng = np.random.default_rng(k * 10 + stride)
+    E, M, bA, bR = 5, 2, 16, 12
+    cin, cout, hw = 24, 40, 11
+    x = np.ldexp(1.0 + rng.integers(0, 4, size=(2, cin, hw, hw)) / 4.0, rng.integers(-14, 14, size=(2, cin, hw, hw)))
+    x[rng.random(x.shape) < 0.4] = 0.0
+    x = (x * rng.choice([-1.0, 1.0], size=x.shape)).astype(np.float32)
+    w = (np.ldexp(1.0 + rng.integers(0, 4, size=(cout, cin, k, k)) / 4.0, rng.integers(-12, 6, size=(cout, cin, k, k)))
+         * rng.choice([-1.0, 1.0], size=(cout, cin, k, k))).astype(np.float32)
+    bW = rng.integers(14, 20, size=cout).astype(np.int32)
+    tab = _v5_e5m2_tables()["zero"]
+    sw = dict(sim_hw_add_OFUF=True, with_OF_opt=True, with_UF_opt=True)
+    _lib.path_stats(reset=True)
+    y = approx_conv2d_v5(t(x), t(w), E, M, bA, t(bW, torch.int32), bR, torch.as_tensor(tab), stride=(stride, stride),
+                         padding=(pad, pad), **sw).cpu().numpy()
+    assert _lib.path_stats(reset=True)["v5mx"] == 1
+    cols = torch.nn.functional.unfold(torch.from_numpy(x), (k, k), padding=pad, stride=stride).transpose(1, 2)
+    cols = cols.reshape(-1, cols.shape[2]).numpy()
+    fl = orc.flags_v5(True, True, True)
+    ref, S = orc.matmul(cols, w.reshape(cout, -1).T, E, M, bA, bW, bR, tab, fl, with_abs=True)
+    got = y.transpose(0, 2, 3, 1).reshape(-1, cout).astype(np.float64)
+    assert np.all(np.abs(got - ref) <= gio.sum_tolerance(S))
