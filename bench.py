@@ -59,7 +59,11 @@ def dominant_kernel(E, M, v5=False):
     in csrc/fp8approx.hip; the bench uses s2n + qbma and the withComp=False tables): the E4M3
     matrix-core form for E4M3 and E5M2 (bf8 conversion), the packed-f16 tile-table kernel for
     E3M4 (gemm_tt16_kernel on every K >= 256 layer; gemm_tt_kernel<4> on the short-K ones), the
-    f32 tile-table kernel for E2M5, the VALU tiled kernel otherwise (the v5 mode)."""
+    f32 tile-table kernel for E2M5, the v5 matrix-core form for E5M2 v5 with the adder wrap, the VALU
+    tiled kernel otherwise."""
+    if v5 and (E, M) == (5, 2):
+        return "gemm_v5mx_kernel", ("implicit-GEMM approx conv / linear, E5M2 v5 integer-adder terms as packed 16-bit "
+                                    "code arithmetic, the codes' bf16 bits summed on the matrix core")
     if v5:
         return "gemm_fast_kernel", f"implicit-GEMM approx conv / linear on the VALU, E{E}M{M} v5 integer-adder terms"
     if (E, M) in ((4, 3), (5, 2)):

@@ -65,7 +65,12 @@ __global__ __launch_bounds__(256) void tbx_decode_a(const float *x, int64_t n, u
 // M = 3 (E4M3) or 2 (E5M2, the same derivation with M-bit mantissas: L = QMc(sig_a sig_b - T / 2^M),
 // saturating at 2 - 2^-M; F7 for u <= 1 + 2^-(M+1) or u in [2, 2 + 2^-M]); the table keeps the
 // 8 x 8 layout (entry m_a * 8 + m_b) for both.
-template <int SW, int M>
+// RW = 2 (option "tbx_rw", the default for undilated rows): a thread computes the same 4 columns
+// of two consecutive output rows; every input row of their union (kh + 1 rows at stride 1,
+// kh + 2 at stride 2, against 2 kh for two threads) is gathered once and feeds both rows'
+// accumulators, each still in (ky, kx) order -- bit-identical outputs, fewer and more independent
+// loads per output (the one-row form waits on its loads 66 % of its cycles, §3f).
+template <int SW, int M, int RW = 1>
 __global__ __launch_bounds__(256) void conv_tbx_kernel(const uint32_t *aw, const float *w, float *y, TbxArgs t,
                                                        const int32_t *bA, const int32_t *bW, const int32_t *bR,
                                                        TablePack tab, uint32_t *gate, const float2 *ep, int ep_act,
@@ -95,19 +100,25 @@ __global__ __launch_bounds__(256) void conv_tbx_kernel(const uint32_t *aw, const
     const char *lut = reinterpret_cast<const char *>(sL);
     const int64_t HW = t.H * t.W;
 
+    const uint32_t hog = ((uint32_t)t.Ho + RW - 1) / RW;  // row groups per plane
     for (uint32_t item = blockIdx.x * blockDim.x + threadIdx.x; item < t.items; item += gridDim.x * blockDim.x) {
         const uint32_t wg = item % t.nwg, r1 = item / t.nwg;
-        const uint32_t ho = r1 % (uint32_t)t.Ho, r2 = r1 / (uint32_t)t.Ho;
+        const uint32_t ho0 = (r1 % hog) * RW, r2 = r1 / hog;
         const uint32_t co = r2 % (uint32_t)t.Cout, img = r2 / (uint32_t)t.Cout;
         const int wb = bW[co];
         bad |= !(wb >= 2 && wb <= 120);
         const int wo0 = (int)wg * TBX_TW, wi0 = wo0 * SW - t.pw;
-        float acc[TBX_TW] = {0.0f, 0.0f, 0.0f, 0.0f};
+        float acc[RW][TBX_TW];
+#pragma unroll
+        for (int j = 0; j < RW; ++j)
+#pragma unroll
+            for (int q = 0; q < TBX_TW; ++q) acc[j][q] = 0.0f;
+        const int nr = RW == 1 ? t.kh : (RW - 1) * SW + t.kh;  // input rows (RW > 1: dh = 1)
         for (int c = 0; c < t.cpg; ++c) {
             const uint32_t *plane = aw + ((int64_t)img * t.Cin + (int64_t)co * t.cpg + c) * HW;
             const float *wk = w + ((int64_t)co * t.cpg + c) * t.kh * KW;
-            for (int ky = 0; ky < t.kh; ++ky) {
-                const int hi = (int)ho * (int)(SW == 1 ? 1 : 2) - t.ph + ky * t.dh;
+            for (int r = 0; r < nr; ++r) {
+                const int hi = (int)ho0 * SW - t.ph + (RW == 1 ? r * t.dh : r);
                 const bool rowok = (uint32_t)hi < (uint32_t)t.H;
                 const uint32_t *row = plane + (int64_t)hi * t.W;
                 uint32_t col[NCOL];
@@ -117,29 +128,38 @@ __global__ __launch_bounds__(256) void conv_tbx_kernel(const uint32_t *aw, const
                     col[j] = (rowok && (uint32_t)wi < (uint32_t)t.W) ? row[wi] : 0u;
                 }
 #pragma unroll
-                for (int kx = 0; kx < KW; ++kx) {
-                    const uint32_t bw = __float_as_uint(wk[ky * KW + kx]), bwa = bw & 0x7FFFFFFFu;
-                    bad |= (bwa != 0u) && ((bwa & LOWM) != 0u || bwa < 0x20800000u || bwa > 0x58800000u);
-                    const float cB = __uint_as_float(bw & 0xFF800000u);
-                    const uint32_t mb8 = ((bwa >> (23 - M)) & MMASK) << 3;
+                for (int j = 0; j < RW; ++j) {
+                    const int ky = r - j * SW;  // this input row's tap for output row ho0 + j
+                    if (ky < 0 || ky >= t.kh) continue;
 #pragma unroll
-                    for (int q = 0; q < TBX_TW; ++q) {
-                        const uint32_t wa = col[q * SW + kx];
-                        const float2 e = *reinterpret_cast<const float2 *>(lut + ((wa & 0x1C0u) | mb8));
-                        const float cab = __uint_as_float(wa & 0xFF800000u) * cB;  // exact
-                        float r = e.x * cab;                                         // exact
-                        const float rs = __fmaf_rn(2.0f, r, -copysignf(twoq, r));    // expo field 0
-                        r = ((__float_as_uint(r) & 0x7F800000u) == q0exp) ? rs : r;
-                        r = (__float_as_uint(cab) == __float_as_uint(e.y)) ? fabsf(r) : r;  // F7
-                        acc[q] += r;
+                    for (int kx = 0; kx < KW; ++kx) {
+                        const uint32_t bw = __float_as_uint(wk[ky * KW + kx]), bwa = bw & 0x7FFFFFFFu;
+                        bad |= (bwa != 0u) && ((bwa & LOWM) != 0u || bwa < 0x20800000u || bwa > 0x58800000u);
+                        const float cB = __uint_as_float(bw & 0xFF800000u);
+                        const uint32_t mb8 = ((bwa >> (23 - M)) & MMASK) << 3;
+#pragma unroll
+                        for (int q = 0; q < TBX_TW; ++q) {
+                            const uint32_t wa = col[q * SW + kx];
+                            const float2 e = *reinterpret_cast<const float2 *>(lut + ((wa & 0x1C0u) | mb8));
+                            const float cab = __uint_as_float(wa & 0xFF800000u) * cB;  // exact
+                            float rv = e.x * cab;                                        // exact
+                            const float rs = __fmaf_rn(2.0f, rv, -copysignf(twoq, rv));  // expo field 0
+                            rv = ((__float_as_uint(rv) & 0x7F800000u) == q0exp) ? rs : rv;
+                            rv = (__float_as_uint(cab) == __float_as_uint(e.y)) ? fabsf(rv) : rv;  // F7
+                            acc[j][q] += rv;
+                        }
                     }
                 }
             }
         }
-        float *yr = y + (((int64_t)img * t.Cout + co) * t.Ho + ho) * t.Wo;
 #pragma unroll
-        for (int q = 0; q < TBX_TW; ++q)
-            if (wo0 + q < t.Wo) yr[wo0 + q] = epi(ep, ep_act, ep_lo, ep_hi, co, acc[q]);
+        for (int j = 0; j < RW; ++j) {
+            if (ho0 + j >= (uint32_t)t.Ho) break;
+            float *yr = y + (((int64_t)img * t.Cout + co) * t.Ho + ho0 + j) * t.Wo;
+#pragma unroll
+            for (int q = 0; q < TBX_TW; ++q)
+                if (wo0 + q < t.Wo) yr[wo0 + q] = epi(ep, ep_act, ep_lo, ep_hi, co, acc[j][q]);
+        }
     }
     if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(gate, 1u);
 }

@@ -1507,6 +1507,9 @@ static bool g_opt_oh_stats = false;  // "oh_stats": the one-hot kernels count in
 // fp32 gather conv_dwg_kernel (5 % slower), 3 conv_dwg_kernel's column mapping over
 // tbx_decode_a's word image.  FP8A_DW=<n> sets it at load.
 static int g_opt_dwx = getenv("FP8A_DW") ? atoi(getenv("FP8A_DW")) : 0;
+// "tbx_rw": output rows per thread of conv_tbx_kernel (1 or 2; 2 needs undilated rows).
+// FP8A_TBX_RW=<n> sets it at load.
+static int g_opt_tbx_rw = getenv("FP8A_TBX_RW") ? atoi(getenv("FP8A_TBX_RW")) : 2;
 
 // Compute units of the current device (cached); 256 (MI355X) when no device is visible.
 static int device_cus() {
@@ -2085,6 +2088,11 @@ int fp8a_set_option(const char *name, int value) {
         g_opt_dwx = value;
         return old;
     }
+    if (strcmp(name, "tbx_rw") == 0) {
+        const int old = g_opt_tbx_rw;
+        g_opt_tbx_rw = value;
+        return old;
+    }
     if (strcmp(name, "oh_correct") == 0) {
         const int old = g_opt_oh_correct ? 1 : 0;
         g_opt_oh_correct = value != 0;
@@ -2476,15 +2484,18 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
             ta.Cin = Cin; ta.H = H; ta.W = W; ta.Cout = Cout; ta.Ho = Ho; ta.Wo = Wo;
             ta.kh = kh; ta.ph = ph; ta.pw = pw; ta.dh = dh; ta.cpg = (int)cig;
             ta.nwg = (uint32_t)nwg;
-            ta.items = (uint32_t)items;
-            const unsigned gb = (unsigned)std::min<int64_t>((items + 255) / 256, 8 * 1024);
+            const bool rw2 = g_opt_tbx_rw == 2 && dh == 1;
+            ta.items = (uint32_t)(rw2 ? Bn * Cout * ((Ho + 1) / 2) * nwg : items);
+            const unsigned gb = (unsigned)std::min<int64_t>((ta.items + 255) / 256, 8 * 1024);
+#define FP8A_TBX(SW_, M_, RW_) conv_tbx_kernel<SW_, M_, RW_><<<gb, 256, 0, s>>>(aw, w, y, ta, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi)
             if (Mw == 2) {
-                if (sw == 1) conv_tbx_kernel<1, 2><<<gb, 256, 0, s>>>(aw, w, y, ta, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi);
-                else conv_tbx_kernel<2, 2><<<gb, 256, 0, s>>>(aw, w, y, ta, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi);
+                if (sw == 1) { if (rw2) FP8A_TBX(1, 2, 2); else FP8A_TBX(1, 2, 1); }
+                else { if (rw2) FP8A_TBX(2, 2, 2); else FP8A_TBX(2, 2, 1); }
             } else {
-                if (sw == 1) conv_tbx_kernel<1, 3><<<gb, 256, 0, s>>>(aw, w, y, ta, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi);
-                else conv_tbx_kernel<2, 3><<<gb, 256, 0, s>>>(aw, w, y, ta, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi);
+                if (sw == 1) { if (rw2) FP8A_TBX(1, 3, 2); else FP8A_TBX(1, 3, 1); }
+                else { if (rw2) FP8A_TBX(2, 3, 2); else FP8A_TBX(2, 3, 1); }
             }
+#undef FP8A_TBX
             rc = hip_check("fp8a_conv2d (tensor-bias groups, E4M3 / E5M2 table form)");
             if (rc) return rc;
         } else if (fast_ok) {

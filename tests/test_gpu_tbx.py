@@ -209,3 +209,38 @@ def test_e5m2_depthwise_layer_sums(cfg):
                             FL | orc.TB, with_abs=True)
         got = y[:, c].reshape(-1, 1).astype(np.float64)
         assert np.all(np.abs(got - ref) <= gio.sum_tolerance(S.astype(np.float64))), f"channel {c}"
+
+
+@pytest.mark.parametrize("fmt", [(4, 3), (5, 2)], ids=["E4M3", "E5M2"])
+@pytest.mark.parametrize("cfg", [dict(C=16, hw=15, s=1), dict(C=24, hw=13, s=2), dict(C=8, hw=1, s=1),
+                                 dict(C=8, hw=6, s=2)])
+def test_two_row_form_bit_identical(fmt, cfg):
+    """Option "tbx_rw" = 2 (two output rows per thread, the default) against 1: the same terms in
+    the same (ky, kx) order per output, so bit-identical outputs (odd Ho, 1-pixel planes)."""
+    from fp8_quantization_amd import _lib
+    rng = np.random.default_rng(cfg["C"] + cfg["hw"] + cfg["s"])
+    E_, M_ = fmt
+    C, hw, s = cfg["C"], cfg["hw"], cfg["s"]
+    if fmt == (4, 3):
+        bA, bR = 10, 9
+        x = _grid(rng, (2, C, hw, hw), bA, zero_frac=0.3)
+        bW = rng.integers(12, 16, size=C).astype(np.int32)
+        w = _grid(rng, (C, 1, 3, 3), bW[:, None, None, None])
+        tab = gio.load("g2_matmul.npz")["E4M3_table_nocomp"]
+    else:
+        bA, bR = 18, 16
+        x = (np.ldexp(1.0 + rng.integers(0, 4, size=(2, C, hw, hw)) / 4.0, rng.integers(-12, 14, size=(2, C, hw, hw)))
+             * rng.choice([-1.0, 1.0], size=(2, C, hw, hw))).astype(np.float32)
+        bW = rng.integers(20, 24, size=C).astype(np.int32)
+        w = (np.ldexp(1.0 + rng.integers(0, 4, size=(C, 1, 3, 3)) / 4.0, rng.integers(-14, 8, size=(C, 1, 3, 3)))
+             * rng.choice([-1.0, 1.0], size=(C, 1, 3, 3))).astype(np.float32)
+        tab = _table_e5m2("zero")
+    old = _lib.set_option("tbx_rw", 1)
+    try:
+        y1, g1 = _dw_raw(x, w, bA, bW, bR, tab, FL, s, 1, fmt=fmt)
+        _lib.set_option("tbx_rw", 2)
+        y2, g2 = _dw_raw(x, w, bA, bW, bR, tab, FL, s, 1, fmt=fmt)
+    finally:
+        _lib.set_option("tbx_rw", old)
+    assert g1 == 0 and g2 == 0
+    assert np.array_equal(y1.view(np.uint32), y2.view(np.uint32))

@@ -7,10 +7,13 @@ set -o pipefail
 OUT=gpurun_out/ev4; mkdir -p $OUT
 declare -A SPEC=(
   [c1_mbv2_noapprox]="dn_gemm_bf16 mobilenet_v2 4 3 512 --no-approx"
-  [c3_mbv2_e5m2_v5]="gemm_fast_kernel mobilenet_v2 5 2 512 --v5-ofuf"
+  [c3_mbv2_e5m2_v5]="gemm_v5mx_kernel mobilenet_v2 5 2 512 --v5-ofuf"
   [c3_mbv2_e5m2_v9]="gemm_f8mx_kernel mobilenet_v2 5 2 512"
   [c4_vit_b16]="gemm_f8mx_kernel vit_b16 4 3 64"
   [c5_r50_e5m2]="gemm_f8mx_kernel resnet50 5 2 512"
+  [c2_r18_e4m3]="gemm_f8mx_kernel resnet18 4 3 512"
+  [mbv2_e4m3]="gemm_f8mx_kernel mobilenet_v2 4 3 512"
+  [c5_r50_e4m3]="gemm_f8mx_kernel resnet50 4 3 512"
 )
 TAGS="$*"; [ -n "$TAGS" ] || TAGS="c1_mbv2_noapprox c3_mbv2_e5m2_v5 c3_mbv2_e5m2_v9 c4_vit_b16 c5_r50_e5m2"
 for t in $TAGS; do

@@ -21,7 +21,8 @@ import collections
 import csv
 import json
 
-OP_KERNELS = "xm_decode_a,xm_decode_b,tt_decode_b,gemm_f8mx_kernel,gemm_tt_kernel,gemm_tt16_kernel,gemm_fast_kernel,splitk_reduce_kernel,gemm_exact_kernel"
+OP_KERNELS = ("xm_decode_a,xm_decode_b,tt_decode_b,v5mx_decode_b,gemm_f8mx_kernel,gemm_v5mx_kernel,gemm_tt_kernel,"
+              "gemm_tt16_kernel,gemm_fast_kernel,splitk_reduce_kernel,gemm_exact_kernel")
 
 
 def read_csv(path):
