@@ -22,7 +22,7 @@ SYMBOLS = ("fp8a_version", "fp8a_last_error", "fp8a_fallback_stats", "fp8a_path_
            "fp8a_conv2d_block_workspace_size", "fp8a_conv2d_block", "fp8a_max_pool2d", "fp8a_im2col",
            "fp8a_fp8_quantize", "fp8a_matmul_qamaa", "fp8a_conv2d_qamaa", "fp8a_matmul_block_workspace_size",
            "fp8a_matmul_block", "fp8a_dense_matmul_workspace_size", "fp8a_dense_matmul",
-           "fp8a_dense_conv2d_workspace_size", "fp8a_dense_conv2d", "fp8a_grouped_conv2d", "fp8a_dense_stats", "fp8a_clock_stats",
+           "fp8a_dense_conv2d_workspace_size", "fp8a_dense_conv2d", "fp8a_grouped_conv2d", "fp8a_dense_conv2d_fused", "fp8a_dense_stats", "fp8a_clock_stats",
            "fp8a_word_image_bytes", "fp8a_word_image_init", "fp8a_conv2d_chain", "fp8a_conv2d_wants_image")
 
 _lib = None
@@ -87,6 +87,8 @@ def load():
         "fp8a_dense_conv2d_workspace_size": ([I64, I64, I64, I64, I64, I, I, I, I, I, I, I, I], SZ),
         "fp8a_dense_conv2d": ([P, P, P, I64, I64, I64, I64, I64, I, I, I, I, I, I, I, I, I, P, SZ, P], I),
         "fp8a_grouped_conv2d": ([P, P, P, I64, I64, I64, I64, I64, I, I, I, I, I, I, I, I, I, P], I),
+        "fp8a_dense_conv2d_fused": ([P, P, P, I64, I64, I64, I64, I64, I, I, I, I, I, I, I, I, I, I,
+                                     P, I, I, I, P, P, P, I, I, I, P, P, P, I, F, F, P, I, I, I, P, P, P, SZ, P], I),
         "fp8a_dense_stats": ([P, I], I),
         "fp8a_clock_stats": ([P, I], I),
     }

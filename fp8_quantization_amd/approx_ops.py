@@ -24,7 +24,7 @@ from .error_tables import get_error_table_NN  # noqa: F401  (re-exported, v9:555
 __all__ = ["custom_matmul_vectorize", "approx_matmul", "approx_matmul_block", "approx_terms", "approx_conv2d", "qamaa_matmul", "qamaa_conv2d",
            "quant_to_fp_any_vectorize_torch", "float_to_fpany_absint_torch", "get_error_table_NN",
            "make_flags", "make_flags_v5", "fp8_fake_quantize", "bn_act_epilogue", "dense_format", "dense_matmul",
-           "dense_conv2d", "grouped_conv2d"]
+           "dense_conv2d", "grouped_conv2d", "dense_conv2d_fused"]
 
 
 def make_flags(with_approx=True, with_s2nn2s_opt=False, quant_btw_mult_accu=True, golden_clip_OF=False,
@@ -849,6 +849,49 @@ def grouped_conv2d(x, w, groups, stride=(1, 1), padding=(0, 0), dilation=(1, 1))
                            [int(v) for v in dilation])
     _prof_end(ev, y.numel() * w.shape[1] * w.shape[2] * w.shape[3], 4 * (x.numel() + w.numel() + y.numel()))
     return y
+
+
+def dense_conv2d_fused(x, w, groups=1, stride=(1, 1), padding=(0, 0), dilation=(1, 1), fmt=None, qin=None, rq=None,
+                       bn=None, oq=None):
+    """A config-1 layer in one launch family (fp8a_dense_conv2d_fused): y = oq(clamp(bn(rq(conv(qin(x), w))))).
+    qin / rq / oq: (maxval, n_bits, mantissa bits, sign bits) of a per-tensor FP8 quantizer or None;
+    bn: (scale_shift [C][2], act, lo, hi) from bn_act_epilogue or None.  Returns (y, biases): each
+    given quantizer's float bias tensor [1] (its custom_bias), keyed "qin" / "rq" / "oq"."""
+    if x.dim() != 4 or w.dim() != 4 or x.shape[1] != w.shape[1] * groups or w.shape[0] % groups:
+        raise AssertionError(f"dense_conv2d_fused: shape mismatch {tuple(x.shape)} * {tuple(w.shape)} / {groups}")
+    L = _lib.load()
+    x = _as_f32(x).contiguous()
+    w = _as_f32(w).contiguous()
+    Bn, Cin, H, W = x.shape
+    Cout, _, kh, kw = w.shape
+    Ho = (H + 2 * padding[0] - dilation[0] * (kh - 1) - 1) // stride[0] + 1
+    Wo = (W + 2 * padding[1] - dilation[1] * (kw - 1) - 1) // stride[1] + 1
+    y = torch.empty((Bn, Cout, Ho, Wo), dtype=torch.float32, device=x.device)
+    keep, biases, qargs = [], {}, []
+    for name, q in (("qin", qin), ("rq", rq), ("oq", oq)):
+        if q is None:
+            qargs += [None, 0, 0, 0, None, None]
+            continue
+        mx = _as_f32(q[0]).reshape(-1).to(x.device).contiguous()
+        b = torch.empty(1, dtype=torch.float32, device=x.device)
+        ib = torch.empty(1, dtype=torch.int32, device=x.device)
+        b._fp8a_i32 = ib
+        keep.append(mx)
+        biases[name] = b
+        qargs += [_lib.dev_ptr(mx), int(q[1]), int(q[2]), int(q[3]), _lib.dev_ptr(b), _lib.dev_ptr(ib)]
+    ep, act, lo, hi = (None, 0, 0.0, 0.0) if bn is None else bn
+    if ep is not None:
+        ep = _as_f32(ep).to(x.device).contiguous()
+    geo = (Bn, Cin, H, W, Cout, kh, kw, stride[0], stride[1], padding[0], padding[1], dilation[0], dilation[1])
+    ws = _workspace(x.device, L.fp8a_dense_conv2d_workspace_size(*geo) if groups == 1 else 16)
+    fmt = dense_format(3) if fmt is None else fmt
+    ev = _prof_start()
+    rc = L.fp8a_dense_conv2d_fused(_lib.dev_ptr(x), _lib.dev_ptr(w), _lib.dev_ptr(y), *geo, int(groups), int(fmt),
+                                   *qargs[:12], _lib.dev_ptr(ep) if ep is not None else None, int(act), float(lo),
+                                   float(hi), *qargs[12:], _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(x.device))
+    _lib.check(rc, "fp8a_dense_conv2d_fused")
+    _prof_end(ev, y.numel() * w.shape[1] * kh * kw, 4 * (x.numel() + w.numel() + y.numel()))
+    return y, biases
 
 
 # ----------------------------------------------------------------------------------- max pool

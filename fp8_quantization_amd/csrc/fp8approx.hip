@@ -2165,9 +2165,20 @@ int fp8a_dense_conv2d(const float *x, const float *w, float *y, int64_t Bn, int6
     return run_dense(a, workspace, workspace_bytes, (hipStream_t)stream);
 }
 
+static int grouped_conv_impl(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
+                             int64_t Cout, int groups, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw,
+                             const DnFuse &fz, hipStream_t stream);
+
 int fp8a_grouped_conv2d(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
                         int64_t Cout, int groups, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw,
                         fp8a_stream_t stream) {
+    return grouped_conv_impl(x, w, y, Bn, Cin, H, W, Cout, groups, kh, kw, sh, sw, ph, pw, dh, dw, DnFuse{},
+                             (hipStream_t)stream);
+}
+
+static int grouped_conv_impl(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
+                             int64_t Cout, int groups, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw,
+                             const DnFuse &fz, hipStream_t stream) {
     if (kh < 1 || kw < 1 || sh < 1 || sw < 1 || dh < 1 || dw < 1 || ph < 0 || pw < 0 || Bn < 0 || Cin < 0 || Cout < 0)
         return fail(FP8A_EINVAL, "bad convolution geometry");
     if (groups < 1 || Cin % groups != 0 || Cout % groups != 0) return fail(FP8A_EINVAL, "channels not divisible by groups");
@@ -2180,10 +2191,11 @@ int fp8a_grouped_conv2d(const float *x, const float *w, float *y, int64_t Bn, in
     a.total = Bn * Cout * Ho * ((Wo + GC_OW - 1) / GC_OW);
     a.cig = (int)(Cin / groups); a.cog = (int)(Cout / groups);
     a.kh = kh; a.kw = kw; a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw; a.dh = dh; a.dw = dw;
+    a.fz = fz;
     if (a.total == 0) return FP8A_OK;
     if (!x || !w || !y) return fail(FP8A_EINVAL, "null pointer");
-    if (a.total + 65536ll * 256 < (1ll << 31)) launch_group_conv<uint32_t>(a, (hipStream_t)stream);
-    else launch_group_conv<int64_t>(a, (hipStream_t)stream);
+    if (a.total + 65536ll * 256 < (1ll << 31)) launch_group_conv<uint32_t>(a, stream);
+    else launch_group_conv<int64_t>(a, stream);
     ++g_paths[PATH_DENSE];
     return hip_check("fp8a grouped conv launch");
 }
@@ -2992,6 +3004,58 @@ int fp8a_fp8_quantize(const float *x, int64_t rows, int64_t inner, const float *
     fp8_quantize_kernel<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(x, rows, inner, maxval, per_row, E,
                                                                            Mbits, sign_bits, out, bias_out, ibias_out);
     return hip_check("fp8a_fp8_quantize");
+}
+
+// The config-1 layer (approx_flag off) in one launch family: fq_in on the loaded input, the exact
+// product (groups = 1: run_dense, the matrix core; groups > 1: dn_group_conv), and per output
+// rq -> eval batch norm -> clamp -> fq_out in the store (gemm_dense.h DnFuse).  Each quantizer
+// writes its bias (the reference quantizer's custom_bias) like fp8a_conv2d_qin.
+static int fused_quantizer(const float *mx, int nbits, int mbits, int sign_bits, float *bias_out, int32_t *ibias_out,
+                           FqIn &f, hipStream_t s) {
+    f = FqIn{};
+    if (!mx) return FP8A_OK;
+    const int qE = nbits - sign_bits - mbits;
+    if (mbits < 1 || qE < 1) return fail(FP8A_EFORMAT, "bad FP8 quantizer format");
+    if (!bias_out || !ibias_out) return fail(FP8A_EINVAL, "null pointer");
+    f = FqIn{mx, qE, mbits, sign_bits};
+    fq_bias_kernel<<<1, 1, 0, s>>>(f, bias_out, ibias_out);
+    return hip_check("fp8a fused quantizer bias");
+}
+
+int fp8a_dense_conv2d_fused(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
+                            int64_t Cout, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw, int groups,
+                            int fmt, const float *in_maxval, int in_nbits, int in_mbits, int in_sign_bits,
+                            float *in_bias_out, int32_t *in_ibias_out, const float *res_maxval, int res_nbits,
+                            int res_mbits, int res_sign_bits, float *res_bias_out, int32_t *res_ibias_out,
+                            const float *bn, int act, float act_lo, float act_hi, const float *out_maxval,
+                            int out_nbits, int out_mbits, int out_sign_bits, float *out_bias_out,
+                            int32_t *out_ibias_out, void *workspace, size_t workspace_bytes, fp8a_stream_t stream) {
+    hipStream_t s = (hipStream_t)stream;
+    DnFuse fz{};
+    int rc = fused_quantizer(in_maxval, in_nbits, in_mbits, in_sign_bits, in_bias_out, in_ibias_out, fz.qin, s);
+    if (!rc) rc = fused_quantizer(res_maxval, res_nbits, res_mbits, res_sign_bits, res_bias_out, res_ibias_out, fz.rq, s);
+    if (!rc) rc = fused_quantizer(out_maxval, out_nbits, out_mbits, out_sign_bits, out_bias_out, out_ibias_out, fz.oq, s);
+    if (rc) return rc;
+    fz.ep = reinterpret_cast<const float2 *>(bn);
+    fz.act = act;
+    fz.lo = act_lo;
+    fz.hi = act_hi;
+    if (groups != 1)
+        return grouped_conv_impl(x, w, y, Bn, Cin, H, W, Cout, groups, kh, kw, sh, sw, ph, pw, dh, dw, fz, s);
+    if (kh < 1 || kw < 1 || sh < 1 || sw < 1 || dh < 1 || dw < 1 || ph < 0 || pw < 0 || Bn < 0 || Cin < 0 || Cout < 0)
+        return fail(FP8A_EINVAL, "bad convolution geometry");
+    const int64_t Ho = (H + 2 * ph - dh * (kh - 1) - 1) / sh + 1;
+    const int64_t Wo = (W + 2 * pw - dw * (kw - 1) - 1) / sw + 1;
+    if (Ho <= 0 || Wo <= 0) return fail(FP8A_EINVAL, "empty convolution output");
+    DenseArgs a = dense_args();
+    a.x = x; a.w = w; a.y = y; a.conv = 1;
+    a.C = Cin; a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo;
+    a.kh = kh; a.kw = kw; a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw; a.dh = dh; a.dw = dw;
+    a.M = Bn * Ho * Wo; a.N = Cout; a.K = Cin * kh * kw;
+    a.sbk = 1; a.sbn = a.K;
+    a.ldc = Cout; a.fmt = fmt;
+    a.fz = fz;
+    return run_dense(a, workspace, workspace_bytes, s);
 }
 
 }  // extern "C"

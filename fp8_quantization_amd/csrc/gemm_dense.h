@@ -28,6 +28,43 @@ constexpr int DN_KC = 128;           // k per LDS stage (one MFMA K-step)
 constexpr int DN_RS = DN_KC + 16;    // LDS row stride, bytes
 constexpr int DN_U = 64;             // fallback unit edge
 
+// The layer tail a config-1 (approx_flag off) BNFusedHijacker runs around its exact product,
+// fused into the product's loads and stores (fp8a_dense_conv2d_fused; quantized_folded_bn.py:
+// 30-83, hijacker.py:77-115): qin = the input's activation quantizer (quantize_input), applied
+// to every A value as it is loaded; then per output value rq (the res quantizer,
+// original_quantize_res), the eval batch norm as scale / shift of its channel, the clamp
+// activation, and oq (the output's activation quantizer when the layer does not quantize its
+// input).  Per-tensor FP8 quantizers (fp8_quantizer.py:97-173: fq_apply); any member off.
+struct DnFuse {
+    FqIn qin, rq, oq;
+    const float2 *ep;
+    int act;
+    float lo, hi;
+};
+struct DnQv {  // the quantizers' maxval and bias, read once per thread
+    float qmx, qb, rmx, rb, omx, ob;
+};
+__device__ __forceinline__ DnQv dn_qv(const DnFuse &f) {
+    DnQv q{};
+    if (f.qin.mx) { q.qmx = *f.qin.mx; q.qb = fq_bias(q.qmx, f.qin.E, f.qin.M); }
+    if (f.rq.mx) { q.rmx = *f.rq.mx; q.rb = fq_bias(q.rmx, f.rq.E, f.rq.M); }
+    if (f.oq.mx) { q.omx = *f.oq.mx; q.ob = fq_bias(q.omx, f.oq.E, f.oq.M); }
+    return q;
+}
+__device__ __forceinline__ float dn_in(const DnFuse &f, const DnQv &q, float v) {
+    return f.qin.mx ? fq_apply(v, q.qmx, q.qb, f.qin.M, f.qin.S) : v;
+}
+__device__ __forceinline__ float dn_out(const DnFuse &f, const DnQv &q, int64_t c, float v) {
+    if (f.rq.mx) v = fq_apply(v, q.rmx, q.rb, f.rq.M, f.rq.S);
+    if (f.ep) {
+        const float2 e = f.ep[c];
+        v = __fmaf_rn(v, e.x, e.y);
+        if (f.act) v = fminf(fmaxf(v, f.lo), f.hi);
+    }
+    if (f.oq.mx) v = fq_apply(v, q.omx, q.ob, f.oq.M, f.oq.S);
+    return v;
+}
+
 struct DenseArgs {
     const float *x;            // A: matmul element (m, k) at x[m * sam + k * sak]; conv: the NCHW input
     const float *w;            // B: element (k, n) at w[k * sbk + n * sbn]
@@ -41,6 +78,7 @@ struct DenseArgs {
     uint8_t *urow, *ucol;          // unit marks [mpad / 64], [npad / 64]
     uint32_t *anymark;             // 1 once any unit is marked
     int fmt;                       // FP8A_DENSE_E4M3 / FP8A_DENSE_E5M2 / FP8A_DENSE_BF16
+    DnFuse fz;                     // the fused layer tail (all off: the plain product)
 };
 
 __device__ unsigned long long g_dense[2];  // [0] launches with marked units, [1] units recomputed
@@ -52,13 +90,21 @@ __device__ __forceinline__ float dn_conv_elem(const DenseArgs &p, int64_t img, i
     return p.x[((img * p.C + c) * p.H + hi) * p.W + wi];
 }
 
-__device__ __forceinline__ float dn_a(const DenseArgs &p, int64_t m, int64_t k) {
+__device__ __forceinline__ float dn_a_raw(const DenseArgs &p, int64_t m, int64_t k) {
     if (!p.conv) return p.x[m * p.sam + k * p.sak];
     const int64_t hw = p.Ho * p.Wo, img = m / hw, pix = m - img * hw, ho = pix / p.Wo, wo = pix - ho * p.Wo;
     const int khw = p.kh * p.kw;
     const int64_t c = k / khw;
     const int t = (int)(k - c * khw), i = t / p.kw, j = t - i * p.kw;
     return dn_conv_elem(p, img, ho, wo, c, i, j);
+}
+// A(m, k) with the fused input quantizer (dn_pack / dn_fix: the rarely-run paths read its maxval
+// per element)
+__device__ __forceinline__ float dn_a(const DenseArgs &p, int64_t m, int64_t k) {
+    const float v = dn_a_raw(p, m, k);
+    if (!p.fz.qin.mx) return v;
+    const float mx = *p.fz.qin.mx;
+    return fq_apply(v, mx, fq_bias(mx, p.fz.qin.E, p.fz.qin.M), p.fz.qin.M, p.fz.qin.S);
 }
 
 // fp8 bytes of two floats (scale 1: the caller has applied the block scale) and back
@@ -267,6 +313,7 @@ __global__ __launch_bounds__(256, 2) void dn_gemm(const DenseArgs p) {
     }
     // lane (r16, g) holds D[4 g + r][r16] of each 16 x 16 block
     const int64_t hw = p.Ho * p.Wo;
+    const DnQv qv = dn_qv(p.fz);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -277,11 +324,11 @@ __global__ __launch_bounds__(256, 2) void dn_gemm(const DenseArgs p) {
                     const int64_t m = m0 + 64 * wr + 16 * i + r16, n = n0 + 64 * wc + 16 * j + 4 * g + r;
                     if (m < p.M && n < p.N) {
                         const int64_t img = m / hw, pix = m - img * hw;
-                        p.y[(img * p.N + n) * hw + pix] = acc[i][j][r];
+                        p.y[(img * p.N + n) * hw + pix] = dn_out(p.fz, qv, n, acc[i][j][r]);
                     }
                 } else {
                     const int64_t m = m0 + 64 * wr + 16 * i + 4 * g + r, n = n0 + 64 * wc + 16 * j + r16;
-                    if (m < p.M && n < p.N) p.y[m * p.ldc + n] = acc[i][j][r];
+                    if (m < p.M && n < p.N) p.y[m * p.ldc + n] = dn_out(p.fz, qv, n, acc[i][j][r]);
                 }
             }
 }
@@ -329,6 +376,7 @@ __global__ __launch_bounds__(256, 2) void dn_gemm_bf16(const DenseArgs p) {
     }
     const float *xrow = CONV ? p.x + img * p.C * p.H * p.W : p.x + (arow ? am : 0) * p.sam;
     const int khw = p.kh * p.kw;
+    const DnQv qv = dn_qv(p.fz);
     float ra[32];
     bool aok = true;
     auto load_a = [&](int64_t k0) {
@@ -349,6 +397,10 @@ __global__ __launch_bounds__(256, 2) void dn_gemm_bf16(const DenseArgs p) {
         } else {
 #pragma unroll
             for (int e = 0; e < 32; ++e) ra[e] = (arow && kb + e < p.K) ? xrow[(kb + e) * p.sak] : 0.0f;
+        }
+        if (p.fz.qin.mx) {  // the fused input quantizer (fq(0) = 0: padding unchanged)
+#pragma unroll
+            for (int e = 0; e < 32; ++e) ra[e] = dn_in(p.fz, qv, ra[e]);
         }
     };
     // B staging: thread = (column tid >> 1, 4 of the stage's 8 16-byte granules)
@@ -454,10 +506,10 @@ __global__ __launch_bounds__(256, 2) void dn_gemm_bf16(const DenseArgs p) {
             const int c = eq + 2 * q;  // the half's channel (conv) / row (matmul)
             if constexpr (CONV) {
                 const int64_t m = m0 + et, n = n0 + 64 * h + c;
-                if (m < p.M && n < p.N) p.y[(eimg * p.N + n) * hw + epix] = ct[c * CP + et];
+                if (m < p.M && n < p.N) p.y[(eimg * p.N + n) * hw + epix] = dn_out(p.fz, qv, n, ct[c * CP + et]);
             } else {
                 const int64_t m = m0 + 64 * h + c, n = n0 + et;
-                if (m < p.M && n < p.N) p.y[m * p.ldc + n] = ct[c * CP + et];
+                if (m < p.M && n < p.N) p.y[m * p.ldc + n] = dn_out(p.fz, qv, n, ct[c * CP + et]);
             }
         }
     }
@@ -495,6 +547,7 @@ __global__ __launch_bounds__(256) void dn_fix(const DenseArgs p) {
         __syncthreads();
     }
     const int64_t hw = p.Ho * p.Wo;
+    const DnQv qv = dn_qv(p.fz);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -503,9 +556,9 @@ __global__ __launch_bounds__(256) void dn_fix(const DenseArgs p) {
             if (m >= p.M || n >= p.N) continue;
             if (p.conv) {
                 const int64_t img = m / hw, pix = m - img * hw;
-                p.y[(img * p.N + n) * hw + pix] = acc[i][j];
+                p.y[(img * p.N + n) * hw + pix] = dn_out(p.fz, qv, n, acc[i][j]);
             } else {
-                p.y[m * p.ldc + n] = acc[i][j];
+                p.y[m * p.ldc + n] = dn_out(p.fz, qv, n, acc[i][j]);
             }
         }
     }
@@ -525,6 +578,7 @@ struct GcArgs {
     float *y;
     int64_t Cin, H, W, Cout, Ho, Wo, total;  // total = Bn Cout Ho ceil(Wo / GC_OW)
     int cig, cog, kh, kw, sh, sw, ph, pw, dh, dw;
+    DnFuse fz;                               // the fused layer tail (DenseArgs)
 };
 constexpr int GC_OW = 4;
 
@@ -533,6 +587,7 @@ __global__ __launch_bounds__(256) void dn_group_conv(const GcArgs p) {
     constexpr int SEG = KW > 0 ? (GC_OW - 1) * SW + KW : 1;
     const I wq = (I)((p.Wo + GC_OW - 1) / GC_OW), Ho = (I)p.Ho, Cout = (I)p.Cout;
     const int kh = p.kh, kw = KW > 0 ? KW : p.kw, sw = KW > 0 ? SW : p.sw;
+    const DnQv qv = dn_qv(p.fz);
     for (I t = (I)blockIdx.x * 256 + (I)threadIdx.x; t < (I)p.total; t += (I)gridDim.x * 256) {
         const I q = t % wq, r = t / wq, ho = r % Ho, plane = r / Ho;  // plane = image Cout + co
         const I co = plane % Cout, n = plane / Cout, c0 = (co / (I)p.cog) * (I)p.cig;
@@ -553,7 +608,7 @@ __global__ __launch_bounds__(256) void dn_group_conv(const GcArgs p) {
 #pragma unroll
                     for (int s = 0; s < SEG; ++s) {
                         const int64_t wi = wi0 + s;
-                        seg[s] = (hok && wi >= 0 && wi < p.W) ? xr[wi] : 0.0f;
+                        seg[s] = (hok && wi >= 0 && wi < p.W) ? dn_in(p.fz, qv, xr[wi]) : 0.0f;
                     }
 #pragma unroll
                     for (int kx = 0; kx < KW; ++kx) {
@@ -567,7 +622,7 @@ __global__ __launch_bounds__(256) void dn_group_conv(const GcArgs p) {
 #pragma unroll
                         for (int j = 0; j < GC_OW; ++j) {
                             const int64_t wi = wi0 + (int64_t)j * sw + (int64_t)kx * p.dw;
-                            acc[j] = __fmaf_rn((hok && wi >= 0 && wi < p.W) ? xr[wi] : 0.0f, wv, acc[j]);
+                            acc[j] = __fmaf_rn((hok && wi >= 0 && wi < p.W) ? dn_in(p.fz, qv, xr[wi]) : 0.0f, wv, acc[j]);
                         }
                     }
                 }
@@ -576,6 +631,6 @@ __global__ __launch_bounds__(256) void dn_group_conv(const GcArgs p) {
         float *yp = p.y + ((int64_t)plane * p.Ho + ho) * p.Wo;
 #pragma unroll
         for (int j = 0; j < GC_OW; ++j)
-            if (wo0 + j < p.Wo) yp[wo0 + j] = acc[j];
+            if (wo0 + j < p.Wo) yp[wo0 + j] = dn_out(p.fz, qv, co, acc[j]);
     }
 }

@@ -9,6 +9,11 @@ res_quantizer_flag, no original_quantize_res / qamaa -- the batch norm and a cla
 (ReLU / ReLU6 / Hardtanh) run inside the conv kernel's store instead of as two more passes over
 the output (fp8a_conv2d_bn_act).  ``fuse_bn_act = False`` on the class or instance, or
 FP8A_FUSE_BN=0 in the environment, keeps the unfused sequence.
+
+Config-1 form (round 4): with approx_flag off and original_quantize_res (BASELINE config 1's
+PTQ run) the whole layer -- input quantizer, exact product, res quantizer, eval batch norm, clamp,
+output quantizer -- runs as one fused exact convolution (fp8a_dense_conv2d_fused), leaving each
+quantizer the custom_bias its own forward would.
 """
 import os
 
@@ -42,6 +47,47 @@ class BNFusedHijacker(QuantizationHijacker):
                 or self.quantize_after_mult_and_add or not self.approx_flag or not self.res_quantizer_flag
                 or not getattr(self, "supports_bn_act_epilogue", False)):
             return None
+        return self._epilogue_params()
+
+    def _per_tensor_fp8(self, mgr):
+        """The FPQuantizer behind a fixed-range QuantizationManager with one maxval, else None."""
+        from .fp8_quantizer import FPQuantizer
+        from .quantization_manager import Qstates
+        q = getattr(mgr, "quantizer", None)
+        if getattr(mgr, "state", None) != Qstates.fix_ranges or not isinstance(q, FPQuantizer) or q.maxval.numel() != 1:
+            return None
+        return q
+
+    def _config1_fused(self, x):
+        """The plan of BASELINE config 1's layer (approx_flag off, original_quantize_res, eval, fixed
+        ranges) as one fused exact convolution (approx_ops.dense_conv2d_fused): (qin, rq, oq
+        FPQuantizers or None, bn epilogue, dense format), or None when the forward is not that form
+        (then the unfused sequence below runs)."""
+        if (not self.fuse_bn_act or self.training or not self.fix_ranges_flag or not self.original_quantize_res
+                or self.approx_flag or self.quantize_after_mult_and_add or not isinstance(self, _ConvNd)
+                or not getattr(self, "supports_bn_act_epilogue", False) or not x.is_cuda):
+            return None
+        from .. import approx_calculation as ac
+        from ..approx_ops import dense_format
+        if not ac.DENSE_EXACT or not (self._qw() and self._qa()):
+            return None
+        fmt = dense_format(self._approx_config()[1])
+        ep = self._epilogue_params()
+        if fmt is None or ep is None:
+            return None
+        aq = self._per_tensor_fp8(self.activation_quantizer)
+        if aq is None:
+            return None
+        qin = aq if self.quantize_input else None
+        rq = None
+        if self.quantize_input and self.res_quantizer_flag:
+            rq = self._per_tensor_fp8(self.res_quantizer)
+            if rq is None:
+                return None
+        oq = aq if not self.quantize_input else None
+        return qin, rq, oq, ep, fmt
+
+    def _epilogue_params(self):
         from ..approx_ops import bn_act_epilogue
         ts = (self.running_mean, self.running_var, self.gamma, self.beta)
         key = tuple((t._version, t.data_ptr(), t.device) for t in ts) + (self.epsilon, id(self.activation_function))
@@ -50,6 +96,19 @@ class BNFusedHijacker(QuantizationHijacker):
             cached = (key, bn_act_epilogue(*ts, self.epsilon, self.activation_function))
             self._bn_act_cache = cached
         return cached[1]
+
+    def _forward_config1_fused(self, x, plan):
+        from ..approx_ops import dense_conv2d_fused
+        qin, rq, oq, ep, fmt = plan
+        qt = lambda q: None if q is None else (q.maxval, q.n_bits, q._mbits_int, q.sign_bits)  # noqa: E731
+        weight, _ = self.get_params()
+        self._check_res_flag()
+        y, b = dense_conv2d_fused(x.detach(), weight.detach(), self.groups, self.stride, self.padding, self.dilation,
+                                  fmt, qin=qt(qin), rq=qt(rq), bn=ep, oq=qt(oq))
+        for name, q in (("qin", qin), ("rq", rq), ("oq", oq)):
+            if q is not None:
+                q.custom_bias = b[name]  # what the quantizer's own forward leaves (fp8_quantizer.py)
+        return y
 
     def block_epilogue_ok(self):
         """Whether forward(x, post=...) can fuse a residual block's tail: the fused BN / activation
@@ -63,6 +122,10 @@ class BNFusedHijacker(QuantizationHijacker):
         tail y = q(clamp(y + residual)) fused into the store (only when block_epilogue_ok()).
         chain: a model_wrap.WordChain (the word-image hand-off between consecutive convolutions);
         it only acts in the fused store, and records there whether the next image was emitted."""
+        if post is None:
+            plan = self._config1_fused(x)
+            if plan is not None:
+                return self._forward_config1_fused(x, plan)
         ep = self._fused_epilogue()
         if post is not None and not self.block_epilogue_ok():
             raise AssertionError("block epilogue requested where the fused store does not run")

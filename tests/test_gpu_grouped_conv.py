@@ -108,3 +108,45 @@ def test_exact_conv_module_routes_to_hip():
     assert _lib.path_stats(reset=True)["dense"] == 1
     ref = orig(x.cpu().double(), m.weight.detach().cpu().double(), m.bias.detach().cpu().double(), 1, 1, 1, 8)
     assert torch.allclose(y.cpu().double(), ref, atol=1e-5, rtol=1e-5)
+
+
+def _fma_bn(r, scale, shift):
+    return (r.double() * scale.double().view(1, -1, 1, 1) + shift.double().view(1, -1, 1, 1)).float()
+
+
+@pytest.mark.parametrize("groups,cin,cout,k,s", [(16, 16, 16, 3, 1), (24, 24, 24, 3, 2), (1, 8, 24, 1, 1), (1, 6, 10, 3, 2)])
+@pytest.mark.parametrize("order", ["in_res", "out"])
+def test_config1_fused_layer(groups, cin, cout, k, s, order):
+    """fp8a_dense_conv2d_fused (BASELINE config 1's layer in one pass) against its stages run
+    separately on the same kernels: fq_in (quantize_input) -> exact conv -> fq_res -> scale / shift
+    -> clamp, or conv -> scale / shift -> clamp -> fq_out; the biases are the quantizers' own."""
+    from fp8_quantization_amd.approx_ops import (dense_conv2d, dense_conv2d_fused, dense_format, fp8_fake_quantize,
+                                                 grouped_conv2d)
+    g = torch.Generator().manual_seed(groups + cin + cout + k + s)
+    x = (torch.randn(2, cin, 13, 13, generator=g) * 2).relu().to(DEV)
+    w = (torch.randn(cout, cin // groups, k, k, generator=g) * 0.3).to(DEV)
+    w, _ = fp8_fake_quantize(w, torch.tensor([2.0]), 8, 3)
+    scale = (torch.rand(cout, generator=g) + 0.5).to(DEV)
+    shift = (torch.randn(cout, generator=g) * 0.1).to(DEV)
+    ep = torch.stack((scale, shift), 1).contiguous()
+    mxi, mxr, mxo = torch.tensor([6.0], device=DEV), torch.tensor([40.0], device=DEV), torch.tensor([6.0], device=DEV)
+    pad = k // 2
+    conv = (lambda t: grouped_conv2d(t, w, groups, (s, s), (pad, pad))) if groups > 1 else \
+        (lambda t: dense_conv2d(t, w, dense_format(3), (s, s), (pad, pad)))
+    if order == "in_res":
+        y, b = dense_conv2d_fused(x, w, groups, (s, s), (pad, pad), qin=(mxi, 8, 3, 1), rq=(mxr, 8, 3, 1),
+                                  bn=(ep, 1, 0.0, 6.0))
+        xq, bi = fp8_fake_quantize(x, mxi, 8, 3)
+        r, br = fp8_fake_quantize(conv(xq), mxr, 8, 3)
+        ref = torch.clamp(_fma_bn(r, scale, shift), 0.0, 6.0)
+        assert torch.equal(b["qin"], bi) and torch.equal(b["rq"], br)
+    else:
+        y, b = dense_conv2d_fused(x, w, groups, (s, s), (pad, pad), bn=(ep, 1, 0.0, 6.0), oq=(mxo, 8, 3, 1))
+        r = conv(x)
+        ref, bo = fp8_fake_quantize(torch.clamp(_fma_bn(r, scale, shift), 0.0, 6.0), mxo, 8, 3)
+        assert torch.equal(b["oq"], bo)
+    # the scale / shift is one fma on both sides (float64 then float32 stands in for it); the sums
+    # of the two paths are the same kernels' -- equal but for rare double-rounding last bits
+    d = (y - ref).abs()
+    assert (d == 0).float().mean() > 0.999
+    assert torch.all(d <= 1e-6 * ref.abs() + 1e-12)
