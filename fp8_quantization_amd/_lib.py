@@ -70,10 +70,10 @@ def load():
                                F, F, P, I, I, I, P, P, P, I, F, F, P, I, I, I, P, P, P, SZ, P], I),
         "fp8a_word_image_bytes": ([I64, I64, I64, I64, I, I], SZ),
         "fp8a_word_image_init": ([P, I64, I64, I64, I64, I, I, P], I),
-        "fp8a_conv2d_wants_image": ([I64, I, I, I, I, I, I, I, P, U], I),
+        "fp8a_conv2d_wants_image": ([I64, I, I, I, I, I, I, I, P, U, I, I, I, I], I),
         "fp8a_conv2d_chain": ([P, P, P, I64, I64, I64, I64, I64, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P, U, P, I,
                                F, F, P, I, I, I, P, P, P, I, F, F, P, I, I, I, P, P, P, P, I, I, P, I, I, I, P, I,
-                               P, SZ, P], I),
+                               I, P, SZ, P], I),
         "fp8a_max_pool2d": ([P, P, I64, I64, I64, I64, I, I, I, I, I, I, P], I),
         "fp8a_im2col": ([P, P, I64, I64, I64, I64, I, I, I, I, I, I, I, I, P], I),
         "fp8a_fp8_quantize": ([P, I64, I64, P, I, I, I, I, P, P, P, P], I),

@@ -155,7 +155,7 @@ class ApproxConv2dMixin(ApproxOpMixin, ChainConsumerMixin):
                 raise TypeError("'NoneType' object is not subscriptable")
             args = dict(flags=flags, stride=self.stride, padding=self.padding, dilation=self.dilation,
                         groups=self.groups, epilogue=epilogue)
-            ch = chain.request(self, x, qin) if chain is not None and self.groups == 1 else None
+            ch = chain.request(self, x, qin) if chain is not None else None
             if ch is not None:
                 args["chain"] = ch
             if qin is not None or post is not None or ch is not None:

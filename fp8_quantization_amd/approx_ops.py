@@ -443,7 +443,7 @@ def _conv2d_chain_op(x: torch.Tensor, w: torch.Tensor, bA: Optional[torch.Tensor
                      out_image: Optional[torch.Tensor], next_ph: int, next_pw: int,
                      next_maxval: Optional[torch.Tensor], next_nbits: int, next_mbits: int, next_sign_bits: int,
                      next_bR: Optional[torch.Tensor], next_Mw: int, bn: Optional[torch.Tensor] = None, act: int = 0,
-                     act_lo: float = 0.0, act_hi: float = 0.0
+                     act_lo: float = 0.0, act_hi: float = 0.0, next_form: int = 0
                      ) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
     """fp8a_conv2d_chain: fp8a_conv2d_block that reads its input's word image (in_image) and / or
     emits the next convolution's (out_image); same results and return values as conv2d_block."""
@@ -466,7 +466,10 @@ def _conv2d_chain_op(x: torch.Tensor, w: torch.Tensor, bA: Optional[torch.Tensor
             raise AssertionError(f"approx_conv2d: residual must be float32 {tuple(y.shape)} on {x.device}")
     if bn is not None and (bn.shape != (Cout, 2) or bn.dtype != torch.float32 or not bn.is_contiguous()):
         raise AssertionError(f"approx_conv2d: epilogue parameters must be contiguous float32 [{Cout}, 2]")
-    for img, shp in ((in_image, (Bn, Cin, H, W, ph, pw)), (out_image, (Bn, Cout, Ho, Wo, next_ph, next_pw))):
+    # (a single-output-channel-group consumer reads table-form words: an image without border)
+    in_pad = (ph, pw) if groups == 1 else (0, 0)
+    out_pad = (next_ph, next_pw) if next_form == 0 else (0, 0)
+    for img, shp in ((in_image, (Bn, Cin, H, W) + in_pad), (out_image, (Bn, Cout, Ho, Wo) + out_pad)):
         if img is not None and img.numel() < L.fp8a_word_image_bytes(*shp):
             raise AssertionError("approx_conv2d: word image smaller than fp8a_word_image_bytes")
     ws = _workspace(x.device, L.fp8a_conv2d_block_workspace_size(Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh,
@@ -480,7 +483,7 @@ def _conv2d_chain_op(x: torch.Tensor, w: torch.Tensor, bA: Optional[torch.Tensor
                              opt(out_maxval), int(out_nbits), int(out_mbits), int(out_sign_bits), _lib.dev_ptr(ob),
                              _lib.dev_ptr(oib), opt(in_image), opt(out_image), int(next_ph), int(next_pw),
                              opt(next_maxval), int(next_nbits), int(next_mbits), int(next_sign_bits), opt(next_bR),
-                             int(next_Mw), _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(x.device))
+                             int(next_Mw), int(next_form), _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(x.device))
     _lib.check(rc, "fp8a_conv2d_chain")
     return y, ib, iib, ob, oib
 
@@ -489,7 +492,7 @@ def _conv2d_chain_op(x: torch.Tensor, w: torch.Tensor, bA: Optional[torch.Tensor
 def _(x, w, bA, bW, bR, table, E, M, flags, stride, padding, dilation, groups, in_maxval, in_nbits, in_mbits,
       in_sign_bits, res, post_act, post_lo, post_hi, out_maxval, out_nbits, out_mbits, out_sign_bits, in_image,
       out_image, next_ph, next_pw, next_maxval, next_nbits, next_mbits, next_sign_bits, next_bR, next_Mw, bn=None,
-      act=0, act_lo=0.0, act_hi=0.0):
+      act=0, act_lo=0.0, act_hi=0.0, next_form=0):
     Bn, _, H, W = x.shape
     Cout, _, kh, kw = w.shape
     Ho = (H + 2 * padding[0] - dilation[0] * (kh - 1) - 1) // stride[0] + 1
@@ -519,12 +522,14 @@ def new_word_image(Bn, C, H, W, ph, pw, device):
     return img
 
 
-def conv2d_wants_image(Cout, kernel, padding, groups, E, M, table, flags):
-    """fp8a_conv2d_wants_image: whether a convolution would read an input word image."""
+def conv2d_wants_image(Cout, kernel, padding, groups, E, M, table, flags, stride=(1, 1), dilation=(1, 1)):
+    """fp8a_conv2d_wants_image: the input word image a convolution would read -- 0 none, 1 the
+    matrix-core form (image of its padding), 2 the tensor-bias table form (image without border)."""
     tab = _table_host(table, M, _uses_table(flags))
-    return bool(_lib.load().fp8a_conv2d_wants_image(int(Cout), int(kernel[0]), int(kernel[1]), int(padding[0]),
-                                                    int(padding[1]), int(groups), int(E), int(M),
-                                                    _lib.host_ptr(tab), int(flags) & ~_lib.TB))
+    return int(_lib.load().fp8a_conv2d_wants_image(int(Cout), int(kernel[0]), int(kernel[1]), int(padding[0]),
+                                                   int(padding[1]), int(groups), int(E), int(M),
+                                                   _lib.host_ptr(tab), int(flags) & ~_lib.TB, int(stride[0]),
+                                                   int(stride[1]), int(dilation[0]), int(dilation[1])))
 
 
 def _quantizer_args(q):
@@ -582,18 +587,19 @@ def approx_conv2d(x, w, E, M, bA, bW, bR, table=None, flags=None, stride=(1, 1),
         if in_img is not None and qin is None:
             raise AssertionError("approx_conv2d: an input word image needs the fused input quantizer")
         if out is not None:
-            oimg, (nph, npw), nq, nbR, nM = out
+            oimg, (nph, npw), nq, nbR, nM = out[:5]
+            nform = out[5] if len(out) > 5 else 0
             nq = _quantizer_args(nq)
             nbR = _bias_dev(nbR, dev)
         else:
-            oimg, nph, npw, nq, nbR, nM = None, 0, 0, (None, 0, 0, 0), None, 0
+            oimg, nph, npw, nq, nbR, nM, nform = None, 0, 0, (None, 0, 0, 0), None, 0, 0
         y, ib, iib, ob, oib = _conv2d_chain_op(
             _as_f32(x), _as_f32(w), None if qin is not None else _bias_dev(bA, dev), bW_, _bias_dev(bR, dev), tab,
             int(E), int(M), int(flags), [int(s) for s in stride], [int(p) for p in padding],
             [int(d) for d in dilation], int(groups), iq[0].to(dev) if iq[0] is not None else None, iq[1], iq[2],
             iq[3], res, int(pact), float(plo), float(phi), oq[0].to(dev) if oq[0] is not None else None, oq[1],
             oq[2], oq[3], in_img, oimg, int(nph), int(npw), nq[0].to(dev) if nq[0] is not None else None, nq[1],
-            nq[2], nq[3], nbR, int(nM), *(epilogue or ()))
+            nq[2], nq[3], nbR, int(nM), *(epilogue or ()), next_form=int(nform))
         ib._fp8a_i32 = iib
         ob._fp8a_i32 = oib
         _prof_end(ev, y.shape[0] * y.shape[2] * y.shape[3] * w.shape[0] * w.shape[1] * w.shape[2] * w.shape[3])

@@ -37,16 +37,18 @@ class WordChain:
         in_img = self.in_image if qin is not None else None
         out = None
         nxt = self.next_layer
-        nq = nxt.chain_input_quantizer() if nxt is not None else None
-        if nq is not None and nxt.chain_wants_image():
+        # (only an ungrouped launch emits; single-output-channel-group layers only consume)
+        nq = nxt.chain_input_quantizer() if nxt is not None and layer.groups == 1 else None
+        form = nxt.chain_wants_image() if nq is not None else 0
+        if form:
             Bn, _, H, W = x.shape
             kh, kw = layer.kernel_size
             Ho = (H + 2 * layer.padding[0] - layer.dilation[0] * (kh - 1) - 1) // layer.stride[0] + 1
             Wo = (W + 2 * layer.padding[1] - layer.dilation[1] * (kw - 1) - 1) // layer.stride[1] + 1
             E, M, _, _ = nxt._approx_config()
-            img = nxt.chain_image((Bn, layer.out_channels, Ho, Wo), x.device)
+            img = nxt.chain_image((Bn, layer.out_channels, Ho, Wo), x.device, form)
             nbR = nxt._default_bias(nxt.get_res_fp_bias(), E, x.device)
-            out = (img, tuple(nxt.padding), (nq.maxval, nq.n_bits, nq._mbits_int, nq.sign_bits), nbR, M)
+            out = (img, tuple(nxt.padding), (nq.maxval, nq.n_bits, nq._mbits_int, nq.sign_bits), nbR, M, form - 1)
         if in_img is None and out is None:
             return None
         return in_img, out
@@ -66,22 +68,26 @@ class ChainConsumerMixin:
         return self._fused_input_quantizer(self._qa())
 
     def chain_wants_image(self):
+        """The input word image this layer's launch would read: 0 none, 1 the matrix-core form, 2 the
+        tensor-bias table form (single-output-channel groups; fp8a_conv2d_wants_image)."""
         E, M, table, flags = self._approx_config()
         key = (E, M, int(flags), tuple(table.reshape(-1).tolist()) if table is not None else None)
         cached = getattr(self, "_chain_wants", None)
         if cached is None or cached[0] != key:
             from .approx_ops import conv2d_wants_image
             cached = (key, conv2d_wants_image(self.out_channels, self.kernel_size, self.padding, self.groups, E, M,
-                                              table, flags))
+                                              table, flags, self.stride, self.dilation))
             self._chain_wants = cached
         return cached[1]
 
-    def chain_image(self, in_shape, device):
-        """This layer's input word image buffer (allocated and initialised once per shape)."""
-        key = (tuple(in_shape), tuple(self.padding), str(device))
+    def chain_image(self, in_shape, device, form=1):
+        """This layer's input word image buffer (allocated and initialised once per shape): with
+        this layer's padding as border (form 1), or none (form 2, the table form's plain words)."""
+        pad = tuple(self.padding) if form == 1 else (0, 0)
+        key = (tuple(in_shape), pad, str(device))
         cached = getattr(self, "_chain_img", None)
         if cached is None or cached[0] != key:
             from .approx_ops import new_word_image
-            cached = (key, new_word_image(*in_shape, self.padding[0], self.padding[1], device))
+            cached = (key, new_word_image(*in_shape, pad[0], pad[1], device))
             self._chain_img = cached
         return cached[1]

@@ -34,8 +34,11 @@ struct TbxArgs {
 // values / the exactness window (tensor-bias decode: every value at its own binade).
 // With fused input quantization (fq.mx set) the values are fq(x) and the quantizer's bias is
 // written to fq_bias / fq_ibias (the kernels' bA).
+// img_hdr: the header of a word image the producing launch emitted into `out` (fp8a_conv2d_chain):
+// nothing to decode unless it is flagged invalid (the quantizer's bias is still written).
 __global__ __launch_bounds__(256) void tbx_decode_a(const float *x, int64_t n, uint32_t *out, uint32_t *gate,
-                                                    FqIn fq, float *fq_bias_out, int32_t *fq_ibias_out, int M = 3) {
+                                                    FqIn fq, float *fq_bias_out, int32_t *fq_ibias_out, int M = 3,
+                                                    const uint32_t *img_hdr = nullptr) {
     const uint32_t lowm = (1u << (23 - M)) - 1u, mmask = (1u << M) - 1u;  // below the grid's mantissa / its bits
     bool bad = false;
     const float fmx = fq.mx ? *fq.mx : 0.0f, fbias = fq.mx ? fq_bias(fmx, fq.E, fq.M) : 0.0f;
@@ -43,6 +46,7 @@ __global__ __launch_bounds__(256) void tbx_decode_a(const float *x, int64_t n, u
         *fq_bias_out = fbias;
         *fq_ibias_out = (int32_t)fbias;
     }
+    if (img_hdr != nullptr && __hip_atomic_load(img_hdr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
     auto word = [&](float v) {
         if (fq.mx) v = fq_apply(v, fmx, fbias, fq.M, fq.S);
         const uint32_t u = __float_as_uint(v), ua = u & 0x7FFFFFFFu;

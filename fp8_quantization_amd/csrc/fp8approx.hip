@@ -134,6 +134,8 @@ struct EmitW {
     FqIn fq;            // the next convolution's input quantizer (per tensor)
     const int32_t *bR;  // its result bias
     int Mw;             // its mantissa width (3: e4m3 words, 2: e5m2)
+    int form;           // 0: gemm_f8mx_kernel's words (zero-bordered image); 1: the tensor-bias table
+                        // form's words (conv_tbx.h tbx_decode_a: a depthwise consumer, no border)
 };
 
 struct GemmArgs {
@@ -369,7 +371,13 @@ __device__ __forceinline__ EmitCtx emit_ctx(const GemmArgs &p) {
     return e;
 }
 __device__ __forceinline__ uint32_t emit_word(const GemmArgs &p, const EmitCtx &e, float v, bool &ok) {
-    return xm_word_a(fq_apply(v, e.mx, e.fb, p.em.fq.M, p.em.fq.S), p.em.Mw, xm_xbias(p.em.Mw), e.emn, e.bR, ok);
+    const float q = fq_apply(v, e.mx, e.fb, p.em.fq.M, p.em.fq.S);
+    if (p.em.form) {  // tbx_decode_a's word of q (a value off the grid / outside the window: invalid)
+        const uint32_t u = __float_as_uint(q), ua = u & 0x7FFFFFFFu, M = (uint32_t)p.em.Mw;
+        ok = ok && (ua == 0u || ((ua & ((1u << (23 - M)) - 1u)) == 0u && ua >= 0x20800000u && ua <= 0x58800000u));
+        return ua == 0u ? 0u : ((u & 0xFF800000u) | (((ua >> (23 - M)) & ((1u << M) - 1u)) << 6));
+    }
+    return xm_word_a(q, p.em.Mw, xm_xbias(p.em.Mw), e.emn, e.bR, ok);
 }
 // word index of NCHW output index o
 __device__ __forceinline__ uint32_t emit_index(const GemmArgs &p, uint32_t uo, uint32_t &wo) {
@@ -2486,11 +2494,14 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
             if (rc) return rc;
         } else if (tbx_ok) {
             gate = (uint32_t *)workspace;
-            uint32_t *aw = (uint32_t *)((char *)workspace + FLAG_BYTES);
+            // the input's table-form words from the producing launch (fp8a_conv2d_chain, next_form 1:
+            // header + [Bn][Cin][H][W] words of fq_in(x)); the pre-pass then runs gated on its header
+            const bool use_img = in_img != nullptr && fq.mx != nullptr;
+            uint32_t *aw = use_img ? const_cast<uint32_t *>(in_img) + 64 : (uint32_t *)((char *)workspace + FLAG_BYTES);
             if (hipMemsetAsync(gate, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a gate reset");
             const int64_t nx = Bn * Cin * H * W;
-            tbx_decode_a<<<(unsigned)std::min<int64_t>((nx + 255) / 256, 8192), 256, 0, s>>>(x, nx, aw, gate, fq, fqb,
-                                                                                                fqi, Mw);
+            tbx_decode_a<<<(unsigned)std::min<int64_t>((nx + 255) / 256, use_img ? 1024 : 8192), 256, 0, s>>>(
+                x, nx, aw, gate, fq, fqb, fqi, Mw, use_img ? in_img : nullptr);
             if (fq.mx) bA = fqi;
             TbxArgs ta;
             ta.Cin = Cin; ta.H = H; ta.W = W; ta.Cout = Cout; ta.Ho = Ho; ta.Wo = Wo;
@@ -2762,11 +2773,20 @@ int fp8a_word_image_init(void *image, int64_t Bn, int64_t C, int64_t H, int64_t 
 // pre-pass (not the fp32-staging form of 1x1 convolutions with few column tiles, not the tile-table
 // or VALU kernels), ungrouped, more than one output channel, a fused input quantizer.
 int fp8a_conv2d_wants_image(int64_t Cout, int kh, int kw, int ph, int pw, int groups, int E, int Mw,
-                            const int32_t *table, uint32_t flags) {
-    if (groups != 1 || Cout <= 1 || no_mx() || check_format(E, Mw) != FP8A_OK) return 0;
+                            const int32_t *table, uint32_t flags, int sh, int sw, int dh, int dw) {
+    if (Cout <= 1 || check_format(E, Mw) != FP8A_OK) return 0;
     TablePack tp;
     int mode;
     if (pack_table(table, Mw, (flags & F_APPROX) != 0, tp, mode) != FP8A_OK) return 0;
+    if (groups > 1 && Cout == groups) {  // single-output-channel groups: the table form's words
+        static const bool no_tbx = getenv("FP8A_NO_TBX") != nullptr;
+        const bool tbx = !no_tbx && g_opt_dwx == 0 && ((E == 4 && Mw == 3) || (E == 5 && Mw == 2)) &&
+                         (mode == TM_NONE || mode == TM_W1U) && (flags & F_S2N) && (flags & F_QBMA) &&
+                         !(flags & (F_GCLIP | F_V5)) && kw == 3 && dw == 1 && sh == sw && (sw == 1 || sw == 2);
+        (void)kh; (void)dh;
+        return tbx ? 2 : 0;
+    }
+    if (groups != 1 || no_mx()) return 0;
     if (!f8_form(E, Mw, flags & ~F_TB, mode) || g_opt_one_hot) return 0;
     if (kh == 1 && kw == 1 && ph == 0 && pw == 0) {  // xm_af32: fp32 staging up to af32_maxct column tiles
         const int64_t bnt = 16 * xm_ncg(Cout), ct = (Cout + bnt - 1) / bnt;
@@ -2784,7 +2804,7 @@ int fp8a_conv2d_chain(const float *x, const float *w, float *y, int64_t Bn, int6
                       int out_nbits, int out_mbits, int out_sign_bits, float *out_bias_out, int32_t *out_ibias_out,
                       const void *in_image, void *out_image, int next_ph, int next_pw, const float *next_maxval,
                       int next_nbits, int next_mbits, int next_sign_bits, const int32_t *next_bR, int next_Mw,
-                      void *workspace, size_t workspace_bytes, fp8a_stream_t stream) {
+                      int next_form, void *workspace, size_t workspace_bytes, fp8a_stream_t stream) {
     hipStream_t s = (hipStream_t)stream;
     if ((in_image && ((uintptr_t)in_image & 255)) || (out_image && ((uintptr_t)out_image & 255)))
         return fail(FP8A_EINVAL, "word images must be 256-byte aligned");
@@ -2813,7 +2833,9 @@ int fp8a_conv2d_chain(const float *x, const float *w, float *y, int64_t Bn, int6
         if (!next_maxval || !next_bR || next_mbits < 1 || qE < 1 || !(next_Mw == 2 || next_Mw == 3) || next_ph < 0 ||
             next_pw < 0)
             return fail(FP8A_EINVAL, "bad next-convolution parameters for the word image");
-        const WordImage wi = word_image(Ho, Wo, next_ph, next_pw);
+        if (next_form != 0 && next_form != 1) return fail(FP8A_EINVAL, "bad word image form");
+        // (the table form's words: the consumer's plain [Bn][C][Ho][Wo] layout, no border)
+        const WordImage wi = next_form ? word_image(Ho, Wo, 0, 0) : word_image(Ho, Wo, next_ph, next_pw);
         const bool can = groups == 1 && Cout > 1 && Ho > 0 && Wo > 0 && Bn * Cout * Ho * Wo < (1ll << 31) &&
                          Bn * Cout * wi.H * wi.W < (1ll << 30);
         // the header: valid (0) with the next quantizer's constants before this launch emits,
@@ -2833,6 +2855,7 @@ int fp8a_conv2d_chain(const float *x, const float *w, float *y, int64_t Bn, int6
             em.fq = FqIn{next_maxval, qE, next_mbits, next_sign_bits};
             em.bR = next_bR;
             em.Mw = next_Mw;
+            em.form = next_form;
         }
     }
     const size_t xq_bytes = fin.mx ? align256((size_t)(Bn * Cin * H * W) * sizeof(float)) : 0;

@@ -110,6 +110,14 @@ class BNFusedHijacker(QuantizationHijacker):
                 q.custom_bias = b[name]  # what the quantizer's own forward leaves (fp8_quantizer.py)
         return y
 
+    def _own_output_quantizer(self):
+        """This layer's activation FPQuantizer when it quantizes its OUTPUT (quantize_input off,
+        fixed ranges, per tensor) and the fused store can apply it (ungrouped, more than one
+        output channel per group -- the block tail's store), else None."""
+        if self.quantize_input or not self._qa() or self.out_channels // self.groups == 1:
+            return None
+        return self._per_tensor_fp8(self.activation_quantizer)
+
     def block_epilogue_ok(self):
         """Whether forward(x, post=...) can fuse a residual block's tail: the fused BN / activation
         store runs, the product is not a tensor-bias (single-output-channel) one, and nothing
@@ -130,6 +138,12 @@ class BNFusedHijacker(QuantizationHijacker):
         if post is not None and not self.block_epilogue_ok():
             raise AssertionError("block epilogue requested where the fused store does not run")
         if ep is not None:
+            own = self._own_output_quantizer() if post is None else None
+            if own is not None:
+                # the layer's own output quantizer (quantize_input off) in the store as well: the
+                # fused tail with no residual and no clamp, same fq_apply as its own forward
+                res, _ = self._core(x, epilogue=ep, post=(None, 0, 0.0, 0.0, own), chain=chain)
+                return res
             res, qa = self._core(x, epilogue=ep, post=post, chain=chain)
             return self._epilogue(res, qa, activation_done=True)
         res, qa = self._core(x)

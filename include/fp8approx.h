@@ -315,15 +315,19 @@ int fp8a_word_image_init(void *image, int64_t Bn, int64_t C, int64_t H, int64_t 
  *   out_image: NULL, or the NEXT convolution's input image to emit while y is stored: the words
  *             of next_fq(y) for a next convolution with padding next_ph / next_pw, input quantizer
  *             next_maxval (per tensor) / next_nbits / next_mbits / next_sign_bits, result bias
- *             next_bR and mantissa width next_Mw (3: E4M3, 2: E5M2).  y is written as well.
+ *             next_bR and mantissa width next_Mw (3: E4M3, 2: E5M2); next_form = the next
+ *             convolution's fp8a_conv2d_wants_image - 1 (0: matrix-core words in an image of
+ *             next_ph / next_pw; 1: table-form words, image of ph = pw = 0).  y is written as well.
  *             Where this call cannot emit (groups > 1, Cout == 1) the image is flagged invalid.
  * Results are bit-identical to the unchained calls.  workspace: fp8a_conv2d_block_workspace_size().
  */
-/* 1 when a convolution of this shape / format would read an in_image (the matrix-core path with its
- * A pre-pass: ungrouped, Cout > 1, E4M3 / E5M2 with s2n + qbma and a {0,1} or zero table, not a
- * 1x1 unpadded convolution staged from fp32), else 0: emitting an image for it would be wasted. */
+/* The word image a convolution of this shape / format would read as in_image: 1 = the matrix-core
+ * path's (ungrouped, Cout > 1, E4M3 / E5M2 with s2n + qbma and a {0,1} or zero table, not a 1x1
+ * unpadded convolution staged from fp32; images of its padding), 2 = the tensor-bias table form's
+ * (single-output-channel groups, 3-wide undilated rows, stride 1 / 2; images with ph = pw = 0),
+ * 0 = none: emitting an image for it would be wasted. */
 int fp8a_conv2d_wants_image(int64_t Cout, int kh, int kw, int ph, int pw, int groups, int E, int Mw,
-                            const int32_t *table, uint32_t flags);
+                            const int32_t *table, uint32_t flags, int sh, int sw, int dh, int dw);
 int fp8a_conv2d_chain(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H,
                       int64_t W, int64_t Cout, int kh, int kw, int sh, int sw, int ph, int pw, int dh,
                       int dw, int groups, int E, int Mw, const int32_t *bA, const int32_t *bW,
@@ -335,7 +339,8 @@ int fp8a_conv2d_chain(const float *x, const float *w, float *y, int64_t Bn, int6
                       float *out_bias_out, int32_t *out_ibias_out, const void *in_image,
                       void *out_image, int next_ph, int next_pw, const float *next_maxval,
                       int next_nbits, int next_mbits, int next_sign_bits, const int32_t *next_bR,
-                      int next_Mw, void *workspace, size_t workspace_bytes, fp8a_stream_t stream);
+                      int next_Mw, int next_form, void *workspace, size_t workspace_bytes,
+                      fp8a_stream_t stream);
 
 /*
  * A linear layer with its neighbours' elementwise work fused (QCustomLinearTorch.run_forward,

@@ -97,7 +97,8 @@ def test_bad_extent_maps_to_assertion_error():
 def test_word_image_queries_are_host_only():
     """fp8a_word_image_bytes / fp8a_conv2d_wants_image (the word-image hand-off,
     fp8a_conv2d_chain) are host logic: sizes of the zero-bordered image behind its 256-B header,
-    and which convolutions would read one (matrix-core path with its A pre-pass)."""
+    and which convolutions would read one (matrix-core path with its A pre-pass: 1; the depthwise
+    table form: 2)."""
     import torch
     L = _lib.load()
     # W % 4 == 0: left border widened to 4 words, rows rounded to a multiple of 4
@@ -107,8 +108,8 @@ def test_word_image_queries_are_host_only():
     fl = _lib.APPROX | _lib.S2N | _lib.QBMA
     z = torch.zeros((8, 8), dtype=torch.int32)
     z4 = torch.zeros((4, 4), dtype=torch.int32)
-    wants = lambda cout, k, p, g, E, M, t, f=fl: L.fp8a_conv2d_wants_image(  # noqa: E731
-        cout, k, k, p, p, g, E, M, _lib.host_ptr(t), f)
+    wants = lambda cout, k, p, g, E, M, t, f=fl, s=1: L.fp8a_conv2d_wants_image(  # noqa: E731
+        cout, k, k, p, p, g, E, M, _lib.host_ptr(t), f, s, s, 1, 1)
     assert wants(64, 3, 1, 1, 4, 3, z) == 1          # 3x3: the A pre-pass runs
     assert wants(64, 3, 1, 1, 5, 2, z4) == 1         # E5M2 too
     assert wants(64, 1, 0, 1, 4, 3, z) == 0          # 1x1, one column tile: staged from fp32
@@ -117,3 +118,8 @@ def test_word_image_queries_are_host_only():
     assert wants(1, 3, 1, 1, 4, 3, z) == 0           # one output channel: tensor-bias path
     assert wants(64, 3, 1, 1, 3, 4, torch.zeros((16, 16), dtype=torch.int32)) == 0  # E3M4: tile-table kernel
     assert wants(64, 3, 1, 1, 4, 3, z, _lib.APPROX | _lib.QBMA) == 0  # no s2n: not the matrix-core form
+    # single-output-channel groups (depthwise): the tensor-bias table form's words (form 2)
+    assert wants(64, 3, 1, 64, 4, 3, z) == 2
+    assert wants(64, 3, 1, 64, 5, 2, z4, s=2) == 2
+    assert wants(64, 5, 2, 64, 4, 3, z) == 0         # 5-wide rows: the general tensor-bias kernel
+    assert wants(64, 3, 1, 64, 3, 4, torch.zeros((16, 16), dtype=torch.int32)) == 0  # E3M4

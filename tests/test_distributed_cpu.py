@@ -7,6 +7,7 @@ import json
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -61,7 +62,9 @@ def _worker(rank, ws, port, q):
         broadcast_model_state(m, src=0)
         state = dict(w=m.weight.tolist(), count=m.count.tolist(), mask=m.mask.tolist(), wdev=str(holder.w.maxval.device),
                      wmax=holder.w.maxval.tolist(), wsign=holder.w.sign_bits)
-        q.put((rank, allg, topk_correct(allg, labels), float(holder.q.maxval[0]), (x @ w), state))
+        # (tensors by value: a shared-memory handle can outlive this process and fail to open)
+        q.put((rank, allg.numpy().copy(), topk_correct(allg, labels), float(holder.q.maxval[0]), (x @ w).numpy().copy(),
+               state))
     finally:
         dist.destroy_process_group()
 
@@ -90,7 +93,7 @@ def test_gloo_world2_gather_and_broadcast():
     res.sort(key=lambda t: t[0])
     full = res[0][4]
     for rank, allg, acc, mx, _, st in res:
-        assert torch.equal(allg, full)          # gathered logits == unsharded logits
+        assert np.array_equal(allg, full)       # gathered logits == unsharded logits
         assert mx == 1.0                        # rank 0's ranges everywhere
         assert acc == res[0][2]
         assert st["wdev"] == "cpu" and st["wmax"] == [[0.5], [2.0], [8.0]] and st["wsign"] == 0
