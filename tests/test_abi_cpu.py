@@ -118,8 +118,10 @@ def test_word_image_queries_are_host_only():
     assert wants(1, 3, 1, 1, 4, 3, z) == 0           # one output channel: tensor-bias path
     assert wants(64, 3, 1, 1, 3, 4, torch.zeros((16, 16), dtype=torch.int32)) == 0  # E3M4: tile-table kernel
     assert wants(64, 3, 1, 1, 4, 3, z, _lib.APPROX | _lib.QBMA) == 0  # no s2n: not the matrix-core form
-    # single-output-channel groups (depthwise): the tensor-bias table form's words (form 2)
-    assert wants(64, 3, 1, 64, 4, 3, z) == 2
-    assert wants(64, 3, 1, 64, 5, 2, z4, s=2) == 2
+    # single-output-channel groups (depthwise): the table form's words (form 2) only with
+    # FP8A_CHAIN_TBX=1 (measured a net loss on MobileNetV2)
+    tbx = 2 if os.environ.get("FP8A_CHAIN_TBX", "0") not in ("", "0") else 0
+    assert wants(64, 3, 1, 64, 4, 3, z) == tbx
+    assert wants(64, 3, 1, 64, 5, 2, z4, s=2) == tbx
     assert wants(64, 5, 2, 64, 4, 3, z) == 0         # 5-wide rows: the general tensor-bias kernel
     assert wants(64, 3, 1, 64, 3, 4, torch.zeros((16, 16), dtype=torch.int32)) == 0  # E3M4
