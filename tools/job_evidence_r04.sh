@@ -11,7 +11,7 @@ declare -A SPEC=(
   [c3_mbv2_e5m2_v9]="gemm_f8mx_kernel mobilenet_v2 5 2 512"
   [c4_vit_b16]="gemm_f8mx_kernel vit_b16 4 3 64"
   [c5_r50_e5m2]="gemm_f8mx_kernel resnet50 5 2 512"
-  [c2_r18_e4m3]="gemm_f8mx_kernel resnet18 4 3 512"
+  [c2_r18_e4m3]="gemm_f8mx_kernel resnet18 4 3 1024"
   [mbv2_e4m3]="gemm_f8mx_kernel mobilenet_v2 4 3 512"
   [c5_r50_e4m3]="gemm_f8mx_kernel resnet50 4 3 512"
 )
