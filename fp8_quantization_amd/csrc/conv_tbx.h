@@ -168,290 +168,9 @@ __global__ __launch_bounds__(256) void conv_tbx_kernel(const uint32_t *aw, const
     if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(gate, 1u);
 }
 
-// ---------------------------------------------------------------------------------------------
-// conv_dwx_kernel: the same table-form terms as conv_tbx_kernel for depthwise convolutions (one
-// input and one output channel per group), reading the fp32 input directly.  Measured on
-// MobileNetV2 (round 3, batch 512): tbx_decode_a + conv_tbx_kernel took 11.2 ms of a 29.5 ms
-// forward -- the word image costs a full write + re-read of every expanded activation, and the
-// per-thread global gathers of conv_tbx_kernel (4-B loads at a 16-B lane stride, per-lane weight
-// loads) ran at ~1 T terms/s.  Here a workgroup owns a BAND: NP (image, channel) planes x TH
-// output rows.  Its input rows (fp32, coalesced along W) are quantized (fused input quantizer),
-// decoded to the same words and staged ONCE in LDS inside a zero border; the plane's 3 x kh taps
-// are decoded once per workgroup into LDS; each thread then computes 4 consecutive outputs of one
-// row from LDS words (6 / 9 word reads per kernel row for stride 1 / 2) in conv_tbx_kernel's
-// order (ky, kx), so the sums are bit-identical to it.  The gate word and the gated exact kernel
-// behind it are unchanged.
-struct DwxArgs {
-    int64_t planes;                 // Bn * C
-    int32_t C, H, W, Ho, Wo, kh, ph, pw, dh;
-    int32_t TH, NP, RG, bands;      // band: NP planes x TH = 4 RG output rows (RG row groups of 4)
-    int32_t IR, IC;                 // staged input rows / columns per plane
-    uint32_t ic_mul, ic_shift;      // fastdiv by IC
-    uint32_t ir_mul, ir_shift;      // fastdiv by IR
-    uint32_t tg_mul, tg_shift;      // fastdiv by RG * Wo (threads per plane)
-    uint32_t ng_mul, ng_shift;      // fastdiv by Wo
-};
-constexpr int DWX_LDS_WORDS = 4096;  // staged words per workgroup (16 KiB: >= 8 workgroups / CU; host-checked)
-
-template <int SW>
-__global__ __launch_bounds__(256) void conv_dwx_kernel(const float *x, const float *w, float *y, DwxArgs t,
-                                                       const int32_t *bA, const int32_t *bW, const int32_t *bR,
-                                                       TablePack tab, uint32_t *gate, const float2 *ep, int ep_act,
-                                                       float ep_lo, float ep_hi, FqIn fq, float *fq_bias_out,
-                                                       int32_t *fq_ibias_out) {
-    constexpr int KW = 3;
-    __shared__ float2 sL[64];
-    // dynamic LDS: the staged words [NP][IR][IC], then per plane and tap (c_b bits, m_b << 3)
-    extern __shared__ __attribute__((aligned(16))) uint32_t dwx_smem[];
-    uint32_t *const sA = dwx_smem;
-    uint2 *const sW = reinterpret_cast<uint2 *>(dwx_smem + ((t.NP * t.IR * t.IC + 1) & ~1));
-    const int tid = threadIdx.x;
-    const float fmx = fq.mx ? *fq.mx : 0.0f, fbias = fq.mx ? fq_bias(fmx, fq.E, fq.M) : 0.0f;
-    const int a_b = fq.mx ? (int)fbias : *bA, r_b = *bR;
-    if (fq.mx && blockIdx.x == 0 && tid == 0) {
-        *fq_bias_out = fbias;
-        *fq_ibias_out = a_b;
-    }
-    bool bad = !(a_b >= 2 && a_b <= 120 && r_b >= 2 && r_b <= 120);
-    if (tid < 64) {  // the table, as conv_tbx_kernel
-        const int ma = tid >> 3, mb = tid & 7;
-        const float u = (1.0f + 0.125f * ma) * (1.0f + 0.125f * mb);
-        const float v = __fmaf_rn(1.0f + 0.125f * ma, 1.0f + 0.125f * mb, -0.125f * (float)tab.raw[ma * 8 + mb]);
-        const float pe = __uint_as_float(__float_as_uint(v) & 0x7F800000u);
-        const float xs = fminf(v, pe * (1.875f - p2(-22))), cc = pe * 1048576.0f * 1.5f;
-        const float L = (xs + cc) - cc;
-        uint32_t f7 = 0xFFFFFFFFu;
-        if (u <= 1.0625f) f7 = 0x80000000u | ((uint32_t)(127 - r_b) << 23);
-        else if (u >= 2.0f && u <= 2.125f) f7 = 0x80000000u | ((uint32_t)(126 - r_b) << 23);
-        sL[tid] = make_float2(L, __uint_as_float(f7));
-    }
-    const int64_t band = blockIdx.x % (uint32_t)t.bands, pg = blockIdx.x / (uint32_t)t.bands;
-    const int64_t plane0 = pg * t.NP;
-    const int ho0 = (int)band * t.TH;
-    const int hi0 = ho0 * SW - t.ph;
-    const int64_t HW = (int64_t)t.H * t.W;
-    // taps: decoded once per workgroup (bad weight / weight bias -> gate)
-    const int ntap = t.NP * t.kh * KW;
-    for (int e = tid; e < ntap; e += 256) {
-        const int p = e / (t.kh * KW), tap = e - p * (t.kh * KW);
-        const int64_t pl = min(plane0 + p, t.planes - 1);
-        const int co = (int)(pl % t.C);
-        const int wb = bW[co];
-        const uint32_t bw = __float_as_uint(w[(int64_t)co * t.kh * KW + tap]), bwa = bw & 0x7FFFFFFFu;
-        bad |= !(wb >= 2 && wb <= 120);
-        bad |= (bwa != 0u) && ((bwa & 0xFFFFFu) != 0u || bwa < 0x20800000u || bwa > 0x58800000u);
-        sW[e] = make_uint2(bw & 0xFF800000u, ((bwa >> 20) & 7u) << 3);
-    }
-    // input band: NP planes x IR rows x IC columns of words, zero outside the image.  All of a
-    // thread's loads are issued before any is used (a load -> LDS store loop waits on each load
-    // in turn; the band's few loads per thread are latency, not bandwidth).
-    const uint32_t nst = (uint32_t)(t.NP * t.IR * t.IC);
-    constexpr int SMAX = DWX_LDS_WORDS / 256;
-    float sv[SMAX];
-    bool sin[SMAX];
-#pragma unroll
-    for (int j = 0; j < SMAX; ++j) {
-        const uint32_t s = tid + 256u * j;
-        sin[j] = false;
-        sv[j] = 0.0f;
-        if (s < nst) {
-            const uint32_t row = fastdiv(s, t.ic_mul, t.ic_shift), col = s - row * (uint32_t)t.IC;
-            const uint32_t p = fastdiv(row, t.ir_mul, t.ir_shift), ir = row - p * (uint32_t)t.IR;
-            const int hi = hi0 + (int)ir, wi = (int)col - t.pw;
-            const int64_t pl = plane0 + p;
-            sin[j] = pl < t.planes && (uint32_t)hi < (uint32_t)t.H && (uint32_t)wi < (uint32_t)t.W;
-            if (sin[j]) sv[j] = x[pl * HW + (int64_t)hi * t.W + wi];
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < SMAX; ++j) {
-        const uint32_t s = tid + 256u * j;
-        if (s < nst) {
-            uint32_t word = 0u;
-            if (sin[j]) {
-                float v = sv[j];
-                if (fq.mx) v = fq_apply(v, fmx, fbias, fq.M, fq.S);
-                const uint32_t u = __float_as_uint(v), ua = u & 0x7FFFFFFFu;
-                bad |= (ua != 0u) && ((ua & 0xFFFFFu) != 0u || ua < 0x20800000u || ua > 0x58800000u);
-                word = ua == 0u ? 0u : ((u & 0xFF800000u) | (((ua >> 20) & 7u) << 6));
-            }
-            sA[s] = word;
-        }
-    }
-    __syncthreads();
-    const uint32_t q0exp = (uint32_t)(127 - r_b) << 23;
-    const float twoq = __uint_as_float((uint32_t)(128 - r_b) << 23);
-    const char *lut = reinterpret_cast<const char *>(sL);
-    // thread -> (plane p, row group rg of 4 output rows, output column c): consecutive lanes on
-    // consecutive columns, so the LDS word reads are conflict-free (stride SW words across lanes;
-    // a row-wise 4-outputs-per-thread mapping read at a 4 SW-word lane stride: 4- / 8-way bank
-    // conflicts, measured 1.4-1.6x slower than conv_tbx_kernel)
-    const uint32_t p = fastdiv((uint32_t)tid, t.tg_mul, t.tg_shift), rem = (uint32_t)tid - p * (uint32_t)(t.RG * t.Wo);
-    const uint32_t rg = fastdiv(rem, t.ng_mul, t.ng_shift), c = rem - rg * (uint32_t)t.Wo;
-    const int64_t pl = plane0 + p;
-    const int hob = ho0 + 4 * (int)rg;
-    if ((int)p < t.NP && pl < t.planes && hob < t.Ho) {
-        constexpr int NR = (TBX_TW - 1) * SW + KW;  // input rows of 4 output rows (kh = 3, dh = 1)
-        const uint32_t *pa = sA + ((int)p * t.IR + 4 * (int)rg * SW) * t.IC + (int)c * SW;
-        uint32_t wd[NR][KW];
-#pragma unroll
-        for (int i = 0; i < NR; ++i)
-#pragma unroll
-            for (int kx = 0; kx < KW; ++kx) wd[i][kx] = pa[i * t.IC + kx];
-        const uint2 *pw8 = sW + (int)p * KW * KW;
-        float acc[TBX_TW] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-        for (int ky = 0; ky < KW; ++ky) {
-#pragma unroll
-            for (int kx = 0; kx < KW; ++kx) {
-                const uint2 tw = pw8[ky * KW + kx];
-                const float cB = __uint_as_float(tw.x);
-                const uint32_t mb8 = tw.y;
-#pragma unroll
-                for (int q = 0; q < TBX_TW; ++q) {  // (ky, kx) order per output, as conv_tbx_kernel
-                    const uint32_t wa = wd[q * SW + ky][kx];
-                    const float2 e = *reinterpret_cast<const float2 *>(lut + ((wa & 0x1C0u) | mb8));
-                    const float cab = __uint_as_float(wa & 0xFF800000u) * cB;  // exact
-                    float v = e.x * cab;                                         // exact
-                    const float rs = __fmaf_rn(2.0f, v, -copysignf(twoq, v));    // expo field 0
-                    v = ((__float_as_uint(v) & 0x7F800000u) == q0exp) ? rs : v;
-                    v = (__float_as_uint(cab) == __float_as_uint(e.y)) ? fabsf(v) : v;  // F7
-                    acc[q] += v;
-                }
-            }
-        }
-        const int co = (int)(pl % t.C);
-        float *yc = y + (pl * t.Ho + hob) * (int64_t)t.Wo + c;
-#pragma unroll
-        for (int q = 0; q < TBX_TW; ++q)
-            if (hob + q < t.Ho) yc[(int64_t)q * t.Wo] = epi(ep, ep_act, ep_lo, ep_hi, co, acc[q]);
-    }
-    if (__syncthreads_or(bad ? 1 : 0) && tid == 0) atomicOr(gate, 1u);
-}
-
-// ---------------------------------------------------------------------------------------------
-// conv_dwg_kernel: the same terms again, as a grid-stride gather that reads the fp32 input
-// directly (no word image, no LDS staging).  Counters on MobileNetV2 (batch 512, SQ_* / wave
-// cycles): conv_tbx_kernel waits 66 % of its cycles with the VALU 12.5 % busy -- it is bound by
-// its gathers (4-B loads at a 16-B lane stride from the word image that tbx_decode_a wrote: a
-// full extra write + read of every expanded activation, 3 ms per forward), not by the ~13
-// operations per term.  Here a thread owns one output COLUMN and 4 consecutive rows (consecutive
-// lanes on consecutive columns: every load instruction covers contiguous bytes), loads its
-// (3 SW + 3) x 3 input window as fp32, applies the fused input quantizer and the word decode per
-// loaded value (spare VALU time), and sums the terms in conv_tbx_kernel's (ky, kx) order, so the
-// outputs are bit-identical to it.  The gate and the gated exact kernel are unchanged.
-struct DwgArgs {
-    int32_t C, H, W, Ho, Wo, ph, pw, RGn;  // RGn: row groups of 4 output rows per plane
-    uint32_t items;                        // planes * RGn * Wo
-    uint32_t wo_mul, wo_shift, rg_mul, rg_shift;
-};
-
-// WORDS: read the word image tbx_decode_a wrote (x is then that image, reinterpreted) instead of
-// the fp32 input -- the column mapping's contiguous loads without the per-load decode.
-template <int SW, bool WORDS>
-__global__ __launch_bounds__(256) void conv_dwg_kernel(const float *x, const float *w, float *y, DwgArgs t,
-                                                       const int32_t *bA, const int32_t *bW, const int32_t *bR,
-                                                       TablePack tab, uint32_t *gate, const float2 *ep, int ep_act,
-                                                       float ep_lo, float ep_hi, FqIn fq, float *fq_bias_out,
-                                                       int32_t *fq_ibias_out) {
-    constexpr int KW = 3, NR = (TBX_TW - 1) * SW + KW;
-    __shared__ float2 sL[64];
-    const int tid = threadIdx.x;
-    const float fmx = (!WORDS && fq.mx) ? *fq.mx : 0.0f, fbias = (!WORDS && fq.mx) ? fq_bias(fmx, fq.E, fq.M) : 0.0f;
-    const int a_b = (!WORDS && fq.mx) ? (int)fbias : *bA, r_b = *bR;
-    if (!WORDS && fq.mx && blockIdx.x == 0 && tid == 0) {
-        *fq_bias_out = fbias;
-        *fq_ibias_out = a_b;
-    }
-    bool bad = !(a_b >= 2 && a_b <= 120 && r_b >= 2 && r_b <= 120);
-    if (tid < 64) {  // the table, as conv_tbx_kernel
-        const int ma = tid >> 3, mb = tid & 7;
-        const float u = (1.0f + 0.125f * ma) * (1.0f + 0.125f * mb);
-        const float v = __fmaf_rn(1.0f + 0.125f * ma, 1.0f + 0.125f * mb, -0.125f * (float)tab.raw[ma * 8 + mb]);
-        const float pe = __uint_as_float(__float_as_uint(v) & 0x7F800000u);
-        const float xs = fminf(v, pe * (1.875f - p2(-22))), cc = pe * 1048576.0f * 1.5f;
-        const float L = (xs + cc) - cc;
-        uint32_t f7 = 0xFFFFFFFFu;
-        if (u <= 1.0625f) f7 = 0x80000000u | ((uint32_t)(127 - r_b) << 23);
-        else if (u >= 2.0f && u <= 2.125f) f7 = 0x80000000u | ((uint32_t)(126 - r_b) << 23);
-        sL[tid] = make_float2(L, __uint_as_float(f7));
-    }
-    __syncthreads();
-    const uint32_t q0exp = (uint32_t)(127 - r_b) << 23;
-    const float twoq = __uint_as_float((uint32_t)(128 - r_b) << 23);
-    const char *lut = reinterpret_cast<const char *>(sL);
-    const int64_t HW = (int64_t)t.H * t.W;
-    for (uint32_t item = blockIdx.x * 256u + tid; item < t.items; item += gridDim.x * 256u) {
-        const uint32_t r1 = fastdiv(item, t.wo_mul, t.wo_shift), c = item - r1 * (uint32_t)t.Wo;
-        const uint32_t pl = fastdiv(r1, t.rg_mul, t.rg_shift), rg = r1 - pl * (uint32_t)t.RGn;
-        const int co = (int)(pl % (uint32_t)t.C);
-        const int hob = 4 * (int)rg, hi0 = hob * SW - t.ph, wi0 = (int)c * SW - t.pw;
-        // taps (one channel per plane: lanes of a plane load the same 9 words)
-        const int wb = bW[co];
-        bad |= !(wb >= 2 && wb <= 120);
-        uint32_t tc[KW * KW], tm[KW * KW];
-#pragma unroll
-        for (int k = 0; k < KW * KW; ++k) {
-            const uint32_t bw = __float_as_uint(w[co * KW * KW + k]), bwa = bw & 0x7FFFFFFFu;
-            bad |= (bwa != 0u) && ((bwa & 0xFFFFFu) != 0u || bwa < 0x20800000u || bwa > 0x58800000u);
-            tc[k] = bw & 0xFF800000u;
-            tm[k] = ((bwa >> 20) & 7u) << 3;
-        }
-        // the input window, fp32 -> (fused quantizer) -> words; zero outside the image
-        const float *xp = x + (int64_t)pl * HW;
-        float xv[NR][KW];
-#pragma unroll
-        for (int i = 0; i < NR; ++i) {
-            const int hi = hi0 + i;
-            const bool rok = (uint32_t)hi < (uint32_t)t.H;
-#pragma unroll
-            for (int kx = 0; kx < KW; ++kx) {
-                const int wi = wi0 + kx;
-                xv[i][kx] = (rok && (uint32_t)wi < (uint32_t)t.W) ? xp[(int64_t)hi * t.W + wi] : 0.0f;
-            }
-        }
-        uint32_t wd[NR][KW];
-#pragma unroll
-        for (int i = 0; i < NR; ++i)
-#pragma unroll
-            for (int kx = 0; kx < KW; ++kx) {
-                if (WORDS) {  // (checked by tbx_decode_a)
-                    wd[i][kx] = __float_as_uint(xv[i][kx]);
-                    continue;
-                }
-                float v = xv[i][kx];
-                if (fq.mx) v = fq_apply(v, fmx, fbias, fq.M, fq.S);
-                const uint32_t u = __float_as_uint(v), ua = u & 0x7FFFFFFFu;
-                bad |= (ua != 0u) && ((ua & 0xFFFFFu) != 0u || ua < 0x20800000u || ua > 0x58800000u);
-                wd[i][kx] = ua == 0u ? 0u : ((u & 0xFF800000u) | (((ua >> 20) & 7u) << 6));
-            }
-        float acc[TBX_TW] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-        for (int ky = 0; ky < KW; ++ky) {
-#pragma unroll
-            for (int kx = 0; kx < KW; ++kx) {
-                const float cB = __uint_as_float(tc[ky * KW + kx]);
-                const uint32_t mb8 = tm[ky * KW + kx];
-#pragma unroll
-                for (int q = 0; q < TBX_TW; ++q) {  // (ky, kx) order per output, as conv_tbx_kernel
-                    const uint32_t wa = wd[q * SW + ky][kx];
-                    const float2 e = *reinterpret_cast<const float2 *>(lut + ((wa & 0x1C0u) | mb8));
-                    const float cab = __uint_as_float(wa & 0xFF800000u) * cB;  // exact
-                    float v = e.x * cab;                                         // exact
-                    const float rs = __fmaf_rn(2.0f, v, -copysignf(twoq, v));    // expo field 0
-                    v = ((__float_as_uint(v) & 0x7F800000u) == q0exp) ? rs : v;
-                    v = (__float_as_uint(cab) == __float_as_uint(e.y)) ? fabsf(v) : v;  // F7
-                    acc[q] += v;
-                }
-            }
-        }
-        float *yc = y + ((int64_t)pl * t.Ho + hob) * t.Wo + c;
-#pragma unroll
-        for (int q = 0; q < TBX_TW; ++q)
-            if (hob + q < t.Ho) yc[(int64_t)q * t.Wo] = epi(ep, ep_act, ep_lo, ep_hi, co, acc[q]);
-    }
-    if (__syncthreads_or(bad ? 1 : 0) && tid == 0) atomicOr(gate, 1u);
-}
+// (round 3's alternative depthwise forms conv_dwx_kernel -- band-staged in LDS -- and
+// conv_dwg_kernel -- an fp32 gather -- measured slower than conv_tbx_kernel and were
+// removed in round 4.)
 
 // ---------------------------------------------------------------------------------------------
 // conv_v5dw_kernel: the v5 integer-adder model's depthwise convolutions (BASELINE config 3 with

@@ -1510,11 +1510,6 @@ static bool g_opt_one_hot = getenv("FP8A_ONE_HOT") != nullptr && atoi(getenv("FP
 // "oh_correct" (diagnostics): 0 skips the one-hot path's correction kernel (dense terms only)
 static bool g_opt_oh_correct = true;
 static bool g_opt_oh_stats = false;  // "oh_stats": the one-hot kernels count into g_ohstat
-// "dwx": the E4M3 depthwise form -- 0 the word-image gather conv_tbx_kernel (+ tbx_decode_a),
-// 1 the band-staged conv_dwx_kernel (measured 1.3x slower on MobileNetV2), 2 the
-// fp32 gather conv_dwg_kernel (5 % slower), 3 conv_dwg_kernel's column mapping over
-// tbx_decode_a's word image.  FP8A_DW=<n> sets it at load.
-static int g_opt_dwx = getenv("FP8A_DW") ? atoi(getenv("FP8A_DW")) : 0;
 // "tbx_rw": output rows per thread of conv_tbx_kernel (1 or 2; 2 needs undilated rows).
 // FP8A_TBX_RW=<n> sets it at load.
 static int g_opt_tbx_rw = getenv("FP8A_TBX_RW") ? atoi(getenv("FP8A_TBX_RW")) : 2;
@@ -2091,11 +2086,6 @@ int fp8a_set_option(const char *name, int value) {
         g_opt_af32_maxct = std::max(0, value);
         return old;
     }
-    if (strcmp(name, "dwx") == 0) {
-        const int old = g_opt_dwx;
-        g_opt_dwx = value;
-        return old;
-    }
     if (strcmp(name, "tbx_rw") == 0) {
         const int old = g_opt_tbx_rw;
         g_opt_tbx_rw = value;
@@ -2341,42 +2331,6 @@ int fp8a_conv2d(const float *x, const float *w, float *y, int64_t Bn, int64_t Ci
 // (fp8_quantizer.py:97-173, per tensor) is applied inside the matrix-core / tensor-bias-table
 // pre-decodes (its bias written to fqb / fqi, which serve as bA), or -- for every other path --
 // into xq (numel(x) floats) by one fake-quant pass first.
-// Band shape of conv_dwx_kernel: NP planes x RG row groups of 4 output rows per 256-thread
-// workgroup, one thread per output column and row group; the shape maximises the fraction of busy
-// threads (rows past Ho in the last band, threads past NP * RG * Wo) within the LDS budget.
-static bool dwx_config(int64_t planes, int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo, int kh, int S, int ph,
-                       int pw, int dh, DwxArgs &d) {
-    if (kh != 3 || dh != 1 || Wo > 256 || H >= (1 << 30) || W >= (1 << 30)) return false;
-    const int IC = (int)(Wo - 1) * S + 3;
-    double best = 0.0;
-    int brg = 0, bnp = 0;
-    for (int rg = 1; rg * Wo <= 256 && 4 * (rg - 1) < Ho; ++rg) {
-        const int IR = (4 * rg - 1) * S + 3;
-        for (int np = 1; np * rg * Wo <= 256; ++np) {
-            if ((int64_t)np * IR * IC > DWX_LDS_WORDS) break;
-            const int64_t bands = (Ho + 4 * rg - 1) / (4 * rg);
-            const double eff = (double)Ho / (double)(bands * 4 * rg) * (double)(np * rg * Wo) / 256.0;
-            if (eff > best + 1e-9) {
-                best = eff;
-                brg = rg;
-                bnp = np;
-            }
-        }
-    }
-    if (brg == 0) return false;
-    d.planes = planes;
-    d.C = (int32_t)C; d.H = (int32_t)H; d.W = (int32_t)W; d.Ho = (int32_t)Ho; d.Wo = (int32_t)Wo;
-    d.kh = kh; d.ph = ph; d.pw = pw; d.dh = dh;
-    d.RG = brg; d.TH = 4 * brg; d.NP = bnp;
-    d.bands = (int32_t)((Ho + d.TH - 1) / d.TH);
-    d.IR = (d.TH - 1) * S + 3;
-    d.IC = IC;
-    fastdiv_params((uint32_t)d.IC, d.ic_mul, d.ic_shift);
-    fastdiv_params((uint32_t)d.IR, d.ir_mul, d.ir_shift);
-    fastdiv_params((uint32_t)(brg * Wo), d.tg_mul, d.tg_shift);
-    fastdiv_params((uint32_t)Wo, d.ng_mul, d.ng_shift);
-    return ((planes + bnp - 1) / bnp) * d.bands < (1ll << 31);
-}
 
 static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
                        int64_t Cout, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw, int groups,
@@ -2428,71 +2382,11 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
                             (flags & F_QBMA) && kw == 3 && dw == 1 && sh == sw && (sw == 1 || sw == 2) &&
                             items < (1ll << 31) && Ho * Wo < (1ll << 31) &&
                             workspace_bytes >= FLAG_BYTES + (size_t)(Bn * Cin * H * W) * 4;
-        // depthwise (one input channel per group): the band-staged form reading fp32 directly
-        // (conv_dwx_kernel), same terms and sum order as conv_tbx_kernel
-        // the fp32 gather form (conv_dwg_kernel): 3x3, undilated, one input channel per group
-        DwgArgs dg;
-        const int64_t rgn = (Ho + 3) / 4, gitems = Bn * Cout * rgn * Wo;
-        const bool dwg_words = g_opt_dwx == 3;  // the same kernel over tbx_decode_a's word image
-        const bool dwg_ok = fast_ok && (g_opt_dwx == 2 || (dwg_words && workspace_bytes >= FLAG_BYTES + (size_t)(Bn * Cin * H * W) * 4)) && E == 4 && Mw == 3 && (mode == TM_NONE || mode == TM_W1U) &&
-                            (flags & F_QBMA) && kh == 3 && kw == 3 && dh == 1 && dw == 1 && sh == sw &&
-                            (sw == 1 || sw == 2) && cig == 1 && gitems < (1ll << 31);
-        DwxArgs da;
-        const bool dwx_ok = !dwg_ok && fast_ok && g_opt_dwx == 1 && E == 4 && Mw == 3 && (mode == TM_NONE || mode == TM_W1U) &&
-                            (flags & F_QBMA) && kw == 3 && dw == 1 && sh == sw && (sw == 1 || sw == 2) && cig == 1 &&
-                            Bn * Cin < (1ll << 40) && dwx_config(Bn * Cin, Cin, H, W, Ho, Wo, kh, sw, ph, pw, dh, da);
-        if (fq.mx && !tbx_ok && !dwx_ok && !dwg_ok) {
+        if (fq.mx && !tbx_ok) {
             rc = materialize();
             if (rc) return rc;
         }
-        if (dwg_ok) {
-            gate = (uint32_t *)workspace;
-            if (hipMemsetAsync(gate, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a gate reset");
-            dg.C = (int32_t)Cout; dg.H = (int32_t)H; dg.W = (int32_t)W; dg.Ho = (int32_t)Ho; dg.Wo = (int32_t)Wo;
-            dg.ph = ph; dg.pw = pw; dg.RGn = (int32_t)rgn;
-            dg.items = (uint32_t)gitems;
-            fastdiv_params((uint32_t)Wo, dg.wo_mul, dg.wo_shift);
-            fastdiv_params((uint32_t)rgn, dg.rg_mul, dg.rg_shift);
-            const unsigned gb = (unsigned)std::min<int64_t>((gitems + 255) / 256, 16 * 1024);
-            const float *src = x;
-            if (dwg_words) {
-                uint32_t *aw = (uint32_t *)((char *)workspace + FLAG_BYTES);
-                const int64_t nx = Bn * Cin * H * W;
-                tbx_decode_a<<<(unsigned)std::min<int64_t>((nx + 255) / 256, 8192), 256, 0, s>>>(x, nx, aw, gate, fq,
-                                                                                                    fqb, fqi);
-                if (fq.mx) bA = fqi;
-                src = reinterpret_cast<const float *>(aw);
-                if (sw == 1)
-                    conv_dwg_kernel<1, true><<<gb, 256, 0, s>>>(src, w, y, dg, bA, bW, bR, tp, gate, ep, act, act_lo,
-                                                                act_hi, fq, fqb, fqi);
-                else
-                    conv_dwg_kernel<2, true><<<gb, 256, 0, s>>>(src, w, y, dg, bA, bW, bR, tp, gate, ep, act, act_lo,
-                                                                act_hi, fq, fqb, fqi);
-            } else if (sw == 1) {
-                conv_dwg_kernel<1, false><<<gb, 256, 0, s>>>(x, w, y, dg, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi,
-                                                             fq, fqb, fqi);
-            } else {
-                conv_dwg_kernel<2, false><<<gb, 256, 0, s>>>(x, w, y, dg, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi,
-                                                             fq, fqb, fqi);
-            }
-            if (fq.mx) bA = fqi;
-            rc = hip_check("fp8a_conv2d (depthwise, E4M3 table form, fp32 gather)");
-            if (rc) return rc;
-        } else if (dwx_ok) {
-            gate = (uint32_t *)workspace;
-            if (hipMemsetAsync(gate, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a gate reset");
-            const unsigned gb = (unsigned)(((da.planes + da.NP - 1) / da.NP) * da.bands);
-            const size_t lds = (size_t)(((da.NP * da.IR * da.IC + 1) & ~1) + 2 * da.NP * kh * 3) * 4;
-            if (sw == 1)
-                conv_dwx_kernel<1><<<gb, 256, lds, s>>>(x, w, y, da, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi, fq,
-                                                      fqb, fqi);
-            else
-                conv_dwx_kernel<2><<<gb, 256, lds, s>>>(x, w, y, da, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi, fq,
-                                                      fqb, fqi);
-            if (fq.mx) bA = fqi;
-            rc = hip_check("fp8a_conv2d (depthwise, E4M3 table form, band-staged)");
-            if (rc) return rc;
-        } else if (tbx_ok) {
+        if (tbx_ok) {
             gate = (uint32_t *)workspace;
             // the input's table-form words from the producing launch (fp8a_conv2d_chain, next_form 1:
             // header + [Bn][Cin][H][W] words of fq_in(x)); the pre-pass then runs gated on its header
@@ -2783,7 +2677,7 @@ int fp8a_conv2d_wants_image(int64_t Cout, int kh, int kw, int ph, int pw, int gr
         // 1.65 ms per forward for 0.85 ms of gated pre-passes saved (19708 -> 19036 images/s)
         static const bool no_tbx = getenv("FP8A_NO_TBX") != nullptr;
         static const bool chain_tbx = getenv("FP8A_CHAIN_TBX") != nullptr && atoi(getenv("FP8A_CHAIN_TBX")) != 0;
-        const bool tbx = chain_tbx && !no_tbx && g_opt_dwx == 0 && ((E == 4 && Mw == 3) || (E == 5 && Mw == 2)) &&
+        const bool tbx = chain_tbx && !no_tbx && ((E == 4 && Mw == 3) || (E == 5 && Mw == 2)) &&
                          (mode == TM_NONE || mode == TM_W1U) && (flags & F_S2N) && (flags & F_QBMA) &&
                          !(flags & (F_GCLIP | F_V5)) && kw == 3 && dw == 1 && sh == sw && (sw == 1 || sw == 2);
         (void)kh; (void)dh;

@@ -4,7 +4,7 @@
 set -o pipefail
 OUT=gpurun_out/r04f; mkdir -p $OUT
 R=$(pwd)
-TESTS=${TESTS:-"tests/test_gpu_tbx.py tests/test_gpu_dwx.py tests/test_gpu_mbv2_layers.py"}
+TESTS=${TESTS:-"tests/test_gpu_tbx.py tests/test_gpu_mbv2_layers.py"}
 timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread $TESTS > $OUT/tests.log 2>&1
 rc=$?; tail -3 $OUT/tests.log; [ $rc -eq 0 ] || exit $rc
 for rw in 2 1; do
