@@ -19,7 +19,7 @@ DENSE_E4M3, DENSE_E5M2, DENSE_BF16 = 0, 1, 2  # fp8a_dense_* operand formats
 SYMBOLS = ("fp8a_version", "fp8a_last_error", "fp8a_fallback_stats", "fp8a_path_stats", "fp8a_set_option", "fp8a_debug_stats", "fp8a_decompose", "fp8a_quant", "fp8a_matmul_workspace_size",
            "fp8a_matmul_workspace_size_mnk", "fp8a_matmul", "fp8a_terms", "fp8a_conv2d_workspace_size", "fp8a_conv2d",
            "fp8a_conv2d_bn_act", "fp8a_conv2d_qin_workspace_size", "fp8a_conv2d_qin",
-           "fp8a_conv2d_block_workspace_size", "fp8a_conv2d_block", "fp8a_max_pool2d", "fp8a_im2col",
+           "fp8a_conv2d_block_workspace_size", "fp8a_conv2d_block", "fp8a_max_pool2d", "fp8a_avg_pool2d_plane", "fp8a_im2col",
            "fp8a_fp8_quantize", "fp8a_matmul_qamaa", "fp8a_conv2d_qamaa", "fp8a_matmul_block_workspace_size",
            "fp8a_matmul_block", "fp8a_dense_matmul_workspace_size", "fp8a_dense_matmul",
            "fp8a_dense_conv2d_workspace_size", "fp8a_dense_conv2d", "fp8a_grouped_conv2d", "fp8a_dense_conv2d_fused", "fp8a_dense_stats", "fp8a_clock_stats",
@@ -75,6 +75,7 @@ def load():
                                F, F, P, I, I, I, P, P, P, I, F, F, P, I, I, I, P, P, P, P, I, I, P, I, I, I, P, I,
                                I, P, SZ, P], I),
         "fp8a_max_pool2d": ([P, P, I64, I64, I64, I64, I, I, I, I, I, I, P], I),
+        "fp8a_avg_pool2d_plane": ([P, P, I64, I64, I64, I64, I, I, I, I, P], I),
         "fp8a_im2col": ([P, P, I64, I64, I64, I64, I, I, I, I, I, I, I, I, P], I),
         "fp8a_fp8_quantize": ([P, I64, I64, P, I, I, I, I, P, P, P, P], I),
         "fp8a_matmul_qamaa": ([P, I64, P, I64, I64, P, I64, I64, I64, P, I, I, I, P], I),

@@ -947,3 +947,40 @@ class MaxPool2d(nn.Module):
 
     def extra_repr(self):
         return f"kernel_size={self.kernel_size}, stride={self.stride}, padding={self.padding} (HIP)"
+
+
+# ----------------------------------------------------------------------------------- avg pool
+@torch.library.custom_op("fp8approx::avg_pool2d_plane", mutates_args=())
+def _avg_pool2d_plane_op(x: torch.Tensor, kernel: list[int], stride: list[int]) -> torch.Tensor:
+    L = _lib.load()
+    x = x.contiguous()
+    Bn, C, H, W = x.shape
+    y = torch.empty((Bn, C, 1, 1), dtype=x.dtype, device=x.device)
+    rc = L.fp8a_avg_pool2d_plane(_lib.dev_ptr(x), _lib.dev_ptr(y), Bn, C, H, W, kernel[0], kernel[1], stride[0],
+                                 stride[1], _lib.stream_ptr(x.device))
+    _lib.check(rc, "fp8a_avg_pool2d_plane")
+    return y
+
+
+@_avg_pool2d_plane_op.register_fake
+def _(x, kernel, stride):
+    return x.new_empty((x.shape[0], x.shape[1], 1, 1))
+
+
+class AvgPool2d(nn.AvgPool2d):
+    """nn.AvgPool2d (padding 0, floor mode, no divisor override) whose output is one value per
+    plane -- the MobileNetV2 head's AvgPool2d(input_size // 32) -- on the HIP kernel
+    fp8a_avg_pool2d_plane: the window summed in row-major order in fp32 and divided by kh kw, as
+    ATen's avg_pool2d does (the same bits).  Other inputs / geometries run torch's pooling; still an
+    nn.AvgPool2d, so quantize_sequential wraps it like the original (model_wrap.py)."""
+
+    def __init__(self, kernel_size, stride=None):
+        super().__init__(kernel_size, stride)
+
+    def forward(self, x):
+        pair = lambda v: [int(v), int(v)] if isinstance(v, int) else [int(t) for t in v]  # noqa: E731
+        k, s = pair(self.kernel_size), pair(self.stride)
+        if (x.dtype == torch.float32 and x.dim() == 4 and x.is_cuda and k[0] <= x.shape[2] < k[0] + s[0]
+                and k[1] <= x.shape[3] < k[1] + s[1] and x.shape[2] * x.shape[3] <= 4096):
+            return _avg_pool2d_plane_op(x, k, s)
+        return super().forward(x)

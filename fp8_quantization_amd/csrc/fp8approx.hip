@@ -1331,6 +1331,41 @@ __global__ __launch_bounds__(256) void max_pool2d_kernel(const float *x, float *
 // thread makes 4 consecutive outputs of one row from two aligned float4 loads + one scalar per
 // input row (27 scalar loads before), one float4 store.  Same scan order (window row, then
 // column) and NaN rule as max_pool2d_kernel, so the same bits.
+// nn.AvgPool2d with one output per plane (fp8a_avg_pool2d_plane; MobileNetV2's head).  ATen's
+// avg_pool2d sums the window in row-major order in fp32 and divides by kh kw once; so does this
+// (the same bits).  ATen reads with one thread per plane (lanes a plane apart: 0.41 ms for the
+// head at batch 512); here a workgroup stages PB consecutive planes through LDS with contiguous
+// loads (plane stride padded odd: conflict-free per-thread sums), then thread = plane.
+__global__ __launch_bounds__(128) void avg_pool_plane_kernel(const float *x, float *y, int64_t planes, int PB, int W,
+                                                             int hw, int ps, int kh, int kw, float inv_hw) {
+    extern __shared__ float ap_sm[];
+    const int tid = threadIdx.x;
+    const int64_t P0 = (int64_t)blockIdx.x * PB;
+    const int npl = (int)min((int64_t)PB, planes - P0), n = npl * hw;
+    const float *xb = x + P0 * hw;
+    for (int d0 = tid; d0 < n; d0 += 4 * 128) {
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = d0 + 128 * u < n ? xb[d0 + 128 * u] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int d = d0 + 128 * u;
+            if (d < n) {
+                const int pl = dw_div(d, hw, inv_hw);
+                ap_sm[pl * ps + d - pl * hw] = v[u];
+            }
+        }
+    }
+    __syncthreads();
+    for (int t = tid; t < npl; t += 128) {
+        const float *s = ap_sm + t * ps;
+        float acc = 0.0f;
+        for (int r = 0; r < kh; ++r)
+            for (int c = 0; c < kw; ++c) acc += s[r * W + c];
+        y[P0 + t] = acc / (float)(kh * kw);
+    }
+}
+
 __global__ __launch_bounds__(256) void max_pool2d_s2k3_kernel(const float *x, float *y, int64_t planes, int H, int W,
                                                              int Ho) {
     const int Wq = W / 8;  // 4-output groups per output row (Wo = W / 2)
@@ -1513,6 +1548,9 @@ static bool g_opt_oh_stats = false;  // "oh_stats": the one-hot kernels count in
 // "tbx_rw": output rows per thread of conv_tbx_kernel (1 or 2; 2 needs undilated rows).
 // FP8A_TBX_RW=<n> sets it at load.
 static int g_opt_tbx_rw = getenv("FP8A_TBX_RW") ? atoi(getenv("FP8A_TBX_RW")) : 2;
+// "dw3": the exact depthwise 3x3 on the LDS-staged dn_dw3_kernel (1, default) or on the general
+// dn_group_conv (0; the same bits).  FP8A_DW3=<n> sets it at load.
+static int g_opt_dw3 = getenv("FP8A_DW3") ? atoi(getenv("FP8A_DW3")) : 1;
 
 // Compute units of the current device (cached); 256 (MI355X) when no device is visible.
 static int device_cus() {
@@ -2052,6 +2090,32 @@ static void launch_group_conv(const GcArgs &a, hipStream_t s) {
     else dn_group_conv<I, 0, 1><<<g, 256, 0, s>>>(a);
 }
 
+// dn_dw3_kernel's block shape: about `target` outputs per workgroup (whole planes when a plane has
+// fewer, else bands of rows of one plane), the staged window within 20 KB of LDS so that eight
+// workgroups fit a CU; false when even 256 outputs' window does not fit (very wide rows).
+static bool plan_dw3(DwArgs &a, int S, size_t &lds) {
+    const int64_t op = (int64_t)a.Ho * a.Wo;
+    for (int target = 2048; target >= 256; target /= 2) {
+        int PB, RB;
+        if (op <= target) {
+            RB = a.Ho;
+            PB = (int)std::min<int64_t>(target / op, a.planes);
+        } else {
+            PB = 1;
+            RB = std::max(1, target / a.Wo);
+        }
+        const int RS = (RB - 1) * S + 3, WS = (a.Wo - 1) * S + 3;
+        const int64_t bytes = ((int64_t)PB * RS * WS + (int64_t)PB * 9) * 4;
+        if (bytes > 20480) continue;
+        a.PB = PB; a.RB = RB; a.nb = (a.Ho + RB - 1) / RB; a.RS = RS; a.WS = WS;
+        a.inv_c = 1.0f / a.C; a.inv_ws = 1.0f / WS; a.inv_pst = 1.0f / (RS * WS);
+        a.inv_wo = 1.0f / a.Wo; a.inv_pout = 1.0f / (RB * a.Wo);
+        lds = (size_t)bytes;
+        return ((a.planes + PB - 1) / PB) * a.nb < (1ll << 24);
+    }
+    return false;
+}
+
 extern "C" {
 
 const char *fp8a_version(void) { return "fp8approx gfx950 r1"; }
@@ -2089,6 +2153,11 @@ int fp8a_set_option(const char *name, int value) {
     if (strcmp(name, "tbx_rw") == 0) {
         const int old = g_opt_tbx_rw;
         g_opt_tbx_rw = value;
+        return old;
+    }
+    if (strcmp(name, "dw3") == 0) {
+        const int old = g_opt_dw3;
+        g_opt_dw3 = value;
         return old;
     }
     if (strcmp(name, "oh_correct") == 0) {
@@ -2192,6 +2261,21 @@ static int grouped_conv_impl(const float *x, const float *w, float *y, int64_t B
     a.fz = fz;
     if (a.total == 0) return FP8A_OK;
     if (!x || !w || !y) return fail(FP8A_EINVAL, "null pointer");
+    if (g_opt_dw3 && a.cig == 1 && a.cog == 1 && kh == 3 && kw == 3 && dh == 1 && dw == 1 && sh == sw &&
+        (sh == 1 || sh == 2)) {
+        DwArgs d{};
+        d.x = x; d.w = w; d.y = y; d.fz = fz;
+        d.planes = Bn * Cout; d.C = (int)Cout; d.H = (int)H; d.W = (int)W; d.Ho = (int)Ho; d.Wo = (int)Wo;
+        d.ph = ph; d.pw = pw;
+        size_t lds = 0;
+        if (H < (1 << 20) && W < (1 << 20) && Cout < (1 << 20) && plan_dw3(d, sh, lds)) {
+            const unsigned g = (unsigned)(((d.planes + d.PB - 1) / d.PB) * d.nb);
+            if (sh == 1) dn_dw3_kernel<1><<<g, 256, lds, stream>>>(d);
+            else dn_dw3_kernel<2><<<g, 256, lds, stream>>>(d);
+            ++g_paths[PATH_DENSE];
+            return hip_check("fp8a depthwise conv launch");
+        }
+    }
     if (a.total + 65536ll * 256 < (1ll << 31)) launch_group_conv<uint32_t>(a, stream);
     else launch_group_conv<int64_t>(a, stream);
     ++g_paths[PATH_DENSE];
@@ -2867,6 +2951,20 @@ int fp8a_max_pool2d(const float *x, float *y, int64_t Bn, int64_t C, int64_t H, 
     max_pool2d_kernel<<<(unsigned)std::min<int64_t>((total + 255) / 256, 65536), 256, 0, (hipStream_t)stream>>>(
         x, y, Bn * C, (int)H, (int)W, (int)Ho, (int)Wo, kh, kw, sh, sw, ph, pw);
     return hip_check("fp8a_max_pool2d");
+}
+
+int fp8a_avg_pool2d_plane(const float *x, float *y, int64_t Bn, int64_t C, int64_t H, int64_t W, int kh, int kw,
+                          int sh, int sw, fp8a_stream_t stream) {
+    if (kh < 1 || kw < 1 || sh < 1 || sw < 1 || kh > H || kw > W || H - kh >= sh || W - kw >= sw)
+        return fail(FP8A_EINVAL, "not a one-output-per-plane pooling window");
+    if (H * W > 4096) return fail(FP8A_EINVAL, "plane over 4096 values");
+    const int64_t planes = Bn * C;
+    if (planes == 0) return FP8A_OK;
+    if (!x || !y) return fail(FP8A_EINVAL, "null pointer");
+    const int hw = (int)(H * W), ps = hw | 1, pb = std::min(128, 8192 / ps);
+    avg_pool_plane_kernel<<<(unsigned)((planes + pb - 1) / pb), 128, (size_t)pb * ps * 4, (hipStream_t)stream>>>(
+        x, y, planes, pb, (int)W, hw, ps, kh, kw, 1.0f / hw);
+    return hip_check("fp8a_avg_pool2d_plane");
 }
 
 int fp8a_matmul_qamaa(const float *A, int64_t lda, const float *B, int64_t sbk, int64_t sbn, float *C, int64_t M,

@@ -564,6 +564,86 @@ __global__ __launch_bounds__(256) void dn_fix(const DenseArgs p) {
     }
 }
 
+// n / d for 0 <= n < 2^22 through the float reciprocal (inv = 1 / d rounded): the float quotient
+// is off by at most one, the remainder's sign and range fix it.
+__device__ __forceinline__ int dw_div(int n, int d, float inv) {
+    int q = (int)((float)n * inv);
+    const int r = n - q * d;
+    q += r < 0 ? -1 : (r >= d ? 1 : 0);
+    return q;
+}
+
+// The exact depthwise 3x3 (one input and one output channel per group, dilation 1, equal strides S
+// = 1 / 2 -- MobileNetV2's depthwise layers in BASELINE config 1), staged through LDS: the
+// workgroup owns PB consecutive planes (image x channel) x RB output rows, loads the input window
+// those rows read -- RS = (RB - 1) S + 3 rows x WS = (Wo - 1) S + 3 columns per plane, the padding
+// and the rows past the plane as zeros -- once, with the input quantizer (qin) applied once per
+// value, and the PB x 9 weights; then thread = output (consecutive lanes = consecutive output
+// columns, so the stores and the LDS reads are contiguous), nine fp32 FMAs in (ky, kx) order from
+// zero, as dn_group_conv (the same bits; it stays the form for every other grouped geometry).
+// HBM-bound: x read once (plus 2 halo rows per band), y written once.
+struct DwArgs {
+    const float *x, *w;
+    float *y;
+    int64_t planes;                // Bn x C
+    int C, H, W, Ho, Wo, ph, pw;
+    int PB, RB, nb, RS, WS;        // planes per block, output rows per band, bands per plane, staged rows / columns
+    float inv_c, inv_ws, inv_pst, inv_wo, inv_pout;
+    DnFuse fz;
+};
+
+template <int S>
+__global__ __launch_bounds__(256) void dn_dw3_kernel(const DwArgs p) {
+    extern __shared__ float dw_sm[];
+    const int tid = threadIdx.x;
+    const int band = (int)(blockIdx.x % (unsigned)p.nb);
+    const int64_t P0 = (int64_t)(blockIdx.x / (unsigned)p.nb) * p.PB;
+    const int npl = (int)min((int64_t)p.PB, p.planes - P0);
+    const int oh0 = band * p.RB, nrow = min(p.RB, p.Ho - oh0), hi0 = oh0 * S - p.ph;
+    const int pst = p.RS * p.WS, nst = npl * pst, pout = p.RB * p.Wo;
+    const int c0 = (int)(P0 % p.C);
+    float *wsm = dw_sm + p.PB * pst;
+    const DnQv qv = dn_qv(p.fz);
+    for (int d = tid; d < npl * 9; d += 256) {
+        int c = c0 + d / 9;
+        c -= dw_div(c, p.C, p.inv_c) * p.C;
+        wsm[d] = p.w[(int64_t)c * 9 + d % 9];
+    }
+    const float *xb = p.x + P0 * p.H * p.W;
+    for (int d0 = tid; d0 < nst; d0 += 4 * 256) {  // four loads in flight per thread
+        float v[4];
+        bool in[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int d = d0 + 256 * u;
+            const int pl = dw_div(d, pst, p.inv_pst), rem = d - pl * pst;
+            const int r = dw_div(rem, p.WS, p.inv_ws), hi = hi0 + r, wi = rem - r * p.WS - p.pw;
+            in[u] = d < nst && hi >= 0 && hi < p.H && wi >= 0 && wi < p.W;
+            v[u] = in[u] ? xb[((int64_t)pl * p.H + hi) * p.W + wi] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int d = d0 + 256 * u;
+            if (d < nst) dw_sm[d] = in[u] ? dn_in(p.fz, qv, v[u]) : 0.0f;
+        }
+    }
+    __syncthreads();
+    for (int e = tid; e < npl * pout; e += 256) {
+        const int pl = dw_div(e, pout, p.inv_pout), rem = e - pl * pout;
+        const int orow = dw_div(rem, p.Wo, p.inv_wo), oc = rem - orow * p.Wo;
+        if (orow >= nrow) continue;
+        const float *xs = dw_sm + pl * pst + orow * S * p.WS + oc * S, *ws = wsm + pl * 9;
+        float acc = 0.0f;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) acc = __fmaf_rn(xs[ky * p.WS + kx], ws[3 * ky + kx], acc);
+        int c = c0 + pl;
+        c -= dw_div(c, p.C, p.inv_c) * p.C;
+        p.y[((P0 + pl) * p.Ho + oh0 + orow) * p.Wo + oc] = dn_out(p.fz, qv, c, acc);
+    }
+}
+
 // The exact grouped / depthwise convolution: QCustomConv2dTorch's per-group im2col + x @ w^T
 // (approx_calculation.py:686-711) and the exact branch of QCustomBNConv2dTorch for groups > 1
 // (x @ y[:, i], :797 -- MobileNetV2's depthwise layers, BASELINE config 1).  One output = fp32

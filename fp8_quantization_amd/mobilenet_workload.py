@@ -13,6 +13,7 @@ import math
 
 from torch import nn
 
+from .approx_ops import AvgPool2d
 from .model_wrap import Flattener, QuantizedModel, fused_block_tail, quantize_model, quantize_sequential
 from .quantization.base_quantized_classes import FP32Acts, QuantizedActivation
 
@@ -57,7 +58,7 @@ class MobileNetV2(nn.Module):
                 feats.append(InvertedResidual(cin, cout, s if i == 0 else 1, expand_ratio=t))
                 cin = cout
         feats.append(nn.Sequential(*_conv_bn_relu6(cin, self.last_channel, 1, 1)))
-        feats.append(nn.AvgPool2d(input_size // 32))
+        feats.append(AvgPool2d(input_size // 32))  # nn.AvgPool2d on the HIP kernel (approx_ops.py)
         self.features = nn.Sequential(*feats)
         self.classifier = nn.Sequential(nn.Dropout(dropout), nn.Linear(self.last_channel, n_class))
         self._init()

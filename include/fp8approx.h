@@ -130,7 +130,8 @@ int fp8a_dense_conv2d(const float *x, const float *w, float *y, int64_t Bn, int6
 /* The exact grouped / depthwise convolution (QCustomConv2dTorch's per-group im2col + x @ w^T,
  * approx_calculation.py:686-711; the exact branch's x @ y[:, i] for groups > 1, :797): NCHW x,
  * w [Cout][Cin / groups][kh][kw], NCHW y, fp32 FMAs in the im2col k order (channel, ky, kx), the
- * padding as zeros.  Any fp32 input; no workspace.  Counted as a dense launch (fp8a_path_stats). */
+ * padding as zeros.  Any fp32 input; no workspace.  Counted as a dense launch (fp8a_path_stats).
+ * Depthwise 3x3 with equal strides 1 / 2 runs an LDS-staged kernel (option "dw3", the same bits). */
 int fp8a_grouped_conv2d(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
                         int64_t Cout, int groups, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw,
                         fp8a_stream_t stream);
@@ -372,6 +373,16 @@ int fp8a_matmul_block(const float *A, int64_t lda, const float *B, int64_t sbk, 
  */
 int fp8a_max_pool2d(const float *x, float *y, int64_t Bn, int64_t C, int64_t H, int64_t W, int kh,
                     int kw, int sh, int sw, int ph, int pw, fp8a_stream_t stream);
+
+/*
+ * nn.AvgPool2d (no padding, floor mode, no divisor override) whose output is one value per plane
+ * -- the window is each plane's top-left kh x kw (kh <= H < kh + sh, likewise W): the
+ * MobileNetV2 head's AvgPool2d(input_size // 32) on the benchmarked step (not an approx op).
+ * y[Bn][C][1][1] = the window summed in row-major order in fp32, divided by kh kw (ATen's
+ * avg_pool2d: the same bits).  FP8A_EINVAL for any other geometry or planes over 4096 values.
+ */
+int fp8a_avg_pool2d_plane(const float *x, float *y, int64_t Bn, int64_t C, int64_t H, int64_t W,
+                          int kh, int kw, int sh, int sw, fp8a_stream_t stream);
 
 /*
  * quantize_after_mult_and_add (qamaa) path of approx_multiply (approx_calculation.py:787-795):

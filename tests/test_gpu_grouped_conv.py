@@ -150,3 +150,50 @@ def test_config1_fused_layer(groups, cin, cout, k, s, order):
     d = (y - ref).abs()
     assert (d == 0).float().mean() > 0.999
     assert torch.all(d <= 1e-6 * ref.abs() + 1e-12)
+
+
+DW3_SHAPES = [  # (Bn, C, H, W, stride, padding): every MobileNetV2 depthwise geometry + ragged ones
+    (2, 32, 112, 112, 1, 1), (2, 96, 112, 112, 2, 1), (2, 144, 56, 56, 1, 1), (2, 144, 56, 56, 2, 1),
+    (3, 192, 28, 28, 1, 1), (3, 192, 28, 28, 2, 1), (4, 384, 14, 14, 1, 1), (4, 576, 14, 14, 2, 1),
+    (5, 960, 7, 7, 1, 1), (1, 3, 5, 9, 1, 1), (2, 5, 13, 7, 2, 1), (1, 4, 9, 300, 1, 1), (1, 6, 11, 10, 1, 0),
+    (2, 7, 12, 13, 2, 2), (1, 2, 1, 1, 1, 1),
+]
+
+
+@pytest.mark.parametrize("shape", DW3_SHAPES, ids=lambda c: "x".join(map(str, c)))
+@pytest.mark.parametrize("fused", [False, True])
+def test_depthwise_lds_form_matches_general_kernel(shape, fused):
+    """The LDS-staged depthwise 3x3 (option "dw3" = 1, the default) against the general
+    dn_group_conv (dw3 = 0): the same fp32 FMAs in the same order, so the same bits -- bands of
+    rows and groups of whole planes, ragged rows, stride 2, padding 0 / 2, a single-pixel plane,
+    non-finite weights, and the config-1 tail (qin on load, rq, scale / shift, clamp)."""
+    from fp8_quantization_amd import _lib
+    from fp8_quantization_amd.approx_ops import dense_conv2d_fused, fp8_fake_quantize, grouped_conv2d
+    Bn, C, H, W, s, p = shape
+    g = torch.Generator().manual_seed(Bn * C + H * W + s)
+    x = (torch.randn(Bn, C, H, W, generator=g) * 2).to(DEV)
+    w = torch.randn(C, 1, 3, 3, generator=g)
+    w[0, 0, 1, 1] = float("inf")
+    w[-1, 0, 2, 0] = float("nan")
+    w = w.to(DEV)
+
+    def run():
+        if not fused:
+            return grouped_conv2d(x, w, C, (s, s), (p, p))
+        wq, _ = fp8_fake_quantize(w, torch.tensor([2.0]), 8, 3)
+        ep = torch.stack((torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g)), 1).to(DEV).contiguous()
+        return dense_conv2d_fused(x, wq, C, (s, s), (p, p), qin=(torch.tensor([6.0], device=DEV), 8, 3, 1),
+                                  rq=(torch.tensor([40.0], device=DEV), 8, 3, 1), bn=(ep, 1, 0.0, 6.0))[0]
+
+    g.manual_seed(1)
+    y_new = run()
+    old = _lib.set_option("dw3", 0)
+    try:
+        g.manual_seed(1)
+        y_old = run()
+    finally:
+        _lib.set_option("dw3", old)
+    assert y_new.shape == y_old.shape
+    assert torch.equal(torch.isnan(y_new), torch.isnan(y_old))
+    fin = ~torch.isnan(y_old)
+    assert torch.equal(y_new[fin], y_old[fin])
