@@ -30,6 +30,14 @@ struct TbxArgs {
     uint32_t nwg, items;  // column groups per row, Bn * Cout * Ho * nwg
 };
 
+__device__ __forceinline__ uint32_t tbx_word(float v, const FqIn &fq, float fmx, float fbias, uint32_t lowm,
+                                             uint32_t mmask, int M, bool &bad) {
+    if (fq.mx) v = fq_apply(v, fmx, fbias, fq.M, fq.S);
+    const uint32_t u = __float_as_uint(v), ua = u & 0x7FFFFFFFu;
+    bad |= (ua != 0u) && ((ua & lowm) != 0u || ua < 0x20800000u || ua > 0x58800000u);
+    return ua == 0u ? 0u : ((u & 0xFF800000u) | (((ua >> (23 - M)) & mmask) << 6));
+}
+
 // x (NCHW floats) -> words: (bits(x) & 0xFF800000) | (m << 6); 0 for zeros; gate on off-grid
 // values / the exactness window (tensor-bias decode: every value at its own binade).
 // With fused input quantization (fq.mx set) the values are fq(x) and the quantizer's bias is
@@ -47,12 +55,7 @@ __global__ __launch_bounds__(256) void tbx_decode_a(const float *x, int64_t n, u
         *fq_ibias_out = (int32_t)fbias;
     }
     if (img_hdr != nullptr && __hip_atomic_load(img_hdr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
-    auto word = [&](float v) {
-        if (fq.mx) v = fq_apply(v, fmx, fbias, fq.M, fq.S);
-        const uint32_t u = __float_as_uint(v), ua = u & 0x7FFFFFFFu;
-        bad |= (ua != 0u) && ((ua & lowm) != 0u || ua < 0x20800000u || ua > 0x58800000u);
-        return ua == 0u ? 0u : ((u & 0xFF800000u) | (((ua >> (23 - M)) & mmask) << 6));
-    };
+    auto word = [&](float v) { return tbx_word(v, fq, fmx, fbias, lowm, mmask, M, bad); };
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     int64_t i0 = 0;
     if ((((uintptr_t)x | (uintptr_t)out) & 15) == 0) {  // 16-byte form over the n / 4 quads
@@ -64,6 +67,35 @@ __global__ __launch_bounds__(256) void tbx_decode_a(const float *x, int64_t n, u
     }
     for (int64_t i = i0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = word(x[i]);
     if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(gate, 1u);
+}
+
+// The table entry (L, F7 trigger) for (m_a, m_b) = (i >> 3, i & 7) at result bias r_b (the
+// derivation in the header; rows / columns past 2^M are unused).
+template <int M>
+__device__ __forceinline__ float2 tbx_lut_entry(int i, const TablePack &tab, int r_b) {
+    constexpr float ULP = 1.0f / (1 << M);  // 2^-M
+    const int ma = i >> 3, mb = i & 7;
+    const int tv = (ma < (1 << M) && mb < (1 << M)) ? tab.raw[(ma << M) | mb] : 0;
+    const float u = (1.0f + ULP * ma) * (1.0f + ULP * mb);  // exact
+    const float v = __fmaf_rn(1.0f + ULP * ma, 1.0f + ULP * mb, -ULP * (float)tv);
+    const float pe = __uint_as_float(__float_as_uint(v) & 0x7F800000u);
+    const float xs = fminf(v, pe * (2.0f - ULP - p2(-22))), cc = pe * (float)(1 << (23 - M)) * 1.5f;
+    const float L = (xs + cc) - cc;  // QMc(V'): RNE at V's binade after the saturating clamp
+    uint32_t f7 = 0xFFFFFFFFu;       // never equal to a product of binades
+    if (u <= 1.0f + 0.5f * ULP) f7 = 0x80000000u | ((uint32_t)(127 - r_b) << 23);
+    else if (u >= 2.0f && u <= 2.0f + ULP) f7 = 0x80000000u | ((uint32_t)(126 - r_b) << 23);
+    return make_float2(L, __uint_as_float(f7));
+}
+
+// One term of the table form: input word wa, the tap's c_b and m_b << 3, the table in LDS.
+__device__ __forceinline__ float tbx_term(uint32_t wa, float cB, uint32_t mb8, const char *lut, uint32_t q0exp,
+                                          float twoq) {
+    const float2 e = *reinterpret_cast<const float2 *>(lut + ((wa & 0x1C0u) | mb8));
+    const float cab = __uint_as_float(wa & 0xFF800000u) * cB;  // exact
+    float rv = e.x * cab;                                        // exact
+    const float rs = __fmaf_rn(2.0f, rv, -copysignf(twoq, rv));  // expo field 0
+    rv = ((__float_as_uint(rv) & 0x7F800000u) == q0exp) ? rs : rv;
+    return (__float_as_uint(cab) == __float_as_uint(e.y)) ? fabsf(rv) : rv;  // F7
 }
 
 // M = 3 (E4M3) or 2 (E5M2, the same derivation with M-bit mantissas: L = QMc(sig_a sig_b - T / 2^M),
@@ -80,24 +112,11 @@ __global__ __launch_bounds__(256) void conv_tbx_kernel(const uint32_t *aw, const
                                                        TablePack tab, uint32_t *gate, const float2 *ep, int ep_act,
                                                        float ep_lo, float ep_hi) {
     constexpr int KW = 3, NCOL = (TBX_TW - 1) * SW + KW;
-    constexpr float ULP = 1.0f / (1 << M);                            // 2^-M
     constexpr uint32_t LOWM = (1u << (23 - M)) - 1u, MMASK = (1u << M) - 1u;
     __shared__ float2 sL[64];
     const int a_b = *bA, r_b = *bR;
     bool bad = !(a_b >= 2 && a_b <= 120 && r_b >= 2 && r_b <= 120);
-    if (threadIdx.x < 64) {
-        const int ma = threadIdx.x >> 3, mb = threadIdx.x & 7;
-        const int tv = (ma < (1 << M) && mb < (1 << M)) ? tab.raw[(ma << M) | mb] : 0;
-        const float u = (1.0f + ULP * ma) * (1.0f + ULP * mb);  // exact
-        const float v = __fmaf_rn(1.0f + ULP * ma, 1.0f + ULP * mb, -ULP * (float)tv);
-        const float pe = __uint_as_float(__float_as_uint(v) & 0x7F800000u);
-        const float xs = fminf(v, pe * (2.0f - ULP - p2(-22))), cc = pe * (float)(1 << (23 - M)) * 1.5f;
-        const float L = (xs + cc) - cc;  // QMc(V'): RNE at V's binade after the saturating clamp
-        uint32_t f7 = 0xFFFFFFFFu;       // never equal to a product of binades
-        if (u <= 1.0f + 0.5f * ULP) f7 = 0x80000000u | ((uint32_t)(127 - r_b) << 23);
-        else if (u >= 2.0f && u <= 2.0f + ULP) f7 = 0x80000000u | ((uint32_t)(126 - r_b) << 23);
-        sL[threadIdx.x] = make_float2(L, __uint_as_float(f7));
-    }
+    if (threadIdx.x < 64) sL[threadIdx.x] = tbx_lut_entry<M>(threadIdx.x, tab, r_b);
     __syncthreads();
     const uint32_t q0exp = (uint32_t)(127 - r_b) << 23;
     const float twoq = __uint_as_float((uint32_t)(128 - r_b) << 23);
@@ -142,16 +161,8 @@ __global__ __launch_bounds__(256) void conv_tbx_kernel(const uint32_t *aw, const
                         const float cB = __uint_as_float(bw & 0xFF800000u);
                         const uint32_t mb8 = ((bwa >> (23 - M)) & MMASK) << 3;
 #pragma unroll
-                        for (int q = 0; q < TBX_TW; ++q) {
-                            const uint32_t wa = col[q * SW + kx];
-                            const float2 e = *reinterpret_cast<const float2 *>(lut + ((wa & 0x1C0u) | mb8));
-                            const float cab = __uint_as_float(wa & 0xFF800000u) * cB;  // exact
-                            float rv = e.x * cab;                                        // exact
-                            const float rs = __fmaf_rn(2.0f, rv, -copysignf(twoq, rv));  // expo field 0
-                            rv = ((__float_as_uint(rv) & 0x7F800000u) == q0exp) ? rs : rv;
-                            rv = (__float_as_uint(cab) == __float_as_uint(e.y)) ? fabsf(rv) : rv;  // F7
-                            acc[j][q] += rv;
-                        }
+                        for (int q = 0; q < TBX_TW; ++q)
+                            acc[j][q] += tbx_term(col[q * SW + kx], cB, mb8, lut, q0exp, twoq);
                     }
                 }
             }
@@ -166,6 +177,104 @@ __global__ __launch_bounds__(256) void conv_tbx_kernel(const uint32_t *aw, const
         }
     }
     if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(gate, 1u);
+}
+
+// conv_tbs_kernel: conv_tbx_kernel for the depthwise 3x3 (one input channel per output, dilation
+// 1, stride S both ways) with tbx_decode_a fused in, staged through LDS (option "tbs", the
+// default): the workgroup owns PB consecutive planes x RB output rows (as dn_dw3_kernel), loads
+// the fp32 input window those rows read once with contiguous loads, applies the input quantizer
+// and the word encoding into LDS (zero words for the padding), builds the table and the taps'
+// (c_b, m_b) once, then thread = 4 consecutive outputs of a row: the window's words by 16-byte LDS
+// reads (rows padded to a multiple of 4 words) and conv_tbx_kernel's terms in (ky, kx) order --
+// the same bits, without the word image's write and read (8 B per input value) and the gathers'
+// load latency.  The gate rules are the pre-pass's and the kernel's (values staged, taps, biases).
+struct TbsArgs {
+    int64_t planes;  // Bn x C
+    int C, H, W, Ho, Wo, ph, pw;
+    int PB, RB, nb, RS, WS, nq;  // planes / block, output rows / band, bands / plane, staged rows, row stride (words), quads / row
+    float inv_c, inv_ws, inv_pst, inv_nq, inv_pq, inv_w, inv_hw;
+};
+
+template <int S, int M>
+__global__ __launch_bounds__(256) void conv_tbs_kernel(const float *x, const float *w, float *y, const TbsArgs t, FqIn fq,
+                                                       float *fq_bias_out, int32_t *fq_ibias_out, const int32_t *bA,
+                                                       const int32_t *bW, const int32_t *bR, TablePack tab,
+                                                       uint32_t *gate, const float2 *ep, int ep_act, float ep_lo,
+                                                       float ep_hi) {
+    constexpr int NCOL = (TBX_TW - 1) * S + 3;
+    constexpr uint32_t LOWM = (1u << (23 - M)) - 1u, MMASK = (1u << M) - 1u;
+    extern __shared__ uint4 tbs_sm[];
+    uint32_t *sw = reinterpret_cast<uint32_t *>(tbs_sm);               // [PB][RS][WS] words
+    float2 *sL = reinterpret_cast<float2 *>(sw + t.PB * t.RS * t.WS);  // the table
+    uint2 *sB = reinterpret_cast<uint2 *>(sL + 64);                    // [PB][9] {c_b bits, m_b << 3}
+    const int tid = threadIdx.x;
+    const float fmx = fq.mx ? *fq.mx : 0.0f, fbias = fq.mx ? fq_bias(fmx, fq.E, fq.M) : 0.0f;
+    if (fq.mx && blockIdx.x == 0 && tid == 0) {
+        *fq_bias_out = fbias;
+        *fq_ibias_out = (int32_t)fbias;
+    }
+    const int a_b = fq.mx ? (int32_t)fbias : *bA, r_b = *bR;
+    bool bad = !(a_b >= 2 && a_b <= 120 && r_b >= 2 && r_b <= 120);
+    if (tid < 64) sL[tid] = tbx_lut_entry<M>(tid, tab, r_b);
+    const int band = (int)(blockIdx.x % (unsigned)t.nb);
+    const int64_t P0 = (int64_t)(blockIdx.x / (unsigned)t.nb) * t.PB;
+    const int npl = (int)min((int64_t)t.PB, t.planes - P0);
+    const int oh0 = band * t.RB, nrow = min(t.RB, t.Ho - oh0), hi0 = oh0 * S - t.ph;
+    const int pst = t.RS * t.WS, c0 = (int)(P0 % t.C);
+    for (int d = tid; d < npl * 9; d += 256) {
+        const int pl = d / 9;
+        int c = c0 + pl;
+        c -= dw_div(c, t.C, t.inv_c) * t.C;
+        const int wb = bW[c];
+        bad |= !(wb >= 2 && wb <= 120);
+        const uint32_t bw = __float_as_uint(w[(int64_t)c * 9 + d - 9 * pl]), bwa = bw & 0x7FFFFFFFu;
+        bad |= (bwa != 0u) && ((bwa & LOWM) != 0u || bwa < 0x20800000u || bwa > 0x58800000u);
+        sB[d] = make_uint2(bw & 0xFF800000u, ((bwa >> (23 - M)) & MMASK) << 3);
+    }
+    dw_stage(x, P0, npl, t.H, t.W, hi0, t.pw, t.RS, t.WS, t.inv_w, t.inv_hw, t.RB == t.Ho, sw,
+             [&](float v) { return tbx_word(v, fq, fmx, fbias, LOWM, MMASK, M, bad); });
+    __syncthreads();
+    const uint32_t q0exp = (uint32_t)(127 - r_b) << 23;
+    const float twoq = __uint_as_float((uint32_t)(128 - r_b) << 23);
+    const char *lut = reinterpret_cast<const char *>(sL);
+    const int pq = t.RB * t.nq;
+    for (int e = tid; e < npl * pq; e += 256) {
+        const int pl = dw_div(e, pq, t.inv_pq), rem = e - pl * pq;
+        const int orow = dw_div(rem, t.nq, t.inv_nq), q = rem - orow * t.nq;
+        if (orow >= nrow) continue;
+        const uint32_t *ws = sw + pl * pst + orow * S * t.WS + 4 * q * S;
+        const uint2 *wb = sB + pl * 9;
+        float acc[TBX_TW] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+            const uint32_t *wr = ws + ky * t.WS;
+            uint32_t col[NCOL];
+            const uint4 a0 = *reinterpret_cast<const uint4 *>(wr);
+            col[0] = a0.x; col[1] = a0.y; col[2] = a0.z; col[3] = a0.w;
+            if constexpr (S == 1) {
+                const uint2 a1 = *reinterpret_cast<const uint2 *>(wr + 4);
+                col[4] = a1.x; col[5] = a1.y;
+            } else {
+                const uint4 a1 = *reinterpret_cast<const uint4 *>(wr + 4);
+                col[4] = a1.x; col[5] = a1.y; col[6] = a1.z; col[7] = a1.w;
+                col[8] = wr[8];
+            }
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+                const uint2 b = wb[3 * ky + kx];
+                const float cB = __uint_as_float(b.x);
+#pragma unroll
+                for (int j = 0; j < TBX_TW; ++j) acc[j] += tbx_term(col[j * S + kx], cB, b.y, lut, q0exp, twoq);
+            }
+        }
+        int co = c0 + pl;
+        co -= dw_div(co, t.C, t.inv_c) * t.C;
+        float *yr = y + ((P0 + pl) * t.Ho + oh0 + orow) * t.Wo;
+#pragma unroll
+        for (int j = 0; j < TBX_TW; ++j)
+            if (4 * q + j < t.Wo) yr[4 * q + j] = epi(ep, ep_act, ep_lo, ep_hi, co, acc[j]);
+    }
+    if (__syncthreads_or(bad ? 1 : 0) && tid == 0) atomicOr(gate, 1u);
 }
 
 // (round 3's alternative depthwise forms conv_dwx_kernel -- band-staged in LDS -- and

@@ -1548,9 +1548,17 @@ static bool g_opt_oh_stats = false;  // "oh_stats": the one-hot kernels count in
 // "tbx_rw": output rows per thread of conv_tbx_kernel (1 or 2; 2 needs undilated rows).
 // FP8A_TBX_RW=<n> sets it at load.
 static int g_opt_tbx_rw = getenv("FP8A_TBX_RW") ? atoi(getenv("FP8A_TBX_RW")) : 2;
+// "tbs": the table-form depthwise 3x3 on the LDS-staged conv_tbs_kernel with the word pre-pass
+// fused (1, default) or on tbx_decode_a + conv_tbx_kernel (0; the same bits).  FP8A_TBS=<n>.
+static int g_opt_tbs = getenv("FP8A_TBS") ? atoi(getenv("FP8A_TBS")) : 1;
 // "dw3": the exact depthwise 3x3 on the LDS-staged dn_dw3_kernel (1, default) or on the general
 // dn_group_conv (0; the same bits).  FP8A_DW3=<n> sets it at load.
 static int g_opt_dw3 = getenv("FP8A_DW3") ? atoi(getenv("FP8A_DW3")) : 1;
+// "dw_target": outputs per workgroup the LDS-staged depthwise kernels aim at (plan_dw3 / plan_tbs;
+// halved until the window fits dw_lds).  FP8A_DW_TARGET=<n>.
+static int g_opt_dw_target = getenv("FP8A_DW_TARGET") ? atoi(getenv("FP8A_DW_TARGET")) : 4096;
+// "dw_lds": the LDS bytes per workgroup those plans allow (FP8A_DW_LDS=<n>, at most 64 KB).
+static int g_opt_dw_lds = getenv("FP8A_DW_LDS") ? atoi(getenv("FP8A_DW_LDS")) : 40960;
 
 // Compute units of the current device (cached); 256 (MI355X) when no device is visible.
 static int device_cus() {
@@ -2091,27 +2099,62 @@ static void launch_group_conv(const GcArgs &a, hipStream_t s) {
 }
 
 // dn_dw3_kernel's block shape: about `target` outputs per workgroup (whole planes when a plane has
-// fewer, else bands of rows of one plane), the staged window within 20 KB of LDS so that eight
-// workgroups fit a CU; false when even 256 outputs' window does not fit (very wide rows).
+// fewer, else bands of rows of one plane), the staged window within dw_lds bytes of LDS (default
+// 40 KB, four workgroups per CU: measured against 2 / 8 / 16 KB-windowed plans, §3l); false when even 256 outputs' window does not fit (very wide rows).
 static bool plan_dw3(DwArgs &a, int S, size_t &lds) {
     const int64_t op = (int64_t)a.Ho * a.Wo;
-    for (int target = 2048; target >= 256; target /= 2) {
+    for (int target = std::max(256, g_opt_dw_target); target >= 256; target /= 2) {
         int PB, RB;
         if (op <= target) {
             RB = a.Ho;
             PB = (int)std::min<int64_t>(target / op, a.planes);
+            if ((int64_t)a.H * a.W % 4 != 0 && PB >= 4) PB &= ~3;  // 16-byte aligned source ranges (dw_stage)
         } else {
             PB = 1;
             RB = std::max(1, target / a.Wo);
         }
-        const int RS = (RB - 1) * S + 3, WS = (a.Wo - 1) * S + 3;
+        const int RS = (RB - 1) * S + 3,
+                  WS = (std::max(a.W + DW_OX, DW_OX - a.pw + (a.Wo - 1) * S + 3) + 3) / 4 * 4;
         const int64_t bytes = ((int64_t)PB * RS * WS + (int64_t)PB * 9) * 4;
-        if (bytes > 20480) continue;
+        if (bytes > std::min(65536, std::max(4096, g_opt_dw_lds))) continue;
         a.PB = PB; a.RB = RB; a.nb = (a.Ho + RB - 1) / RB; a.RS = RS; a.WS = WS;
         a.inv_c = 1.0f / a.C; a.inv_ws = 1.0f / WS; a.inv_pst = 1.0f / (RS * WS);
         a.inv_wo = 1.0f / a.Wo; a.inv_pout = 1.0f / (RB * a.Wo);
+        a.inv_w = 1.0f / a.W; a.inv_hw = 1.0f / (a.H * a.W);
         lds = (size_t)bytes;
         return ((a.planes + PB - 1) / PB) * a.nb < (1ll << 24);
+    }
+    return false;
+}
+
+// conv_tbs_kernel's block shape: dn_dw3_kernel's plan with quads of outputs and rows of staged
+// words padded to a multiple of 4 (16-byte LDS reads).
+static bool plan_tbs(TbsArgs &a, int S, int64_t planes, int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
+                     int ph, int pw, size_t &lds) {
+    if (H >= (1 << 20) || W >= (1 << 20) || C >= (1 << 20)) return false;
+    a.planes = planes; a.C = (int)C; a.H = (int)H; a.W = (int)W; a.Ho = (int)Ho; a.Wo = (int)Wo; a.ph = ph; a.pw = pw;
+    const int nq = (int)((Wo + TBX_TW - 1) / TBX_TW);
+    const int WS = ((4 * nq - 1) * S + 3 + 3) / 4 * 4;
+    const int64_t op = Ho * Wo;
+    for (int target = std::max(256, g_opt_dw_target); target >= 256; target /= 2) {
+        int PB, RB;
+        if (op <= target) {
+            RB = (int)Ho;
+            PB = (int)std::min<int64_t>(target / op, planes);
+            if (H * W % 4 != 0 && PB >= 4) PB &= ~3;  // 16-byte aligned source ranges (dw_stage)
+        } else {
+            PB = 1;
+            RB = std::max(1, (int)(target / Wo));
+        }
+        const int RS = (RB - 1) * S + 3;
+        const int64_t bytes = (int64_t)PB * RS * WS * 4 + 512 + (int64_t)PB * 9 * 8;
+        if (bytes > std::min(65536, std::max(4096, g_opt_dw_lds))) continue;
+        a.PB = PB; a.RB = RB; a.nb = (int)((Ho + RB - 1) / RB); a.RS = RS; a.WS = WS; a.nq = nq;
+        a.inv_c = 1.0f / a.C; a.inv_ws = 1.0f / WS; a.inv_pst = 1.0f / (RS * WS);
+        a.inv_nq = 1.0f / nq; a.inv_pq = 1.0f / (RB * nq);
+        a.inv_w = 1.0f / a.W; a.inv_hw = 1.0f / (a.H * a.W);
+        lds = (size_t)bytes;
+        return ((planes + PB - 1) / PB) * a.nb < (1ll << 24);
     }
     return false;
 }
@@ -2153,6 +2196,21 @@ int fp8a_set_option(const char *name, int value) {
     if (strcmp(name, "tbx_rw") == 0) {
         const int old = g_opt_tbx_rw;
         g_opt_tbx_rw = value;
+        return old;
+    }
+    if (strcmp(name, "tbs") == 0) {
+        const int old = g_opt_tbs;
+        g_opt_tbs = value;
+        return old;
+    }
+    if (strcmp(name, "dw_lds") == 0) {
+        const int old = g_opt_dw_lds;
+        g_opt_dw_lds = std::min(65536, std::max(4096, value));
+        return old;
+    }
+    if (strcmp(name, "dw_target") == 0) {
+        const int old = g_opt_dw_target;
+        g_opt_dw_target = std::max(256, value);
         return old;
     }
     if (strcmp(name, "dw3") == 0) {
@@ -2261,7 +2319,7 @@ static int grouped_conv_impl(const float *x, const float *w, float *y, int64_t B
     a.fz = fz;
     if (a.total == 0) return FP8A_OK;
     if (!x || !w || !y) return fail(FP8A_EINVAL, "null pointer");
-    if (g_opt_dw3 && a.cig == 1 && a.cog == 1 && kh == 3 && kw == 3 && dh == 1 && dw == 1 && sh == sw &&
+    if (g_opt_dw3 && a.cig == 1 && a.cog == 1 && kh == 3 && kw == 3 && dh == 1 && dw == 1 && sh == sw && pw <= DW_OX &&
         (sh == 1 || sh == 2)) {
         DwArgs d{};
         d.x = x; d.w = w; d.y = y; d.fz = fz;
@@ -2477,6 +2535,19 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
             const bool use_img = in_img != nullptr && fq.mx != nullptr;
             uint32_t *aw = use_img ? const_cast<uint32_t *>(in_img) + 64 : (uint32_t *)((char *)workspace + FLAG_BYTES);
             if (hipMemsetAsync(gate, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a gate reset");
+            TbsArgs tb{};
+            size_t tlds = 0;
+            if (g_opt_tbs && !use_img && cig == 1 && kh == 3 && dh == 1 && plan_tbs(tb, sw, Bn * Cout, Cout, H, W, Ho, Wo,
+                                                                                  ph, pw, tlds)) {
+                const unsigned gb = (unsigned)(((tb.planes + tb.PB - 1) / tb.PB) * tb.nb);
+#define FP8A_TBS(S_, M_) conv_tbs_kernel<S_, M_><<<gb, 256, tlds, s>>>(x, w, y, tb, fq, fqb, fqi, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi)
+                if (Mw == 2) { if (sw == 1) FP8A_TBS(1, 2); else FP8A_TBS(2, 2); }
+                else { if (sw == 1) FP8A_TBS(1, 3); else FP8A_TBS(2, 3); }
+#undef FP8A_TBS
+                if (fq.mx) bA = fqi;
+                rc = hip_check("fp8a_conv2d (tensor-bias groups, staged table form)");
+                if (rc) return rc;
+            } else {
             const int64_t nx = Bn * Cin * H * W;
             tbx_decode_a<<<(unsigned)std::min<int64_t>((nx + 255) / 256, use_img ? 1024 : 8192), 256, 0, s>>>(
                 x, nx, aw, gate, fq, fqb, fqi, Mw, use_img ? in_img : nullptr);
@@ -2499,6 +2570,7 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
 #undef FP8A_TBX
             rc = hip_check("fp8a_conv2d (tensor-bias groups, E4M3 / E5M2 table form)");
             if (rc) return rc;
+            }
         } else if (fast_ok) {
             gate = (uint32_t *)workspace;
             if (hipMemsetAsync(gate, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a gate reset");

@@ -573,22 +573,87 @@ __device__ __forceinline__ int dw_div(int n, int d, float inv) {
     return q;
 }
 
+// Stage the input window of a depthwise workgroup (dn_dw3_kernel, conv_tbs_kernel) into LDS.  The
+// rows the workgroup reads are one contiguous range of x -- whole planes, or a band of full rows
+// of one plane -- so it is read with 16-byte loads (four in flight per thread) when the range is
+// 16-byte aligned, and each value is scattered to its [plane][row][column] slot of the padded
+// window (RS rows x WS columns per plane, WS a multiple of 4) as f(value); the slots no value
+// lands on (padding, rows past the plane) are zero.  P0 / hi0: the first plane / window row.
+// ox: the LDS column of input column 0 (the left padding is the ox columns before it).  With ox
+// and W multiples of 4 each 16-byte load lands on one 16-byte LDS slot (one conflict-free write).
+template <typename T, typename F>
+__device__ __forceinline__ void dw_stage(const float *x, int64_t P0, int npl, int H, int W, int hi0, int ox, int RS,
+                                         int WS, float inv_w, float inv_hw, bool plane_mode, T *sm, F f) {
+    const int pst = RS * WS, nst = npl * pst, tid = threadIdx.x, hw = H * W;
+    for (int d = 4 * tid; d < nst; d += 4 * 256) *reinterpret_cast<uint4 *>(sm + d) = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    // source range [g0, g0 + n): element i -> plane i / hw, row, column
+    const int rlo = plane_mode ? 0 : max(hi0, 0), rhi = plane_mode ? H : min(hi0 + RS, H);
+    const int n = plane_mode ? npl * hw : (rhi - rlo) * W;
+    const float *src = x + P0 * hw + (int64_t)rlo * W;
+    auto put = [&](int i, float v) {
+        int pl = dw_div(i, hw, inv_hw);
+        const int rem = i - pl * hw, row = dw_div(rem, W, inv_w) + rlo, col = rem - (row - rlo) * W;
+        const int r = row - hi0, c = col + ox;
+        if (r >= 0 && r < RS && c < WS) sm[pl * pst + r * WS + c] = f(v);
+    };
+    const bool slots = ((W | ox) & 3) == 0;
+    if (((((uintptr_t)src) | (uintptr_t)n) & 3) == 0 && (((uintptr_t)src) & 15) == 0) {
+        const int n4 = n >> 2;
+        for (int q0 = tid; q0 < n4; q0 += 4 * 256) {
+            float4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                v[u] = q0 + 256 * u < n4 ? reinterpret_cast<const float4 *>(src)[q0 + 256 * u] : make_float4(0, 0, 0, 0);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int q = q0 + 256 * u;
+                if (q >= n4) break;
+                if (slots) {  // the four values share a row: one 16-byte slot
+                    const int i = 4 * q, pl = dw_div(i, hw, inv_hw), rem = i - pl * hw;
+                    const int rr = dw_div(rem, W, inv_w), r = rr + rlo - hi0, col = rem - rr * W;
+                    if (r >= 0 && r < RS) {
+                        const T o[4] = {f(v[u].x), f(v[u].y), f(v[u].z), f(v[u].w)};
+                        *reinterpret_cast<uint4 *>(sm + pl * pst + r * WS + col + ox) =
+                            *reinterpret_cast<const uint4 *>(o);
+                    }
+                    continue;
+                }
+                put(4 * q, v[u].x);
+                put(4 * q + 1, v[u].y);
+                put(4 * q + 2, v[u].z);
+                put(4 * q + 3, v[u].w);
+            }
+        }
+    } else {
+        for (int i0 = tid; i0 < n; i0 += 4 * 256) {
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = i0 + 256 * u < n ? src[i0 + 256 * u] : 0.0f;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i0 + 256 * u < n) put(i0 + 256 * u, v[u]);
+        }
+    }
+}
+
 // The exact depthwise 3x3 (one input and one output channel per group, dilation 1, equal strides S
 // = 1 / 2 -- MobileNetV2's depthwise layers in BASELINE config 1), staged through LDS: the
 // workgroup owns PB consecutive planes (image x channel) x RB output rows, loads the input window
-// those rows read -- RS = (RB - 1) S + 3 rows x WS = (Wo - 1) S + 3 columns per plane, the padding
-// and the rows past the plane as zeros -- once, with the input quantizer (qin) applied once per
-// value, and the PB x 9 weights; then thread = output (consecutive lanes = consecutive output
+// those rows read -- RS = (RB - 1) S + 3 rows x WS >= (Wo - 1) S + 3 columns per plane, the padding
+// and the rows past the plane as zeros (dw_stage: 16-byte loads) -- once, with the input quantizer
+// (qin) applied once per value, and the PB x 9 weights; then thread = output (consecutive lanes = consecutive output
 // columns, so the stores and the LDS reads are contiguous), nine fp32 FMAs in (ky, kx) order from
 // zero, as dn_group_conv (the same bits; it stays the form for every other grouped geometry).
 // HBM-bound: x read once (plus 2 halo rows per band), y written once.
+constexpr int DW_OX = 4;  // dn_dw3_kernel's LDS column of input column 0 (padding pw <= 4 before it)
 struct DwArgs {
     const float *x, *w;
     float *y;
     int64_t planes;                // Bn x C
     int C, H, W, Ho, Wo, ph, pw;
     int PB, RB, nb, RS, WS;        // planes per block, output rows per band, bands per plane, staged rows / columns
-    float inv_c, inv_ws, inv_pst, inv_wo, inv_pout;
+    float inv_c, inv_ws, inv_pst, inv_wo, inv_pout, inv_w, inv_hw;
     DnFuse fz;
 };
 
@@ -600,7 +665,7 @@ __global__ __launch_bounds__(256) void dn_dw3_kernel(const DwArgs p) {
     const int64_t P0 = (int64_t)(blockIdx.x / (unsigned)p.nb) * p.PB;
     const int npl = (int)min((int64_t)p.PB, p.planes - P0);
     const int oh0 = band * p.RB, nrow = min(p.RB, p.Ho - oh0), hi0 = oh0 * S - p.ph;
-    const int pst = p.RS * p.WS, nst = npl * pst, pout = p.RB * p.Wo;
+    const int pst = p.RS * p.WS, pout = p.RB * p.Wo;
     const int c0 = (int)(P0 % p.C);
     float *wsm = dw_sm + p.PB * pst;
     const DnQv qv = dn_qv(p.fz);
@@ -609,30 +674,14 @@ __global__ __launch_bounds__(256) void dn_dw3_kernel(const DwArgs p) {
         c -= dw_div(c, p.C, p.inv_c) * p.C;
         wsm[d] = p.w[(int64_t)c * 9 + d % 9];
     }
-    const float *xb = p.x + P0 * p.H * p.W;
-    for (int d0 = tid; d0 < nst; d0 += 4 * 256) {  // four loads in flight per thread
-        float v[4];
-        bool in[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int d = d0 + 256 * u;
-            const int pl = dw_div(d, pst, p.inv_pst), rem = d - pl * pst;
-            const int r = dw_div(rem, p.WS, p.inv_ws), hi = hi0 + r, wi = rem - r * p.WS - p.pw;
-            in[u] = d < nst && hi >= 0 && hi < p.H && wi >= 0 && wi < p.W;
-            v[u] = in[u] ? xb[((int64_t)pl * p.H + hi) * p.W + wi] : 0.0f;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int d = d0 + 256 * u;
-            if (d < nst) dw_sm[d] = in[u] ? dn_in(p.fz, qv, v[u]) : 0.0f;
-        }
-    }
+    dw_stage(p.x, P0, npl, p.H, p.W, hi0, DW_OX, p.RS, p.WS, p.inv_w, p.inv_hw, p.RB == p.Ho, dw_sm,
+             [&](float v) { return dn_in(p.fz, qv, v); });
     __syncthreads();
     for (int e = tid; e < npl * pout; e += 256) {
         const int pl = dw_div(e, pout, p.inv_pout), rem = e - pl * pout;
         const int orow = dw_div(rem, p.Wo, p.inv_wo), oc = rem - orow * p.Wo;
         if (orow >= nrow) continue;
-        const float *xs = dw_sm + pl * pst + orow * S * p.WS + oc * S, *ws = wsm + pl * 9;
+        const float *xs = dw_sm + pl * pst + orow * S * p.WS + oc * S + DW_OX - p.pw, *ws = wsm + pl * 9;
         float acc = 0.0f;
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky)

@@ -213,10 +213,14 @@ def test_e5m2_depthwise_layer_sums(cfg):
 
 @pytest.mark.parametrize("fmt", [(4, 3), (5, 2)], ids=["E4M3", "E5M2"])
 @pytest.mark.parametrize("cfg", [dict(C=16, hw=15, s=1), dict(C=24, hw=13, s=2), dict(C=8, hw=1, s=1),
-                                 dict(C=8, hw=6, s=2)])
-def test_two_row_form_bit_identical(fmt, cfg):
-    """Option "tbx_rw" = 2 (two output rows per thread, the default) against 1: the same terms in
-    the same (ky, kx) order per output, so bit-identical outputs (odd Ho, 1-pixel planes)."""
+                                 dict(C=8, hw=6, s=2), dict(C=32, hw=112, s=1), dict(C=12, hw=56, s=2),
+                                 dict(C=40, hw=7, s=1), dict(C=20, hw=14, s=2)])
+def test_two_row_and_staged_forms_bit_identical(fmt, cfg):
+    """The depthwise table form's three kernels on the same layer: conv_tbx_kernel with option
+    "tbx_rw" = 1 and 2 (two output rows per thread) after the word pre-pass, and the LDS-staged
+    conv_tbs_kernel (option "tbs", the default: pre-pass fused, bands of rows of one plane or groups
+    of whole planes) -- the same terms in the same (ky, kx) order per output, so bit-identical
+    outputs (odd Ho, 1-pixel planes, ragged quads, MobileNetV2's 112 / 56 / 14 / 7 planes)."""
     from fp8_quantization_amd import _lib
     rng = np.random.default_rng(cfg["C"] + cfg["hw"] + cfg["s"])
     E_, M_ = fmt
@@ -235,12 +239,45 @@ def test_two_row_form_bit_identical(fmt, cfg):
         w = (np.ldexp(1.0 + rng.integers(0, 4, size=(C, 1, 3, 3)) / 4.0, rng.integers(-14, 8, size=(C, 1, 3, 3)))
              * rng.choice([-1.0, 1.0], size=(C, 1, 3, 3))).astype(np.float32)
         tab = _table_e5m2("zero")
-    old = _lib.set_option("tbx_rw", 1)
+    old, old_tbs = _lib.set_option("tbx_rw", 1), _lib.set_option("tbs", 0)
     try:
         y1, g1 = _dw_raw(x, w, bA, bW, bR, tab, FL, s, 1, fmt=fmt)
         _lib.set_option("tbx_rw", 2)
         y2, g2 = _dw_raw(x, w, bA, bW, bR, tab, FL, s, 1, fmt=fmt)
+        _lib.set_option("tbs", 1)
+        y3, g3 = _dw_raw(x, w, bA, bW, bR, tab, FL, s, 1, fmt=fmt)
     finally:
         _lib.set_option("tbx_rw", old)
-    assert g1 == 0 and g2 == 0
+        _lib.set_option("tbs", old_tbs)
+    assert g1 == 0 and g2 == 0 and g3 == 0
     assert np.array_equal(y1.view(np.uint32), y2.view(np.uint32))
+    assert np.array_equal(y1.view(np.uint32), y3.view(np.uint32))
+
+
+@pytest.mark.parametrize("fmt", [(4, 3), (5, 2)], ids=["E4M3", "E5M2"])
+def test_staged_form_full_model_bit_identical(fmt):
+    """A full-size MobileNetV2 (224 x 224, width 1: every depthwise geometry of the benchmark) in
+    the fixed-range state: logits with the staged depthwise form (input quantizer and BN epilogue
+    fused into it) equal those of the pre-pass + gather form to the bit."""
+    from fp8_quantization_amd import _lib
+    from fp8_quantization_amd.mobilenet_workload import mobilenet_v2_approx
+    torch.manual_seed(5)
+    m = mobilenet_v2_approx(input_size=224, n_class=1000, bn_stats_batches=1, device=DEV, withComp=False,
+                            expo_width=fmt[0], mant_width=fmt[1]).to(DEV).eval()
+    g = torch.Generator().manual_seed(2)
+    m.quantized()
+    m.estimate_ranges()
+    with torch.no_grad():
+        m(torch.randn((2, 3, 224, 224), generator=g).to(DEV))
+    m.fix_ranges()
+    x = torch.randn((2, 3, 224, 224), generator=g).to(DEV)
+    with torch.no_grad():
+        y1 = m(x).cpu().numpy()
+    old = _lib.set_option("tbs", 0)
+    try:
+        with torch.no_grad():
+            y0 = m(x).cpu().numpy()
+    finally:
+        _lib.set_option("tbs", old)
+    assert np.isfinite(y1).all()
+    assert np.array_equal(y0.view(np.uint32), y1.view(np.uint32))
