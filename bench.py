@@ -374,8 +374,8 @@ def run(args, dev, rank=0, world=1):
             res["roofline"] = {
                 "bound": "hbm",
                 "kernel": "dn_gemm_bf16 (csrc/gemm_dense.h: the exact product on the bf16 matrix core, "
-                          "implicit-GEMM conv / matmul, groups = 1) and dn_group_conv (the depthwise convs, fp32 "
-                          "FMAs); timed per op with its operand packing and gated fp32 units",
+                          "implicit-GEMM conv / matmul, groups = 1) and dn_dw3_kernel (the depthwise convs, LDS-staged "
+                          "fp32 FMAs); timed per op with its operand packing and gated fp32 units",
                 "achieved": gbs,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
