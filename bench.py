@@ -398,7 +398,7 @@ def run(args, dev, rank=0, world=1):
                                         "recomputed by the literal restatement")
         if paths is not None:
             res["gemm_paths"] = dict(paths, note="timed steps only: approx GEMM launches per kernel path "
-                                                 "(fp8a_path_stats; one_hot = opt-in E4M3 one-hot path)")
+                                                 "(fp8a_path_stats)")
         if world == 1 and not args.no_cpu_baseline and (args.expo_width, args.mant_width) == (4, 3) \
                 and not args.no_approx:
             res["cpu_baseline"] = cpu_baseline(shapes, get_error_table_NN(4, 3, args.with_comp, 3), args.cpu_columns)

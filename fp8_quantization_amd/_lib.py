@@ -16,7 +16,7 @@ V5, OFUF, OF_OPT, UF_OPT = 32, 64, 128, 256  # v5 integer-adder model (include/f
 OK, EINVAL, EFORMAT, EHIP = 0, -1, -2, -3
 DENSE_E4M3, DENSE_E5M2, DENSE_BF16 = 0, 1, 2  # fp8a_dense_* operand formats
 
-SYMBOLS = ("fp8a_version", "fp8a_last_error", "fp8a_fallback_stats", "fp8a_path_stats", "fp8a_set_option", "fp8a_debug_stats", "fp8a_decompose", "fp8a_quant", "fp8a_matmul_workspace_size",
+SYMBOLS = ("fp8a_version", "fp8a_last_error", "fp8a_fallback_stats", "fp8a_path_stats", "fp8a_set_option", "fp8a_decompose", "fp8a_quant", "fp8a_matmul_workspace_size",
            "fp8a_matmul_workspace_size_mnk", "fp8a_matmul", "fp8a_terms", "fp8a_conv2d_workspace_size", "fp8a_conv2d",
            "fp8a_conv2d_bn_act", "fp8a_conv2d_qin_workspace_size", "fp8a_conv2d_qin",
            "fp8a_conv2d_block_workspace_size", "fp8a_conv2d_block", "fp8a_max_pool2d", "fp8a_avg_pool2d_plane", "fp8a_im2col",
@@ -50,7 +50,6 @@ def load():
         "fp8a_fallback_stats": ([P, I], I),
         "fp8a_path_stats": ([P, I], I),
         "fp8a_set_option": ([ctypes.c_char_p, I], I),
-        "fp8a_debug_stats": ([P, I], I),
         "fp8a_decompose": ([P, I64, I64, I64, I, I, P, I64, U, P, P, P], I),
         "fp8a_quant": ([P, I64, I, I, P, U, P, P], I),
         "fp8a_matmul_workspace_size": ([], SZ),
@@ -143,32 +142,33 @@ def fallback_stats(reset=False):
     return dict(exact_launches=int(out[0]), exact_units=int(out[1]), f32_reruns=int(out[2]), tb_launches=int(out[3]))
 
 
-PATHS = ("one_hot", "f8mx", "tt", "tt16", "fast", "exact", "dense", "v5mx")
+PATHS = ("f8mx", "tt", "tt16", "fast", "exact", "dense", "v5mx")
 
 
 def path_stats(reset=False):
     """fp8a_path_stats: launches per GEMM path since load / the last reset."""
     L = load()
-    out = (ctypes.c_uint64 * 8)()
+    out = (ctypes.c_uint64 * len(PATHS))()
     check(L.fp8a_path_stats(ctypes.cast(out, ctypes.c_void_p), 1 if reset else 0), "fp8a_path_stats")
     return {k: int(v) for k, v in zip(PATHS, out)}
 
 
+_option_gen = 0
+
+
+def option_generation():
+    """Incremented by every set_option call (caches of option-dependent host decisions key on it)."""
+    return _option_gen
+
+
 def set_option(name, value):
     """fp8a_set_option: returns the previous value."""
+    global _option_gen
     rc = load().fp8a_set_option(name.encode(), int(value))
     if rc < 0:
         check(rc, "fp8a_set_option")
+    _option_gen += 1
     return rc
-
-
-def debug_stats(reset=False):
-    """fp8a_debug_stats (counted while set_option("oh_stats", 1)): the one-hot path's candidate
-    entries, excluded weights, nonempty / examined (A element, 64-column tile) segments."""
-    L = load()
-    out = (ctypes.c_uint64 * 4)()
-    check(L.fp8a_debug_stats(ctypes.cast(out, ctypes.c_void_p), 1 if reset else 0), "fp8a_debug_stats")
-    return dict(entries=int(out[0]), excluded=int(out[1]), segments_nonempty=int(out[2]), segments=int(out[3]))
 
 
 def dense_stats(reset=False):

@@ -433,7 +433,9 @@ def _(x, w, bA, bW, bR, table, E, M, flags, stride, padding, dilation, groups, i
     return x.new_empty((Bn, Cout, Ho, Wo)), one, onei, one.clone(), onei.clone()
 
 
-@torch.library.custom_op("fp8approx::conv2d_chain", mutates_args=("out_image",))
+# in_image is mutated too: an image that arrived invalid is re-decoded in place by the consumer's
+# gated pre-pass (xm_decode_a / tbx_decode_a write its words from x)
+@torch.library.custom_op("fp8approx::conv2d_chain", mutates_args=("in_image", "out_image"))
 def _conv2d_chain_op(x: torch.Tensor, w: torch.Tensor, bA: Optional[torch.Tensor], bW: torch.Tensor,
                      bR: torch.Tensor, table: torch.Tensor, E: int, M: int, flags: int, stride: list[int],
                      padding: list[int], dilation: list[int], groups: int, in_maxval: Optional[torch.Tensor],

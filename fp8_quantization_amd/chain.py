@@ -70,11 +70,16 @@ class ChainConsumerMixin:
     def chain_wants_image(self):
         """The input word image this layer's launch would read: 0 none, 1 the matrix-core form, 2 the
         tensor-bias table form (single-output-channel groups; fp8a_conv2d_wants_image)."""
-        E, M, table, flags = self._approx_config()
-        key = (E, M, int(flags), tuple(table.reshape(-1).tolist()) if table is not None else None)
+        # keyed on the layer's approx parameters and the library's option generation (an option such
+        # as af32_maxct changes the answer), so the table is not rebuilt and re-listed every forward
+        from . import _lib
+        p = self.custom_approx_params
+        key = (tuple(sorted((k, v) for k, v in p.items() if isinstance(v, (bool, int, float, str)))),
+               _lib.option_generation())
         cached = getattr(self, "_chain_wants", None)
         if cached is None or cached[0] != key:
             from .approx_ops import conv2d_wants_image
+            E, M, table, flags = self._approx_config()
             cached = (key, conv2d_wants_image(self.out_channels, self.kernel_size, self.padding, self.groups, E, M,
                                               table, flags, self.stride, self.dilation))
             self._chain_wants = cached

@@ -1,5 +1,5 @@
 // conv_tbx.h -- E4M3 depthwise (single-output-channel groups) with the tensor-bias semantics,
-// table form (included by fp8approx.hip inside namespace fp8a, after conv_tb_fast_kernel).
+// table form.
 //
 // The reference takes single-column products down its tensor-bias path (approx_calculation.py:
 // 800-809): with int32-tensor biases >= 2, param_prepare's integer powers make
@@ -22,6 +22,12 @@
 // consecutive outputs of one row and gathers the input words they share once.  Off-grid inputs,
 // the exactness window and the bias window raise the gate word and conv_tb_direct_kernel
 // recomputes the launch exactly (as behind conv_tb_fast_kernel).
+#pragma once
+#include "fp8approx_common.h"
+#include "gemm_dense.h"
+#include "gemm_f8mx.h"
+
+namespace fp8a {
 constexpr int TBX_TW = 4;  // outputs per thread along wo
 
 struct TbxArgs {
@@ -385,3 +391,5 @@ __global__ __launch_bounds__(256) void conv_v5dw_kernel(const uint32_t *aw, cons
     }
     if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(gate, 1u);
 }
+
+}  // namespace fp8a

@@ -1,13 +1,10 @@
-// fp8approx.hip -- MI355X (gfx950) kernels and C-ABI of the approx-FP8 matmul/conv engine.
-//
-// Hot path: approx_v9 (revollllt/FP8_quantization, approx/approx_matmul_whole_v9.py:10-169)
-// as a register-blocked VALU GEMM.  The approximate product cannot use MFMA (its mantissa
-// product depends on a per-pair error table and a per-product re-quantisation), so the kernel
-// is VALU-bound: 64x64 output tile per 256-thread workgroup, 4x4 outputs per thread, K staged
-// through LDS 16 deep.  Operands are decoded (sign / exponent / mantissa / table row) ONCE per
-// workgroup while staging; the inner loop costs 8 VALU ops per product without an error table,
-// 11 with the E4M3 table, 14 with E3M4/E2M5 compensation tables.  See DESIGN.md for the
-// derivation and the exactness argument.
+// fp8approx.hip -- the C-ABI (include/fp8approx.h) of the MI355X (gfx950) approx-FP8 matmul/conv
+// engine: argument checks, table packing, workspace layout, the host dispatch of the GEMM paths
+// (run_gemm), the convolution / linear entry points, and the small kernels (split-K reduce, gated
+// exact kernel, tensor-bias depthwise forms, fake quantizer, pooling, the exact product of
+// gemm_dense.h).  The approx GEMM kernel families are compiled in their own units (k_*.hip,
+// fp8approx_launch.h).  Hot path: approx_v9 (revollllt/FP8_quantization,
+// approx/approx_matmul_whole_v9.py:10-169); DESIGN.md has the derivations and the exactness argument.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -20,7 +17,14 @@
 #include <string>
 
 #include "../../include/fp8approx.h"
-#include "fp8approx_device.h"
+#include "fp8approx_common.h"
+#include "fp8approx_launch.h"
+#include "gemm_f8mx.h"
+#include "gemm_v5mx.h"
+#include "gemm_tt.h"
+#include "gemm_tt16.h"
+#include "gemm_dense.h"
+#include "conv_tbx.h"
 
 namespace fp8a {
 
@@ -37,22 +41,6 @@ static int hip_check(const char *what) {
     if (e != hipSuccess) return fail(FP8A_EHIP, std::string(what) + ": " + hipGetErrorString(e));
     return FP8A_OK;
 }
-
-// ------------------------------------------------------------------------- table packing
-// The error table (get_error_table_NN, v9:555-592) is a host constant; it is analysed on the
-// host and packed into the launch arguments so the hot loop reads one register per operand:
-//   TM_W1U  : entries in {0,1}   -> 1 bit / entry, 2^M bits per row      (E4M3)
-//   TM_W2S/U: entries in [-2,1] / [0,3] -> 2 bits / entry, R = 2^M*2/32 words per row
-//   TM_LUT  : anything else -> float LUT in LDS (E2M5 no-comp: entries up to 5)
-enum TMode : int { TM_NONE = 0, TM_W1U = 1, TM_W2S1 = 2, TM_W2U1 = 3, TM_W2S2 = 4, TM_W2U2 = 5, TM_LUT = 6,
-                   TM_QAMAA = 7 /* quantize_after_mult_and_add: term = fq(a*b), no decode */,
-                   TM_V5 = 8 /* v5 integer-adder model: code sum + compensation LUT, OF/UF wrap */,
-                   TM_F8 = 9 /* E4M3 with s2n + qbma, table in {0,1}: LDS term LUT + hardware fp8 Q_R */ };
-
-struct TablePack {
-    uint32_t rows[64][2];  // packed rows for the bit modes (2^M <= 64)
-    int8_t raw[1024];      // the full table (2^M x 2^M), row-major; exact path and LUT mode
-};
 
 static int pack_table(const int32_t *table, int M, bool approx, TablePack &tp, int &mode) {
     memset(&tp, 0, sizeof(tp));
@@ -92,835 +80,11 @@ static int pack_table(const int32_t *table, int M, bool approx, TablePack &tp, i
     return FP8A_OK;
 }
 
-// ------------------------------------------------------------------------- GEMM arguments
-// FP8 fake quantizer of the activations (quantize_to_fp8_ste_MM, fp8_quantizer.py:97-173),
-// per tensor: the bias from maxval, then clamp / binade step / round.  fp8_quantize_kernel and the
-// fused input quantization of the approx ops (fp8a_conv2d_qin) share these, bit for bit.
-struct FqIn {
-    const float *mx;  // device maxval [1]; nullptr = the input is already quantized
-    int E, M, S;      // exponent / mantissa / sign bits of the quantizer
-};
-
-__device__ __forceinline__ float fq_bias(float mx, int E, int M) {
-    return rintf((float)(1 << E) - log2f(mx) + log2f(2.0f - p2(-M)) - 1.0f);
-}
-
-__device__ __forceinline__ float fq_apply(float v, float mx, float bias, int M, int sign_bits) {
-    const float xc = fminf(fmaxf(v, sign_bits ? -mx : 0.0f), mx);
-    int e;
-    frexpf(xc, &e);
-    const float ls = (xc == 0.0f) ? 1.0f : fmaxf((float)(e - 1) + bias, 1.0f);
-    const int k = (int)(ls - (float)M - bias);
-    const float sc = p2(k);
-    // sc is a power of two: x / sc == x * 2^-k exactly (same exact quotient, one rounding) while
-    // 2^-k is finite -- a multiply instead of the IEEE division sequence
-    return (k >= -126) ? rintf(xc * p2(-k)) * sc : rintf(xc / sc) * sc;
-}
-
-// Word-image hand-off (round 4, fp8a_conv2d_chain): a convolution's store also writes the NEXT
-// convolution's pre-decoded A operand -- its zero-bordered word image (gemm_f8mx.h: the word of
-// fq_next(y) for every output element y) -- so the next launch skips its xm_decode_a pass (which
-// reads y back and writes the image: 8 B of HBM traffic per element).  Same words as that pass,
-// bit for bit: the same fq_apply / xm_word_a on the same float.  An element outside the
-// matrix-core window sets the image's header word, and the consumer's gated pre-pass then
-// re-decodes its input from y (the fp32 output is always written).
-struct EmitW {
-    uint32_t *w;        // the image's words [Bn][C][awH][awW] (nullptr: no emission)
-    uint32_t *invalid;  // the image's header word
-    int awH, awW, awph, awpw;
-    int Wo;
-    uint32_t hw_mul, hw_shift, wo_mul, wo_shift;  // fastdiv by Ho * Wo and Wo (output index < 2^31)
-    uint32_t hw;
-    FqIn fq;            // the next convolution's input quantizer (per tensor)
-    const int32_t *bR;  // its result bias
-    int Mw;             // its mantissa width (3: e4m3 words, 2: e5m2)
-    int form;           // 0: gemm_f8mx_kernel's words (zero-bordered image); 1: the tensor-bias table
-                        // form's words (conv_tbx.h tbx_decode_a: a depthwise consumer, no border)
-};
-
-struct GemmArgs {
-    const float *A;
-    int64_t lda;
-    const float *B;
-    int64_t sbk, sbn;
-    float *C;
-    int64_t ldc;
-    int64_t M, N, K;
-    int E, Mw;
-    uint32_t kexp, kdc;  // 0x7F800000 and (23 - Mw) << 23 as launch arguments: opaque SGPR operands
-                         // keep q_fast at one v_and_or_b32 / one v_add_u32 (see make_qc)
-    const int32_t *bA;
-    const int32_t *bB;
-    int64_t bBs;
-    const int32_t *bR;
-    uint32_t flags;
-    // output mapping: rowmajor C[m*ldc + n], or NCHW C[(m/hw)*ctot*hw + (coff+n)*hw + m%hw]
-    int nchw;
-    int64_t hw, ctot, coff;
-    uint32_t *flag;  // device word: set by the fast kernel when the exact kernel must run (FB_* bits)
-    // per-unit fallback marks (64 x 64 output units): urow[row unit] / ucol[column unit] for an
-    // operand outside the fast path's window, utile[row unit * nuc + column unit] for a tile whose
-    // terms left it; the gated exact kernel recomputes only the marked units.  nullptr (a
-    // workspace without room for them): any fallback recomputes the whole launch.
-    uint8_t *urow, *ucol, *utile;
-    int64_t nur, nuc;
-    // split-K: block b works on tile b % tiles over k in [s*kchunk, (s+1)*kchunk), s = b / tiles;
-    // with splits > 1 it writes its partial tile to part + s*M*N (the output layout with
-    // ctot = N, coff = 0, ldc = N) and splitk_reduce_kernel sums the splits in order
-    int splits;
-    int64_t kchunk;
-    float *part;
-    // implicit-GEMM convolution: A(m, k) gathered from NCHW x (no im2col image), m = (b, ho, wo),
-    // k = (c, ky, kx) within the group -- the reference's im2col order (approx_calculation.py:745)
-    int conv;
-    const float *X;
-    int64_t Cin, H, W, Ho, Wo, cbase;
-    int kh, kw, sh, sw, ph, pw, dh, dw;
-    uint32_t kk_mul, kk_shift, kw_mul, kw_shift;  // fast division by kh*kw and by kw
-    // qamaa: the res quantizer's FP8 fake quantizer (fp8_quantizer.py:97-173) per product
-    const float *qmax;
-    int qE, qM, qsign;
-    // fused eval-mode BatchNorm + activation epilogue (BNFusedHijacker: F.batch_norm then ReLU /
-    // ReLU6 / Hardtanh): per output channel {scale, shift}; ep_act clamps to [ep_lo, ep_hi]
-    const float2 *ep;
-    int ep_act;
-    float ep_lo, ep_hi;
-    // pre-decoded operands of the matrix-core E4M3 kernel (gemm_f8mx.h): A words (conv: the
-    // group's [Bn][aw_c][H][W] slice; matrix: [M][awld]), B column pairs [Kpad][npad / 2]
-    const uint32_t *aw;
-    int64_t awld, aw_c;
-    int64_t awH, awW;  // conv: the word image's height / width (H + 2 ph, W + 2 pw when zero-padded)
-    int awph, awpw;    // conv: x's offset inside the word image (the zero border's width)
-    int wfmt;          // pre-decoded operand format: 0 = gemm_f8mx_kernel's, 1 = gemm_tt_kernel's, 2 = gemm_tt16_kernel's,
-                       // 3 = gemm_oh_kernel's (u16 A codes in the same image layout, gemm_oh.h)
-    int ttf7;          // gemm_tt_kernel: the table has negative entries (the F7 sign rule)
-    int af32;          // gemm_f8mx_kernel reads A as fp32 and decodes it while staging (no A pre-pass)
-    int xncg;          // gemm_f8mx_kernel's column groups per tile (4: 128 x 64, 2: 128 x 32, 1: 256 x 16)
-    const uint2 *bqw;
-    // the one-hot E4M3 path (gemm_oh.h): B codes [npad][kpad] (u8), B block scales [npad][kpad / 4]
-    // (E8M0), the sorted candidate lists [kpad][npad / 64][64] (u32) and their count blocks
-    // [kpad][npad / 64][OH_CB] (u8) and the correction slice (split-K partial layout); the A shift
-    // sA = 6 - bA is derived on the device (bA may be the fused input quantizer's)
-    const uint8_t *ohb, *ohs, *ohc;
-    const uint32_t *ohl;
-    float *ohd;
-    int ohstats;  // count into g_ohstat (diagnostics)
-    const uint32_t *lutw;  // the LDS table image (XM_LUT_WORDS words), written by xm_decode_b
-    // E5M2 (gemm_f8mx_kernel XF = 1): per (K-step, 16-column group) the nonzero B elements' exponent
-    // range, (max e_b + 128) | (min e_b + 128) << 8 ([kpad][npad / 16]; 0xFF00 when all are zero)
-    const uint16_t *ebr;
-    int xm_vmin;  // the smallest binade of the table value V' (0: V' >= 1, -1 with a {0,1} table)
-    int64_t npad;
-    // fused input quantization (fp8a_conv2d_qin): A = fq(X); the quantizer's bias is written to
-    // fq_bias / fq_ibias by the A pre-decode, and bA points at fq_ibias
-    FqIn fqin;
-    float *fq_bias;
-    int32_t *fq_ibias;
-    // block-output epilogue (fp8a_conv2d_block): after BN / activation, y += res (same index as
-    // y), then the post clamp (post_act), then the block's output quantizer (post_fq)
-    const float *res;
-    int post_act;
-    float post_lo, post_hi;
-    FqIn post_fq;
-    EmitW em;              // word-image emission for the next convolution (em.w nullptr: off)
-    const uint32_t *gate;  // xm_decode_a: run only if *gate != 0 (the input image arrived invalid)
-    const uint32_t *in_img; // the input's word image (header + words) a previous launch emitted, or nullptr
-    TablePack tab;
-};
-
-// Fallback flag word bits: FB_ANY = some output unit needs the exact kernel, FB_ALL = every
-// unit does (a bias outside the exactness window, or no unit marks in the workspace).  (Bits
-// 1-4 belong to gemm_tt16_kernel's f16 window, gemm_tt16.h.)
-constexpr uint32_t FB_ANY = 1u, FB_ALL = 32u;
-// FB_HALF: an E5M2 tile of gemm_f8mx_kernel's plain form met the result grid's top binade and
-// asks the halved-block form (XF = 2) to recompute it; its unit marks carry UT_HALF.  Unit mark
-// bits: UT_EXACT = recompute in the exact kernel, UT_HALF = recompute in the halved-block form
-// (kept set by a halved-block tile that fails, so the tiles sharing the unit still see it).
-constexpr uint32_t FB_HALF = 64u;
-constexpr uint8_t UT_EXACT = 1u, UT_HALF = 2u;
-
-// Fallback flag value of a block that found a bad operand: FB_ANY once the unit marks are
-// written, FB_ALL too without them (or when `all`).
-__device__ __forceinline__ uint32_t fb_bits(const GemmArgs &p, bool all = false) {
-    return (all || p.urow == nullptr) ? (FB_ANY | FB_ALL) : FB_ANY;
-}
-
 // Fallback statistics since load (or the last reset): [0] launches whose gated exact kernel
 // ran, [1] 64 x 64 output units it recomputed, [2] launches rerun in gemm_tt_kernel's f32 form
 // (gemm_tt16_kernel's f16 window left), [3] tensor-bias launches recomputed by
 // conv_tb_direct_kernel.  Read with fp8a_fallback_stats (include/fp8approx.h).
 __device__ unsigned long long g_fallback[4];
-// In-kernel clock of gemm_f8mx_kernel (diagnostic build only: -DFP8A_CLOCK_STAMP=1, tools/clock_probe.py):
-// thread 0 of every workgroup adds its s_memtime and s_memrealtime (100 MHz) deltas; the clock the
-// chip held = sum dt / sum dr x 100 MHz (MI355X_MICROARCH.md, DVFS give-back item 6).  Nothing
-// else reads g_clk; the product build compiles no stamp.
-#ifndef FP8A_CLOCK_STAMP
-#define FP8A_CLOCK_STAMP 0
-#endif
-__device__ unsigned long long g_clk[3];
-#if FP8A_CLOCK_STAMP
-#define FP8A_CLK_BEGIN const uint64_t clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
-#define FP8A_CLK_END                                                                                   \
-    if (threadIdx.x == 0) {                                                                            \
-        const uint64_t clk_t1 = __builtin_amdgcn_s_memtime(), clk_r1 = __builtin_amdgcn_s_memrealtime(); \
-        atomicAdd(&g_clk[0], (unsigned long long)(clk_t1 - clk_t0));                                   \
-        atomicAdd(&g_clk[1], (unsigned long long)(clk_r1 - clk_r0));                                   \
-        atomicAdd(&g_clk[2], 1ull);                                                                    \
-    }
-#else
-#define FP8A_CLK_BEGIN
-#define FP8A_CLK_END
-#endif
-// Diagnostic counters of the one-hot path (fp8a_debug_stats): [0] candidate entries the correction
-// kernel processed, [1] excluded weights (outside their MX block's window), [2] (A element, 64-column
-// tile) segments with at least one candidate, [3] A elements x 64-column tiles examined.
-__device__ unsigned long long g_ohstat[4];
-
-// Mark the row units of output rows [m_lo, m_hi) / the column unit of column n / the units of
-// the output tile (m0 .. m0 + rows - 1, n0 .. n0 + 63) for the exact kernel (plain byte stores:
-// every writer stores 1).  The caller raises the flag word (fb_bits).
-__device__ __forceinline__ void fb_rows(const GemmArgs &p, int64_t m_lo, int64_t m_hi) {
-    if (p.urow == nullptr || m_hi <= m_lo) return;
-    for (int64_t u = m_lo >> 6; u <= (m_hi - 1) >> 6; ++u) p.urow[u] = 1;
-}
-__device__ __forceinline__ void fb_col(const GemmArgs &p, int64_t n) {
-    if (p.ucol != nullptr) p.ucol[n >> 6] = 1;
-}
-__device__ __forceinline__ void fb_tile(const GemmArgs &p, int64_t m0, int64_t rows, int64_t n0,
-                                        uint8_t mark = UT_EXACT) {
-    if (p.utile == nullptr) return;
-    const int64_t hi = min(m0 + rows, p.M);
-    for (int64_t u = m0 >> 6; u <= (hi - 1) >> 6; ++u) p.utile[u * p.nuc + (n0 >> 6)] = mark;
-}
-
-// The block-output epilogue on one value / four values of the output at index o; pb = the post
-// quantizer's bias (post_bias()).
-__device__ __forceinline__ float post_bias(const GemmArgs &p) {
-    return p.post_fq.mx ? fq_bias(*p.post_fq.mx, p.post_fq.E, p.post_fq.M) : 0.0f;
-}
-
-__device__ __forceinline__ float post_tail(const GemmArgs &p, float v, float pb) {
-    if (p.post_act) v = fminf(fmaxf(v, p.post_lo), p.post_hi);
-    if (p.post_fq.mx) v = fq_apply(v, *p.post_fq.mx, pb, p.post_fq.M, p.post_fq.S);
-    return v;
-}
-
-__device__ __forceinline__ float post1(const GemmArgs &p, int64_t o, float v, float pb) {
-    if (p.res) v += p.res[o];
-    return post_tail(p, v, pb);
-}
-
-__device__ __forceinline__ float4 post4(const GemmArgs &p, int64_t o, float4 v, float pb) {
-    if (p.res) {
-        const float4 r = *reinterpret_cast<const float4 *>(p.res + o);
-        v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
-    }
-    return make_float4(post_tail(p, v.x, pb), post_tail(p, v.y, pb), post_tail(p, v.z, pb), post_tail(p, v.w, pb));
-}
-
-// y = x * scale + shift with scale = gamma * invstd, shift = beta - mean * scale (ATen's eval
-// batch-norm transform), then the activation clamp; c = output channel
-__device__ __forceinline__ float epi(const float2 *ep, int act, float lo, float hi, int64_t c, float x) {
-    if (ep == nullptr) return x;
-    const float2 e = ep[c];
-    const float v = __fmaf_rn(x, e.x, e.y);
-    return act ? fminf(fmaxf(v, lo), hi) : v;
-}
-
-// n / d for 0 <= n < 2^31 via one mulhi: q = (mulhi(n, mul) + n) >> shift (Granlund-Montgomery).
-static void fastdiv_params(uint32_t d, uint32_t &mul, uint32_t &shift) {
-    uint32_t l = 0;
-    while ((1ull << l) < d) ++l;
-    shift = l;
-    mul = (uint32_t)(((1ull << 32) * ((1ull << l) - d)) / d + 1);
-}
-
-__device__ __forceinline__ uint32_t fastdiv(uint32_t n, uint32_t mul, uint32_t shift) {
-    return (__umulhi(n, mul) + n) >> shift;
-}
-
-constexpr int BM = 64, BN = 64, BK = 16, TM = 4, TN = 4, NT = 256;
-constexpr int AP = BM + 4, BP = BN + 4;
-
-__device__ __forceinline__ uint32_t xm_word_a(float x, int M, int xb, uint32_t emnA, int bR, bool &ok);  // gemm_f8mx.h
-__host__ __device__ constexpr int xm_xbias(int Mw);
-
-// A = 0 as an A word of the matrix-core path (gemm_f8mx.h): cvt scale 2^126 (the code is 0), row 0.
-// Nonzero words keep se <= 252, so a zero word is the one with se = 253, and the E5M2 halved form's
-// se + 1 (254: 2^127) still flushes it to 0.
-constexpr uint32_t XM_ZERO_WORD = 253u << 23;
-
-// Word-image emission (EmitW): one word per final output value at NCHW output index o (< 2^31,
-// the host checks).  The next quantizer's constants sit in the image's header (emit_prep_kernel:
-// [1] maxval, [2] its float bias, [3] 2^(1 - bias) bits, [4] bR), made wave-uniform (SGPRs) once
-// per epilogue: the matrix-core kernel runs at its 80-VGPR budget, and per-thread copies of them
-// (or their recomputation from maxval) in VGPRs made it spill.
-struct EmitCtx {
-    float mx, fb;
-    uint32_t emn;
-    int bR;
-};
-__device__ __forceinline__ EmitCtx emit_ctx(const GemmArgs &p) {
-    EmitCtx e{};
-    if (p.em.w == nullptr) return e;
-    const uint4 h = *reinterpret_cast<const uint4 *>(p.em.invalid);  // header words 0-3 (uniform: SGPRs)
-    e.mx = __uint_as_float(__builtin_amdgcn_readfirstlane(h.y));
-    e.fb = __uint_as_float(__builtin_amdgcn_readfirstlane(h.z));
-    e.emn = __builtin_amdgcn_readfirstlane(h.w);
-    e.bR = __builtin_amdgcn_readfirstlane((int)p.em.invalid[4]);
-    return e;
-}
-__device__ __forceinline__ uint32_t emit_word(const GemmArgs &p, const EmitCtx &e, float v, bool &ok) {
-    const float q = fq_apply(v, e.mx, e.fb, p.em.fq.M, p.em.fq.S);
-    if (p.em.form) {  // tbx_decode_a's word of q (a value off the grid / outside the window: invalid)
-        const uint32_t u = __float_as_uint(q), ua = u & 0x7FFFFFFFu, M = (uint32_t)p.em.Mw;
-        ok = ok && (ua == 0u || ((ua & ((1u << (23 - M)) - 1u)) == 0u && ua >= 0x20800000u && ua <= 0x58800000u));
-        return ua == 0u ? 0u : ((u & 0xFF800000u) | (((ua >> (23 - M)) & ((1u << M) - 1u)) << 6));
-    }
-    return xm_word_a(q, p.em.Mw, xm_xbias(p.em.Mw), e.emn, e.bR, ok);
-}
-// word index of NCHW output index o
-__device__ __forceinline__ uint32_t emit_index(const GemmArgs &p, uint32_t uo, uint32_t &wo) {
-    const uint32_t plane = fastdiv(uo, p.em.hw_mul, p.em.hw_shift), pix = uo - plane * p.em.hw;
-    const uint32_t ho = fastdiv(pix, p.em.wo_mul, p.em.wo_shift);
-    wo = pix - ho * (uint32_t)p.em.Wo;
-    return (plane * (uint32_t)p.em.awH + ho + (uint32_t)p.em.awph) * (uint32_t)p.em.awW + wo + (uint32_t)p.em.awpw;
-}
-// Max of v over the wave, then one atomicMax into *dst (v >= 0; 0 records nothing) unless *dst
-// already holds at least v -- every wave of a launch records into the same word, and the read
-// first keeps the atomics (serialised on one L2 line) to the few waves that raise it.  Every lane
-// of the wave must call it.
-__device__ __forceinline__ void wave_max_atomic(uint32_t *dst, uint32_t v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off));
-    if ((threadIdx.x & 63) == 0 && v != 0u && v > __hip_atomic_load(dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-        atomicMax(dst, v);
-}
-// 255 - the scale exponent of a nonzero word (the E5M2 halved-block decision reads the largest,
-// gemm_f8mx.h xm_needs_halving; the header's word 5 collects it for the consumer)
-__device__ __forceinline__ uint32_t word_sehi(uint32_t w) { return w == XM_ZERO_WORD ? 0u : 255u - (w >> 23); }
-
-__device__ __forceinline__ void emit1(const GemmArgs &p, const EmitCtx &e, int64_t o, float v, uint32_t &sehi) {
-    uint32_t wo;
-    const uint32_t wi = emit_index(p, (uint32_t)o, wo);
-    bool ok = true;
-    const uint32_t w = emit_word(p, e, v, ok);
-    p.em.w[wi] = w;
-    sehi = max(sehi, word_sehi(w));
-    if (!ok) atomicOr(p.em.invalid, 1u);
-}
-// four consecutive outputs (o % 4 == 0 in an NCHW plane of hw % 4 == 0): one 16-B store when
-// they sit in one row of the image (Wo % 4 == 0: always; the interior rows start 16-B aligned)
-__device__ __forceinline__ void emit4(const GemmArgs &p, const EmitCtx &e, int64_t o, float4 v, uint32_t &sehi) {
-    uint32_t wo;
-    const uint32_t wi = emit_index(p, (uint32_t)o, wo);
-    bool ok0 = true, ok1 = true, ok2 = true, ok3 = true;
-    const uint4 w = make_uint4(emit_word(p, e, v.x, ok0), emit_word(p, e, v.y, ok1), emit_word(p, e, v.z, ok2),
-                               emit_word(p, e, v.w, ok3));
-    sehi = max(max(sehi, max(word_sehi(w.x), word_sehi(w.y))), max(word_sehi(w.z), word_sehi(w.w)));
-    if (wo + 3 < (uint32_t)p.em.Wo && (wi & 3u) == 0u) {
-        *reinterpret_cast<uint4 *>(p.em.w + wi) = w;
-    } else {
-        p.em.w[wi] = w.x;
-        uint32_t wo1;
-        p.em.w[emit_index(p, (uint32_t)o + 1, wo1)] = w.y;
-        p.em.w[emit_index(p, (uint32_t)o + 2, wo1)] = w.z;
-        p.em.w[emit_index(p, (uint32_t)o + 3, wo1)] = w.w;
-    }
-    if (!(ok0 && ok1 && ok2 && ok3)) atomicOr(p.em.invalid, 1u);
-}
-
-__device__ __forceinline__ int64_t out_index(const GemmArgs &p, int64_t m, int64_t n) {
-    if (!p.nchw) return m * p.ldc + n;
-    const int64_t img = m / p.hw, pix = m - img * p.hw;
-    return (img * p.ctot + p.coff + n) * p.hw + pix;
-}
-
-// Fast-path operand decode straight from the float32 bit pattern (int-bias semantics).
-//   returns ok: x is exactly a value of the (M, b) grid (any exponent: A/B are decoded with
-//               clip_OF=False, v9:58-59) and |x| is 0 or in [2^-62, 2^50] (exactness window:
-//               every product and table term a normal float, every Q_R constant finite,
-//               DESIGN.md §3).  Otherwise the launch is flagged and the exact kernel reruns it.
-//   m        : the M-bit mantissa code = the top M bits of the fp32 mantissa (the s2n scale-up
-//               by 2^M, v9:53, leaves the fp32 mantissa untouched)
-//   c        : sign(x) * 2^floor(log2|x|): the scale of the error-table term.  Scale-up and
-//               scale-back of s2n cancel in it; without s2n a subnormal operand fails the
-//               reference's norm mask (v9:87), so c = 0 there, as for zeros.
-__device__ __forceinline__ bool stage_decode(float x, int M, uint32_t emn, bool s2n, float &c, uint32_t &m) {
-    const uint32_t u = __float_as_uint(x);
-    const uint32_t ua = u & 0x7FFFFFFFu;
-    const uint32_t ex = ua & 0x7F800000u;
-    const bool sub = ua < emn;  // |x| < min_norm = 2^(1-b)
-    const uint32_t sh = (uint32_t)(23 - M) + (sub ? ((emn - ex) >> 23) : 0u);
-    const bool grid = (sh < 24u) ? ((ua & ((1u << sh) - 1u)) == 0u) : (ua == 0u);
-    const bool win = (ua == 0u) || (ua >= 0x20800000u /*2^-62*/ && ua <= 0x58800000u /*2^50*/);
-    m = (ua >> (23 - M)) & ((1u << M) - 1u);
-    c = (ua == 0u || (!s2n && sub)) ? 0.0f : __uint_as_float(u & 0xFF800000u);
-    return grid && win;
-}
-
-// Writes one thread's TM x TN outputs (rows m0 + ty*TM + i, columns n0 + tx*TN + j) to the
-// output mapping, or to its split-K partial slice (same layout); applies the fused BN/activation
-// epilogue when unsplit.
-// EMIT = false compiles the word-image emission out (gemm_f8mx_kernel's non-emitting instances:
-// the emission code alone pushed that kernel past its 80-VGPR budget).
-template <bool EMIT = true>
-__device__ __forceinline__ void store_tile(const GemmArgs &p, int64_t split, int64_t m0, int64_t n0, int ty, int tx,
-                                           float (&acc)[TM][TN]) {
-    const bool partial = p.splits > 1;
-    float *const C = partial ? p.part + split * p.M * p.N : p.C;
-    const int64_t ldc = partial ? p.N : p.ldc, ctot = partial ? p.N : p.ctot, coff = partial ? 0 : p.coff;
-    const int64_t nb = n0 + tx * TN;
-    if (!partial && p.ep != nullptr) {  // fused BN + activation (split-K applies it in the reduction)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int64_t ch = p.coff + min<int64_t>(nb + j, p.N - 1);
-#pragma unroll
-            for (int i = 0; i < TM; ++i) acc[i][j] = epi(p.ep, p.ep_act, p.ep_lo, p.ep_hi, ch, acc[i][j]);
-        }
-    }
-    const float pb = partial ? 0.0f : post_bias(p);
-    const GemmArgs &q = p;
-    // word-image emission from each final value (the split-K reduction emits instead)
-    const bool emit = EMIT && !partial && p.em.w != nullptr;
-    const EmitCtx ec = EMIT ? emit_ctx(p) : EmitCtx{};
-    uint32_t sehi = 0;
-    auto fin1 = [&](int64_t o, float v) {
-        if (partial) return v;
-        v = post1(q, o, v, pb);
-        if (emit) emit1(q, ec, o, v, sehi);
-        return v;
-    };
-    auto fin4 = [&](int64_t o, float4 v) {
-        if (partial) return v;
-        v = post4(q, o, v, pb);
-        if (emit) emit4(q, ec, o, v, sehi);
-        return v;
-    };
-    if (!p.nchw) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            const int64_t m = m0 + ty * TM + i;
-            if (m >= p.M) continue;
-            if (nb + TN <= p.N && ((ldc & 3) == 0) && ((((uintptr_t)C) & 15) == 0)) {
-                *reinterpret_cast<float4 *>(&C[m * ldc + nb]) =
-                    fin4(m * ldc + nb, make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]));
-            } else {
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-                    if (nb + j < p.N) C[m * ldc + nb + j] = fin1(m * ldc + nb + j, acc[i][j]);
-            }
-        }
-    } else {
-        // NCHW: the thread's 4 rows are 4 consecutive pixels; when they lie in one image and
-        // start 16-B aligned, each output channel gets one float4 store.
-        const int64_t mb = m0 + ty * TM;
-        const int64_t img = mb / p.hw, pix = mb - img * p.hw;
-        const bool vec = (pix + TM <= p.hw) && (mb + TM <= p.M) && ((p.hw & 3) == 0) &&
-                         ((((uintptr_t)C) & 15) == 0);
-        if (vec) {
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-                if (nb + j < p.N) {
-                    const int64_t o = (img * ctot + coff + nb + j) * p.hw + pix;
-                    *reinterpret_cast<float4 *>(&C[o]) = fin4(o, make_float4(acc[0][j], acc[1][j], acc[2][j], acc[3][j]));
-                }
-        } else {
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                const int64_t m = mb + i;
-                if (m >= p.M) continue;
-                const int64_t im = m / p.hw, px = m - im * p.hw;
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-                    if (nb + j < p.N) {
-                        const int64_t o = (im * ctot + coff + nb + j) * p.hw + px;
-                        C[o] = fin1(o, acc[i][j]);
-                    }
-            }
-        }
-    }
-    if (emit) wave_max_atomic(p.em.invalid + 5, sehi);
-}
-
-template <bool S2N, bool QBMA, bool GCLIP, int TMODE>
-__global__ __launch_bounds__(NT) void gemm_fast_kernel(const GemmArgs p) {
-    constexpr bool QAMAA = TMODE == TM_QAMAA;
-    constexpr bool V5 = TMODE == TM_V5;
-    constexpr bool F8 = TMODE == TM_F8;
-    constexpr bool TBL = TMODE != TM_NONE && !QAMAA && !F8;
-    constexpr int R = (TMODE == TM_W2S2 || TMODE == TM_W2U2) ? 2 : 1;
-    constexpr bool SGN = (TMODE == TM_W2S1 || TMODE == TM_W2S2 || TMODE == TM_LUT);
-
-    __shared__ __attribute__((aligned(16))) float sA[BK][AP];
-    __shared__ __attribute__((aligned(16))) float sB[BK][BP];
-    __shared__ __attribute__((aligned(16))) float sAc[TBL ? BK : 1][AP];
-    __shared__ __attribute__((aligned(16))) uint32_t sAr[(TBL || F8) ? R * BK : 1][AP];
-    __shared__ __attribute__((aligned(16))) float sBc[TBL ? BK : 1][BP];
-    __shared__ __attribute__((aligned(16))) uint32_t sBm[(TBL || F8) ? BK : 1][BP];
-    // F8: the normalised term V'(sign a, m_a, m_b) = min(sig_a sig_b - T[m_a][m_b] 2^-M, top of
-    // its binade), 17 rows (2 signs x 8 codes + a zero row) x 2 copies x 8 (see F8_ROW)
-    __shared__ __attribute__((aligned(16))) float sF8[F8 ? 17 * 16 : 1];
-    __shared__ float sLut[TMODE == TM_LUT ? 1024 : 1];
-    __shared__ int32_t sLutI[V5 ? 1024 : 1];
-    __shared__ uint32_t sRows[TBL ? 64 * 2 : 1];
-
-    const int tid = threadIdx.x;
-    const int ty = tid >> 4, tx = tid & 15;
-    const int64_t num_mt = (p.M + BM - 1) / BM;
-    const int64_t tiles = num_mt * ((p.N + BN - 1) / BN);
-    const int64_t bid = (int64_t)blockIdx.x % tiles, split = (int64_t)blockIdx.x / tiles;
-    const int64_t m0 = (bid % num_mt) * BM;   // consecutive blocks: same column tile, so the
-    const int64_t n0 = (bid / num_mt) * BN;   // B tile is shared by the 8 XCDs' L2s
-    const int64_t kbeg = split * p.kchunk, kend = min(p.K, kbeg + p.kchunk);
-    const int M = p.Mw;
-    const int bA = QAMAA ? 0 : *p.bA, bR = QAMAA ? 0 : *p.bR;
-    const QC qc = make_qc(p.E, M, bR, p.kexp, p.kdc);
-    FQ fq;
-    if (QAMAA) fq = make_fq(*p.qmax, p.qE, p.qM, p.qsign);
-    const uint32_t emnA = (uint32_t)(128 - bA) << 23;
-    const float ulpM = p2(-M);
-
-    // F8 Q_R: the result grid of bias bR (floor step 2^(-2-bR), binades from 2^(1-bR)) is the
-    // OCP e4m3 grid scaled by 2^(7-bR), so Q_R(y) = 2^(7-bR) * cvt_fp8(y / 2^(7-bR)) (RNE) for y
-    // already clamped to Q_R's bound (the clamp scales with y's binade, so it is folded into the
-    // LUT value V'), except beyond the e4m3 range (NaN: flagged in the epilogue, the exact kernel
-    // reruns the launch)
-    const float f8S = F8 ? __uint_as_float((uint32_t)min(max(134 - bR, 1), 254) << 23) : 0.0f;
-    if (F8) {
-        for (int e = tid; e < 17 * 16; e += NT) {
-            const int r = e >> 4, mb = e & 7;  // both 8-entry copies of a row hold the same values
-            float v = 0.0f;
-            if (r < 16) {
-                const int ma = r & 7;
-                const float t = (float)p.tab.raw[ma * 8 + mb];
-                v = __fmaf_rn(1.0f + 0.125f * ma, 1.0f + 0.125f * mb, -t * 0.125f);  // exact
-                // Q_R's pre-clamp bound 2^e (2 - 2^-M - 2^-22) (QC::kb): the mantissa saturates
-                // instead of carrying, and on the subnormal grid the top tie rounds down
-                v = fminf(v, __uint_as_float(__float_as_uint(v) & 0x7F800000u) * (1.875f - p2(-22)));
-                if (r >= 8) v = -v;
-            }
-            sF8[e] = v;
-        }
-        __syncthreads();
-    }
-    if (TBL) {
-        const int n = 1 << M;
-        for (int i = tid; i < n * 2; i += NT) sRows[i] = p.tab.rows[i >> 1][i & 1];
-        if (TMODE == TM_LUT)
-            for (int i = tid; i < n * n; i += NT) sLut[i] = (float)p.tab.raw[i];
-        if (V5)
-            for (int i = tid; i < n * n; i += NT) sLutI[i] = p.tab.raw[i];
-        __syncthreads();
-    }
-
-    // B staging map: n-contiguous B reads along n, k-contiguous (W[N][K]) along k
-    const bool b_ncontig = (p.sbn == 1);
-    int bcol[4], bkk[4];
-    uint32_t emnB[4];
-    int bbv[4];
-    // Q_R constants 2^(1-bR), 2^(-bR-M), 1.5 * 2^(1-bR+23-M) stay normal; decode fields fit
-    bool bias_ok = bR >= -100 && bR <= 120 && bA >= -100 && bA <= 120;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int e = tid + NT * r;
-        bcol[r] = b_ncontig ? (e & 63) : (e >> 4);
-        bkk[r] = b_ncontig ? (e >> 6) : (e & 15);
-        const int64_t n = n0 + bcol[r];
-        const int bb = (!QAMAA && n < p.N) ? p.bB[n * p.bBs] : 0;
-        bias_ok = bias_ok && bb >= -100 && bb <= 120;
-        // v5: every decoded term 2^(e - bR) (1 + m/2^M) stays a normal float, so the ldexp form
-        // below equals the reference's pow(2, e - bR) * (1 + m/2^M)
-        if (V5) bias_ok = bias_ok && bA + bb <= 120;
-        emnB[r] = (uint32_t)(128 - bb) << 23;
-        bbv[r] = V5 ? bb : 0;
-    }
-    DFmt fA5 = {};
-    int32_t v5max = 0;
-    if (V5) {
-        fA5 = dfmt(p.E, M, bA, false);
-        v5max = ((1 << p.E) << M) - 1;
-    }
-
-    // implicit-conv row of this thread (fixed across k tiles)
-    bool crow_ok = false;
-    int64_t cxoff = 0, chi0 = 0, cwi0 = 0;
-    if (p.conv) {
-        const int64_t m = m0 + (tid & 63);
-        crow_ok = m < p.M;
-        const int64_t hw = p.Ho * p.Wo;
-        const int64_t img = crow_ok ? m / hw : 0, pix = crow_ok ? m - img * hw : 0;
-        const int64_t ho = pix / p.Wo, wo = pix - ho * p.Wo;
-        cxoff = (img * p.Cin + p.cbase) * p.H * p.W;
-        chi0 = ho * p.sh - p.ph;
-        cwi0 = wo * p.sw - p.pw;
-    }
-
-    float acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = 0.0f;
-
-    // per-thread staging slots (fixed across k tiles)
-    int arow[(BM * BK) / NT], akk[(BM * BK) / NT];
-#pragma unroll
-    for (int r = 0; r < (BM * BK) / NT; ++r) {
-        const int e = tid + NT * r;
-        arow[r] = p.conv ? (tid & 63) : (e >> 4);       // conv: lanes along m (consecutive pixels)
-        akk[r] = p.conv ? ((tid >> 6) + 4 * r) : (e & 15);  // matrix: lanes along k (row-major A)
-    }
-    float xa[(BM * BK) / NT], xb[(BN * BK) / NT];
-    // global -> registers for the tile at k0 (issued one tile ahead of its use)
-    auto load_tile = [&](int64_t k0) {
-#pragma unroll
-        for (int r = 0; r < (BM * BK) / NT; ++r) {
-            float x = 0.0f;
-            const int64_t k = k0 + akk[r];
-            if (!p.conv) {
-                const int64_t m = m0 + arow[r];
-                if (m < p.M && k < kend) x = p.A[m * p.lda + k];
-            } else if (crow_ok && k < kend) {  // implicit im2col
-                const uint32_t c = fastdiv((uint32_t)k, p.kk_mul, p.kk_shift);
-                const uint32_t t = (uint32_t)k - c * (uint32_t)(p.kh * p.kw);
-                const uint32_t ky = fastdiv(t, p.kw_mul, p.kw_shift);
-                const uint32_t kx = t - ky * (uint32_t)p.kw;
-                const int64_t hi = chi0 + (int64_t)ky * p.dh, wi = cwi0 + (int64_t)kx * p.dw;
-                if (hi >= 0 && hi < p.H && wi >= 0 && wi < p.W) x = p.X[cxoff + ((int64_t)c * p.H + hi) * p.W + wi];
-            }
-            xa[r] = x;
-        }
-#pragma unroll
-        for (int r = 0; r < (BN * BK) / NT; ++r) {
-            const int64_t n = n0 + bcol[r], k = k0 + bkk[r];
-            xb[r] = (n < p.N && k < kend) ? p.B[k * p.sbk + n * p.sbn] : 0.0f;
-        }
-    };
-    load_tile(kbeg);
-
-    for (int64_t k0 = kbeg; k0 < kend; k0 += BK) {
-        bool bad = !bias_ok;
-        // ---- decode + stage A (64 x 16)
-#pragma unroll
-        for (int r = 0; r < (BM * BK) / NT; ++r) {
-            const int row = arow[r], kk = akk[r];
-            const float x = xa[r];
-            float c;
-            uint32_t mc;
-            if (V5) {  // exact decode with clip_OF (v5:22, 27-38): any fp32 input
-                int e, m;
-                exact_dec(x, fA5, true, e, m);
-                sA[kk][row] = __int_as_float((e << M) + m);
-                sAc[kk][row] = __uint_as_float(x < 0.0f ? 0x80000000u : 0u);
-                sAr[kk][row] = (uint32_t)m << M;
-                continue;
-            }
-            if (F8) {
-                // cvt scale 2^(7-bR) / |c| (applied to x' = V' * c_b inside the conversion) and the
-                // byte offset of the LUT row; rows with ty even / odd read copies on disjoint banks
-                bad |= !stage_decode(x, M, emnA, true, c, mc);
-                const uint32_t cb = __float_as_uint(c);
-                const int se = 261 - bR - (int)((cb >> 23) & 0xFFu);
-                const bool zero = (cb & 0x7FFFFFFFu) == 0u;
-                bad |= !zero && (se < 1 || se > 254);
-                sA[kk][row] = zero ? f8S : __uint_as_float((uint32_t)min(max(se, 1), 254) << 23);
-                const uint32_t rr = zero ? 16u : ((cb >> 31) * 8u + mc);
-                sAr[kk][row] = (rr * 16u + (uint32_t)((row >> 2) & 1) * 8u) * 4u;
-                continue;
-            }
-            if (!QAMAA) bad |= !stage_decode(x, M, emnA, S2N, c, mc);
-            sA[kk][row] = x;
-            if (TBL) {
-                sAc[kk][row] = c * ulpM;  // the 2^-M of mult_result_mant's table term (v9:182)
-                if (TMODE == TM_LUT) {
-                    sAr[kk][row] = mc << M;
-                } else {
-                    sAr[kk][row] = sRows[mc * 2];
-                    if (R == 2) sAr[BK + kk][row] = sRows[mc * 2 + 1];
-                }
-            }
-        }
-        // ---- decode + stage B (16 x 64)
-#pragma unroll
-        for (int r = 0; r < (BN * BK) / NT; ++r) {
-            const int col = bcol[r], kk = bkk[r];
-            const float x = xb[r];
-            float c;
-            uint32_t mc;
-            if (V5) {  // B code with the product's exponent offset folded in: -(bA + bB - bR) << M
-                int e, m;
-                exact_dec(x, dfmt(p.E, M, bbv[r], false), true, e, m);
-                sB[kk][col] = __int_as_float(((e - (bA + bbv[r] - bR)) << M) + m);
-                sBc[kk][col] = __uint_as_float(x < 0.0f ? 0x80000000u : 0u);
-                sBm[kk][col] = (uint32_t)m;
-                continue;
-            }
-            if (F8) {
-                bad |= !stage_decode(x, M, emnB[r], true, c, mc);
-                sB[kk][col] = c;  // sign(b) 2^floor(log2|b|), 0 for b = 0
-                sBm[kk][col] = mc * 4u;
-                continue;
-            }
-            if (!QAMAA) bad |= !stage_decode(x, M, emnB[r], S2N, c, mc);
-            sB[kk][col] = x;
-            if (TBL) {
-                sBc[kk][col] = c;
-                sBm[kk][col] = (TMODE == TM_LUT || TMODE == TM_W1U) ? mc : mc * 2u;
-            }
-        }
-        // Off-grid operands / biases outside the exact window: flag the launch; the gated
-        // exact kernel that follows on the stream then recomputes the whole product.
-        const int anybad = __syncthreads_or(bad ? 1 : 0);
-        if (anybad && tid == 0) {
-            fb_tile(p, m0, BM, n0);  // (every column tile staging the bad rows marks itself)
-            atomicOr(p.flag, fb_bits(p));
-        }
-        if (k0 + BK < kend) load_tile(k0 + BK);  // next tile's loads fly during this tile's math
-
-        // fp32 accumulation in k order: measured max |error| ~3e-7 x sum|terms| at K = 4608 on
-        // realistic data, 30x inside the 1e-5 parity tolerance
-        float (&tacc)[TM][TN] = acc;
-
-        // v5 terms of zero operands are not zero (the code sum of a zero is still decoded), so
-        // the zero padding of a ragged last K-tile must not be summed there
-        const int kk_end = V5 ? (int)min<int64_t>(BK, kend - k0) : BK;
-#pragma unroll 2
-        for (int kk = 0; kk < kk_end; ++kk) {
-            const float4 a4 = *reinterpret_cast<const float4 *>(&sA[kk][ty * TM]);
-            const float4 b4 = *reinterpret_cast<const float4 *>(&sB[kk][tx * TN]);
-            const float a[TM] = {a4.x, a4.y, a4.z, a4.w};
-            const float b[TN] = {b4.x, b4.y, b4.z, b4.w};
-            if (QAMAA) {
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) tacc[i][j] += fq_fast(a[i] * b[j], fq);
-            } else if (F8) {
-                // a = scales, b = c_b; term = Q_R(V' * c_a * c_b) via the scaled fp8 round trip
-                const uint4 ia4 = *reinterpret_cast<const uint4 *>(&sAr[kk][ty * TM]);
-                const uint4 ib4 = *reinterpret_cast<const uint4 *>(&sBm[kk][tx * TN]);
-                const uint32_t ia[TM] = {ia4.x, ia4.y, ia4.z, ia4.w};
-                const uint32_t ib[TN] = {ib4.x, ib4.y, ib4.z, ib4.w};
-                const char *lut = reinterpret_cast<const char *>(sF8);
-#pragma unroll
-                for (int i = 0; i < TM; ++i) {
-                    float xv[TN];
-#pragma unroll
-                    for (int j = 0; j < TN; ++j)
-                        xv[j] = *reinterpret_cast<const float *>(lut + (ia[i] + ib[j])) * b[j];
-                    typedef short s2 __attribute__((ext_vector_type(2)));
-                    s2 code = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32((s2){0, 0}, xv[0], xv[1], a[i], false);
-                    code = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(code, xv[2], xv[3], a[i], true);
-                    const uint32_t cu = __builtin_bit_cast(uint32_t, code);
-                    const auto lo = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(cu, f8S, false);
-                    const auto hi = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(cu, f8S, true);
-                    tacc[i][0] += lo[0];
-                    tacc[i][1] += lo[1];
-                    tacc[i][2] += hi[0];
-                    tacc[i][3] += hi[1];
-                }
-            } else if (V5) {
-                const float4 ac4 = *reinterpret_cast<const float4 *>(&sAc[kk][ty * TM]);
-                const uint4 ar4 = *reinterpret_cast<const uint4 *>(&sAr[kk][ty * TM]);
-                const float4 bc4 = *reinterpret_cast<const float4 *>(&sBc[kk][tx * TN]);
-                const uint4 bm4 = *reinterpret_cast<const uint4 *>(&sBm[kk][tx * TN]);
-                const uint32_t as[TM] = {__float_as_uint(ac4.x), __float_as_uint(ac4.y), __float_as_uint(ac4.z),
-                                         __float_as_uint(ac4.w)};
-                const uint32_t bs[TN] = {__float_as_uint(bc4.x), __float_as_uint(bc4.y), __float_as_uint(bc4.z),
-                                         __float_as_uint(bc4.w)};
-                const uint32_t ar[TM] = {ar4.x, ar4.y, ar4.z, ar4.w};
-                const uint32_t bm[TN] = {bm4.x, bm4.y, bm4.z, bm4.w};
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) {
-                        int32_t r = __float_as_int(a[i]) + __float_as_int(b[j]) + sLutI[ar[i] + bm[j]];
-                        r = v5_ofuf(r, v5max, M, p.flags);
-                        const int32_t e = r >> M, m = r & ((1 << M) - 1);
-                        // expo 0: m * 2^(1-bR-M); else (2^M + m) * 2^(e-bR-M) (also for e < 0)
-                        const float v = (e == 0) ? ldexpf((float)m, 1 - bR - M)
-                                                 : ldexpf((float)(m + (1 << M)), e - bR - M);
-                        tacc[i][j] += __uint_as_float(__float_as_uint(v) ^ as[i] ^ bs[j]);
-                    }
-            } else if (!TBL) {
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) {
-                        const float g = a[i] * b[j];
-                        tacc[i][j] += QBMA ? q_fast<GCLIP, true>(g, qc) : g;
-                    }
-            } else {
-                const float4 ac4 = *reinterpret_cast<const float4 *>(&sAc[kk][ty * TM]);
-                const uint4 ar4 = *reinterpret_cast<const uint4 *>(&sAr[kk][ty * TM]);
-                const uint4 ar4h = (R == 2) ? *reinterpret_cast<const uint4 *>(&sAr[BK + kk][ty * TM]) : make_uint4(0, 0, 0, 0);
-                const float4 bc4 = *reinterpret_cast<const float4 *>(&sBc[kk][tx * TN]);
-                const uint4 bm4 = *reinterpret_cast<const uint4 *>(&sBm[kk][tx * TN]);
-                const float ac[TM] = {ac4.x, ac4.y, ac4.z, ac4.w};
-                const uint32_t ar0[TM] = {ar4.x, ar4.y, ar4.z, ar4.w};
-                const uint32_t ar1[TM] = {ar4h.x, ar4h.y, ar4h.z, ar4h.w};
-                const float bc[TN] = {bc4.x, bc4.y, bc4.z, bc4.w};
-                const uint32_t bm[TN] = {bm4.x, bm4.y, bm4.z, bm4.w};
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) {
-                        // v0 = a*b - t*cA*cB is exactly representable, so one
-                        // fused op yields it; g = a*b is formed only where a mask needs it.
-                        const float cab = ac[i] * bc[j];
-                        constexpr bool NEED_G = !S2N || (QBMA && SGN);
-                        // g = a*b is exact (two (M+1)-bit significands); formed only where a mask
-                        // needs it, and then the table term is folded into one fma on it
-                        const float g = NEED_G ? a[i] * b[j] : 0.0f;
-                        float v0;
-                        if (TMODE == TM_W1U) {
-                            const int t = __builtin_amdgcn_sbfe((int)ar0[i], bm[j], 1);
-                            const float tc = __uint_as_float(__float_as_uint(cab) & (uint32_t)t);
-                            v0 = NEED_G ? g - tc : __fmaf_rn(a[i], b[j], -tc);
-                        } else {
-                            float tf;  // the table entry
-                            if (TMODE == TM_LUT) {
-                                tf = sLut[ar0[i] + bm[j]];
-                            } else {
-                                const uint32_t w = (R == 2 && (bm[j] & 32u)) ? ar1[i] : ar0[i];
-                                const int t = SGN ? (int)__builtin_amdgcn_sbfe((int)w, bm[j], 2)
-                                                  : (int)__builtin_amdgcn_ubfe(w, bm[j], 2);
-                                tf = (float)t;
-                            }
-                            v0 = NEED_G ? __fmaf_rn(-tf, cab, g) : __fmaf_rn(a[i], b[j], -(tf * cab));
-                        }
-                        if (!S2N) v0 = (fabsf(g) >= qc.mnR) ? v0 : g;  // norm mask, v9:87
-                        // F7: the sign comes from Q_R(g), which is -0 (sign +1) for g in [-thr, 0);
-                        // v0 has g's sign, so for every g >= -thr the term is |v0|
-                        if (S2N && QBMA && SGN) v0 = (g >= -qc.thr) ? fabsf(v0) : v0;
-                        tacc[i][j] += QBMA ? q_fast<GCLIP>(v0, qc) : v0;
-                    }
-            }
-        }
-        __syncthreads();
-    }
-
-    if (F8) {  // a term beyond the e4m3 range came back NaN: the exact kernel reruns the launch
-        bool nan = false;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) nan |= __builtin_isnan(acc[i][j]);
-        if (__syncthreads_or(nan ? 1 : 0) && tid == 0) {
-            fb_tile(p, m0, BM, n0);
-            atomicOr(p.flag, fb_bits(p));
-        }
-    }
-    // ---- epilogue
-    store_tile(p, split, m0, n0, ty, tx, acc);
-}
-
-#include "gemm_f8mx.h"
-#include "gemm_v5mx.h"
-#include "gemm_tt.h"
-#include "gemm_tt16.h"
-#include "gemm_oh.h"
-#include "gemm_dense.h"
 
 // Sums the split-K partials in split order (deterministic) and writes the output mapping.
 // Partial layout: row-major [M][N] (rowmajor output) or [img][N][hw] (NCHW output).
@@ -929,7 +93,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs p) {
     const float pb = post_bias(p);
     const EmitCtx ec = emit_ctx(p);
     uint32_t sehi = 0;
-    const int S = p.splits + (p.ohd ? 1 : 0);  // (the one-hot path's correction slice follows the partials)
+    const int S = p.splits;
     const bool vec = p.nchw ? ((p.hw & 3) == 0) : ((p.N & 3) == 0 && (p.ldc & 3) == 0);
     const bool aligned = ((((uintptr_t)p.C) & 15) == 0) && ((((uintptr_t)p.part) & 15) == 0) && ((MN & 3) == 0) &&
                          ((((uintptr_t)p.res) & 15) == 0);
@@ -1275,7 +439,6 @@ __global__ __launch_bounds__(256) void conv_tb_fast_kernel(const float *x, const
     if (live) y[((img * Cout + co) * Ho + ho) * Wo + wo] = epi(ep, ep_act, ep_lo, ep_hi, co, acc);
 }
 
-#include "conv_tbx.h"
 
 // FP8 fake quantizer (fp8_quantizer.py:97-173), one sign bit.
 __global__ __launch_bounds__(256) void fp8_quantize_kernel(const float *x, int64_t rows, int64_t inner,
@@ -1400,56 +563,18 @@ __global__ __launch_bounds__(256) void max_pool2d_s2k3_kernel(const float *x, fl
 }
 
 // ------------------------------------------------------------------------- host dispatch
-template <bool S2N, bool QBMA, bool GCLIP>
-static void launch_fast_t(int mode, const GemmArgs &a, dim3 grid, hipStream_t s) {
-    switch (mode) {
-        case TM_NONE: gemm_fast_kernel<S2N, QBMA, GCLIP, TM_NONE><<<grid, NT, 0, s>>>(a); break;
-        case TM_W1U: gemm_fast_kernel<S2N, QBMA, GCLIP, TM_W1U><<<grid, NT, 0, s>>>(a); break;
-        case TM_W2S1: gemm_fast_kernel<S2N, QBMA, GCLIP, TM_W2S1><<<grid, NT, 0, s>>>(a); break;
-        case TM_W2U1: gemm_fast_kernel<S2N, QBMA, GCLIP, TM_W2U1><<<grid, NT, 0, s>>>(a); break;
-        case TM_W2S2: gemm_fast_kernel<S2N, QBMA, GCLIP, TM_W2S2><<<grid, NT, 0, s>>>(a); break;
-        case TM_W2U2: gemm_fast_kernel<S2N, QBMA, GCLIP, TM_W2U2><<<grid, NT, 0, s>>>(a); break;
-        case TM_LUT: gemm_fast_kernel<S2N, QBMA, GCLIP, TM_LUT><<<grid, NT, 0, s>>>(a); break;
-        default: gemm_fast_kernel<false, false, false, TM_QAMAA><<<grid, NT, 0, s>>>(a); break;
-    }
-}
-
-template <int NCG, int RB, int XF>
-static void launch_f8mx_t(const GemmArgs &a, hipStream_t s) {
-    using Cf = XmCfg<NCG, RB>;
-    const int64_t xt = ((a.M + Cf::BMT - 1) / Cf::BMT) * ((a.N + Cf::BNT - 1) / Cf::BNT);
-    const dim3 g((unsigned)(xt * a.splits));
-    // (the emitting instances only where this launch writes the next convolution's word image
-    // from its own store: unsplit, fp8a_conv2d_chain)
-    const bool emit = a.em.w != nullptr && a.splits == 1;
-    if (a.af32) {
-        if (emit) gemm_f8mx_kernel<NCG, RB, true, XF, true><<<g, Cf::NT, 0, s>>>(a);
-        else gemm_f8mx_kernel<NCG, RB, true, XF, false><<<g, Cf::NT, 0, s>>>(a);
-    } else {
-        if (emit) gemm_f8mx_kernel<NCG, RB, false, XF, true><<<g, Cf::NT, 0, s>>>(a);
-        else gemm_f8mx_kernel<NCG, RB, false, XF, false><<<g, Cf::NT, 0, s>>>(a);
-    }
-}
-template <int XF>
-static void launch_f8mx_f(const GemmArgs &a, hipStream_t s) {
-    if (a.xncg == 1) {
-        launch_f8mx_t<1, 4, XF>(a, s);
-    } else if constexpr (XF == 2) {
-        launch_f8mx_t<2, 4, XF>(a, s);  // (the halved-block form: at most 32 columns, gemm_f8mx.h)
-    } else {
-        if (a.xncg == 2) launch_f8mx_t<2, 4, XF>(a, s);
-        else launch_f8mx_t<4, 8, XF>(a, s);
-    }
-}
+// The GEMM kernel families are instantiated and launched in their own translation units
+// (fp8approx_launch.h): gemm_fast_kernel in k_fast.hip, gemm_f8mx_kernel in k_f8mx.hip, the
+// tile-table kernels in k_tt.hip, the v5 form in k_v5.hip.
 // E4M3 (XF 0) or E5M2 (mant_width 2) result grid; E5M2 launches both its kernels, the plain one
 // (XF 1) over every tile and the halved-block one (XF 2), which recomputes only the tiles the plain
 // one marked UT_HALF (the top binade, gemm_f8mx.h) and exits at once without FB_HALF
 static void launch_f8mx(const GemmArgs &a, hipStream_t s) {
     if (a.Mw == 2) {
-        launch_f8mx_f<1>(a, s);
-        launch_f8mx_f<2>(a, s);
+        launch_f8mx_xf1(a, s);
+        launch_f8mx_xf2(a, s);
     } else {
-        launch_f8mx_f<0>(a, s);
+        launch_f8mx_xf0(a, s);
     }
 }
 
@@ -1474,56 +599,30 @@ static int xm_ncg(int64_t N) {
 
 static void launch_fast(int mode, const GemmArgs &a, hipStream_t s) {
     const int64_t tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-    dim3 grid((unsigned)(tiles * a.splits));
+    const dim3 grid((unsigned)(tiles * a.splits));
     if (mode == TM_V5) {  // the v5 model has no s2n / qbma / golden-clip variants
-        if (a.aw && a.wfmt == 4) {  // the matrix-core form (gemm_v5mx.h), per OF / UF switch pair
-            const dim3 gv((unsigned)(((a.M + V5_BMT - 1) / V5_BMT) * ((a.N + V5_BNT - 1) / V5_BNT) * a.splits));
-            const bool uf = a.flags & F_UF, of = a.flags & F_OF;
-            if (uf && of) gemm_v5mx_kernel<true, true><<<gv, 256, 0, s>>>(a);
-            else if (uf) gemm_v5mx_kernel<true, false><<<gv, 256, 0, s>>>(a);
-            else if (of) gemm_v5mx_kernel<false, true><<<gv, 256, 0, s>>>(a);
-            else gemm_v5mx_kernel<false, false><<<gv, 256, 0, s>>>(a);
-            return;
-        }
-        gemm_fast_kernel<false, false, false, TM_V5><<<grid, NT, 0, s>>>(a);
+        if (a.aw && a.wfmt == 4) launch_v5mx(a, s);  // the matrix-core form (gemm_v5mx.h)
+        else launch_fast_p0(TM_V5, false, a, grid, s);
         return;
     }
-    if (a.aw && a.wfmt == 2) {  // E3M4: the packed-f16 tile-table kernel (run_gemm)
-        const int bm = a.ttf7 ? Tt16Cfg<true>::BMR : Tt16Cfg<false>::BMR;
-        const dim3 g16((unsigned)(((a.M + bm - 1) / bm) * ((a.N + BN - 1) / BN) * a.splits));
-        a.ttf7 ? gemm_tt16_kernel<true><<<g16, NT, 0, s>>>(a) : gemm_tt16_kernel<false><<<g16, NT, 0, s>>>(a);
-        // gated: reruns the launch in the f32 form when a tile left the f16 window (flag bits 1-4)
-        a.ttf7 ? gemm_tt_kernel<4, true, true><<<grid, NT, 0, s>>>(a) : gemm_tt_kernel<4, false, true><<<grid, NT, 0, s>>>(a);
+    if (mode == TM_QAMAA) {
+        launch_fast_p0(TM_QAMAA, false, a, grid, s);
         return;
     }
-    if (a.aw && a.wfmt == 1) {  // the tile-table kernel on pre-decoded operands (run_gemm)
-        if (a.Mw == 4) {
-            a.ttf7 ? gemm_tt_kernel<4, true, false><<<grid, NT, 0, s>>>(a) : gemm_tt_kernel<4, false, false><<<grid, NT, 0, s>>>(a);
-        } else {  // 128-row tiles on 8-wave workgroups
-            static_assert(tt_rh<5>() == 2 && tt_rh<4>() == 1, "gemm_tt_kernel launch shapes");
-            const dim3 g5((unsigned)(((a.M + 127) / 128) * ((a.N + BN - 1) / BN) * a.splits));
-            gemm_tt_kernel<5, false, false><<<g5, 2 * NT, 0, s>>>(a);
-        }
+    if (a.aw && (a.wfmt == 1 || a.wfmt == 2)) {  // E3M4 / E2M5: the tile-table kernels (run_gemm)
+        launch_tt(a, grid, s);
         return;
     }
     if (mode == TM_F8) {  // s2n + qbma, no golden clip (selected in run_gemm)
         // matrix-core accumulation on pre-decoded operands (gemm_f8mx.h) when run_gemm staged
         // them, else the VALU-accumulating form
-        if (a.aw || a.af32) {
-            launch_f8mx(a, s);
-        }
-        else
-            gemm_fast_kernel<true, true, false, TM_F8><<<grid, NT, 0, s>>>(a);
+        if (a.aw || a.af32) launch_f8mx(a, s);
+        else launch_fast_p3(TM_F8, false, a, grid, s);
         return;
     }
     const bool s2n = a.flags & F_S2N, q = a.flags & F_QBMA, gc = a.flags & F_GCLIP;
-    if (s2n) {
-        if (q) { gc ? launch_fast_t<true, true, true>(mode, a, grid, s) : launch_fast_t<true, true, false>(mode, a, grid, s); }
-        else   { gc ? launch_fast_t<true, false, true>(mode, a, grid, s) : launch_fast_t<true, false, false>(mode, a, grid, s); }
-    } else {
-        if (q) { gc ? launch_fast_t<false, true, true>(mode, a, grid, s) : launch_fast_t<false, true, false>(mode, a, grid, s); }
-        else   { gc ? launch_fast_t<false, false, true>(mode, a, grid, s) : launch_fast_t<false, false, false>(mode, a, grid, s); }
-    }
+    if (s2n) q ? launch_fast_p3(mode, gc, a, grid, s) : launch_fast_p2(mode, gc, a, grid, s);
+    else q ? launch_fast_p1(mode, gc, a, grid, s) : launch_fast_p0(mode, gc, a, grid, s);
 }
 
 static int check_format(int E, int Mw) {
@@ -1535,16 +634,10 @@ static int check_format(int E, int Mw) {
 constexpr size_t FLAG_BYTES = 256;  // workspace prefix holding the off-grid flag word
 
 // Launch paths taken by run_gemm since load (fp8a_path_stats): host-side counters.
-enum { PATH_OH = 0, PATH_F8MX = 1, PATH_TT = 2, PATH_TT16 = 3, PATH_FAST = 4, PATH_EXACT = 5, PATH_DENSE = 6,
-       PATH_V5MX = 7, PATH_N = 8 };
+enum { PATH_F8MX = 0, PATH_TT = 1, PATH_TT16 = 2, PATH_FAST = 3, PATH_EXACT = 4, PATH_DENSE = 5, PATH_V5MX = 6,
+       PATH_N = 7 };
 static std::atomic<uint64_t> g_paths[PATH_N];
-// Options (fp8a_set_option): "one_hot" -- the E4M3 one-hot path (gemm_oh.h), default off: its
-// dense GEMM beats gemm_f8mx_kernel by 1.6x, but the 1.1% candidate pairs of the benchmark network
-// cost more to correct than that saves ("One-hot path").  FP8A_ONE_HOT=1 turns it on at load.
-static bool g_opt_one_hot = getenv("FP8A_ONE_HOT") != nullptr && atoi(getenv("FP8A_ONE_HOT")) != 0;
-// "oh_correct" (diagnostics): 0 skips the one-hot path's correction kernel (dense terms only)
-static bool g_opt_oh_correct = true;
-static bool g_opt_oh_stats = false;  // "oh_stats": the one-hot kernels count into g_ohstat
+// Options (fp8a_set_option):
 // "tbx_rw": output rows per thread of conv_tbx_kernel (1 or 2; 2 needs undilated rows).
 // FP8A_TBX_RW=<n> sets it at load.
 static int g_opt_tbx_rw = getenv("FP8A_TBX_RW") ? atoi(getenv("FP8A_TBX_RW")) : 2;
@@ -1587,39 +680,6 @@ static int device_cus() {
 // multiplies the tile count and divides the round length, and adds a pass that writes and
 // re-reads S*M*N partial floats (charged at 2 TB/s).  Each split keeps at least 16 K-tiles.
 // FP8A_SPLITK=<S> forces S (experiments).
-// The one-hot path's split-K factor (gemm_oh.h): the same round model for its tiles (256 x 64 or
-// 128 x 128, 2 workgroups per CU, ~2e11 products/s per workgroup slot); splits are multiples of
-// OH_KC and keep at least 8 chunks each.  FP8A_SPLITK_OH=<S> forces S.
-static int oh_tnw(int64_t N) { return (N % 128 == 0) ? 2 : 1; }
-static int choose_splits_oh(int64_t M, int64_t N, int64_t K) {
-    static int forced = -1;
-    if (forced < 0) {
-        const char *e = getenv("FP8A_SPLITK_OH");
-        forced = e ? std::max(0, atoi(e)) : 0;
-    }
-    const int64_t kc = (K + 31) / 32;
-    if (forced > 0) return (int)std::max<int64_t>(1, std::min<int64_t>(forced, kc));
-    const int tnw = oh_tnw(N);
-    const int64_t tm = 256 / tnw, tn = 64 * tnw;
-    const int64_t tiles = ((M + tm - 1) / tm) * ((N + tn - 1) / tn);
-    const double slots = 2.0 * device_cus();
-    const double t_round = (double)tm * tn * K / 2.0e11;
-    const double t_split = 2.0 * (double)M * N * sizeof(float) / 2.0e12;
-    double best = 1e300;
-    int bs = 1;
-    for (int S = 1; S <= 8; ++S) {
-        if (S > 1 && kc < 8 * S) break;
-        const double q = (double)tiles * S / slots, fl = std::floor(q), fr = q - fl;
-        const double rounds = fl + (fr > 1e-9 ? std::min(1.0, 0.4 + 1.1 * fr) : 0.0);
-        const double t = rounds / S * t_round + (S > 1 ? S * t_split : 0.0);
-        if (t < best * (1.0 - 1e-3)) {
-            best = t;
-            bs = S;
-        }
-    }
-    return bs;
-}
-
 static int choose_splits(int64_t M, int64_t N, int64_t K) {
     static int forced = -1;
     if (forced < 0) {
@@ -1677,27 +737,12 @@ static size_t splitk_bytes(int64_t M, int64_t N, int64_t K) {
     return S > 1 ? align256((size_t)S * (size_t)M * (size_t)N * sizeof(float)) : 0;
 }
 
-// The one-hot path's buffers after the head (gemm_oh.h): the split-K partials plus the correction
-// slice ((S + 1) x M x N floats), the u16 A codes, the B codes / block scales and the candidate
-// lists / count blocks.  conv_words: the conv word image's element count (0: a matrix A).
-static int64_t oh_kpad(int64_t K) { return (K + 31) / 32 * 32; }
-static int64_t oh_npad(int64_t N) { return (N + 127) / 128 * 128; }
-static size_t oh_operand_bytes(int64_t M, int64_t N, int64_t K, int64_t conv_words) {
-    const int64_t kpad = oh_kpad(K), npad = oh_npad(N), nct = npad / 64;
-    const int64_t aw = conv_words > 0 ? conv_words : M * kpad;
-    const int S = choose_splits_oh(M, N, K);
-    return align256((size_t)(S + 1) * M * N * sizeof(float)) + align256((size_t)aw * 2) +
-           align256((size_t)(npad * kpad)) + align256((size_t)(npad * kpad / 4)) +
-           align256((size_t)(kpad * nct * 64 * 4)) + align256((size_t)(kpad * nct * 72));
-}
 
-// flag word + unit marks + the larger of the two E4M3 pre-decoded paths: split-K partials + the
-// matrix-core kernel's operands (gemm_f8mx.h), or the one-hot path's (gemm_oh.h).  conv_words:
-// the conv word image's element count, 0 for a matrix A.
+// flag word + unit marks + split-K partials + the matrix-core kernels' pre-decoded operands
+// (gemm_f8mx.h).  conv_words: the conv word image's element count, 0 for a matrix A.
 static size_t gemm_workspace_bytes(int64_t M, int64_t N, int64_t K, int64_t conv_words) {
     const int64_t a_words = conv_words > 0 ? conv_words : M * ((K + BK - 1) / BK * BK);
-    const size_t xm = splitk_bytes(M, N, K) + xm_operand_bytes(N, K, a_words);
-    return head_bytes(M, N) + std::max(xm, oh_operand_bytes(M, N, K, conv_words));
+    return head_bytes(M, N) + splitk_bytes(M, N, K) + xm_operand_bytes(N, K, a_words);
 }
 
 // The table + hardware-fp8 form applies (TM_F8; run_gemm then takes the matrix-core kernel when
@@ -1847,68 +892,6 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     if (hipMemsetAsync(ws, 0, units ? FLAG_BYTES + (size_t)(a.nur + a.nuc + a.nur * a.nuc) : sizeof(uint32_t), s) !=
         hipSuccess)
         return hip_check("fp8a flag reset");
-    // E4M3 (TM_F8 flags): the one-hot dense matrix-core GEMM + candidate correction (gemm_oh.h) when
-    // the workspace holds its buffers and the option is on (default off)
-    if (mode == TM_F8 && a.Mw == 3 && g_opt_one_hot && !no_mx() && units) {
-        const int64_t kpad = oh_kpad(a.K), npad = oh_npad(a.N), nct = npad / 64;
-        const WordImage wi = word_image(a.H, a.W, a.ph, a.pw);
-        const int64_t conv_words = a.conv ? (a.M / (a.Ho * a.Wo)) * a.aw_c * wi.H * wi.W : 0;
-        const int64_t a_words = a.conv ? conv_words : a.M * kpad;
-        const int S = choose_splits_oh(a.M, a.N, a.K);
-        const bool fits32 = a_words < (1ll << 30) && npad * kpad < (1ll << 31) && kpad * nct * 64 * 4 < (1ll << 31);
-        if (fits32 && ws_bytes >= head + oh_operand_bytes(a.M, a.N, a.K, conv_words)) {
-            a.awH = wi.H; a.awW = wi.W; a.awph = wi.ph; a.awpw = wi.pw;
-            const size_t MN4 = (size_t)a.M * a.N * sizeof(float);
-            char *base = (char *)ws + head;
-            a.splits = S;
-            a.kchunk = ((kpad / 32 + S - 1) / S) * 32;  // split boundaries on chunk boundaries
-            a.part = (float *)base;
-            a.ohd = (float *)(base + (size_t)(S > 1 ? S : 0) * MN4);  // the correction slice after the partials
-            base += align256((size_t)(S + 1) * MN4);
-            a.aw = (const uint32_t *)base;
-            base += align256((size_t)a_words * 2);
-            a.ohb = (const uint8_t *)base;
-            base += align256((size_t)(npad * kpad));
-            a.ohs = (const uint8_t *)base;
-            base += align256((size_t)(npad * kpad / 4));
-            a.ohl = (const uint32_t *)base;
-            base += align256((size_t)(kpad * nct * 64 * 4));
-            a.ohc = (const uint8_t *)base;
-            a.awld = kpad;
-            a.npad = npad;
-            a.wfmt = 3;
-            a.ohstats = g_opt_oh_stats ? 1 : 0;
-            const int64_t rows = a.conv ? a.M / (a.Ho * a.Wo) : a.M, cols = a_words / std::max<int64_t>(rows, 1);
-            const dim3 ga((unsigned)std::min<int64_t>((cols + 255) / 256, 64), (unsigned)std::min<int64_t>(rows, 1024));
-            xm_decode_a<<<ga, 256, 0, s>>>(a);
-            oh_decode_b<<<dim3((unsigned)(kpad / 4), (unsigned)nct), 64, 0, s>>>(a, kpad);
-            rc = hip_check("fp8a one-hot pre-decode launch");
-            if (rc) return rc;
-            const int64_t ctiles = ((a.M + 127) / 128) * ((a.N + OH_CT - 1) / OH_CT);
-            if (g_opt_oh_correct) oh_correct_kernel<<<(unsigned)ctiles, 256, 0, s>>>(a);
-            else if (hipMemsetAsync(a.ohd, 0, (size_t)a.M * a.N * sizeof(float), s) != hipSuccess)
-                return hip_check("fp8a correction slice fill");
-            rc = hip_check("fp8a one-hot correction launch");
-            if (rc) return rc;
-            const int tnw = oh_tnw(a.N);
-            const int64_t tm = 256 / tnw, tn = 64 * tnw;
-            const unsigned g = (unsigned)(((a.M + tm - 1) / tm) * ((a.N + tn - 1) / tn) * S);
-            if (tnw == 2) gemm_oh_kernel<2><<<g, 256, 0, s>>>(a);
-            else gemm_oh_kernel<1><<<g, 256, 0, s>>>(a);
-            rc = hip_check("fp8a one-hot gemm launch");
-            if (rc) return rc;
-            if (S > 1) {
-                const unsigned rb = (unsigned)std::min<int64_t>((a.M * a.N / 4 + 255) / 256 + 1, 8192);
-                splitk_reduce_kernel<<<rb, 256, 0, s>>>(a);
-                rc = hip_check("fp8a split-K reduce launch");
-                if (rc) return rc;
-            }
-            const unsigned ublocks = (unsigned)std::min<int64_t>(a.nur * a.nuc, 4096);
-            gemm_exact_kernel<<<ublocks, 256, 0, s>>>(a);
-            ++g_paths[PATH_OH];
-            return hip_check("fp8a gated exact gemm launch");
-        }
-    }
     // the matrix-core E4M3 kernel and the tile-table kernel (E3M4 / E2M5) need their pre-decoded
     // operands in the workspace (else gemm_fast_kernel runs); FP8A_NO_MX=1 forces the latter
     a.aw = nullptr;
@@ -1971,6 +954,14 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
         return fail(FP8A_EINVAL, "internal: fused input quantization without the matrix-core path");
     if (mode == TM_F8 && a.Mw != 3 && !a.aw) mode = mode0;  // (gemm_fast_kernel's TM_F8 form is E4M3 only)
     ++g_paths[!a.aw ? PATH_FAST : a.wfmt == 0 ? PATH_F8MX : a.wfmt == 1 ? PATH_TT : a.wfmt == 4 ? PATH_V5MX : PATH_TT16];
+    // word-image emission (fp8a_conv2d_chain): every store form emits the next convolution's words
+    // except the v5 matrix-core kernel's (gemm_v5mx_kernel: store_tile<false>); its unsplit launch
+    // marks the image invalid instead (emit_prep_kernel set the header valid before this launch), so
+    // the consumer's gated pre-pass re-decodes its input from y
+    if (a.em.w != nullptr && a.aw && a.wfmt == 4 && a.splits == 1) {
+        if (hipMemsetAsync(a.em.invalid, 1, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a word image header");
+        a.em.w = nullptr;
+    }
     launch_fast(mode, a, s);
     rc = hip_check("fp8a fast gemm launch");
     if (rc) return rc;
@@ -2131,7 +1122,7 @@ static bool plan_dw3(DwArgs &a, int S, size_t &lds) {
 // words padded to a multiple of 4 (16-byte LDS reads).
 static bool plan_tbs(TbsArgs &a, int S, int64_t planes, int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
                      int ph, int pw, size_t &lds) {
-    if (H >= (1 << 20) || W >= (1 << 20) || C >= (1 << 20)) return false;
+    if (H >= (1 << 20) || W >= (1 << 20) || C >= (1 << 20) || H * W >= (1ll << 22)) return false;  // (as plan_dw3's caller)
     a.planes = planes; a.C = (int)C; a.H = (int)H; a.W = (int)W; a.Ho = (int)Ho; a.Wo = (int)Wo; a.ph = ph; a.pw = pw;
     const int nq = (int)((Wo + TBX_TW - 1) / TBX_TW);
     const int WS = ((4 * nq - 1) * S + 3 + 3) / 4 * 4;
@@ -2173,16 +1164,6 @@ int fp8a_path_stats(uint64_t *out, int reset) {
 
 int fp8a_set_option(const char *name, int value) {
     if (name == nullptr) return fail(FP8A_EINVAL, "null pointer");
-    if (strcmp(name, "one_hot") == 0) {
-        const int old = g_opt_one_hot ? 1 : 0;
-        g_opt_one_hot = value != 0;
-        return old;
-    }
-    if (strcmp(name, "oh_stats") == 0) {
-        const int old = g_opt_oh_stats ? 1 : 0;
-        g_opt_oh_stats = value != 0;
-        return old;
-    }
     if (strcmp(name, "xm_ncg") == 0) {
         const int old = g_opt_xm_ncg;
         g_opt_xm_ncg = value;
@@ -2218,33 +1199,17 @@ int fp8a_set_option(const char *name, int value) {
         g_opt_dw3 = value;
         return old;
     }
-    if (strcmp(name, "oh_correct") == 0) {
-        const int old = g_opt_oh_correct ? 1 : 0;
-        g_opt_oh_correct = value != 0;
-        return old;
-    }
     return fail(FP8A_EINVAL, std::string("unknown option ") + name);
-}
-
-int fp8a_debug_stats(uint64_t *out, int reset) {
-    if (out == nullptr) return fail(FP8A_EINVAL, "null pointer");
-    unsigned long long v[4] = {0, 0, 0, 0};
-    if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(v, HIP_SYMBOL(g_ohstat), sizeof(v)) != hipSuccess)
-        return hip_check("fp8a_debug_stats");
-    for (int i = 0; i < 4; ++i) out[i] = v[i];
-    if (reset) {
-        const unsigned long long z[4] = {0, 0, 0, 0};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_ohstat), z, sizeof(z)) != hipSuccess) return hip_check("fp8a_debug_stats");
-    }
-    return FP8A_OK;
 }
 
 int fp8a_fallback_stats(uint64_t *out, int reset) {
     if (out == nullptr) return fail(FP8A_EINVAL, "null pointer");
-    unsigned long long v[4] = {0, 0, 0, 0};
-    if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(v, HIP_SYMBOL(g_fallback), sizeof(v)) != hipSuccess)
+    unsigned long long v[4] = {0, 0, 0, 0}, tt = 0;
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(v, HIP_SYMBOL(g_fallback), sizeof(v)) != hipSuccess ||
+        tt_rerun_stats(&tt, reset != 0) != 0)
         return hip_check("fp8a_fallback_stats");
     for (int i = 0; i < 4; ++i) out[i] = v[i];
+    out[2] = tt;  // (gemm_tt_kernel's f32 reruns: k_tt.hip's counter)
     if (reset) {
         const unsigned long long z[4] = {0, 0, 0, 0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_fallback), z, sizeof(z)) != hipSuccess) return hip_check("fp8a_fallback_stats");
@@ -2326,7 +1291,9 @@ static int grouped_conv_impl(const float *x, const float *w, float *y, int64_t B
         d.planes = Bn * Cout; d.C = (int)Cout; d.H = (int)H; d.W = (int)W; d.Ho = (int)Ho; d.Wo = (int)Wo;
         d.ph = ph; d.pw = pw;
         size_t lds = 0;
-        if (H < (1 << 20) && W < (1 << 20) && Cout < (1 << 20) && plan_dw3(d, sh, lds)) {
+        // (the staged kernels index a plane in 32-bit ints and divide by float reciprocals, dw_div:
+        // planes of at most 2^22 values; larger ones take dn_group_conv)
+        if (H < (1 << 20) && W < (1 << 20) && Cout < (1 << 20) && H * W < (1ll << 22) && plan_dw3(d, sh, lds)) {
             const unsigned g = (unsigned)(((d.planes + d.PB - 1) / d.PB) * d.nb);
             if (sh == 1) dn_dw3_kernel<1><<<g, 256, lds, stream>>>(d);
             else dn_dw3_kernel<2><<<g, 256, lds, stream>>>(d);
@@ -2342,14 +1309,15 @@ static int grouped_conv_impl(const float *x, const float *w, float *y, int64_t B
 
 int fp8a_clock_stats(uint64_t *out, int reset) {
     if (out == nullptr) return fail(FP8A_EINVAL, "null pointer");
+    if (hipDeviceSynchronize() != hipSuccess) return hip_check("fp8a_clock_stats");
     unsigned long long v[3] = {0, 0, 0};
-    if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(v, HIP_SYMBOL(g_clk), sizeof(v)) != hipSuccess)
-        return hip_check("fp8a_clock_stats");
-    for (int i = 0; i < 3; ++i) out[i] = v[i];
-    if (reset) {
-        const unsigned long long z[3] = {0, 0, 0};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_clk), z, sizeof(z)) != hipSuccess) return hip_check("fp8a_clock_stats");
+    int (*parts[3])(unsigned long long *, bool) = {f8mx_clock_xf0, f8mx_clock_xf1, f8mx_clock_xf2};
+    for (auto f : parts) {
+        unsigned long long w[3] = {0, 0, 0};
+        if (f(w, reset != 0) != 0) return hip_check("fp8a_clock_stats");
+        for (int i = 0; i < 3; ++i) v[i] += w[i];
     }
+    for (int i = 0; i < 3; ++i) out[i] = v[i];
     return FP8A_OK;
 }
 
@@ -2840,7 +1808,7 @@ int fp8a_conv2d_wants_image(int64_t Cout, int kh, int kw, int ph, int pw, int gr
         return tbx ? 2 : 0;
     }
     if (groups != 1 || no_mx()) return 0;
-    if (!f8_form(E, Mw, flags & ~F_TB, mode) || g_opt_one_hot) return 0;
+    if (!f8_form(E, Mw, flags & ~F_TB, mode)) return 0;
     if (kh == 1 && kw == 1 && ph == 0 && pw == 0) {  // xm_af32: fp32 staging up to af32_maxct column tiles
         const int64_t bnt = 16 * xm_ncg(Cout), ct = (Cout + bnt - 1) / bnt;
         if (ct <= g_opt_af32_maxct) return 0;
@@ -2855,7 +1823,7 @@ int fp8a_conv2d_chain(const float *x, const float *w, float *y, int64_t Bn, int6
                       int in_nbits, int in_mbits, int in_sign_bits, float *in_bias_out, int32_t *in_ibias_out,
                       const float *res, int post_act, float post_lo, float post_hi, const float *out_maxval,
                       int out_nbits, int out_mbits, int out_sign_bits, float *out_bias_out, int32_t *out_ibias_out,
-                      const void *in_image, void *out_image, int next_ph, int next_pw, const float *next_maxval,
+                      void *in_image, void *out_image, int next_ph, int next_pw, const float *next_maxval,
                       int next_nbits, int next_mbits, int next_sign_bits, const int32_t *next_bR, int next_Mw,
                       int next_form, void *workspace, size_t workspace_bytes, fp8a_stream_t stream) {
     hipStream_t s = (hipStream_t)stream;

@@ -1,5 +1,4 @@
-// gemm_dense.h -- the exact (non-approx) product on the matrix core (included by fp8approx.hip
-// inside namespace fp8a, after gemm_oh.h).  DESIGN.md §3e.
+// gemm_dense.h -- the exact (non-approx) product on the matrix core.  DESIGN.md §3e.
 //
 // The reference's non-approx branch is a plain fp32 contraction of FP8-quantized operands:
 // `x @ y` (approx_calculation.py:797, 811 -- the im2col form for convs; QuantizationHijacker
@@ -22,6 +21,11 @@
 //                    pixels.
 //   dn_fix        -- the marked 64 x 64 units again in fp32 FMAs from the original operands (a
 //                    no-op launch when nothing is marked; counted by fp8a_dense_stats).
+#pragma once
+#include "fp8approx_common.h"
+#include "gemm_f8mx.h"
+
+namespace fp8a {
 
 constexpr int DN_T = 128;            // tile rows = tile columns
 constexpr int DN_KC = 128;           // k per LDS stage (one MFMA K-step)
@@ -763,3 +767,5 @@ __global__ __launch_bounds__(256) void dn_group_conv(const GcArgs p) {
             if (wo0 + j < p.Wo) yp[wo0 + j] = dn_out(p.fz, qv, co, acc[j]);
     }
 }
+
+}  // namespace fp8a

@@ -1,5 +1,4 @@
-// gemm_f8mx.h -- the E4M3 fast path with matrix-core accumulation (included by fp8approx.hip,
-// inside namespace fp8a, after GemmArgs / stage_decode / store_tile).  DESIGN.md §3a.
+// gemm_f8mx.h -- the E4M3 fast path with matrix-core accumulation.  DESIGN.md §3a.
 //
 // Same arithmetic as gemm_fast_kernel<.., TM_F8>: for on-grid E4M3 operands with
 // s2n and per-product quantization (v9:51-113), each term is
@@ -57,6 +56,10 @@
 // 3.5 that the reference clamps to the largest subnormal 3.  Rows are 8 s_a + m_a with m_a < 4;
 // B codes m_b < 4 and 8 = zero.  A term past the e5m2 range converts to inf / NaN and the tile
 // falls back, as for E4M3.
+#pragma once
+#include "fp8approx_common.h"
+
+namespace fp8a {
 
 typedef int xm_v8i __attribute__((ext_vector_type(8)));
 typedef float xm_v16f __attribute__((ext_vector_type(16)));
@@ -231,21 +234,6 @@ __device__ __forceinline__ uint32_t tt16_word_a(float x, uint32_t emnA, int bA, 
     return (h << 16) | h | (mc * TT16_RSH);
 }
 
-// gemm_oh_kernel's A code (wfmt 3, gemm_oh.h): u16, low byte the bf8 (e5m2) byte of sign(a) *
-// 2^(e_a - sA) -- the one-hot operand's nonzero byte --, high byte 8 m_a (its position); zeros 0.
-// ok = on the (3, bA) grid, e_a - sA inside bf8's normal exponents [-14, 15] and the correction's
-// fp8 conversion scale 2^(7 - bR - e_a) a normal E8M0 value.
-__device__ __forceinline__ uint32_t oh_code_a(float x, uint32_t emnA, int sA, int bR, bool &ok) {
-    float c;
-    uint32_t mc;
-    ok = stage_decode(x, 3, emnA, true, c, mc);
-    const uint32_t cb = __float_as_uint(c);
-    if ((cb & 0x7FFFFFFFu) == 0u) return 0u;
-    const int ea = (int)((cb >> 23) & 0xFFu) - 127, e = ea - sA + 15, se = 134 - bR - ea;
-    ok = ok && e >= 1 && e <= 30 && se >= 1 && se <= 254;
-    return ((cb >> 31) << 7) | ((uint32_t)min(max(e, 1), 30) << 2) | (mc << 11);
-}
-
 // A word of the v5 matrix-core form (xm_decode_a, wfmt 4; gemm_v5mx.h): (sign << 15 | code << 5) in both halves
 __device__ __forceinline__ uint32_t v5_word_a(float v, const DFmt &f) {
     int e, m;
@@ -264,6 +252,7 @@ __device__ __forceinline__ void xm_record_se(const GemmArgs &p, uint32_t sehi) {
 // inside a border of zero words (the padding the convolution reads, so the wave-independent
 // kernel gathers without bounds checks; no border for gemm_f8mx_kernel); matrix: A [M][lda] ->
 // words [M][awld] (columns >= K zero words).
+#if FP8A_OWN_F8MX_DECODE
 __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
     // fused input quantization: A = fq(X) with the quantizer's own bias, which becomes bA
     const float fmx = p.fqin.mx ? *p.fqin.mx : 0.0f;
@@ -294,7 +283,6 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
     auto word = [&](float v, bool &ok) {
         if (p.fqin.mx) v = fq_apply(v, fmx, fbias, p.fqin.M, p.fqin.S);
         if (p.wfmt == 4) return v5_word_a(v, fv5);
-        if (p.wfmt == 3) return oh_code_a(v, emnA, 6 - bA, bR, ok);
         if (p.wfmt == 2) return tt16_word_a(v, emnA, bA, ok, win);
         if (p.wfmt) return tt_word_a(v, p.Mw, emnA, ok);
         const uint32_t w = xm_word_a(v, p.Mw, xm_xbias(p.Mw), emnA, bR, ok);
@@ -302,17 +290,8 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
         return w;
     };
     const uint32_t zw = p.wfmt ? 0u : XM_ZERO_WORD;  // the word of a zero (padding, columns >= K)
-    // stores: 32-bit words, or the one-hot path's 16-bit codes (wfmt 3) at the same indices
-    const bool u16 = p.wfmt == 3;
-    uint16_t *const out16 = reinterpret_cast<uint16_t *>(out);
-    auto st1 = [&](int64_t i, uint32_t w) {
-        if (u16) out16[i] = (uint16_t)w;
-        else out[i] = w;
-    };
-    auto st4 = [&](int64_t i, uint4 w) {  // i % 4 == 0
-        if (u16) *reinterpret_cast<uint2 *>(out16 + i) = make_uint2(w.x | (w.y << 16), w.z | (w.w << 16));
-        else *reinterpret_cast<uint4 *>(out + i) = w;
-    };
+    auto st1 = [&](int64_t i, uint32_t w) { out[i] = w; };
+    auto st4 = [&](int64_t i, uint4 w) { *reinterpret_cast<uint4 *>(out + i) = w; };  // i % 4 == 0
     if (p.conv && (p.awph | p.awpw)) {  // zero-bordered image (< 2^30 words, run_gemm): 32-bit index math
         // interior: four input elements per thread step along W, one 16-B load and one 16-B store
         // when W % 4 == 0 (run_gemm's word_image aligns the interior rows), else one element;
@@ -403,10 +382,14 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
     if (__syncthreads_or(win ? 0 : 1) && threadIdx.x == 0) atomicOr(p.flag, 4u);  // gemm_tt16_kernel's window (A)
     xm_record_se(p, sehi);
 }
+#else
+__global__ void xm_decode_a(const GemmArgs p);
+#endif  // FP8A_OWN_F8MX_DECODE
 
 // B pre-pass: per (k, pair Q) of the padded [Kpad][npad / 2] pair grid, the addend pair
 // ((s_b << 15) + (e_b << 7) per bf16 half, 0 for a zero B) and the pair's byte offset in the
 // static table ((code0 + 9 code1) * 32); out-of-range elements are zeros.
+#if FP8A_OWN_F8MX_DECODE
 __global__ __launch_bounds__(256) void xm_decode_b(const GemmArgs p, int64_t kpad) {
     // (af32: A's bias -- maybe the fused input quantizer's, not written yet -- is checked by the GEMM)
     const int bA = p.af32 ? 0 : *p.bA, bR = *p.bR;
@@ -473,7 +456,32 @@ __global__ __launch_bounds__(256) void xm_decode_b(const GemmArgs p, int64_t kpa
     }
     if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, fb_bits(p, biasbad));
 }
+#else
+__global__ void xm_decode_b(const GemmArgs p, int64_t kpad);
+#endif  // FP8A_OWN_F8MX_DECODE
 
+#if FP8A_OWN_F8MX
+// In-kernel clock of gemm_f8mx_kernel (diagnostic build only: -DFP8A_CLOCK_STAMP=1, tools/clock_probe.py):
+// thread 0 of every workgroup adds its s_memtime and s_memrealtime (100 MHz) deltas; the clock the
+// chip held = sum dt / sum dr x 100 MHz (MI355X_MICROARCH.md, DVFS give-back item 6).  Nothing
+// else reads g_clk; the product build compiles no stamp.
+#ifndef FP8A_CLOCK_STAMP
+#define FP8A_CLOCK_STAMP 0
+#endif
+__device__ unsigned long long g_clk[3];
+#if FP8A_CLOCK_STAMP
+#define FP8A_CLK_BEGIN const uint64_t clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
+#define FP8A_CLK_END                                                                                   \
+    if (threadIdx.x == 0) {                                                                            \
+        const uint64_t clk_t1 = __builtin_amdgcn_s_memtime(), clk_r1 = __builtin_amdgcn_s_memrealtime(); \
+        atomicAdd(&g_clk[0], (unsigned long long)(clk_t1 - clk_t0));                                   \
+        atomicAdd(&g_clk[1], (unsigned long long)(clk_r1 - clk_r0));                                   \
+        atomicAdd(&g_clk[2], 1ull);                                                                    \
+    }
+#else
+#define FP8A_CLK_BEGIN
+#define FP8A_CLK_END
+#endif
 #ifndef XM_WAVES
 #define XM_WAVES 6  // register bound: 80 VGPRs, 6 waves / SIMD (the LDS allows 6 workgroups / CU)
 #endif
@@ -539,14 +547,11 @@ __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs
     const uint32_t hq8 = (uint32_t)(p.npad / 2) * 8u;  // bytes per K-step of the B pair grid
     // (NT is a multiple of 8 TXN, so the unit's column block is the same for every u)
     const int q4 = tid & 3, btx = (tid >> 3) % TXN;
-    int bkk[BU];
-    uint32_t boff[BU];
-#pragma unroll
-    for (int u = 0; u < BU; ++u) {
-        const int e = min(tid + NT * u, NBU - 1);
-        bkk[u] = 2 * (e / (8 * TXN)) + ((e >> 2) & 1);
-        boff[u] = (uint32_t)(kbeg + bkk[u]) * hq8 + (uint32_t)(n0 / 2 + 2 * btx) * 8u;  // pair 2 btx: 16-B aligned
-    }
+    // unit u = the thread's unit 0 moved by u * NT: (NT a multiple of 8 TXN) the same column block,
+    // K-step + u * BKU -- the per-unit offsets are uniform (soffset / immediates), one VGPR each
+    constexpr int BKU = 2 * (NT / (8 * TXN));
+    const int bkk0 = 2 * (tid / (8 * TXN)) + ((tid >> 2) & 1);
+    const uint32_t boff0 = (uint32_t)(kbeg + bkk0) * hq8 + (uint32_t)(n0 / 2 + 2 * btx) * 8u;  // pair 2 btx: 16-B aligned
     const bool build = NBU % NT == 0 || tid < NBU;  // (NCG = 1: half the threads build)
     const __amdgpu_buffer_rsrc_t brsrc =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint2 *>(p.bqw), (short)0, -1, 0x00020000);
@@ -607,15 +612,17 @@ __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs
             ko = __builtin_amdgcn_readfirstlane(ko);
 #pragma unroll
             for (int i = 0; i < APR; ++i) {
+                // (K-steps past the group's last channel become zero words at staging: a select on the
+                // loaded value here made the compiler wait for the prefetch right after issuing it)
                 wa[i][r] = __builtin_amdgcn_raw_buffer_load_b32(arsrc, (int)aoff[i], (int)ko, 0);
-                if (!AF32 && p.conv && k0 + 2 * akp + r >= K32) wa[i][r] = XM_ZERO_WORD;  // past the group's last channel (uniform)
             }
         }
         if (build) {
             const uint32_t kb = __builtin_amdgcn_readfirstlane((uint32_t)(k0 - kbeg) * hq8);
 #pragma unroll
             for (int u = 0; u < BU; ++u)  // (add0, off0, add1, off1) of pairs 2 btx, 2 btx + 1
-                wbq[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(brsrc, (int)boff[u], (int)kb, 0));
+                wbq[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                       brsrc, (int)boff0, (int)(kb + (uint32_t)(u * BKU) * hq8), 0));
         }
     };
     load_tile(kbeg);
@@ -665,6 +672,13 @@ __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs
                     }
                 }
         }
+        if (!AF32 && p.conv) {  // K-steps past the group's last channel (wave-uniform): zero words
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+                if (k0 + 2 * akp + r >= K32)
+#pragma unroll
+                    for (int i = 0; i < APR; ++i) wa[i][r] = XM_ZERO_WORD;
+        }
 #pragma unroll
         for (int i = 0; i < APR; ++i)
             *reinterpret_cast<uint2 *>(&sm.aw[akp][2 * (arow + 64 * i)]) = make_uint2(wa[i][0], wa[i][1]);
@@ -678,7 +692,7 @@ __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs
                 const xm_u2 a0 = __builtin_bit_cast(xm_u2, b.x), a1 = __builtin_bit_cast(xm_u2, b.z);
                 const xm_u2 n0 = __builtin_bit_cast(xm_u2, b.x ^ 0x80008000u), n1 = __builtin_bit_cast(xm_u2, b.z ^ 0x80008000u);
                 auto pk = [](uint32_t v, xm_u2 ad) { return __builtin_bit_cast(uint32_t, __builtin_bit_cast(xm_u2, v) + ad); };
-                uint32_t *d = &sm.tt[bkk[u]][btx * 32 + q4 * 4];
+                uint32_t *d = &sm.tt[bkk0 + u * BKU][btx * 32 + q4 * 4];
                 *reinterpret_cast<uint4 *>(d) = make_uint4(pk(s0.x, a0), pk(s1.x, a1), pk(s0.y, a0), pk(s1.y, a1));
                 *reinterpret_cast<uint4 *>(d + 16) = make_uint4(pk(s0.x, n0), pk(s1.x, n1), pk(s0.y, n0), pk(s1.y, n1));
             }
@@ -826,3 +840,6 @@ __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs
     }
     FP8A_CLK_END
 }
+#endif  // FP8A_OWN_F8MX
+
+}  // namespace fp8a

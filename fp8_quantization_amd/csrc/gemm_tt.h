@@ -1,5 +1,4 @@
-// gemm_tt.h -- the tile-table kernel for the wider-mantissa formats (E3M4, E2M5), included by
-// fp8approx.hip after gemm_f8mx.h (inside namespace fp8a).  DESIGN.md §3b.
+// gemm_tt.h -- the tile-table kernel for the wider-mantissa formats (E3M4, E2M5).  DESIGN.md §3b.
 //
 // Same term as gemm_fast_kernel's table modes (v9:51-113) for on-grid operands
 // with s2n and per-product quantization, no golden clip:
@@ -22,6 +21,11 @@
 // Operands are pre-decoded once per launch: an A element becomes c_a's sign and exponent bits
 // (mantissa field zero) | m_a x the table row stride in its low bits; a B element c_b's bits | m_b.
 // The pre-passes carry the fallback checks into the flag word (gemm_exact_kernel reruns).
+#pragma once
+#include "fp8approx_common.h"
+#include "gemm_f8mx.h"
+
+namespace fp8a {
 
 constexpr int TT_IMG_FLOATS = 2048;       // static image: V [m_b][m_a] then sig_a sig_b [m_b][m_a]
 
@@ -34,6 +38,7 @@ template <int MW, bool F7> struct TtCfg {
 
 // B pre-pass for gemm_tt_kernel: words [Kpad][Npad] (c_b's bits | m_b, 0 for zeros and padding),
 // and (block 0) the static image V / sig_a sig_b.
+#if FP8A_OWN_TT
 __global__ __launch_bounds__(256) void tt_decode_b(const GemmArgs p, int64_t kpad) {
     const int bA = *p.bA, bR = *p.bR, M = p.Mw, nm = 1 << M;
     const bool biasbad = !(xm_bias_ok(bA) && xm_bias_ok(bR));  // every output unit falls back
@@ -80,6 +85,9 @@ __global__ __launch_bounds__(256) void tt_decode_b(const GemmArgs p, int64_t kpa
     if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, fb_bits(p, biasbad));
     if (p.wfmt == 2 && __syncthreads_or(win ? 0 : 1) && threadIdx.x == 0) atomicOr(p.flag, 8u);  // (B, image)
 }
+#else
+__global__ void tt_decode_b(const GemmArgs p, int64_t kpad);
+#endif  // FP8A_OWN_TT
 
 // Row halves per tile: E2M5 runs 128-row tiles on 8-wave workgroups that share one table build
 // (its 32-row table makes the build ~20 % of the work at 64 rows; 99.5 -> 79.8 ms on the ResNet-18
@@ -100,13 +108,18 @@ template <int MW, bool F7> struct TtSmem {
 
 // A16: the A words are gemm_tt16_kernel's (E3M4; c_a 2^bA as f16 in the high half, m_a x 68 in the
 // low bits), and the kernel runs only when that kernel left its f16 window (flag bit 1).
+#if FP8A_OWN_TT
+// launches rerun in the f32 form (fp8a_fallback_stats [2], read by tt_rerun_stats in k_tt.hip)
+__device__ unsigned long long g_tt_reruns;
+#endif
+#if FP8A_OWN_TT
 template <int MW, bool F7, bool A16>
 __global__ __launch_bounds__(NT * tt_rh<MW>()) void gemm_tt_kernel(const GemmArgs p) {
     constexpr int TT_RH = tt_rh<MW>();
     using C = TtCfg<MW, F7>;
     if (A16) {
         if ((__hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 30u) == 0u) return;
-        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_fallback[2], 1ull);
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_tt_reruns, 1ull);
     }
     constexpr int NM = C::NM, XK = C::XK;
     static_assert(C::UNITS <= NT && XK >= 1 && XK <= 4, "tile-table configuration");
@@ -177,8 +190,7 @@ __global__ __launch_bounds__(NT * tt_rh<MW>()) void gemm_tt_kernel(const GemmArg
                 ko = 4u * (uint32_t)k0;
             }
             ko = __builtin_amdgcn_readfirstlane(ko);
-            wa = __builtin_amdgcn_raw_buffer_load_b32(arsrc, (int)aoff, (int)ko, 0);
-            if (p.conv && k0 + akk >= K32) wa = 0u;  // past the group's last channel (uniform)
+            wa = __builtin_amdgcn_raw_buffer_load_b32(arsrc, (int)aoff, (int)ko, 0);  // (past K: zeroed at staging)
         }
         const uint32_t kb = __builtin_amdgcn_readfirstlane((uint32_t)(k0 - kbeg) * npad4);
         if (bunit) wb = __builtin_amdgcn_raw_buffer_load_b32(brsrc, (int)boff, (int)kb, 0);
@@ -192,7 +204,9 @@ __global__ __launch_bounds__(NT * tt_rh<MW>()) void gemm_tt_kernel(const GemmArg
     __syncthreads();  // the static image is in LDS
 
     for (int k0 = kbeg; k0 < kend; k0 += XK) {
-        if (astage) aw[akk][arow] = wa;
+        // (K-steps past the group's last channel: zero words, selected here where the loads have
+        // landed -- a select at load time made the compiler wait for the prefetch at once)
+        if (astage) aw[akk][arow] = (p.conv && k0 + akk >= K32) ? 0u : wa;
         if (bunit) {  // build: tt[bkk][m_a][bcol] = V(m_a, m_b) c_b for the unit's 16 rows
             const float cb = __uint_as_float(wb & TT_EXP);
             const int mb = (int)(wb & (uint32_t)(NM - 1));
@@ -286,3 +300,6 @@ __global__ __launch_bounds__(NT * tt_rh<MW>()) void gemm_tt_kernel(const GemmArg
         }
     }
 }
+#endif  // FP8A_OWN_TT
+
+}  // namespace fp8a

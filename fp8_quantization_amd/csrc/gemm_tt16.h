@@ -1,5 +1,4 @@
-// gemm_tt16.h -- the E3M4 tile-table kernel in packed f16 with matrix-core summation, included
-// by fp8approx.hip after gemm_tt.h (inside namespace fp8a).  DESIGN.md §3c.
+// gemm_tt16.h -- the E3M4 tile-table kernel in packed f16 with matrix-core summation.  DESIGN.md §3c.
 //
 // Same term as gemm_tt_kernel<4, F7> (gemm_tt.h; v9:51-113):
 //     term = Q_R(V(m_a, m_b) c_a c_b),   V = min(sig_a sig_b - T[m_a][m_b] 2^-4, kb x its binade)
@@ -27,6 +26,12 @@
 // Lane = (row r16 of each 16-row block, K-step g of the 4-step tile); per A element the lane
 // reads its 16 columns (four ds_read_b64, conflict-free: rows 136 B and K-steps 2176 B apart)
 // and spends 6 packed ops per column pair.
+#pragma once
+#include "fp8approx_common.h"
+#include "gemm_f8mx.h"
+#include "gemm_tt.h"
+
+namespace fp8a {
 
 template <bool F7> struct Tt16Cfg {
     static constexpr int RB = 8;             // 16-row blocks per wave
@@ -49,6 +54,7 @@ template <bool F7> struct Tt16Smem {
     } u;
 };
 
+#if FP8A_OWN_TT
 template <bool F7>
 __global__ __launch_bounds__(NT, 6) void gemm_tt16_kernel(const GemmArgs p) {
     using Cf = Tt16Cfg<F7>;
@@ -132,8 +138,7 @@ __global__ __launch_bounds__(NT, 6) void gemm_tt16_kernel(const GemmArgs p) {
         ko = __builtin_amdgcn_readfirstlane(ko);
 #pragma unroll
         for (int i = 0; i < APT; ++i) {
-            wa[i] = __builtin_amdgcn_raw_buffer_load_b32(arsrc, (int)aoff[i], (int)ko, 0);
-            if (p.conv && k0 + akk >= K32) wa[i] = 0u;  // past the group's last channel (uniform)
+            wa[i] = __builtin_amdgcn_raw_buffer_load_b32(arsrc, (int)aoff[i], (int)ko, 0);  // (past K: zeroed at staging)
         }
         const uint32_t kb = __builtin_amdgcn_readfirstlane((uint32_t)(k0 - kbeg) * npad4);
         wb = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(brsrc, (int)boff, (int)kb, 0));
@@ -160,7 +165,8 @@ __global__ __launch_bounds__(NT, 6) void gemm_tt16_kernel(const GemmArgs p) {
 
     for (int k0 = kbeg; k0 < kend; k0 += TT16_XK) {
 #pragma unroll
-        for (int i = 0; i < APT; ++i) S.aw[akk * AWS + arow + 64 * i] = wa[i];
+        for (int i = 0; i < APT; ++i)  // (K-steps past the group's last channel: zero words)
+            S.aw[akk * AWS + arow + 64 * i] = (p.conv && k0 + akk >= K32) ? 0u : wa[i];
         {  // build: tt[bkk][m_a][cp] = (V(m_a, m_b1) c_b1' : V(m_a, m_b0) c_b0') for m_a = 8 rp .. 8 rp + 7
             auto cbf16 = [&](uint32_t w) -> uint32_t {  // f32 c_b bits -> f16 c_b' bits (0 for a zero B)
                 const int e = (int)((w >> 23) & 0xFFu) + sb16;  // f16 exponent field; <= 0: subnormal
@@ -257,3 +263,6 @@ __global__ __launch_bounds__(NT, 6) void gemm_tt16_kernel(const GemmArgs p) {
         store_tile(p, split, m0 + 64 * hs, n0, ety, etx, acc);
     }
 }
+#endif  // FP8A_OWN_TT
+
+}  // namespace fp8a

@@ -1,5 +1,5 @@
-// gemm_v5mx.h -- the v5 integer-adder model's GEMM / implicit-GEMM convolution on the matrix core
-// (included by fp8approx.hip inside namespace fp8a, after gemm_f8mx.h).  DESIGN.md §3g.
+// gemm_v5mx.h -- the v5 integer-adder model's GEMM / implicit-GEMM convolution on the matrix core.
+// DESIGN.md §3h.
 //
 // The v5 term (exact_term_v5, fp8approx_device.h; the reference's approx_mult_new,
 // approx_matmul_whole_v5.py:155-182) is integer arithmetic on the operands' codes:
@@ -35,6 +35,11 @@
 // rows; per (block, K-step) 2 ds_read_b128 fetch the 16 columns' table words of its m_a, 8
 // column pairs give 16 bf16 terms, 2 MFMAs (16x16x32, 8 terms per lane) sum them.
 // E5M2 (M = 2) only; E4M3 / E3M4 v5 and the unwrapped adder keep gemm_fast_kernel<TM_V5>.
+#pragma once
+#include "fp8approx_common.h"
+#include "gemm_f8mx.h"
+
+namespace fp8a {
 
 constexpr int V5_BMT = 128, V5_BNT = 32, V5_TTW = 4 * 16 + 8;  // table words per K-step: [m_a][16 pairs] + pad
 constexpr uint32_t V5_OFF = 0x20002000u;
@@ -43,6 +48,7 @@ constexpr uint32_t V5_OFF = 0x20002000u;
 
 // B pre-pass: per (k, n) of [kpad][npad] the four table words (m_a = 0..3) of the column as
 // u16 lanes (uint2: m_a 0 | 1 << 16, 2 | 3 << 16); padding entries are zero (masked / dropped).
+#if FP8A_OWN_V5
 __global__ __launch_bounds__(256) void v5mx_decode_b(const GemmArgs p, int64_t kpad) {
     const int a_b = *p.bA, r_b = *p.bR, M = p.Mw;
     uint2 *out = reinterpret_cast<uint2 *>(const_cast<uint2 *>(p.bqw));
@@ -72,6 +78,9 @@ __global__ __launch_bounds__(256) void v5mx_decode_b(const GemmArgs p, int64_t k
         out[i] = o;
     }
 }
+#else
+__global__ void v5mx_decode_b(const GemmArgs p, int64_t kpad);
+#endif  // FP8A_OWN_V5
 
 typedef unsigned short v5_u2 __attribute__((ext_vector_type(2)));
 typedef short v5_s8 __attribute__((ext_vector_type(8)));
@@ -92,6 +101,7 @@ __device__ __forceinline__ uint32_t v5_bits(uint32_t e, uint32_t w) {
     return __builtin_bit_cast(uint32_t, t) & 0x8FE08FE0u;
 }
 
+#if FP8A_OWN_V5
 template <bool UF, bool OF>
 __global__ __launch_bounds__(256) void gemm_v5mx_kernel(const GemmArgs p) {
     constexpr int NT = 256, BMT = V5_BMT, BNT = V5_BNT, APR = BMT / 64, SR = 4096 / BNT, CP = BNT + 1;
@@ -247,3 +257,6 @@ __global__ __launch_bounds__(256) void gemm_v5mx_kernel(const GemmArgs p) {
         for (int j = 0; j < TN; ++j) acc[i][j] = ct[(64 * sub + ety * TM + i) * CP + cb * TN + j];
     store_tile<false>(p, split, m0 + 64 * sub, n0, ety, cb, acc);
 }
+#endif  // FP8A_OWN_V5
+
+}  // namespace fp8a

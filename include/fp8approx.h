@@ -66,24 +66,21 @@ const char *fp8a_last_error(void);
 int fp8a_fallback_stats(uint64_t *out, int reset);
 
 /*
- * Launch paths the GEMM entry points took since load (host-side counters, no device sync), out[8]:
- *   [0] E4M3 one-hot dense matrix-core GEMM + candidate correction (gemm_oh.h),
- *   [1] E4M3 per-pair matrix-core kernel (gemm_f8mx.h), [2] gemm_tt_kernel (E3M4 / E2M5),
- *   [3] gemm_tt16_kernel (E3M4), [4] gemm_fast_kernel (VALU tiled), [5] the exact kernel alone
- *   (tensor-bias products), [6] the dense exact product (fp8a_dense_*), [7] the v5 matrix-core form (gemm_v5mx.h).  reset != 0 zeroes them after reading.
+ * Launch paths the GEMM entry points took since load (host-side counters, no device sync), out[7]:
+ *   [0] E4M3 / E5M2 per-pair matrix-core kernel (gemm_f8mx.h), [1] gemm_tt_kernel (E3M4 / E2M5),
+ *   [2] gemm_tt16_kernel (E3M4), [3] gemm_fast_kernel (VALU tiled), [4] the exact kernel alone
+ *   (tensor-bias products), [5] the dense exact product (fp8a_dense_*), [6] the v5 matrix-core
+ *   form (gemm_v5mx.h).  reset != 0 zeroes them after reading.
  */
 int fp8a_path_stats(uint64_t *out, int reset);
 
 /*
- * Runtime options (A/B measurements, tests, diagnostics): "one_hot" (default 0; the environment
- * variable FP8A_ONE_HOT=1 sets 1 at load) -- whether E4M3 products take the one-hot path when the
- * workspace holds its buffers, else gemm_f8mx_kernel (same results; the one-hot path is slower on
- * the benchmark network); "oh_correct" (default 1; 0 leaves the
- * one-hot path's candidate pairs uncorrected: NOT the reference's result, timing ablations only);
- * "oh_stats" (default 0) -- count fp8a_debug_stats; "dwx" (FP8A_DW=<n> sets it at load) -- the
- * E4M3 depthwise form: 0 the word-image gather (tbx_decode_a + conv_tbx_kernel), 1 the
- * band-staged conv_dwx_kernel, 2 the fp32 gather conv_dwg_kernel, 3 conv_dwg_kernel over the
- * word image (identical sums);
+ * Runtime options (A/B measurements, tests, diagnostics):
+ * "tbx_rw" (default 2; FP8A_TBX_RW) -- output rows per thread of the table-form depthwise kernel;
+ * "tbs" (default 1; FP8A_TBS) -- the LDS-staged table-form depthwise kernel (0: the word-image
+ * gather); "dw3" (default 1; FP8A_DW3) -- the LDS-staged exact depthwise 3x3 (0: the general
+ * grouped kernel); "dw_target" / "dw_lds" -- outputs / LDS bytes per workgroup of those staged
+ * kernels;
  * "xm_ncg" (default 0 = by N; FP8A_XM_NCG) -- gemm_f8mx_kernel's tile width forced to 16 x 1 / 2
  * / 4 columns; "af32_maxct" (default 3; FP8A_AF32_MAXCT) -- the most column tiles for which a 1x1
  * conv / matrix A is decoded inside gemm_f8mx_kernel instead of by its pre-pass (0 = never).
@@ -91,14 +88,6 @@ int fp8a_path_stats(uint64_t *out, int reset);
  * for an unknown name.  Not synchronised with launches in flight on other threads.
  */
 int fp8a_set_option(const char *name, int value);
-
-/*
- * Diagnostic counters of the E4M3 one-hot path, counted only while the option "oh_stats" is 1
- * (out[4]): [0] candidate entries the correction kernel processed, [1] weights excluded from
- * their MX block's window, [2] (A element, 64-column tile) segments holding a candidate, [3] (A
- * element, 64-column tile) segments examined.  Synchronises the device; reset != 0 zeroes them.
- */
-int fp8a_debug_stats(uint64_t *out, int reset);
 
 /*
  * The exact (non-approx) product on the matrix core -- the reference's `x @ y` of FP8-quantized
@@ -312,14 +301,16 @@ int fp8a_word_image_init(void *image, int64_t Bn, int64_t C, int64_t H, int64_t 
  *             call emitted (same Bn, Cin, H, W, ph, pw; needs in_maxval: the words hold
  *             fq_in(x)).  Where the matrix-core path runs, its words replace the A pre-pass; an
  *             image flagged invalid (an element outside the path's window) is re-decoded from x,
- *             which must be the fp32 tensor the emitting call wrote.  Elsewhere it is ignored.
+ *             which must be the fp32 tensor the emitting call wrote -- that re-decode rewrites the
+             image's words in place (hence non-const).  Elsewhere it is ignored.
  *   out_image: NULL, or the NEXT convolution's input image to emit while y is stored: the words
  *             of next_fq(y) for a next convolution with padding next_ph / next_pw, input quantizer
  *             next_maxval (per tensor) / next_nbits / next_mbits / next_sign_bits, result bias
  *             next_bR and mantissa width next_Mw (3: E4M3, 2: E5M2); next_form = the next
  *             convolution's fp8a_conv2d_wants_image - 1 (0: matrix-core words in an image of
  *             next_ph / next_pw; 1: table-form words, image of ph = pw = 0).  y is written as well.
- *             Where this call cannot emit (groups > 1, Cout == 1) the image is flagged invalid.
+ *             Where this call cannot emit (groups > 1, Cout == 1, or the v5 matrix-core form, whose
+             store does not emit) the image is flagged invalid.
  * Results are bit-identical to the unchained calls.  workspace: fp8a_conv2d_block_workspace_size().
  */
 /* The word image a convolution of this shape / format would read as in_image: 1 = the matrix-core
@@ -337,7 +328,7 @@ int fp8a_conv2d_chain(const float *x, const float *w, float *y, int64_t Bn, int6
                       int in_mbits, int in_sign_bits, float *in_bias_out, int32_t *in_ibias_out,
                       const float *res, int post_act, float post_lo, float post_hi,
                       const float *out_maxval, int out_nbits, int out_mbits, int out_sign_bits,
-                      float *out_bias_out, int32_t *out_ibias_out, const void *in_image,
+                      float *out_bias_out, int32_t *out_ibias_out, void *in_image,
                       void *out_image, int next_ph, int next_pw, const float *next_maxval,
                       int next_nbits, int next_mbits, int next_sign_bits, const int32_t *next_bR,
                       int next_Mw, int next_form, void *workspace, size_t workspace_bytes,

@@ -142,6 +142,36 @@ def test_grouped_producer_flags_invalid():
     assert int(img[:4].view(torch.int32).item()) != 0
 
 
+def test_v5_producer_flags_invalid():
+    """A producer on the v5 matrix-core form (gemm_v5mx_kernel, whose store does not emit) feeding
+    a v9 E5M2 consumer: the image comes back flagged invalid and the consumer, which then
+    re-decodes y, gives the unchained result."""
+    from fp8_quantization_amd import _lib
+    from fp8_quantization_amd.approx_ops import approx_conv2d, make_flags, make_flags_v5, new_word_image
+    from fp8_quantization_amd.error_tables import get_error_table_NN
+    g = torch.Generator().manual_seed(5)
+    x = _grid(g, (2, 16, 10, 10), 2).to(DEV)
+    w1 = _grid(g, (32, 16, 3, 3), 2, -8, 0, 0.0).to(DEV)
+    w2 = _grid(g, (32, 32, 3, 3), 2, -8, 0, 0.0).to(DEV)
+    zero = torch.zeros((4, 4), dtype=torch.int32)
+    tab = get_error_table_NN(5, 2, False, 3, zero_table_ext=True)
+    bW = torch.full((32,), 22, dtype=torch.int32, device=DEV)
+    qin2 = (torch.tensor([5.5], device=DEV), 8, 2, 1)
+    bR2 = torch.tensor([16], dtype=torch.int32, device=DEV)
+    img = new_word_image(2, 32, 10, 10, 1, 1, DEV)
+    _lib.path_stats(reset=True)
+    out = approx_conv2d(x, w1, 5, 2, 18, bW, 14, zero, flags=make_flags_v5(True, True, True), padding=(1, 1),
+                        chain=(None, (img, (1, 1), qin2, bR2, 2)))
+    y = out[0]
+    assert _lib.path_stats(reset=True)["v5mx"] >= 1
+    torch.cuda.synchronize()
+    assert int(img[:4].view(torch.int32).item()) != 0
+    args2 = dict(flags=make_flags(True, True, True), padding=(1, 1))
+    z, _, _ = approx_conv2d(y, w2, 5, 2, None, bW, bR2, tab, qin=qin2, **args2)
+    z2, _, _ = approx_conv2d(y, w2, 5, 2, None, bW, bR2, tab, qin=qin2, chain=(img, None), **args2)
+    assert torch.equal(_bits(z), _bits(z2))
+
+
 @pytest.mark.parametrize("arch,fmt", [("resnet18", (4, 3)), ("resnet50", (4, 3)), ("resnet18", (5, 2))])
 def test_model_logits_identical_with_chain(arch, fmt, monkeypatch):
     from fp8_quantization_amd import chain, resnet_workload as rw

@@ -32,16 +32,13 @@ def _native():
     _lib.load()
 
 
-@pytest.fixture(params=["one_hot", "f8mx"])
-def path(request):
-    """Both E4M3 paths: the one-hot dense GEMM + correction (gemm_oh.h, the default) and the
-    per-pair matrix-core kernel (gemm_f8mx.h); the launch's path is read back from the library's
-    path counters."""
+@pytest.fixture
+def path():
+    """The E4M3 per-pair matrix-core kernel (gemm_f8mx.h); the launch's path is read back from the
+    library's path counters."""
     from fp8_quantization_amd import _lib
-    old = _lib.set_option("one_hot", request.param == "one_hot")
     _lib.path_stats(reset=True)
-    yield request.param
-    _lib.set_option("one_hot", old)
+    yield "f8mx"
 
 
 def _ran(path):
@@ -162,10 +159,6 @@ def _sum_operands(Mr, K, N, seed):
 def test_fallback_recomputes_only_marked_units(case, path, ncg):
     """ncg: gemm_f8mx_kernel's tile (4: 128 x 64, 1: 256 x 16 -- option "xm_ncg")."""
     from fp8_quantization_amd import _lib
-    if case == "term_out_of_range" and path == "one_hot":
-        pytest.skip("the one-hot path has no e4m3 range limit (test_terms_beyond_e4m3_range)")
-    if ncg != 4 and path == "one_hot":
-        pytest.skip("tile shapes of gemm_f8mx_kernel only")
     old_ncg = _lib.set_option("xm_ncg", ncg)
     try:
         _fallback_case(case, ncg)

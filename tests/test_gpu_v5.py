@@ -163,14 +163,10 @@ def _e5m2_codes(bias):
 
 
 def _v5_e5m2_tables():
-    from fp8_quantization_amd.approx_v5 import get_comp_table_NN
-    tabs = {"zero": np.zeros((4, 4), np.int32)}
-    try:
-        tabs["v5comp"] = np.asarray(get_comp_table_NN(5, 2, True, 3), np.int32).reshape(4, 4)
-    except Exception:  # (no v5 table for this format)
-        pass
-    tabs["signed"] = np.array([[0, -1, 2, 0], [1, 0, -2, 1], [0, 3, 0, -1], [-3, 1, 1, 0]], np.int32)
-    return tabs
+    # (v5 has no compensation table for E5M2: approx_matmul_whole_v5.py:540 raises, so the
+    # reference-table case is the zero table; "signed" exercises the table path's arithmetic)
+    return {"zero": np.zeros((4, 4), np.int32),
+            "signed": np.array([[0, -1, 2, 0], [1, 0, -2, 1], [0, 3, 0, -1], [-3, 1, 1, 0]], np.int32)}
 
 
 SWITCHES = [dict(sim_hw_add_OFUF=True), dict(sim_hw_add_OFUF=True, with_UF_opt=True),
@@ -180,17 +176,14 @@ SW_IDS = ["wrap", "wrap_uf", "wrap_of", "wrap_of_uf"]
 
 @pytest.mark.parametrize("sw", SWITCHES, ids=SW_IDS)
 @pytest.mark.parametrize("biases", [(16, 16, 12), (12, 20, 30), (20, 10, 2), (8, 8, -20)])
-@pytest.mark.parametrize("table", ["zero", "signed", "v5comp"])
+@pytest.mark.parametrize("table", ["zero", "signed"])
 def test_v5mx_every_code_pair_bitexact(sw, biases, table):
     """gemm_v5mx_kernel (E5M2, the adder wrap on): every one of the 256 x 256 code pairs as a
     K = 1 product equals the oracle's v5 term bit for bit, for each OF / UF switch pair (the
     ragged last K-tile masks the seven padded K-steps)."""
     from fp8_quantization_amd import _lib
     from fp8_quantization_amd.approx_v5 import approx_matmul_v5
-    tabs = _v5_e5m2_tables()
-    if table not in tabs:
-        pytest.skip("no v5 E5M2 compensation table")
-    tab = tabs[table]
+    tab = _v5_e5m2_tables()[table]
     bA, bB, bR = biases
     A = _e5m2_codes(bA).reshape(-1, 1)
     B = _e5m2_codes(bB).reshape(1, -1)
