@@ -159,6 +159,24 @@ def pmc_files():
                   key=lambda n: (n[5:7], n), reverse=True)
 
 
+def pmc_summary(kernel, arch, E, M, batch, strict=False):
+    """(file name, summary dict) of the newest committed PMC summary recorded for this kernel,
+    workload, format and batch (profiles/pmc_r<round>*.json, tools/prof_summary.py); the workload's
+    other-kernel summary when not strict; (None, {}) when there is none."""
+    found = {}
+    for name in pmc_files():
+        try:
+            with open(os.path.join(ROOT, "profiles", name)) as f:
+                j = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if (j.get("arch"), j.get("E"), j.get("M"), j.get("batch", 256)) == (arch, E, M, batch):
+            found.setdefault(j.get("kernel"), (name, j))
+    if kernel in found or strict:
+        return found.get(kernel, (None, {}))
+    return next(iter(found.values()), (None, {}))
+
+
 def pmc_traffic(kernel, arch, E, M, batch, strict=False):
     """Per-launch HBM bytes of the approx GEMM kernel from a committed rocprofv3 PMC summary
     (profiles/pmc_r<round>*.json, tools/prof_summary.py) recorded for this same kernel, workload,
@@ -292,6 +310,8 @@ def run(args, dev, rank=0, world=1):
             fa._lib.fallback_stats(reset=True)  # (synchronises: outside the timed region)
             fa._lib.path_stats(reset=True)
             fa._lib.dense_stats(reset=True)
+            fa._lib.kernel_time(reset=True)
+            fa._lib.kernel_timing(True)  # HIP events around each GEMM's product kernel (fp8a_kernel_timing)
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step()
@@ -300,11 +320,14 @@ def run(args, dev, rank=0, world=1):
             dist.barrier()
         elapsed = time.perf_counter() - t0
         prof, am._PROFILE = am._PROFILE or [], None
+        if cuda:
+            fa._lib.kernel_timing(False)
     # how many launches / 64x64 output units of the timed steps left the fast path (a regression
     # there would otherwise be invisible in the line)
     fallback = fa._lib.fallback_stats() if cuda else None
     paths = {k: v for k, v in fa._lib.path_stats().items() if v} if cuda else None
     dense_fb = fa._lib.dense_stats() if cuda else None
+    ktime = fa._lib.kernel_time(reset=True) if cuda else {}
 
     op_ms = sum(s.elapsed_time(e) for (s, e, _, _) in prof)
     op_macs = sum(m for (_, _, m, _) in prof)
@@ -319,7 +342,19 @@ def run(args, dev, rank=0, world=1):
         kernel, kdesc = dominant_kernel(args.expo_width, args.mant_width, args.v5_ofuf)
         launches = max(1, len(prof))
         avg_s = op_ms / 1e3 / launches
-        achieved = 2.0 * (op_macs / launches) / avg_s / 1e12 if avg_s > 0 else None
+        op_achieved = 2.0 * (op_macs / launches) / avg_s / 1e12 if avg_s > 0 else None
+        # the dominant kernel alone (fp8a_kernel_time: HIP events around each product-kernel launch,
+        # on its stream, over the timed steps): its path's launches, time and approx-MACs
+        kpath = {"gemm_f8mx_kernel": "f8mx", "gemm_tt16_kernel": "tt16", "gemm_tt_kernel": "tt",
+                 "gemm_v5mx_kernel": "v5mx", "gemm_fast_kernel": "fast"}[kernel]
+        kt = ktime.get(kpath, {})
+        k_s = kt.get("ms", 0.0) / 1e3
+        k_avg_s = k_s / kt["launches"] if kt.get("launches") else 0.0
+        achieved = 2.0 * kt["macs"] / k_s / 1e12 if k_s > 0 else None
+        pmc_name, pmc = pmc_summary(kernel, args.arch, args.expo_width, args.mant_width, args.batch)
+        traffic = pmc.get("bytes_per_launch")
+        # HBM: the PMC bytes per dispatch of the kernel x its timed dispatches / its timed time
+        hbm_gbs = traffic * kt["dispatches"] / k_s / 1e9 if (traffic and k_s > 0) else None
         res = {
             "metric": metric_name(args.arch, args.expo_width, args.mant_width, args.v5_ofuf, args.no_approx),
             "value": images / elapsed,
@@ -356,15 +391,35 @@ def run(args, dev, rank=0, world=1):
             },
             "roofline": {
                 "bound": "valu",
-                "kernel": f"{kernel} ({kdesc}); timed per op with its operand pre-decode, split-K reduce and "
+                "kernel": f"{kernel} ({kdesc}); achieved / frac: the kernel alone (HIP events around its "
+                          "launches); op_*: the whole approx op with its operand pre-decode, split-K reduce and "
                           "gated exact kernels",
                 "achieved": achieved,
                 "peak": FP32_VALU_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved / FP32_VALU_PEAK_TFLOPS if achieved else None,
-                "traffic": pmc_traffic(kernel, args.arch, args.expo_width, args.mant_width, args.batch),
-                "algorithmic": f"2 FLOP per approx-MAC; {op_macs / launches:.4g} approx-MAC per launch avg over "
-                               f"{launches} launches, {avg_s * 1e3:.3f} ms avg launch (HIP events)",
+                "kernel_frac": achieved / FP32_VALU_PEAK_TFLOPS if achieved else None,
+                "kernel_avg_ms": k_avg_s * 1e3 if k_avg_s else None,
+                "op_achieved": op_achieved,
+                "op_frac": op_achieved / FP32_VALU_PEAK_TFLOPS if op_achieved else None,
+                "op_avg_ms": avg_s * 1e3,
+                "traffic": traffic,
+                "hbm_gbs": hbm_gbs,
+                "hbm_frac": hbm_gbs / HBM_PEAK_GBS if hbm_gbs else None,
+                "valu_busy": pmc.get("valu_busy"),
+                "valu_insts_per_simd_cycle": pmc.get("valu_instr_per_simd_cycle"),
+                "wave_cycles": pmc.get("wave_cycles"),
+                "pmc_summary": f"profiles/{pmc_name}" if pmc_name else None,
+                "algorithmic": f"2 FLOP per approx-MAC; kernel: {kt.get('macs', 0) / max(1, kt.get('launches', 0)):.4g} "
+                               f"approx-MAC per launch over {kt.get('launches', 0)} launches "
+                               f"({kt.get('dispatches', 0)} dispatches), {k_avg_s * 1e3:.3f} ms avg launch; op: "
+                               f"{op_macs / launches:.4g} approx-MAC per launch over {launches} launches, "
+                               f"{avg_s * 1e3:.3f} ms avg (HIP events)",
+                "hbm_note": "hbm_gbs = PMC HBM bytes per dispatch of the kernel (traffic, FETCH_SIZE x 2 + WRITE_SIZE, "
+                            "tools/prof_summary.py) x its timed dispatches / its timed time; valu_busy = rocprof's "
+                            "VALUBusy (4 x SQ_ACTIVE_INST_VALU / (SIMDs x GRBM_GUI_ACTIVE per XCD)), summed over "
+                            "resident waves, so it counts a wave's cycles inside a VALU instruction, not VALU pipe "
+                            "occupancy; wave_cycles: SQ_WAIT_ANY / SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY shares",
                 "approx_macs_per_s": op_macs / (op_ms / 1e3) if op_ms > 0 else None,
                 "gemm_share_of_step": op_ms / 1e3 / elapsed,
             },

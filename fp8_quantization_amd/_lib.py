@@ -16,7 +16,7 @@ V5, OFUF, OF_OPT, UF_OPT = 32, 64, 128, 256  # v5 integer-adder model (include/f
 OK, EINVAL, EFORMAT, EHIP = 0, -1, -2, -3
 DENSE_E4M3, DENSE_E5M2, DENSE_BF16 = 0, 1, 2  # fp8a_dense_* operand formats
 
-SYMBOLS = ("fp8a_version", "fp8a_last_error", "fp8a_fallback_stats", "fp8a_path_stats", "fp8a_set_option", "fp8a_decompose", "fp8a_quant", "fp8a_matmul_workspace_size",
+SYMBOLS = ("fp8a_version", "fp8a_last_error", "fp8a_fallback_stats", "fp8a_path_stats", "fp8a_kernel_timing", "fp8a_kernel_time", "fp8a_set_option", "fp8a_decompose", "fp8a_quant", "fp8a_matmul_workspace_size",
            "fp8a_matmul_workspace_size_mnk", "fp8a_matmul", "fp8a_terms", "fp8a_conv2d_workspace_size", "fp8a_conv2d",
            "fp8a_conv2d_bn_act", "fp8a_conv2d_qin_workspace_size", "fp8a_conv2d_qin",
            "fp8a_conv2d_block_workspace_size", "fp8a_conv2d_block", "fp8a_max_pool2d", "fp8a_avg_pool2d_plane", "fp8a_im2col",
@@ -49,6 +49,8 @@ def load():
         "fp8a_last_error": ([], ctypes.c_char_p),
         "fp8a_fallback_stats": ([P, I], I),
         "fp8a_path_stats": ([P, I], I),
+        "fp8a_kernel_timing": ([I], I),
+        "fp8a_kernel_time": ([P, I], I),
         "fp8a_set_option": ([ctypes.c_char_p, I], I),
         "fp8a_decompose": ([P, I64, I64, I64, I, I, P, I64, U, P, P, P], I),
         "fp8a_quant": ([P, I64, I, I, P, U, P, P], I),
@@ -151,6 +153,22 @@ def path_stats(reset=False):
     out = (ctypes.c_uint64 * len(PATHS))()
     check(L.fp8a_path_stats(ctypes.cast(out, ctypes.c_void_p), 1 if reset else 0), "fp8a_path_stats")
     return {k: int(v) for k, v in zip(PATHS, out)}
+
+
+def kernel_timing(enable):
+    """fp8a_kernel_timing: record HIP events around every GEMM's product kernel; returns the
+    previous state."""
+    return int(load().fp8a_kernel_timing(1 if enable else 0))
+
+
+def kernel_time(reset=False):
+    """fp8a_kernel_time: {path: dict(ms, launches, dispatches, macs)} of the recorded launches
+    (synchronises on their events)."""
+    L = load()
+    out = (ctypes.c_double * (4 * len(PATHS)))()
+    check(L.fp8a_kernel_time(ctypes.cast(out, ctypes.c_void_p), 1 if reset else 0), "fp8a_kernel_time")
+    return {k: dict(ms=out[4 * i], launches=int(out[4 * i + 1]), dispatches=int(out[4 * i + 2]), macs=out[4 * i + 3])
+            for i, k in enumerate(PATHS) if out[4 * i + 1] > 0}
 
 
 _option_gen = 0

@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <string>
+#include <vector>
 
 #include "../../include/fp8approx.h"
 #include "fp8approx_common.h"
@@ -637,6 +638,33 @@ constexpr size_t FLAG_BYTES = 256;  // workspace prefix holding the off-grid fla
 enum { PATH_F8MX = 0, PATH_TT = 1, PATH_TT16 = 2, PATH_FAST = 3, PATH_EXACT = 4, PATH_DENSE = 5, PATH_V5MX = 6,
        PATH_N = 7 };
 static std::atomic<uint64_t> g_paths[PATH_N];
+
+// Kernel timing (fp8a_kernel_timing / fp8a_kernel_time): while on, run_gemm brackets the product
+// kernel launch(es) of every GEMM (launch_fast: gemm_f8mx_kernel, gemm_tt*_kernel, gemm_v5mx_kernel
+// or gemm_fast_kernel -- not the operand pre-passes, split-K reduce or gated exact kernel) with HIP
+// events on the launching stream, so a benchmark can report the dominant kernel's own time next to
+// the op's.  Host-side, single-threaded use (benchmarks); events come from a pool.
+struct KernelEv {
+    hipEvent_t a, b;
+    int path, dispatches;
+    double macs;
+};
+static bool g_ktime = false;
+static std::vector<KernelEv> g_kev;
+static std::vector<hipEvent_t> g_evpool;
+static hipEvent_t pool_event() {
+    if (!g_evpool.empty()) {
+        hipEvent_t e = g_evpool.back();
+        g_evpool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return e;
+}
 // Options (fp8a_set_option):
 // "tbx_rw": output rows per thread of conv_tbx_kernel (1 or 2; 2 needs undilated rows).
 // FP8A_TBX_RW=<n> sets it at load.
@@ -962,7 +990,21 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
         if (hipMemsetAsync(a.em.invalid, 1, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a word image header");
         a.em.w = nullptr;
     }
+    KernelEv kev{};
+    if (g_ktime) {
+        kev.a = pool_event();
+        kev.b = pool_event();
+        kev.path = !a.aw ? PATH_FAST : a.wfmt == 0 ? PATH_F8MX : a.wfmt == 1 ? PATH_TT : a.wfmt == 4 ? PATH_V5MX : PATH_TT16;
+        // (E5M2: the plain and the halved-block form; E3M4 f16 form: + its gated f32 rerun)
+        kev.dispatches = (a.aw && ((a.wfmt == 0 && a.Mw == 2) || a.wfmt == 2)) ? 2 : 1;
+        kev.macs = (double)a.M * (double)a.N * (double)a.K;
+        if (kev.a && kev.b) (void)hipEventRecord(kev.a, s);
+    }
     launch_fast(mode, a, s);
+    if (g_ktime && kev.a && kev.b) {
+        (void)hipEventRecord(kev.b, s);
+        g_kev.push_back(kev);
+    }
     rc = hip_check("fp8a fast gemm launch");
     if (rc) return rc;
     if (a.splits > 1) {
@@ -1159,6 +1201,34 @@ const char *fp8a_last_error(void) { return g_err.c_str(); }
 int fp8a_path_stats(uint64_t *out, int reset) {
     if (out == nullptr) return fail(FP8A_EINVAL, "null pointer");
     for (int i = 0; i < PATH_N; ++i) out[i] = reset ? g_paths[i].exchange(0) : g_paths[i].load();
+    return FP8A_OK;
+}
+
+int fp8a_kernel_timing(int enable) {
+    const int old = g_ktime ? 1 : 0;
+    g_ktime = enable != 0;
+    return old;
+}
+
+int fp8a_kernel_time(double *out, int reset) {
+    if (out == nullptr) return fail(FP8A_EINVAL, "null pointer");
+    for (int i = 0; i < 4 * PATH_N; ++i) out[i] = 0.0;
+    for (const KernelEv &e : g_kev) {
+        if (hipEventSynchronize(e.b) != hipSuccess) return hip_check("fp8a_kernel_time");
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, e.a, e.b) != hipSuccess) return hip_check("fp8a_kernel_time");
+        out[4 * e.path] += ms;
+        out[4 * e.path + 1] += 1.0;
+        out[4 * e.path + 2] += e.dispatches;
+        out[4 * e.path + 3] += e.macs;
+    }
+    if (reset) {
+        for (const KernelEv &e : g_kev) {
+            g_evpool.push_back(e.a);
+            g_evpool.push_back(e.b);
+        }
+        g_kev.clear();
+    }
     return FP8A_OK;
 }
 

@@ -483,7 +483,11 @@ __device__ unsigned long long g_clk[3];
 #define FP8A_CLK_END
 #endif
 #ifndef XM_WAVES
-#define XM_WAVES 6  // register bound: 80 VGPRs, 6 waves / SIMD (the LDS allows 6 workgroups / CU)
+// register bound: 5 waves / SIMD (<= 96 VGPRs; the 128 x 64 instance needs 82).  At 6 waves (80
+// VGPRs) that instance spilled 4-30 VGPRs to scratch inside its K loop, and a scratch load's vmcnt
+// wait also waited for the tile prefetch issued before it (in-order vmcnt): ResNet-18 layer set
+// 28.7 -> 25.5 ms, bench 11835 -> 12454 images/s at 5 waves (round 5)
+#define XM_WAVES 5
 #endif
 // The GEMM.  Tile BMT x BNT (XmCfg), 4 waves; wave wv = column group wc = wv % NCG (the 16
 // columns 16 wc .. 16 wc + 15, column blocks tx = 4 wc + c of the tile table) and row group

@@ -75,6 +75,17 @@ int fp8a_fallback_stats(uint64_t *out, int reset);
 int fp8a_path_stats(uint64_t *out, int reset);
 
 /*
+ * Kernel timing for benchmarks: while enabled (fp8a_kernel_timing(1); returns the previous
+ * state), every GEMM records HIP events on its stream around its product kernel launch(es) only
+ * (not its operand pre-passes, split-K reduction or gated exact kernel).  fp8a_kernel_time
+ * synchronises on the recorded events and writes, per launch path in fp8a_path_stats order,
+ * out[4 * path + 0..3] = (summed kernel milliseconds, launches, kernel dispatches, approx-MACs
+ * M * N * K); reset != 0 forgets the recorded launches.  Host-side, single-threaded use.
+ */
+int fp8a_kernel_timing(int enable);
+int fp8a_kernel_time(double *out, int reset);
+
+/*
  * Runtime options (A/B measurements, tests, diagnostics):
  * "tbx_rw" (default 2; FP8A_TBX_RW) -- output rows per thread of the table-form depthwise kernel;
  * "tbs" (default 1; FP8A_TBS) -- the LDS-staged table-form depthwise kernel (0: the word-image

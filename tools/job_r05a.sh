@@ -4,7 +4,7 @@
 # 2. SQ counters of the ResNet-18 l3.c2 dispatch (tools/gemm_bench.py), three PMC passes whose
 #    WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY should close against SQ_WAVE_CYCLES.
 set -o pipefail
-R=$(pwd); OUT=$R/gpurun_out/r05a; mkdir -p $OUT
+R=$(pwd); OUT=$R/gpurun_out/${1:-r05a}; mkdir -p $OUT
 timeout -k 10 120 tools/bin/seg_bench 400 > $OUT/seg_bench.txt 2>&1 || exit $?
 cat $OUT/seg_bench.txt
 cd /tmp && export TMPDIR=/tmp

@@ -104,9 +104,19 @@ def main():
                        "bytes_per_launch = (2 x FETCH_SIZE + WRITE_SIZE) x 1024: FETCH_SIZE reads half the bytes of "
                        "4- and 16-B-per-lane buffer loads (tools/fetch_cal.hip, MI355X_MICROARCH.md HBM section)",
                   arch=a.arch, E=a.E, M=a.M, batch=a.batch)
+        pj["kernel"] = KERNEL
         if "FETCH_SIZE" in pm and "WRITE_SIZE" in pm:
             pj.update(kernel=KERNEL, bytes_per_launch=(FETCH_CAL * pm["FETCH_SIZE"] + pm["WRITE_SIZE"]) * 1024.0,
                       fetch_kb=pm["FETCH_SIZE"], write_kb=pm["WRITE_SIZE"])
+        if "SQ_ACTIVE_INST_VALU" in pm and "GRBM_GUI_ACTIVE" in pm:
+            # rocprof's VALUBusy (gfx9 formula: 4 x SQ_ACTIVE_INST_VALU / (SIMDs x GRBM_GUI_ACTIVE per XCD);
+            # SQ_ACTIVE_INST_VALU is quad-cycles summed over resident waves)
+            pj["valu_busy"] = 4.0 * pm["SQ_ACTIVE_INST_VALU"] / (1024.0 * pm["GRBM_GUI_ACTIVE"] / 8.0)
+        if "SQ_WAVE_CYCLES" in pm and pm["SQ_WAVE_CYCLES"] > 0:
+            pj["wave_cycles"] = {k[3:].lower(): pm[k] / pm["SQ_WAVE_CYCLES"] for k in
+                                 ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY") if k in pm}
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in pm and "GRBM_GUI_ACTIVE" in pm:
+            pj["mfma_busy"] = pm["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * pm["GRBM_GUI_ACTIVE"] / 8.0)
         if "SQ_INSTS_VALU" in pm and "GRBM_GUI_ACTIVE" in pm:
             # GRBM_GUI_ACTIVE is summed over the 8 XCDs; 1024 SIMDs; a wave64 VALU op issues in 2 cycles
             cyc = pm["GRBM_GUI_ACTIVE"] / 8.0

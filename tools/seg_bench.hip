@@ -29,10 +29,11 @@ struct Stage {
     uint32_t aw[XBK / 2][AWQ];
 };
 
-enum { P_LDS = 1, P_CVT = 2, P_MFMA = 4, P_BUILD = 8, P_BAR = 16, P_STAGE = 32 };
+enum { P_LDS = 1, P_CVT = 2, P_MFMA = 4, P_BUILD = 8, P_BAR = 16, P_STAGE = 32, P_GLOAD = 64 };
 
 template <int P, int WAVES>
-__global__ __launch_bounds__(256, WAVES) void seg(const uint32_t *seed, float *out, unsigned long long *cyc, int tiles) {
+__global__ __launch_bounds__(256, WAVES) void seg(const uint32_t *seed, float *out, unsigned long long *cyc, int tiles,
+                                                  const uint32_t *gbuf) {
     __shared__ __attribute__((aligned(16))) Stage sm;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     // fill LDS with plausible data: table words = random bf16 pairs near 1.0, A words = se << 23 | row << 3
@@ -65,11 +66,26 @@ __global__ __launch_bounds__(256, WAVES) void seg(const uint32_t *seed, float *o
     const uint32_t wvo = (uint32_t)wv * 512u;
     typedef const volatile __attribute__((address_space(3))) uint64_t lds_u64;
     uint32_t stw = seed[tid & 1023];
+    // P_GLOAD: the kernel's per-tile global traffic -- per thread 4 A words (b32, lane-consecutive
+    // rows, a K-step's plane offset in the uniform soffset) and 2 B pair units (b128), one tile ahead
+    const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(gbuf), (short)0, -1, 0x00020000);
+    const uint32_t gA = (uint32_t)(blockIdx.x * 128 + lane) * 4u, gB = (uint32_t)(blockIdx.x * 256 + tid) * 16u;
+    uint32_t ga[4] = {0, 0, 0, 0};
+    uint4 gb[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+    auto gload = [&](int it) {
+        const uint32_t ko = (uint32_t)((it * 8 + 2 * wv) & 1023) * 262144u;  // 1 MiB per K-step plane
+        for (int i = 0; i < 4; ++i)
+            ga[i] = __builtin_amdgcn_raw_buffer_load_b32(grs, (int)(gA + 256u * (i >> 1)), (int)(ko + 1048576u * (i & 1)), 0);
+        for (int u = 0; u < 2; ++u)
+            gb[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(grs, (int)(gB + 4096u * u), (int)(ko & 0x3FFFFFu), 0));
+    };
+    if (P & P_GLOAD) gload(0);
     __syncthreads();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     for (int it = 0; it < tiles; ++it) {
         if (P & P_STAGE) {
             stw = stw * 1664525u + 1013904223u;
+            if (P & P_GLOAD) stw ^= ga[0] ^ ga[1] ^ ga[2] ^ ga[3] ^ gb[0].x ^ gb[1].y;
             *reinterpret_cast<uint2 *>(&sm.aw[wv][2 * lane]) = make_uint2((110u << 23) | (stw & 0x78u), (111u << 23) | ((stw >> 8) & 0x78u));
             *reinterpret_cast<uint2 *>(&sm.aw[wv][2 * (lane + 64)]) = make_uint2((112u << 23) | ((stw >> 4) & 0x78u), (110u << 23) | ((stw >> 12) & 0x78u));
         }
@@ -88,6 +104,7 @@ __global__ __launch_bounds__(256, WAVES) void seg(const uint32_t *seed, float *o
             }
         }
         if (P & P_BAR) __syncthreads();
+        if ((P & P_GLOAD) && it + 1 < tiles) gload(it + 1);
         {
             const int r16 = lane & 15, g = lane >> 4;
             const uint32_t base = wvo + (uint32_t)(2 * g) * (uint32_t)(TTK * 4);
@@ -140,19 +157,20 @@ __global__ __launch_bounds__(256, WAVES) void seg(const uint32_t *seed, float *o
     if (tid == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
-typedef void (*kfn)(const uint32_t *, float *, unsigned long long *, int);
+typedef void (*kfn)(const uint32_t *, float *, unsigned long long *, int, const uint32_t *);
 
 template <int P, int W>
-static void run(const char *name, int cus, const uint32_t *seed, float *out, unsigned long long *cyc, int tiles) {
+static void run(const char *name, int cus, const uint32_t *seed, float *out, unsigned long long *cyc, int tiles,
+                const uint32_t *gbuf) {
     const int blocks = cus * W;  // one workgroup = one wave per SIMD; W workgroups per CU
     kfn f = seg<P, W>;
-    f<<<blocks, 256>>>(seed, out, cyc, 4);
+    f<<<blocks, 256>>>(seed, out, cyc, 4, gbuf);
     hipDeviceSynchronize();
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
     hipEventRecord(a);
-    f<<<blocks, 256>>>(seed, out, cyc, tiles);
+    f<<<blocks, 256>>>(seed, out, cyc, tiles, gbuf);
     hipEventRecord(b);
     hipEventSynchronize(b);
     float ms;
@@ -186,22 +204,29 @@ int main(int argc, char **argv) {
     uint32_t x = 12345;
     for (int i = 0; i < 1024; ++i) hs[i] = (x = x * 1664525u + 1013904223u);
     hipMemcpy(seed, hs, 4096, hipMemcpyHostToDevice);
+    uint32_t *gbuf;  // 1 GiB + margin of words for the global-load variants (L2 / MALL / HBM mix)
+    hipMalloc(&gbuf, (1ull << 30) + (64ull << 20));
+    hipMemset(gbuf, 0, (1ull << 30) + (64ull << 20));
     constexpr int ALL = P_LDS | P_CVT | P_MFMA | P_BUILD | P_BAR | P_STAGE;
-    run<ALL, 6>("full (stage+build+bar+lds+cvt+mfma)", cus, seed, out, cyc, tiles);
-    run<ALL, 4>("full", cus, seed, out, cyc, tiles);
-    run<ALL, 2>("full", cus, seed, out, cyc, tiles);
-    run<ALL & ~P_BAR, 6>("no barriers", cus, seed, out, cyc, tiles);
-    run<ALL & ~(P_BUILD | P_STAGE), 6>("no build/stage (bar kept)", cus, seed, out, cyc, tiles);
-    run<P_LDS | P_CVT | P_MFMA, 6>("segment only (lds+cvt+mfma)", cus, seed, out, cyc, tiles);
-    run<P_LDS | P_CVT | P_MFMA, 4>("segment only", cus, seed, out, cyc, tiles);
-    run<P_LDS | P_CVT | P_MFMA, 2>("segment only", cus, seed, out, cyc, tiles);
-    run<P_CVT | P_MFMA, 6>("cvt+mfma (no table reads)", cus, seed, out, cyc, tiles);
-    run<P_LDS | P_MFMA, 6>("lds+mfma (no cvt)", cus, seed, out, cyc, tiles);
-    run<P_LDS | P_CVT, 6>("lds+cvt (no mfma)", cus, seed, out, cyc, tiles);
-    run<P_CVT, 6>("cvt only", cus, seed, out, cyc, tiles);
-    run<P_LDS, 6>("lds only", cus, seed, out, cyc, tiles);
-    run<ALL & ~P_CVT, 6>("full minus cvt", cus, seed, out, cyc, tiles);
-    run<ALL & ~P_LDS, 6>("full minus table reads", cus, seed, out, cyc, tiles);
-    run<ALL & ~P_MFMA, 6>("full minus mfma", cus, seed, out, cyc, tiles);
+    constexpr int ALLG = ALL | P_GLOAD;
+    run<ALLG, 5>("full + global loads", cus, seed, out, cyc, tiles, gbuf);
+    run<ALLG, 6>("full + global loads", cus, seed, out, cyc, tiles, gbuf);
+    run<ALL, 5>("full (stage+build+bar+lds+cvt+mfma)", cus, seed, out, cyc, tiles, gbuf);
+    run<ALL, 6>("full (stage+build+bar+lds+cvt+mfma)", cus, seed, out, cyc, tiles, gbuf);
+    run<ALL, 4>("full", cus, seed, out, cyc, tiles, gbuf);
+    run<ALL, 2>("full", cus, seed, out, cyc, tiles, gbuf);
+    run<ALL & ~P_BAR, 6>("no barriers", cus, seed, out, cyc, tiles, gbuf);
+    run<ALL & ~(P_BUILD | P_STAGE), 6>("no build/stage (bar kept)", cus, seed, out, cyc, tiles, gbuf);
+    run<P_LDS | P_CVT | P_MFMA, 6>("segment only (lds+cvt+mfma)", cus, seed, out, cyc, tiles, gbuf);
+    run<P_LDS | P_CVT | P_MFMA, 4>("segment only", cus, seed, out, cyc, tiles, gbuf);
+    run<P_LDS | P_CVT | P_MFMA, 2>("segment only", cus, seed, out, cyc, tiles, gbuf);
+    run<P_CVT | P_MFMA, 6>("cvt+mfma (no table reads)", cus, seed, out, cyc, tiles, gbuf);
+    run<P_LDS | P_MFMA, 6>("lds+mfma (no cvt)", cus, seed, out, cyc, tiles, gbuf);
+    run<P_LDS | P_CVT, 6>("lds+cvt (no mfma)", cus, seed, out, cyc, tiles, gbuf);
+    run<P_CVT, 6>("cvt only", cus, seed, out, cyc, tiles, gbuf);
+    run<P_LDS, 6>("lds only", cus, seed, out, cyc, tiles, gbuf);
+    run<ALL & ~P_CVT, 6>("full minus cvt", cus, seed, out, cyc, tiles, gbuf);
+    run<ALL & ~P_LDS, 6>("full minus table reads", cus, seed, out, cyc, tiles, gbuf);
+    run<ALL & ~P_MFMA, 6>("full minus mfma", cus, seed, out, cyc, tiles, gbuf);
     return 0;
 }
