@@ -90,7 +90,8 @@ def load():
         "fp8a_dense_conv2d": ([P, P, P, I64, I64, I64, I64, I64, I, I, I, I, I, I, I, I, I, P, SZ, P], I),
         "fp8a_grouped_conv2d": ([P, P, P, I64, I64, I64, I64, I64, I, I, I, I, I, I, I, I, I, P], I),
         "fp8a_dense_conv2d_fused": ([P, P, P, I64, I64, I64, I64, I64, I, I, I, I, I, I, I, I, I, I,
-                                     P, I, I, I, P, P, P, I, I, I, P, P, P, I, F, F, P, I, I, I, P, P, P, SZ, P], I),
+                                     P, I, I, I, I, P, P, P, I, I, I, P, P, P, I, I, I, P, P, P, I, F, F,
+                                     P, I, I, I, P, P, P, SZ, P], I),
         "fp8a_dense_stats": ([P, I], I),
         "fp8a_clock_stats": ([P, I], I),
     }

@@ -860,11 +860,13 @@ def grouped_conv2d(x, w, groups, stride=(1, 1), padding=(0, 0), dilation=(1, 1))
 
 
 def dense_conv2d_fused(x, w, groups=1, stride=(1, 1), padding=(0, 0), dilation=(1, 1), fmt=None, qin=None, rq=None,
-                       bn=None, oq=None):
-    """A config-1 layer in one launch family (fp8a_dense_conv2d_fused): y = oq(clamp(bn(rq(conv(qin(x), w))))).
+                       bn=None, oq=None, wq=None):
+    """A config-1 layer in one launch family (fp8a_dense_conv2d_fused): y = oq(clamp(bn(rq(conv(qin(x), wq(w)))))).
     qin / rq / oq: (maxval, n_bits, mantissa bits, sign bits) of a per-tensor FP8 quantizer or None;
-    bn: (scale_shift [C][2], act, lo, hi) from bn_act_epilogue or None.  Returns (y, biases): each
-    given quantizer's float bias tensor [1] (its custom_bias), keyed "qin" / "rq" / "oq"."""
+    wq: the same for the weight quantizer, per tensor or per output channel (maxval [Cout]); bn:
+    (scale_shift [C][2], act, lo, hi) from bn_act_epilogue or None.  Returns (y, biases): each
+    given quantizer's float bias tensor (its custom_bias: [1], or [Cout, 1, 1, 1] for a per-channel
+    wq, as fp8_fake_quantize returns it), keyed "qin" / "rq" / "oq" / "wq"."""
     if x.dim() != 4 or w.dim() != 4 or x.shape[1] != w.shape[1] * groups or w.shape[0] % groups:
         raise AssertionError(f"dense_conv2d_fused: shape mismatch {tuple(x.shape)} * {tuple(w.shape)} / {groups}")
     L = _lib.load()
@@ -876,17 +878,25 @@ def dense_conv2d_fused(x, w, groups=1, stride=(1, 1), padding=(0, 0), dilation=(
     Wo = (W + 2 * padding[1] - dilation[1] * (kw - 1) - 1) // stride[1] + 1
     y = torch.empty((Bn, Cout, Ho, Wo), dtype=torch.float32, device=x.device)
     keep, biases, qargs = [], {}, []
-    for name, q in (("qin", qin), ("rq", rq), ("oq", oq)):
+    for name, q in (("wq", wq), ("qin", qin), ("rq", rq), ("oq", oq)):
         if q is None:
-            qargs += [None, 0, 0, 0, None, None]
+            qargs += [None, 0, 0, 0, None, None] if name != "wq" else [None, 0, 0, 0, 0, None, None]
             continue
         mx = _as_f32(q[0]).reshape(-1).to(x.device).contiguous()
-        b = torch.empty(1, dtype=torch.float32, device=x.device)
-        ib = torch.empty(1, dtype=torch.int32, device=x.device)
-        b._fp8a_i32 = ib
+        rows = mx.numel()
+        if name == "wq" and rows not in (1, Cout):
+            raise AssertionError(f"dense_conv2d_fused: weight quantizer with {rows} maxvals for {Cout} channels")
+        if name != "wq" and rows != 1:
+            raise AssertionError(f"dense_conv2d_fused: {name} must be a per-tensor quantizer")
+        b = torch.empty(rows, dtype=torch.float32, device=x.device)
+        ib = torch.empty(rows, dtype=torch.int32, device=x.device)
         keep.append(mx)
+        head = [_lib.dev_ptr(mx)] + ([int(rows > 1)] if name == "wq" else [])
+        qargs += head + [int(q[1]), int(q[2]), int(q[3]), _lib.dev_ptr(b), _lib.dev_ptr(ib)]
+        if rows > 1:
+            b = b.view(-1, 1, 1, 1)
+        b._fp8a_i32 = ib
         biases[name] = b
-        qargs += [_lib.dev_ptr(mx), int(q[1]), int(q[2]), int(q[3]), _lib.dev_ptr(b), _lib.dev_ptr(ib)]
     ep, act, lo, hi = (None, 0, 0.0, 0.0) if bn is None else bn
     if ep is not None:
         ep = _as_f32(ep).to(x.device).contiguous()
@@ -895,8 +905,8 @@ def dense_conv2d_fused(x, w, groups=1, stride=(1, 1), padding=(0, 0), dilation=(
     fmt = dense_format(3) if fmt is None else fmt
     ev = _prof_start()
     rc = L.fp8a_dense_conv2d_fused(_lib.dev_ptr(x), _lib.dev_ptr(w), _lib.dev_ptr(y), *geo, int(groups), int(fmt),
-                                   *qargs[:12], _lib.dev_ptr(ep) if ep is not None else None, int(act), float(lo),
-                                   float(hi), *qargs[12:], _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(x.device))
+                                   *qargs[:19], _lib.dev_ptr(ep) if ep is not None else None, int(act), float(lo),
+                                   float(hi), *qargs[19:], _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(x.device))
     _lib.check(rc, "fp8a_dense_conv2d_fused")
     _prof_end(ev, y.numel() * w.shape[1] * kh * kw, 4 * (x.numel() + w.numel() + y.numel()))
     return y, biases

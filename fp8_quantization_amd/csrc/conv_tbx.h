@@ -306,11 +306,19 @@ __global__ __launch_bounds__(256) void conv_tbs_kernel(const float *x, const flo
 //
 // A word: sign(a) << 31 | (m_a * 8) << 16 | c_a (c_a < 2^7); the zero word (0) is the code of +0,
 // which is also what the reference's im2col padding decodes to.
+// fq.mx set: x is unquantized; the activation quantizer is applied to each value first and its
+// bias (the decode's bA) written to fqb / fqi, as xm_decode_a does.
 __global__ __launch_bounds__(256) void v5dw_decode_a(const float *x, int64_t n, uint32_t *out, int E, int M,
-                                                     const int32_t *bA) {
-    const DFmt f = dfmt(E, M, *bA, false);
+                                                     const int32_t *bA, FqIn fq, float *fqb, int32_t *fqi) {
+    const float fmx = fq.mx ? *fq.mx : 0.0f, fbias = fq.mx ? fq_bias(fmx, fq.E, fq.M) : 0.0f;
+    if (fq.mx && blockIdx.x == 0 && threadIdx.x == 0) {
+        *fqb = fbias;
+        *fqi = (int32_t)fbias;
+    }
+    const DFmt f = dfmt(E, M, fq.mx ? (int)fbias : *bA, false);
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const float v = x[i];
+        float v = x[i];
+        if (fq.mx) v = fq_apply(v, fmx, fbias, fq.M, fq.S);
         int e, m;
         exact_dec(v, f, true, e, m);
         out[i] = (v < 0.0f ? 0x80000000u : 0u) | ((uint32_t)(m * 8) << 16) | (uint32_t)(e * (1 << M) + m);

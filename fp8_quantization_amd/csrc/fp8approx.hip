@@ -672,8 +672,9 @@ static int g_opt_tbx_rw = getenv("FP8A_TBX_RW") ? atoi(getenv("FP8A_TBX_RW")) : 
 // "tbs": the table-form depthwise 3x3 on the LDS-staged conv_tbs_kernel with the word pre-pass
 // fused (1, default) or on tbx_decode_a + conv_tbx_kernel (0; the same bits).  FP8A_TBS=<n>.
 static int g_opt_tbs = getenv("FP8A_TBS") ? atoi(getenv("FP8A_TBS")) : 1;
-// "dw3": the exact depthwise 3x3 on the LDS-staged dn_dw3_kernel (1, default) or on the general
-// dn_group_conv (0; the same bits).  FP8A_DW3=<n> sets it at load.
+// "dw3": the exact depthwise 3x3 on the LDS-staged dn_dw3_kernel (1, default), its LDS-DMA-staged
+// form dn_dw3g_kernel (2) or the general dn_group_conv (0); the same bits.  FP8A_DW3=<n> sets it
+// at load.
 static int g_opt_dw3 = getenv("FP8A_DW3") ? atoi(getenv("FP8A_DW3")) : 1;
 // "dw_target": outputs per workgroup the LDS-staged depthwise kernels aim at (plan_dw3 / plan_tbs;
 // halved until the window fits dw_lds).  FP8A_DW_TARGET=<n>.
@@ -784,6 +785,13 @@ static bool f8_form(int E, int Mw, uint32_t flags, int table_mode) {
     const bool fmt = (E == 4 && Mw == 3) || (E == 5 && Mw == 2 && !no_f8_e5);
     return !no_f8 && !(flags & F_V5) && fmt && (table_mode == TM_NONE || table_mode == TM_W1U) &&
            (flags & F_S2N) && (flags & F_QBMA) && !(flags & F_GCLIP) && !(flags & F_TB);
+}
+
+// v5 (E5M2, adder wrap on): the matrix-core form of gemm_v5mx.h; FP8A_NO_V5MX=1 keeps
+// gemm_fast_kernel<TM_V5> (A/B runs)
+static bool v5mx_form(int Mw, uint32_t flags, int table_mode) {
+    static const bool no_v5mx = getenv("FP8A_NO_V5MX") != nullptr;
+    return table_mode == TM_V5 && Mw == 2 && (flags & F_OFUF) && !no_v5mx;
 }
 
 // The tile-table kernel (gemm_tt_kernel) applies: E3M4 / E2M5 (mantissa 4 or 5), any table mode
@@ -924,10 +932,7 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     // operands in the workspace (else gemm_fast_kernel runs); FP8A_NO_MX=1 forces the latter
     a.aw = nullptr;
     const bool tt = mode != TM_F8 && tt_form(a.Mw, a.flags, a.tab);
-    // v5 (E5M2, adder wrap on): the matrix-core form of gemm_v5mx.h; FP8A_NO_V5MX=1 keeps
-    // gemm_fast_kernel<TM_V5> (A/B runs)
-    static const bool no_v5mx = getenv("FP8A_NO_V5MX") != nullptr;
-    const bool v5mx = mode == TM_V5 && a.Mw == 2 && (a.flags & F_OFUF) && !no_v5mx;
+    const bool v5mx = v5mx_form(a.Mw, a.flags, mode);
     if ((mode == TM_F8 || tt || v5mx) && !no_mx()) {
         const int64_t kpad = kt * BK, npad = (a.N + BN - 1) / BN * BN;
         const size_t off = head + (a.splits > 1 ? splitk_bytes(a.M, a.N, a.K) : 0);
@@ -1053,14 +1058,31 @@ static size_t dense_ws_bytes(int64_t M, int64_t N, int64_t K) {
     const int64_t mpad = round_up(std::max<int64_t>(M, 1), DN_T), npad = round_up(std::max<int64_t>(N, 1), DN_T);
     const int64_t kpad = round_up(std::max<int64_t>(K, 1), 32);
     // byte images at 2 B per element (the bf16 form; the fp8 forms use the first half)
-    return al256((size_t)(mpad / DN_U + npad / DN_U) + 4) + al256((size_t)(2 * mpad * kpad)) +
+    return al256(4 * (size_t)(mpad / DN_U + npad / DN_U) + 4) + al256((size_t)(2 * mpad * kpad)) +
            al256((size_t)(mpad * kpad / 32)) + al256((size_t)(2 * npad * kpad)) + al256((size_t)(npad * kpad / 32));
+}
+
+// A fresh, well-mixed nonzero mark tag per dense call (the dense path's marks are never cleared)
+static uint32_t next_dense_gen() {
+    static std::atomic<uint32_t> ctr{0};
+    uint32_t g;
+    do {
+        g = (ctr.fetch_add(1) + 1) * 0x9E3779B1u;
+        g ^= g >> 15;
+    } while (g == 0u);
+    return g;
 }
 
 static int run_dense(DenseArgs a, void *ws, size_t wsb, hipStream_t s) {
     if (a.M < 0 || a.N < 0 || a.K < 0) return fail(FP8A_EINVAL, "negative extent");
     if (a.fmt != FP8A_DENSE_E4M3 && a.fmt != FP8A_DENSE_E5M2 && a.fmt != FP8A_DENSE_BF16)
         return fail(FP8A_EINVAL, "unknown dense operand format");
+    const bool qout = a.fz.qin.mx || a.fz.rq.mx || a.fz.oq.mx || a.fz.wq.mx;
+    if (qout && (a.M == 0 || a.K == 0)) {  // no pack pass to leave the quantizers' biases
+        dn_bias_kernel<<<(unsigned)std::max<int64_t>(1, (a.N + 255) / 256), 256, 0, s>>>(a.fz, a.N);
+        const int rc = hip_check("fp8a dense quantizer biases");
+        if (rc) return rc;
+    }
     if (a.M == 0 || a.N == 0) return FP8A_OK;
     ++g_paths[PATH_DENSE];
     if (a.K == 0) {
@@ -1075,16 +1097,18 @@ static int run_dense(DenseArgs a, void *ws, size_t wsb, hipStream_t s) {
     if (a.kpad / 32 > 65535) return fail(FP8A_EINVAL, "K too large for the dense path (> 2097120)");
     if (ws == nullptr || wsb < dense_ws_bytes(a.M, a.N, a.K)) return fail(FP8A_EINVAL, "workspace too small");
     uint8_t *w = static_cast<uint8_t *>(ws);
-    const size_t nmark = (size_t)(a.mpad / DN_U + a.npad / DN_U) + 4;
+    // the unit marks hold this call's tag, so no call clears them: a stale word matches the tag
+    // only by chance (2^-32 per word), and then its unit is merely recomputed in fp32 by dn_fix
+    const size_t nmark = 4 * (size_t)(a.mpad / DN_U + a.npad / DN_U) + 4;
     a.anymark = reinterpret_cast<uint32_t *>(w);
-    a.urow = w + 4;
-    a.ucol = w + 4 + a.mpad / DN_U;
+    a.urow = a.anymark + 1;
+    a.ucol = a.urow + a.mpad / DN_U;
+    a.gen = next_dense_gen();
     w += al256(nmark);
     a.qa = w;  w += al256((size_t)(2 * a.mpad * a.kpad));
     a.qas = w; w += al256((size_t)(a.mpad * a.kpad / 32));
     a.qb = w;  w += al256((size_t)(2 * a.npad * a.kpad));
     a.qbs = w;
-    if (hipMemsetAsync(a.anymark, 0, nmark, s) != hipSuccess) return hip_check("fp8a dense marks");
     const dim3 ga((unsigned)((a.mpad + 255) / 256), (unsigned)(a.kpad / 32));
     const dim3 gb((unsigned)((a.npad + 255) / 256), (unsigned)(a.kpad / 32));
     const unsigned tiles = (unsigned)((a.mpad / DN_T) * (a.npad / DN_T));
@@ -1134,7 +1158,7 @@ static void launch_group_conv(const GcArgs &a, hipStream_t s) {
 // dn_dw3_kernel's block shape: about `target` outputs per workgroup (whole planes when a plane has
 // fewer, else bands of rows of one plane), the staged window within dw_lds bytes of LDS (default
 // 40 KB, four workgroups per CU: measured against 2 / 8 / 16 KB-windowed plans, §3l); false when even 256 outputs' window does not fit (very wide rows).
-static bool plan_dw3(DwArgs &a, int S, size_t &lds) {
+static bool plan_dw3(DwArgs &a, int S, size_t &lds, bool raw = false) {
     const int64_t op = (int64_t)a.Ho * a.Wo;
     for (int target = std::max(256, g_opt_dw_target); target >= 256; target /= 2) {
         int PB, RB;
@@ -1148,7 +1172,10 @@ static bool plan_dw3(DwArgs &a, int S, size_t &lds) {
         }
         const int RS = (RB - 1) * S + 3,
                   WS = (std::max(a.W + DW_OX, DW_OX - a.pw + (a.Wo - 1) * S + 3) + 3) / 4 * 4;
-        const int64_t bytes = ((int64_t)PB * RS * WS + (int64_t)PB * 9) * 4;
+        // raw (dn_dw3g_kernel): the unpadded source range from its 16-byte-aligned start
+        const int64_t nsrc = RB == a.Ho ? (int64_t)PB * a.H * a.W : (int64_t)std::min(RS, a.H) * a.W;
+        a.nimg = (int)(4 * ((nsrc + 6) / 4));
+        const int64_t bytes = ((raw ? (int64_t)a.nimg : (int64_t)PB * RS * WS) + (int64_t)PB * 9) * 4;
         if (bytes > std::min(65536, std::max(4096, g_opt_dw_lds))) continue;
         a.PB = PB; a.RB = RB; a.nb = (a.Ho + RB - 1) / RB; a.RS = RS; a.WS = WS;
         a.inv_c = 1.0f / a.C; a.inv_ws = 1.0f / WS; a.inv_pst = 1.0f / (RS * WS);
@@ -1352,7 +1379,13 @@ static int grouped_conv_impl(const float *x, const float *w, float *y, int64_t B
     a.cig = (int)(Cin / groups); a.cog = (int)(Cout / groups);
     a.kh = kh; a.kw = kw; a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw; a.dh = dh; a.dw = dw;
     a.fz = fz;
-    if (a.total == 0) return FP8A_OK;
+    if (a.total == 0) {  // (no kernel to leave the fused quantizers' biases)
+        if (fz.qin.mx || fz.rq.mx || fz.oq.mx || fz.wq.mx) {
+            dn_bias_kernel<<<(unsigned)std::max<int64_t>(1, (Cout + 255) / 256), 256, 0, stream>>>(fz, Cout);
+            return hip_check("fp8a grouped conv quantizer biases");
+        }
+        return FP8A_OK;
+    }
     if (!x || !w || !y) return fail(FP8A_EINVAL, "null pointer");
     if (g_opt_dw3 && a.cig == 1 && a.cog == 1 && kh == 3 && kw == 3 && dh == 1 && dw == 1 && sh == sw && pw <= DW_OX &&
         (sh == 1 || sh == 2)) {
@@ -1363,9 +1396,13 @@ static int grouped_conv_impl(const float *x, const float *w, float *y, int64_t B
         size_t lds = 0;
         // (the staged kernels index a plane in 32-bit ints and divide by float reciprocals, dw_div:
         // planes of at most 2^22 values; larger ones take dn_group_conv)
-        if (H < (1 << 20) && W < (1 << 20) && Cout < (1 << 20) && H * W < (1ll << 22) && plan_dw3(d, sh, lds)) {
+        d.nx = Bn * Cin * H * W;
+        const bool raw = g_opt_dw3 == 2;
+        if (H < (1 << 20) && W < (1 << 20) && Cout < (1 << 20) && H * W < (1ll << 22) && plan_dw3(d, sh, lds, raw)) {
             const unsigned g = (unsigned)(((d.planes + d.PB - 1) / d.PB) * d.nb);
-            if (sh == 1) dn_dw3_kernel<1><<<g, 256, lds, stream>>>(d);
+            if (raw && sh == 1) dn_dw3g_kernel<1><<<g, 256, lds, stream>>>(d);
+            else if (raw) dn_dw3g_kernel<2><<<g, 256, lds, stream>>>(d);
+            else if (sh == 1) dn_dw3_kernel<1><<<g, 256, lds, stream>>>(d);
             else dn_dw3_kernel<2><<<g, 256, lds, stream>>>(d);
             ++g_paths[PATH_DENSE];
             return hip_check("fp8a depthwise conv launch");
@@ -1512,6 +1549,14 @@ int fp8a_conv2d(const float *x, const float *w, float *y, int64_t Bn, int64_t Ci
 // pre-decodes (its bias written to fqb / fqi, which serve as bA), or -- for every other path --
 // into xq (numel(x) floats) by one fake-quant pass first.
 
+// A quantizer's bias (quantize_to_fp8_ste_MM's custom_bias) from its maxval, where no kernel of
+// the launch family writes it.
+__global__ void fq_bias_kernel(FqIn fq, float *bias_out, int32_t *ibias_out) {
+    const float b = fq_bias(*fq.mx, fq.E, fq.M);
+    *bias_out = b;
+    *ibias_out = (int32_t)b;
+}
+
 static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
                        int64_t Cout, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw, int groups,
                        int E, int Mw, const int32_t *bA, const int32_t *bW, const int32_t *bR, const int32_t *table,
@@ -1640,10 +1685,14 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
         int mode;
         rc = pack_table(table, Mw, (flags & (F_APPROX | F_V5)) != 0, tp, mode);
         if (rc) return rc;
+        if (flags & F_V5) mode = TM_V5;  // (as run_gemm)
         const WordImage wi = word_image(H, W, ph, pw);
         const int64_t a_words = Bn * cig * wi.H * wi.W;  // as xm_a_words / run_gemm
         const int64_t kpad = (Kg + BK - 1) / BK * BK, npad = (cog + BN - 1) / BN * BN;
-        const bool fused = f8_form(E, Mw, flags & ~F_TB, mode) && !no_mx() && a_words < (1ll << 30) &&
+        // (run_gemm's matrix-core forms: every one applies fq in its A pre-decode, xm_decode_a)
+        const uint32_t gf = flags & ~F_TB;
+        const bool form = f8_form(E, Mw, gf, mode) || tt_form(Mw, gf, tp) || v5mx_form(Mw, gf, mode);
+        const bool fused = form && !no_mx() && a_words < (1ll << 30) &&
                            kpad * npad * 4 < (1ll << 32) &&
                            workspace_bytes >= gemm_workspace_bytes(Mrows, cog, Kg, a_words);
         if (!fused) {
@@ -1654,10 +1703,6 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
     // v5 depthwise: one direct launch (a GEMM per single-column group would be `groups` launches of
     // N = 1 tiles: MobileNetV2 E5M2 v5 ran at ~500 images/s that way)
     if ((flags & F_V5) && cog == 1 && !post && groups > 1) {
-        if (fq.mx) {
-            rc = materialize();
-            if (rc) return rc;
-        }
         TablePack tp;
         int mode;
         rc = pack_table(table, Mw, true, tp, mode);
@@ -1677,7 +1722,10 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
             uint32_t *aw = (uint32_t *)((char *)workspace + FLAG_BYTES);
             uint2 *bwd = (uint2 *)((char *)workspace + FLAG_BYTES + awb);
             if (hipMemsetAsync(gate, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a gate reset");
-            v5dw_decode_a<<<(unsigned)std::min<int64_t>((nx + 255) / 256, 8192), 256, 0, s>>>(x, nx, aw, E, Mw, bA);
+            // (the input quantizer applied here, its bias written for the kernels after: bA = fqi)
+            v5dw_decode_a<<<(unsigned)std::min<int64_t>((nx + 255) / 256, 8192), 256, 0, s>>>(x, nx, aw, E, Mw, bA, fq,
+                                                                                               fqb, fqi);
+            if (fq.mx) bA = fqi;
             const int64_t nb = Cout * kh * kw;
             v5dw_decode_b<<<(unsigned)std::min<int64_t>((nb + 255) / 256, 1024), 256, 0, s>>>(w, nb, kh * kw, bwd, E, Mw,
                                                                                                bA, bW, bR, tp);
@@ -1696,10 +1744,15 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
             ++g_paths[PATH_FAST];
         } else {
             ++g_paths[PATH_EXACT];
+            if (fq.mx) {
+                fq_bias_kernel<<<1, 1, 0, s>>>(fq, fqb, fqi);
+                bA = fqi;
+            }
         }
+        // (x unquantized when fq is set: the literal kernel applies fq to every loaded value)
         conv_tb_direct_kernel<false><<<(unsigned)std::min<int64_t>((total + 255) / 256, 16384), 256, 0, s>>>(
             x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups, Ho, Wo, E, Mw, bA, bW, bR, tp, flags,
-            gate, ep, act, act_lo, act_hi, FqIn{});
+            gate, ep, act, act_lo, act_hi, fq);
         return hip_check("fp8a_conv2d (v5 depthwise, direct)");
     }
     for (int g = 0; g < groups; ++g) {
@@ -1769,12 +1822,6 @@ int fp8a_conv2d_qin(const float *x, const float *w, float *y, int64_t Bn, int64_
                        FqIn{in_maxval, qE, in_mbits, in_sign_bits}, in_bias_out, in_ibias_out, xq);
 }
 
-// The output quantizer's bias (quantize_to_fp8_ste_MM's custom_bias) from its maxval.
-__global__ void fq_bias_kernel(FqIn fq, float *bias_out, int32_t *ibias_out) {
-    const float b = fq_bias(*fq.mx, fq.E, fq.M);
-    *bias_out = b;
-    *ibias_out = (int32_t)b;
-}
 
 size_t fp8a_conv2d_block_workspace_size(int64_t Bn, int64_t Cin, int64_t H, int64_t W, int64_t Cout, int kh,
                                         int kw, int sh, int sw, int ph, int pw, int dh, int dw, int groups) {
@@ -2139,31 +2186,38 @@ int fp8a_fp8_quantize(const float *x, int64_t rows, int64_t inner, const float *
 // rq -> eval batch norm -> clamp -> fq_out in the store (gemm_dense.h DnFuse).  Each quantizer
 // writes its bias (the reference quantizer's custom_bias) like fp8a_conv2d_qin.
 static int fused_quantizer(const float *mx, int nbits, int mbits, int sign_bits, float *bias_out, int32_t *ibias_out,
-                           FqIn &f, hipStream_t s) {
+                           FqIn &f) {
     f = FqIn{};
     if (!mx) return FP8A_OK;
     const int qE = nbits - sign_bits - mbits;
     if (mbits < 1 || qE < 1) return fail(FP8A_EFORMAT, "bad FP8 quantizer format");
     if (!bias_out || !ibias_out) return fail(FP8A_EINVAL, "null pointer");
     f = FqIn{mx, qE, mbits, sign_bits};
-    fq_bias_kernel<<<1, 1, 0, s>>>(f, bias_out, ibias_out);
-    return hip_check("fp8a fused quantizer bias");
+    return FP8A_OK;
 }
 
 int fp8a_dense_conv2d_fused(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
                             int64_t Cout, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw, int groups,
-                            int fmt, const float *in_maxval, int in_nbits, int in_mbits, int in_sign_bits,
-                            float *in_bias_out, int32_t *in_ibias_out, const float *res_maxval, int res_nbits,
-                            int res_mbits, int res_sign_bits, float *res_bias_out, int32_t *res_ibias_out,
-                            const float *bn, int act, float act_lo, float act_hi, const float *out_maxval,
-                            int out_nbits, int out_mbits, int out_sign_bits, float *out_bias_out,
-                            int32_t *out_ibias_out, void *workspace, size_t workspace_bytes, fp8a_stream_t stream) {
+                            int fmt, const float *w_maxval, int w_per_channel, int w_nbits, int w_mbits,
+                            int w_sign_bits, float *w_bias_out, int32_t *w_ibias_out, const float *in_maxval,
+                            int in_nbits, int in_mbits, int in_sign_bits, float *in_bias_out, int32_t *in_ibias_out,
+                            const float *res_maxval, int res_nbits, int res_mbits, int res_sign_bits,
+                            float *res_bias_out, int32_t *res_ibias_out, const float *bn, int act, float act_lo,
+                            float act_hi, const float *out_maxval, int out_nbits, int out_mbits, int out_sign_bits,
+                            float *out_bias_out, int32_t *out_ibias_out, void *workspace, size_t workspace_bytes,
+                            fp8a_stream_t stream) {
     hipStream_t s = (hipStream_t)stream;
     DnFuse fz{};
-    int rc = fused_quantizer(in_maxval, in_nbits, in_mbits, in_sign_bits, in_bias_out, in_ibias_out, fz.qin, s);
-    if (!rc) rc = fused_quantizer(res_maxval, res_nbits, res_mbits, res_sign_bits, res_bias_out, res_ibias_out, fz.rq, s);
-    if (!rc) rc = fused_quantizer(out_maxval, out_nbits, out_mbits, out_sign_bits, out_bias_out, out_ibias_out, fz.oq, s);
+    int rc = fused_quantizer(w_maxval, w_nbits, w_mbits, w_sign_bits, w_bias_out, w_ibias_out, fz.wq);
+    if (!rc) rc = fused_quantizer(in_maxval, in_nbits, in_mbits, in_sign_bits, in_bias_out, in_ibias_out, fz.qin);
+    if (!rc) rc = fused_quantizer(res_maxval, res_nbits, res_mbits, res_sign_bits, res_bias_out, res_ibias_out, fz.rq);
+    if (!rc) rc = fused_quantizer(out_maxval, out_nbits, out_mbits, out_sign_bits, out_bias_out, out_ibias_out, fz.oq);
     if (rc) return rc;
+    fz.wq_row = w_maxval && w_per_channel ? 1 : 0;
+    fz.bo[0] = in_bias_out; fz.ibo[0] = in_ibias_out;
+    fz.bo[1] = res_bias_out; fz.ibo[1] = res_ibias_out;
+    fz.bo[2] = out_bias_out; fz.ibo[2] = out_ibias_out;
+    fz.bo[3] = w_bias_out; fz.ibo[3] = w_ibias_out;
     fz.ep = reinterpret_cast<const float2 *>(bn);
     fz.act = act;
     fz.lo = act_lo;

@@ -41,9 +41,13 @@ constexpr int DN_U = 64;             // fallback unit edge
 // input).  Per-tensor FP8 quantizers (fp8_quantizer.py:97-173: fq_apply); any member off.
 struct DnFuse {
     FqIn qin, rq, oq;
+    FqIn wq;           // the weight quantizer, on every B (weight) value as it is loaded
+    int wq_row;        // 1: wq.mx holds one maxval per output channel (per-channel weights)
     const float2 *ep;
     int act;
     float lo, hi;
+    float *bo[4];      // the bias outputs (custom_bias) of qin, rq, oq, wq; int32 copies in ibo
+    int32_t *ibo[4];
 };
 struct DnQv {  // the quantizers' maxval and bias, read once per thread
     float qmx, qb, rmx, rb, omx, ob;
@@ -54,6 +58,37 @@ __device__ __forceinline__ DnQv dn_qv(const DnFuse &f) {
     if (f.rq.mx) { q.rmx = *f.rq.mx; q.rb = fq_bias(q.rmx, f.rq.E, f.rq.M); }
     if (f.oq.mx) { q.omx = *f.oq.mx; q.ob = fq_bias(q.omx, f.oq.E, f.oq.M); }
     return q;
+}
+// The weight quantizer of output channel n: maxval and bias
+__device__ __forceinline__ float dn_wmx(const DnFuse &f, int64_t n) { return f.wq_row ? f.wq.mx[n] : *f.wq.mx; }
+__device__ __forceinline__ float dn_wq(const DnFuse &f, float mx, float b, float v) {
+    return f.wq.mx ? fq_apply(v, mx, b, f.wq.M, f.wq.S) : v;
+}
+__device__ __forceinline__ float dn_w(const DnFuse &f, int64_t n, float v) {
+    if (!f.wq.mx) return v;
+    const float mx = dn_wmx(f, n);
+    return fq_apply(v, mx, fq_bias(mx, f.wq.E, f.wq.M), f.wq.M, f.wq.S);
+}
+__device__ __forceinline__ void dn_put_bias(const FqIn &q, const float *mx, float *bo, int32_t *ibo, int64_t i) {
+    const float b = fq_bias(*mx, q.E, q.M);
+    bo[i] = b;
+    ibo[i] = (int32_t)b;
+}
+// The fused quantizers' bias outputs (what each reference quantizer's forward leaves in custom_bias),
+// written by the first kernel of the layer: the per-tensor ones by channel 0's thread, a per-channel
+// weight quantizer's by each channel's
+__device__ __forceinline__ void dn_bias_out(const DnFuse &f, int64_t n) {
+    if (n == 0) {
+        if (f.qin.mx) dn_put_bias(f.qin, f.qin.mx, f.bo[0], f.ibo[0], 0);
+        if (f.rq.mx) dn_put_bias(f.rq, f.rq.mx, f.bo[1], f.ibo[1], 0);
+        if (f.oq.mx) dn_put_bias(f.oq, f.oq.mx, f.bo[2], f.ibo[2], 0);
+    }
+    if (f.wq.mx && (f.wq_row || n == 0)) dn_put_bias(f.wq, f.wq.mx + (f.wq_row ? n : 0), f.bo[3], f.ibo[3], f.wq_row ? n : 0);
+}
+// ... with no product to run (empty reduction or output): one thread per channel
+__global__ __launch_bounds__(256) void dn_bias_kernel(const DnFuse f, int64_t N) {
+    const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (n < N || n == 0) dn_bias_out(f, n);
 }
 __device__ __forceinline__ float dn_in(const DnFuse &f, const DnQv &q, float v) {
     return f.qin.mx ? fq_apply(v, q.qmx, q.qb, f.qin.M, f.qin.S) : v;
@@ -79,8 +114,9 @@ struct DenseArgs {
     int64_t C, H, W, Ho, Wo;
     int kh, kw, sh, sw, ph, pw, dh, dw;
     uint8_t *qa, *qas, *qb, *qbs;  // byte images [mpad|npad][kpad] and E8M0 scales [..][kpad / 32]
-    uint8_t *urow, *ucol;          // unit marks [mpad / 64], [npad / 64]
-    uint32_t *anymark;             // 1 once any unit is marked
+    uint32_t *urow, *ucol;         // unit marks [mpad / 64], [npad / 64]: == gen when marked
+    uint32_t *anymark;             // gen once any unit is marked
+    uint32_t gen;                  // this call's mark tag (run_dense: no clearing pass between calls)
     int fmt;                       // FP8A_DENSE_E4M3 / FP8A_DENSE_E5M2 / FP8A_DENSE_BF16
     DnFuse fz;                     // the fused layer tail (all off: the plain product)
 };
@@ -143,9 +179,15 @@ __global__ __launch_bounds__(256) void dn_pack(const DenseArgs p) {
     for (int e = 0; e < 32; ++e) v[e] = 0.0f;
     if (r < rows) {
         if (ISB) {
+            float wmx = 0.0f, wb = 0.0f;
+            if (p.fz.wq.mx) {
+                wmx = dn_wmx(p.fz, r);
+                wb = fq_bias(wmx, p.fz.wq.E, p.fz.wq.M);
+            }
+            if (kb == 0) dn_bias_out(p.fz, r);
 #pragma unroll
             for (int e = 0; e < 32; ++e)
-                if (k0 + e < p.K) v[e] = p.w[(k0 + e) * p.sbk + r * p.sbn];
+                if (k0 + e < p.K) v[e] = dn_wq(p.fz, wmx, wb, p.w[(k0 + e) * p.sbk + r * p.sbn]);
         } else if (p.conv) {
             const int64_t hw = p.Ho * p.Wo, img = r / hw, pix = r - img * hw, ho = pix / p.Wo, wo = pix - ho * p.Wo;
             const int khw = p.kh * p.kw;
@@ -180,8 +222,8 @@ __global__ __launch_bounds__(256) void dn_pack(const DenseArgs p) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) q[t] = make_uint4(wd[4 * t], wd[4 * t + 1], wd[4 * t + 2], wd[4 * t + 3]);
         if (!ok) {
-            (ISB ? p.ucol : p.urow)[r / DN_U] = 1;
-            *p.anymark = 1u;
+            (ISB ? p.ucol : p.urow)[r / DN_U] = p.gen;
+            *p.anymark = p.gen;
         }
         return;
     }
@@ -216,8 +258,8 @@ __global__ __launch_bounds__(256) void dn_pack(const DenseArgs p) {
     *reinterpret_cast<uint4 *>(q + 16) = make_uint4(wd[4], wd[5], wd[6], wd[7]);
     (ISB ? p.qbs : p.qas)[r * (p.kpad / 32) + kb] = (uint8_t)(ok ? s + 127 : 127);
     if (!ok) {
-        (ISB ? p.ucol : p.urow)[r / DN_U] = 1;
-        *p.anymark = 1u;
+        (ISB ? p.ucol : p.urow)[r / DN_U] = p.gen;
+        *p.anymark = p.gen;
     }
 }
 
@@ -468,8 +510,8 @@ __global__ __launch_bounds__(256, 2) void dn_gemm_bf16(const DenseArgs p) {
         __syncthreads();
     }
     if (!aok) {
-        p.urow[am / DN_U] = 1;
-        *p.anymark = 1u;
+        p.urow[am / DN_U] = p.gen;
+        *p.anymark = p.gen;
     }
     // epilogue through LDS, half the tile at a time (64 channels x 128 pixels for convs, 64 rows x
     // 128 columns for matmuls), so every store instruction writes 64 consecutive floats of one
@@ -522,14 +564,14 @@ __global__ __launch_bounds__(256, 2) void dn_gemm_bf16(const DenseArgs p) {
 // The marked units in fp32 (fmaf, k order) from the original operands.
 // A persistent grid over the units: nothing to do (one word read) unless a unit is marked.
 __global__ __launch_bounds__(256) void dn_fix(const DenseArgs p) {
-    if (*p.anymark == 0u) return;
+    if (*p.anymark != p.gen) return;
     const int64_t num_um = p.mpad / DN_U, units = num_um * (p.npad / DN_U);
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_dense[0], 1ull);
     __shared__ float sa[16][DN_U + 1], sb[16][DN_U + 1];
     const int tid = threadIdx.x, ty = tid & 15, tx = tid >> 4;
     for (int64_t u = blockIdx.x; u < units; u += gridDim.x) {
     const int64_t um = u % num_um, un = u / num_um;
-    if (!(p.urow[um] | p.ucol[un])) continue;
+    if (p.urow[um] != p.gen && p.ucol[un] != p.gen) continue;
     if (tid == 0) atomicAdd(&g_dense[1], 1ull);
     const int64_t m0 = um * DN_U, n0 = un * DN_U;
     float acc[4][4] = {};
@@ -539,7 +581,7 @@ __global__ __launch_bounds__(256) void dn_fix(const DenseArgs p) {
             const int idx = tid + 256 * e, kk = idx >> 6, rr = idx & 63;
             const int64_t k = k0 + kk, m = m0 + rr, n = n0 + rr;
             sa[kk][rr] = (k < p.K && m < p.M) ? dn_a(p, m, k) : 0.0f;
-            sb[kk][rr] = (k < p.K && n < p.N) ? p.w[k * p.sbk + n * p.sbn] : 0.0f;
+            sb[kk][rr] = (k < p.K && n < p.N) ? dn_w(p.fz, n, p.w[k * p.sbk + n * p.sbn]) : 0.0f;
         }
         __syncthreads();
 #pragma unroll
@@ -659,6 +701,8 @@ struct DwArgs {
     int PB, RB, nb, RS, WS;        // planes per block, output rows per band, bands per plane, staged rows / columns
     float inv_c, inv_ws, inv_pst, inv_wo, inv_pout, inv_w, inv_hw;
     DnFuse fz;
+    int64_t nx;                    // floats in x (dn_dw3g_kernel: the last 16-byte chunk's bound)
+    int nimg;                      // dn_dw3g_kernel: LDS floats of the raw image (the weights follow)
 };
 
 template <int S>
@@ -676,8 +720,10 @@ __global__ __launch_bounds__(256) void dn_dw3_kernel(const DwArgs p) {
     for (int d = tid; d < npl * 9; d += 256) {
         int c = c0 + d / 9;
         c -= dw_div(c, p.C, p.inv_c) * p.C;
-        wsm[d] = p.w[(int64_t)c * 9 + d % 9];
+        wsm[d] = dn_w(p.fz, c, p.w[(int64_t)c * 9 + d % 9]);
     }
+    if (blockIdx.x == 0)
+        for (int c = tid; c < p.C; c += 256) dn_bias_out(p.fz, c);
     dw_stage(p.x, P0, npl, p.H, p.W, hi0, DW_OX, p.RS, p.WS, p.inv_w, p.inv_hw, p.RB == p.Ho, dw_sm,
              [&](float v) { return dn_in(p.fz, qv, v); });
     __syncthreads();
@@ -691,6 +737,85 @@ __global__ __launch_bounds__(256) void dn_dw3_kernel(const DwArgs p) {
         for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
             for (int kx = 0; kx < 3; ++kx) acc = __fmaf_rn(xs[ky * p.WS + kx], ws[3 * ky + kx], acc);
+        int c = c0 + pl;
+        c -= dw_div(c, p.C, p.inv_c) * p.C;
+        p.y[((P0 + pl) * p.Ho + oh0 + orow) * p.Wo + oc] = dn_out(p.fz, qv, c, acc);
+    }
+}
+
+// dn_dw3_kernel with the window staged by LDS-DMA (option "dw3" = 2): the workgroup's source
+// range of x -- whole planes, or a band of full rows of one plane, one contiguous range -- is copied
+// raw into LDS by global_load_lds_dwordx4 (16-byte chunks from the range's 16-byte-aligned start,
+// `lead` floats before it), every chunk of the window in flight at once and no VGPR holding any of
+// it; dn_dw3_kernel's register-staged form keeps four 16-byte loads per thread in flight and spent
+// 41 % of its wave cycles waiting (§3l).  The padding is not stored: an output's taps read 0 for
+// rows / columns outside the plane (the same fma(0, w, acc) as the zero-padded window, so the
+// same bits, non-finite weights included).  The input quantizer, when fused, runs once per value
+// over the landed image in place.  Chunks reaching past x's last float are copied per float.
+template <int S>
+__global__ __launch_bounds__(256) void dn_dw3g_kernel(const DwArgs p) {
+    extern __shared__ float dw_sm[];
+    const int tid = threadIdx.x, wv = tid >> 6;
+    const int band = (int)(blockIdx.x % (unsigned)p.nb);
+    const int64_t P0 = (int64_t)(blockIdx.x / (unsigned)p.nb) * p.PB;
+    const int npl = (int)min((int64_t)p.PB, p.planes - P0);
+    const int oh0 = band * p.RB, nrow = min(p.RB, p.Ho - oh0), hi0 = oh0 * S - p.ph;
+    const int hw = p.H * p.W, pout = p.RB * p.Wo;
+    const bool plane_mode = p.RB == p.Ho;
+    const int rlo = plane_mode ? 0 : max(hi0, 0), rhi = plane_mode ? p.H : min(hi0 + p.RS, p.H);
+    const int n = plane_mode ? npl * hw : (rhi - rlo) * p.W;
+    const int64_t g0 = P0 * hw + (int64_t)rlo * p.W, a0 = g0 & ~(int64_t)3;
+    const int lead = (int)(g0 - a0), nq = (lead + n + 3) >> 2;
+    float *img = dw_sm, *wsm = dw_sm + p.nimg;
+    const float *src = p.x + a0;
+    for (int q0 = 0; q0 < nq; q0 += 256) {
+        const int q = q0 + tid;
+        if (q < nq) {
+            if (a0 + 4 * (int64_t)q + 4 <= p.nx) {
+                __builtin_amdgcn_global_load_lds(src + 4 * q, img + 4 * (q0 + 64 * wv), 16, 0, 0);
+            } else {  // (the tensor's last floats: never read past x)
+                for (int e = 0; e < 4; ++e)
+                    if (a0 + 4 * (int64_t)q + e < p.nx) img[4 * q + e] = src[4 * q + e];
+            }
+        }
+    }
+    const int c0 = (int)(P0 % p.C);
+    const DnQv qv = dn_qv(p.fz);
+    for (int d = tid; d < npl * 9; d += 256) {
+        int c = c0 + d / 9;
+        c -= dw_div(c, p.C, p.inv_c) * p.C;
+        wsm[d] = dn_w(p.fz, c, p.w[(int64_t)c * 9 + d % 9]);
+    }
+    if (blockIdx.x == 0)
+        for (int c = tid; c < p.C; c += 256) dn_bias_out(p.fz, c);
+    __syncthreads();  // (waits for the LDS-DMA: vmcnt(0) before the barrier)
+    if (p.fz.qin.mx) {
+        for (int i = 4 * tid; i < 4 * nq; i += 1024) {
+            float4 v = *reinterpret_cast<const float4 *>(img + i);
+            v.x = dn_in(p.fz, qv, v.x);
+            v.y = dn_in(p.fz, qv, v.y);
+            v.z = dn_in(p.fz, qv, v.z);
+            v.w = dn_in(p.fz, qv, v.w);
+            *reinterpret_cast<float4 *>(img + i) = v;
+        }
+        __syncthreads();
+    }
+    for (int e = tid; e < npl * pout; e += 256) {
+        const int pl = dw_div(e, pout, p.inv_pout), rem = e - pl * pout;
+        const int orow = dw_div(rem, p.Wo, p.inv_wo), oc = rem - orow * p.Wo;
+        if (orow >= nrow) continue;
+        const int r0 = (oh0 + orow) * S - p.ph, cl = oc * S - p.pw;
+        const float *xs = img + lead + pl * hw + (r0 - rlo) * p.W + cl, *ws = wsm + pl * 9;
+        float acc = 0.0f;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+            const bool rok = (unsigned)(r0 + ky) < (unsigned)p.H;
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+                const bool ok = rok && (unsigned)(cl + kx) < (unsigned)p.W;
+                acc = __fmaf_rn(ok ? xs[ky * p.W + kx] : 0.0f, ws[3 * ky + kx], acc);
+            }
+        }
         int c = c0 + pl;
         c -= dw_div(c, p.C, p.inv_c) * p.C;
         p.y[((P0 + pl) * p.Ho + oh0 + orow) * p.Wo + oc] = dn_out(p.fz, qv, c, acc);
@@ -721,6 +846,8 @@ __global__ __launch_bounds__(256) void dn_group_conv(const GcArgs p) {
     const I wq = (I)((p.Wo + GC_OW - 1) / GC_OW), Ho = (I)p.Ho, Cout = (I)p.Cout;
     const int kh = p.kh, kw = KW > 0 ? KW : p.kw, sw = KW > 0 ? SW : p.sw;
     const DnQv qv = dn_qv(p.fz);
+    if (blockIdx.x == 0)
+        for (int64_t c = threadIdx.x; c < p.Cout; c += 256) dn_bias_out(p.fz, c);
     for (I t = (I)blockIdx.x * 256 + (I)threadIdx.x; t < (I)p.total; t += (I)gridDim.x * 256) {
         const I q = t % wq, r = t / wq, ho = r % Ho, plane = r / Ho;  // plane = image Cout + co
         const I co = plane % Cout, n = plane / Cout, c0 = (co / (I)p.cog) * (I)p.cig;
@@ -729,6 +856,11 @@ __global__ __launch_bounds__(256) void dn_group_conv(const GcArgs p) {
 #pragma unroll
         for (int j = 0; j < GC_OW; ++j) acc[j] = 0.0f;
         const float *wp = p.w + (int64_t)co * p.cig * kh * kw;
+        float wmx = 0.0f, wb = 0.0f;
+        if (p.fz.wq.mx) {
+            wmx = dn_wmx(p.fz, co);
+            wb = fq_bias(wmx, p.fz.wq.E, p.fz.wq.M);
+        }
         for (int ci = 0; ci < p.cig; ++ci) {
             const float *xp = p.x + ((int64_t)n * p.Cin + c0 + ci) * p.H * p.W;
             for (int ky = 0; ky < kh; ++ky) {
@@ -745,13 +877,13 @@ __global__ __launch_bounds__(256) void dn_group_conv(const GcArgs p) {
                     }
 #pragma unroll
                     for (int kx = 0; kx < KW; ++kx) {
-                        const float wv = wr[kx];
+                        const float wv = dn_wq(p.fz, wmx, wb, wr[kx]);
 #pragma unroll
                         for (int j = 0; j < GC_OW; ++j) acc[j] = __fmaf_rn(seg[j * SW + kx], wv, acc[j]);
                     }
                 } else {
                     for (int kx = 0; kx < kw; ++kx) {
-                        const float wv = wr[kx];
+                        const float wv = dn_wq(p.fz, wmx, wb, wr[kx]);
 #pragma unroll
                         for (int j = 0; j < GC_OW; ++j) {
                             const int64_t wi = wi0 + (int64_t)j * sw + (int64_t)kx * p.dw;

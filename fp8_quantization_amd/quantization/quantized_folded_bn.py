@@ -101,14 +101,34 @@ class BNFusedHijacker(QuantizationHijacker):
         from ..approx_ops import dense_conv2d_fused
         qin, rq, oq, ep, fmt = plan
         qt = lambda q: None if q is None else (q.maxval, q.n_bits, q._mbits_int, q.sign_bits)  # noqa: E731
-        weight, _ = self.get_params()
+        wq = self._fused_weight_quantizer()
+        if wq is None:  # get_params' weight quantizer as its own pass
+            weight, _ = self.get_params()
+        else:  # ... or inside the product's weight loads (the same values, hijacker.py:113-120)
+            weight, _ = self.get_weight_bias()
         self._check_res_flag()
         y, b = dense_conv2d_fused(x.detach(), weight.detach(), self.groups, self.stride, self.padding, self.dilation,
-                                  fmt, qin=qt(qin), rq=qt(rq), bn=ep, oq=qt(oq))
-        for name, q in (("qin", qin), ("rq", rq), ("oq", oq)):
+                                  fmt, qin=qt(qin), rq=qt(rq), bn=ep, oq=qt(oq), wq=qt(wq))
+        for name, q in (("qin", qin), ("rq", rq), ("oq", oq), ("wq", wq)):
             if q is not None:
                 q.custom_bias = b[name]  # what the quantizer's own forward leaves (fp8_quantizer.py)
         return y
+
+    def _fused_weight_quantizer(self):
+        """The weight FPQuantizer when the fused product can apply it to the weights as it loads
+        them: weights quantized (_qw), fixed ranges (so its forward is the bare quantizer,
+        quantization_manager.py), one maxval per tensor or per output channel; else None."""
+        if not self._qw():
+            return None
+        from .fp8_quantizer import FPQuantizer
+        from .quantization_manager import Qstates
+        mgr = self.weight_quantizer
+        q = getattr(mgr, "quantizer", None)
+        if getattr(mgr, "state", None) != Qstates.fix_ranges or not isinstance(q, FPQuantizer):
+            return None
+        if q.maxval.numel() not in (1, self.out_channels) or q.maxval.device != self.weight.device:
+            return None
+        return q
 
     def _own_output_quantizer(self):
         """This layer's activation FPQuantizer when it quantizes its OUTPUT (quantize_input off,

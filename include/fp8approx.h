@@ -140,18 +140,23 @@ int fp8a_grouped_conv2d(const float *x, const float *w, float *y, int64_t Bn, in
  *   y = fq_out(clamp(bn(fq_res(conv(fq_in(x), w)))))
  * fq_in = the input's activation quantizer (quantize_input), fq_res = the res quantizer
  * (original_quantize_res), bn = eval batch norm as [Cout][2] {scale, shift} floats, clamp =
- * [act_lo, act_hi] when act, fq_out = the output's activation quantizer; every member optional
- * (maxval / bn NULL).  Per-tensor FP8 quantizers (quantize_to_fp8_ste_MM), each writing its bias
- * (custom_bias) to *_bias_out / *_ibias_out.  groups = 1: the dense product (fmt as
- * fp8a_dense_conv2d, its workspace); groups > 1: fp8a_grouped_conv2d's kernel (no workspace). */
+ * [act_lo, act_hi] when act, fq_out = the output's activation quantizer, and w read through the
+ * weight quantizer fq_w (get_params' quantize_weights, hijacker.py:113-120); every member optional
+ * (maxval / bn NULL).  FP8 quantizers (quantize_to_fp8_ste_MM): per tensor, fq_w also per output
+ * channel (w_per_channel: w_maxval [Cout], biases [Cout]); each writes its bias (custom_bias) to
+ * *_bias_out / *_ibias_out from inside the layer's first kernel.  groups = 1: the dense product
+ * (fmt as fp8a_dense_conv2d, its workspace); groups > 1: fp8a_grouped_conv2d's kernel (no
+ * workspace). */
 int fp8a_dense_conv2d_fused(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H, int64_t W,
                             int64_t Cout, int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw, int groups,
-                            int fmt, const float *in_maxval, int in_nbits, int in_mbits, int in_sign_bits,
-                            float *in_bias_out, int32_t *in_ibias_out, const float *res_maxval, int res_nbits,
-                            int res_mbits, int res_sign_bits, float *res_bias_out, int32_t *res_ibias_out,
-                            const float *bn, int act, float act_lo, float act_hi, const float *out_maxval,
-                            int out_nbits, int out_mbits, int out_sign_bits, float *out_bias_out,
-                            int32_t *out_ibias_out, void *workspace, size_t workspace_bytes, fp8a_stream_t stream);
+                            int fmt, const float *w_maxval, int w_per_channel, int w_nbits, int w_mbits,
+                            int w_sign_bits, float *w_bias_out, int32_t *w_ibias_out, const float *in_maxval,
+                            int in_nbits, int in_mbits, int in_sign_bits, float *in_bias_out, int32_t *in_ibias_out,
+                            const float *res_maxval, int res_nbits, int res_mbits, int res_sign_bits,
+                            float *res_bias_out, int32_t *res_ibias_out, const float *bn, int act, float act_lo,
+                            float act_hi, const float *out_maxval, int out_nbits, int out_mbits, int out_sign_bits,
+                            float *out_bias_out, int32_t *out_ibias_out, void *workspace, size_t workspace_bytes,
+                            fp8a_stream_t stream);
 /* Dense-path counters since load / the last reset (out[2]): [0] launches with units recomputed in
  * fp32, [1] 64 x 64 units recomputed.  Synchronises the device. */
 int fp8a_dense_stats(uint64_t *out, int reset);

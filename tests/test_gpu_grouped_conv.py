@@ -152,6 +152,56 @@ def test_config1_fused_layer(groups, cin, cout, k, s, order):
     assert torch.all(d <= 1e-6 * ref.abs() + 1e-12)
 
 
+@pytest.mark.parametrize("groups,cin,cout,k,s,bn_", [(1, 8, 24, 1, 1, 2), (1, 6, 10, 3, 2, 2), (16, 16, 16, 3, 1, 2),
+                                                  (24, 24, 24, 3, 2, 2), (4, 8, 12, 3, 1, 2), (1, 8, 24, 1, 1, 0),
+                                                  (16, 16, 16, 3, 1, 0)])
+@pytest.mark.parametrize("per_channel", [False, True])
+def test_config1_fused_weight_quantizer(groups, cin, cout, k, s, bn_, per_channel):
+    """The weight quantizer inside the fused layer (fp8a_dense_conv2d_fused's w_maxval: applied to
+    every weight as the product loads it) against the weights quantized first by fp8a_fp8_quantize:
+    the same bits out, and the same custom_bias ([1], or [Cout, 1, 1, 1] per channel) -- on the
+    dense product, the LDS depthwise kernel, the general grouped kernel, and an empty batch (no
+    product: the biases still written)."""
+    from fp8_quantization_amd.approx_ops import dense_conv2d_fused, fp8_fake_quantize
+    g = torch.Generator().manual_seed(groups + cin + cout + k + s + per_channel)
+    x = (torch.randn(bn_, cin, 11, 12, generator=g) * 2).relu().to(DEV)
+    w = (torch.randn(cout, cin // groups, k, k, generator=g) * 0.3).to(DEV)
+    mxw = (torch.rand(cout, generator=g) + 0.2 if per_channel else torch.tensor([0.7])).to(DEV)
+    wq, bw = fp8_fake_quantize(w, mxw, 8, 3, per_row=per_channel)
+    scale = (torch.rand(cout, generator=g) + 0.5).to(DEV)
+    shift = (torch.randn(cout, generator=g) * 0.1).to(DEV)
+    ep = torch.stack((scale, shift), 1).contiguous()
+    kw = dict(qin=(torch.tensor([6.0], device=DEV), 8, 3, 1), rq=(torch.tensor([40.0], device=DEV), 8, 3, 1),
+              bn=(ep, 1, 0.0, 6.0))
+    pad = k // 2
+    y_ref, b_ref = dense_conv2d_fused(x, wq, groups, (s, s), (pad, pad), **kw)
+    y, b = dense_conv2d_fused(x, w, groups, (s, s), (pad, pad), wq=(mxw, 8, 3, 1), **kw)
+    assert torch.equal(y, y_ref)
+    assert b["wq"].shape == bw.shape and torch.equal(b["wq"], bw)
+    assert torch.equal(b["wq"]._fp8a_i32.cpu(), bw._fp8a_i32.cpu())
+    assert torch.equal(b["qin"], b_ref["qin"]) and torch.equal(b["rq"], b_ref["rq"])
+
+
+def test_dense_marks_tagged_per_call():
+    """The dense path's fallback marks carry a per-call tag instead of being cleared: a call that
+    marks every unit (fp32 operands off the bf16 grid, all recomputed by dn_fix) followed, in the
+    same workspace, by calls that mark none and some -- each against the float64 product."""
+    from fp8_quantization_amd import _lib
+    from fp8_quantization_amd.approx_ops import dense_conv2d, dense_format
+    g = torch.Generator().manual_seed(5)
+    w = (torch.randn(70, 9, 3, 3, generator=g) * 0.3).bfloat16().float()
+    xs = [torch.randn(2, 9, 20, 20, generator=g), torch.randn(2, 9, 20, 20, generator=g).bfloat16().float()]
+    x3 = xs[1].clone()
+    x3[1, 4, 7, 7] = 1.0 + 2.0 ** -20  # one unit off the grid
+    xs.append(x3)
+    _lib.dense_stats(reset=True)
+    for x in xs:
+        y = dense_conv2d(x.to(DEV), w.to(DEV), dense_format(3), (1, 1), (1, 1))
+        ref = torch.nn.functional.conv2d(x.double(), w.double(), padding=1)
+        assert torch.allclose(y.cpu().double(), ref, atol=1e-4, rtol=1e-5)
+    assert _lib.dense_stats()["fp32_launches"] == 2  # the first and third calls recomputed units; the second none
+
+
 DW3_SHAPES = [  # (Bn, C, H, W, stride, padding): every MobileNetV2 depthwise geometry + ragged ones
     (2, 32, 112, 112, 1, 1), (2, 96, 112, 112, 2, 1), (2, 144, 56, 56, 1, 1), (2, 144, 56, 56, 2, 1),
     (3, 192, 28, 28, 1, 1), (3, 192, 28, 28, 2, 1), (4, 384, 14, 14, 1, 1), (4, 576, 14, 14, 2, 1),
@@ -162,9 +212,11 @@ DW3_SHAPES = [  # (Bn, C, H, W, stride, padding): every MobileNetV2 depthwise ge
 
 @pytest.mark.parametrize("shape", DW3_SHAPES, ids=lambda c: "x".join(map(str, c)))
 @pytest.mark.parametrize("fused", [False, True])
-def test_depthwise_lds_form_matches_general_kernel(shape, fused):
-    """The LDS-staged depthwise 3x3 (option "dw3" = 1, the default) against the general
-    dn_group_conv (dw3 = 0): the same fp32 FMAs in the same order, so the same bits -- bands of
+@pytest.mark.parametrize("form", [1, 2])
+def test_depthwise_lds_form_matches_general_kernel(shape, fused, form):
+    """The LDS-staged depthwise 3x3 (option "dw3" = 1: register-staged dn_dw3_kernel; 2: the
+    LDS-DMA-staged dn_dw3g_kernel) against the general dn_group_conv (dw3 = 0): the same fp32 FMAs
+    in the same order, so the same bits -- bands of
     rows and groups of whole planes, ragged rows, stride 2, padding 0 / 2, a single-pixel plane,
     non-finite weights, and the config-1 tail (qin on load, rq, scale / shift, clamp)."""
     from fp8_quantization_amd import _lib
@@ -185,8 +237,12 @@ def test_depthwise_lds_form_matches_general_kernel(shape, fused):
         return dense_conv2d_fused(x, wq, C, (s, s), (p, p), qin=(torch.tensor([6.0], device=DEV), 8, 3, 1),
                                   rq=(torch.tensor([40.0], device=DEV), 8, 3, 1), bn=(ep, 1, 0.0, 6.0))[0]
 
-    g.manual_seed(1)
-    y_new = run()
+    old = _lib.set_option("dw3", form)
+    try:
+        g.manual_seed(1)
+        y_new = run()
+    finally:
+        _lib.set_option("dw3", old)
     old = _lib.set_option("dw3", 0)
     try:
         g.manual_seed(1)

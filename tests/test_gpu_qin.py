@@ -5,10 +5,10 @@ model_wrap.fused_block_tail): logits with it on and off.
 
 In the fixed-range approx forward the layer's input fake-quant (quantize_to_fp8_ste_MM,
 fp8_quantizer.py:97-173) runs inside the approx op: inside the operand pre-decode of the E4M3
-matrix-core and tensor-bias table kernels, or as one fake-quant pass into the workspace for every
-other path.  Checked here, bit for bit, against the unfused sequence (fp8a_fp8_quantize, then the
-plain convolution): outputs, the quantizer's float / int32 bias, every path (E4M3 GEMM and
-depthwise, E3M4 GEMM and depthwise, with and without the BN epilogue); and at model level,
+matrix-core (E4M3 / E5M2, the E3M4 / E2M5 tile-table, the v5 word) and tensor-bias table kernels and
+of the v5 depthwise word form, or as one fake-quant pass into the workspace for every other path.  Checked here, bit for bit, against the unfused sequence (fp8a_fp8_quantize, then the
+plain convolution): outputs, the quantizer's float / int32 bias, every path (E4M3, E3M4, E2M5
+and v5 E5M2 GEMM and depthwise, with and without the BN epilogue); and at model level,
 logits with the fusion on and off.
 """
 import numpy as np
@@ -30,7 +30,8 @@ def _native():
     _lib.load()
 
 
-@pytest.mark.parametrize("fmt", [(4, 3, "E4M3", "nocomp"), (3, 4, "E3M4", "comp3")])
+@pytest.mark.parametrize("fmt", [(4, 3, "E4M3", "nocomp"), (3, 4, "E3M4", "comp3"), (2, 5, "E2M5", "comp5"),
+                                 (2, 5, "E2M5", "nocomp"), (5, 2, "E5M2", "v5"), (5, 2, "E5M2", "v5_of_uf")])
 @pytest.mark.parametrize("layer", ["gemm", "depthwise", "depthwise_s2", "conv1x1"])
 @pytest.mark.parametrize("bn", [False, True])
 def test_fused_equals_quantize_then_conv(fmt, layer, bn):
@@ -55,8 +56,13 @@ def test_fused_equals_quantize_then_conv(fmt, layer, bn):
     wmax = wf.abs().reshape(w_shape[0], -1).amax(1)
     wq, wb = fp8_fake_quantize(wf, wmax, 8, M, per_row=True)
     bR = torch.tensor([2 ** (E - 1) + 6], dtype=torch.int32, device=DEV)
-    tab = gio.load("g2_matmul.npz")[f"{fname}_table_{tname}"]
-    fl = orc.flags_of(approx=True, s2n=True, qbma=True)
+    if tname.startswith("v5"):  # the v5 adder model with the wrap (its matrix-core form) and its options
+        tab = np.zeros((4, 4), np.int32)
+        tab[1:, 1:] = rng.integers(-3, 4, (3, 3))
+        fl = orc.flags_v5(True, tname == "v5_of_uf", tname == "v5_of_uf")
+    else:
+        tab = gio.load("g2_matmul.npz")[f"{fname}_table_{tname}"]
+        fl = orc.flags_of(approx=True, s2n=True, qbma=True)
     ep = None
     if bn:
         cout = w_shape[0]
