@@ -452,7 +452,7 @@ __global__ __launch_bounds__(256) void fp8_quantize_kernel(const float *x, int64
         const int64_t r = per_row ? idx / inner : 0;
         const float mx = maxval[r];
         const float bias = fq_bias(mx, E, M);
-        out[idx] = fq_apply(x[idx], mx, bias, M, sign_bits);
+        out[idx] = fq_apply_fast(x[idx], mx, bias, M, sign_bits);
         if ((idx % inner) == 0) {
             if (bias_out) bias_out[r] = bias;
             if (ibias_out) ibias_out[r] = (int32_t)bias;
@@ -672,10 +672,10 @@ static int g_opt_tbx_rw = getenv("FP8A_TBX_RW") ? atoi(getenv("FP8A_TBX_RW")) : 
 // "tbs": the table-form depthwise 3x3 on the LDS-staged conv_tbs_kernel with the word pre-pass
 // fused (1, default) or on tbx_decode_a + conv_tbx_kernel (0; the same bits).  FP8A_TBS=<n>.
 static int g_opt_tbs = getenv("FP8A_TBS") ? atoi(getenv("FP8A_TBS")) : 1;
-// "dw3": the exact depthwise 3x3 on the LDS-staged dn_dw3_kernel (1, default), its LDS-DMA-staged
-// form dn_dw3g_kernel (2) or the general dn_group_conv (0); the same bits.  FP8A_DW3=<n> sets it
-// at load.
-static int g_opt_dw3 = getenv("FP8A_DW3") ? atoi(getenv("FP8A_DW3")) : 1;
+// "dw3": the exact depthwise 3x3 on the LDS-DMA-staged, 4-outputs-per-thread dn_dw3g_kernel (2,
+// default: config 1 26.1k -> 28.3k images/s), the register-staged dn_dw3_kernel (1) or the general
+// dn_group_conv (0); the same bits.  FP8A_DW3=<n> sets it at load.
+static int g_opt_dw3 = getenv("FP8A_DW3") ? atoi(getenv("FP8A_DW3")) : 2;
 // "dw_target": outputs per workgroup the LDS-staged depthwise kernels aim at (plan_dw3 / plan_tbs;
 // halved until the window fits dw_lds).  FP8A_DW_TARGET=<n>.
 static int g_opt_dw_target = getenv("FP8A_DW_TARGET") ? atoi(getenv("FP8A_DW_TARGET")) : 4096;
@@ -1181,6 +1181,7 @@ static bool plan_dw3(DwArgs &a, int S, size_t &lds, bool raw = false) {
         a.inv_c = 1.0f / a.C; a.inv_ws = 1.0f / WS; a.inv_pst = 1.0f / (RS * WS);
         a.inv_wo = 1.0f / a.Wo; a.inv_pout = 1.0f / (RB * a.Wo);
         a.inv_w = 1.0f / a.W; a.inv_hw = 1.0f / (a.H * a.W);
+        a.inv_nqd = 1.0f / ((a.Wo + 3) / 4); a.inv_pq = 1.0f / (RB * ((a.Wo + 3) / 4));
         lds = (size_t)bytes;
         return ((a.planes + PB - 1) / PB) * a.nb < (1ll << 24);
     }

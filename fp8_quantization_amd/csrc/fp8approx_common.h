@@ -48,8 +48,14 @@ __device__ __forceinline__ float fq_bias(float mx, int E, int M) {
     return rintf((float)(1 << E) - log2f(mx) + log2f(2.0f - p2(-M)) - 1.0f);
 }
 
-__device__ __forceinline__ float fq_apply(float v, float mx, float bias, int M, int sign_bits) {
-    const float xc = fminf(fmaxf(v, sign_bits ? -mx : 0.0f), mx);
+// quantize_to_fp8_ste_MM's forward (fp8_quantizer.py:97-173) on one value, bias = fq_bias(mx):
+//   xc = clamp(v), ls = max(floor(log2 |xc|) + bias, 1) (1 for xc = 0), k = ls - M - bias,
+//   q = rint(xc / 2^k) 2^k.
+// A normal-float xc at or above the quantizer's smallest normal binade 2^(1 - bias) has k =
+// floor(log2 |xc|) - M: q is xc rounded to M fraction bits (RNE), done on the float's bits (a carry
+// moves it to the next binade, as the rounding does).  Below it (or zero) the quantum is the fixed
+// 2^(1 - M - bias).  A non-finite or huge bias (degenerate maxval) takes the literal formula.
+__device__ __forceinline__ float fq_apply_lit(float xc, float bias, int M) {
     int e;
     frexpf(xc, &e);
     const float ls = (xc == 0.0f) ? 1.0f : fmaxf((float)(e - 1) + bias, 1.0f);
@@ -58,6 +64,28 @@ __device__ __forceinline__ float fq_apply(float v, float mx, float bias, int M, 
     // sc is a power of two: x / sc == x * 2^-k exactly (same exact quotient, one rounding) while
     // 2^-k is finite -- a multiply instead of the IEEE division sequence
     return (k >= -126) ? rintf(xc * p2(-k)) * sc : rintf(xc / sc) * sc;
+}
+// The literal formula with the clamp: the form inside the GEMM kernels (loads, epilogues, word
+// emission), where fq_apply_fast's extra live constants cost a wave per SIMD
+__device__ __forceinline__ float fq_apply(float v, float mx, float bias, int M, int sign_bits) {
+    return fq_apply_lit(fminf(fmaxf(v, sign_bits ? -mx : 0.0f), mx), bias, M);
+}
+// The same bits with fewer VALU operations: the streaming passes (the fake-quant kernel, operand
+// pre-decodes, depthwise window stages), which are VALU-bound
+__device__ __forceinline__ float fq_apply_fast(float v, float mx, float bias, int M, int sign_bits) {
+    const float xc = fminf(fmaxf(v, sign_bits ? -mx : 0.0f), mx);
+    if (!(fabsf(bias) < 1048576.0f)) return fq_apply_lit(xc, bias, M);
+    const int ib = (int)bias, sh = 23 - M;
+    uint32_t u = __float_as_uint(xc);
+    u = (u + ((1u << (sh - 1)) - 1u) + ((u >> sh) & 1u)) & ~((1u << sh) - 1u);
+    const float t1 = ldexpf(1.0f, 1 - ib), ax = fabsf(xc);
+    // (a float subnormal at or above 2^(1 - bias), bias > 127: per-binade steps below the float's
+    // normal range -- the literal formula)
+    if (ax < 1.17549435e-38f && ax >= t1) return fq_apply_lit(xc, bias, M);
+    const int k = 1 - M - ib;
+    const float sc = p2(k);
+    const float lo = (k >= -126) ? rintf(xc * p2(-k)) * sc : rintf(xc / sc) * sc;
+    return ax >= t1 ? __uint_as_float(u) : lo;
 }
 
 // Word-image hand-off (round 4, fp8a_conv2d_chain): a convolution's store also writes the NEXT

@@ -93,6 +93,10 @@ __global__ __launch_bounds__(256) void dn_bias_kernel(const DnFuse f, int64_t N)
 __device__ __forceinline__ float dn_in(const DnFuse &f, const DnQv &q, float v) {
     return f.qin.mx ? fq_apply(v, q.qmx, q.qb, f.qin.M, f.qin.S) : v;
 }
+// ... with fq_apply_fast (the depthwise window stages: VALU-bound)
+__device__ __forceinline__ float dn_in_fast(const DnFuse &f, const DnQv &q, float v) {
+    return f.qin.mx ? fq_apply_fast(v, q.qmx, q.qb, f.qin.M, f.qin.S) : v;
+}
 __device__ __forceinline__ float dn_out(const DnFuse &f, const DnQv &q, int64_t c, float v) {
     if (f.rq.mx) v = fq_apply(v, q.rmx, q.rb, f.rq.M, f.rq.S);
     if (f.ep) {
@@ -703,6 +707,7 @@ struct DwArgs {
     DnFuse fz;
     int64_t nx;                    // floats in x (dn_dw3g_kernel: the last 16-byte chunk's bound)
     int nimg;                      // dn_dw3g_kernel: LDS floats of the raw image (the weights follow)
+    float inv_pq, inv_nqd;         // dn_dw3g_kernel: 1 / (quads per plane band), 1 / (quads per row)
 };
 
 template <int S>
@@ -725,7 +730,7 @@ __global__ __launch_bounds__(256) void dn_dw3_kernel(const DwArgs p) {
     if (blockIdx.x == 0)
         for (int c = tid; c < p.C; c += 256) dn_bias_out(p.fz, c);
     dw_stage(p.x, P0, npl, p.H, p.W, hi0, DW_OX, p.RS, p.WS, p.inv_w, p.inv_hw, p.RB == p.Ho, dw_sm,
-             [&](float v) { return dn_in(p.fz, qv, v); });
+             [&](float v) { return dn_in_fast(p.fz, qv, v); });
     __syncthreads();
     for (int e = tid; e < npl * pout; e += 256) {
         const int pl = dw_div(e, pout, p.inv_pout), rem = e - pl * pout;
@@ -750,7 +755,7 @@ __global__ __launch_bounds__(256) void dn_dw3_kernel(const DwArgs p) {
 // it; dn_dw3_kernel's register-staged form keeps four 16-byte loads per thread in flight and spent
 // 41 % of its wave cycles waiting (§3l).  The padding is not stored: an output's taps read 0 for
 // rows / columns outside the plane (the same fma(0, w, acc) as the zero-padded window, so the
-// same bits, non-finite weights included).  The input quantizer, when fused, runs once per value
+// same bits, non-finite weights included).  A thread computes 4 consecutive outputs of a row.  The input quantizer, when fused, runs once per value
 // over the landed image in place.  Chunks reaching past x's last float are copied per float.
 template <int S>
 __global__ __launch_bounds__(256) void dn_dw3g_kernel(const DwArgs p) {
@@ -760,7 +765,7 @@ __global__ __launch_bounds__(256) void dn_dw3g_kernel(const DwArgs p) {
     const int64_t P0 = (int64_t)(blockIdx.x / (unsigned)p.nb) * p.PB;
     const int npl = (int)min((int64_t)p.PB, p.planes - P0);
     const int oh0 = band * p.RB, nrow = min(p.RB, p.Ho - oh0), hi0 = oh0 * S - p.ph;
-    const int hw = p.H * p.W, pout = p.RB * p.Wo;
+    const int hw = p.H * p.W;
     const bool plane_mode = p.RB == p.Ho;
     const int rlo = plane_mode ? 0 : max(hi0, 0), rhi = plane_mode ? p.H : min(hi0 + p.RS, p.H);
     const int n = plane_mode ? npl * hw : (rhi - rlo) * p.W;
@@ -792,33 +797,55 @@ __global__ __launch_bounds__(256) void dn_dw3g_kernel(const DwArgs p) {
     if (p.fz.qin.mx) {
         for (int i = 4 * tid; i < 4 * nq; i += 1024) {
             float4 v = *reinterpret_cast<const float4 *>(img + i);
-            v.x = dn_in(p.fz, qv, v.x);
-            v.y = dn_in(p.fz, qv, v.y);
-            v.z = dn_in(p.fz, qv, v.z);
-            v.w = dn_in(p.fz, qv, v.w);
+            v.x = dn_in_fast(p.fz, qv, v.x);
+            v.y = dn_in_fast(p.fz, qv, v.y);
+            v.z = dn_in_fast(p.fz, qv, v.z);
+            v.w = dn_in_fast(p.fz, qv, v.w);
             *reinterpret_cast<float4 *>(img + i) = v;
         }
         __syncthreads();
     }
-    for (int e = tid; e < npl * pout; e += 256) {
-        const int pl = dw_div(e, pout, p.inv_pout), rem = e - pl * pout;
-        const int orow = dw_div(rem, p.Wo, p.inv_wo), oc = rem - orow * p.Wo;
+    // thread = 4 consecutive outputs of one row (a quad): the 3 x (3 S + 3) input window they share
+    // read once, the plane's 9 weights once, the index arithmetic once per quad
+    constexpr int NC = 3 * S + 3;
+    const int nqd = (p.Wo + 3) >> 2, pq = p.RB * nqd;
+    for (int e = tid; e < npl * pq; e += 256) {
+        const int pl = dw_div(e, pq, p.inv_pq), rem = e - pl * pq;
+        const int orow = dw_div(rem, nqd, p.inv_nqd), qd = rem - orow * nqd;
         if (orow >= nrow) continue;
-        const int r0 = (oh0 + orow) * S - p.ph, cl = oc * S - p.pw;
+        const int r0 = (oh0 + orow) * S - p.ph, cl = 4 * S * qd - p.pw;
         const float *xs = img + lead + pl * hw + (r0 - rlo) * p.W + cl, *ws = wsm + pl * 9;
-        float acc = 0.0f;
+        float wv[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) wv[t] = ws[t];
+        bool cok[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) cok[c] = (unsigned)(cl + c) < (unsigned)p.W;
+        float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky) {
             const bool rok = (unsigned)(r0 + ky) < (unsigned)p.H;
+            float v[NC];
 #pragma unroll
-            for (int kx = 0; kx < 3; ++kx) {
-                const bool ok = rok && (unsigned)(cl + kx) < (unsigned)p.W;
-                acc = __fmaf_rn(ok ? xs[ky * p.W + kx] : 0.0f, ws[3 * ky + kx], acc);
-            }
+            for (int c = 0; c < NC; ++c) v[c] = (rok && cok[c]) ? xs[ky * p.W + c] : 0.0f;
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[j] = __fmaf_rn(v[j * S + kx], wv[3 * ky + kx], acc[j]);
         }
         int c = c0 + pl;
         c -= dw_div(c, p.C, p.inv_c) * p.C;
-        p.y[((P0 + pl) * p.Ho + oh0 + orow) * p.Wo + oc] = dn_out(p.fz, qv, c, acc);
+        float *yo = p.y + ((P0 + pl) * p.Ho + oh0 + orow) * p.Wo + 4 * qd;
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = dn_out(p.fz, qv, c, acc[j]);
+        if ((p.Wo & 3) == 0) {
+            *reinterpret_cast<float4 *>(yo) = make_float4(o[0], o[1], o[2], o[3]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (4 * qd + j < p.Wo) yo[j] = o[j];
+        }
     }
 }
 

@@ -89,9 +89,9 @@ int fp8a_kernel_time(double *out, int reset);
  * Runtime options (A/B measurements, tests, diagnostics):
  * "tbx_rw" (default 2; FP8A_TBX_RW) -- output rows per thread of the table-form depthwise kernel;
  * "tbs" (default 1; FP8A_TBS) -- the LDS-staged table-form depthwise kernel (0: the word-image
- * gather); "dw3" (default 1; FP8A_DW3) -- the LDS-staged exact depthwise 3x3 (0: the general
- * grouped kernel); "dw_target" / "dw_lds" -- outputs / LDS bytes per workgroup of those staged
- * kernels;
+ * gather); "dw3" (default 2; FP8A_DW3) -- the exact depthwise 3x3: 2 = window staged by LDS-DMA,
+ * 4 outputs per thread; 1 = register-staged window; 0 = the general grouped kernel (same bits);
+ * "dw_target" / "dw_lds" -- outputs / LDS bytes per workgroup of those staged kernels;
  * "xm_ncg" (default 0 = by N; FP8A_XM_NCG) -- gemm_f8mx_kernel's tile width forced to 16 x 1 / 2
  * / 4 columns; "af32_maxct" (default 3; FP8A_AF32_MAXCT) -- the most column tiles for which a 1x1
  * conv / matrix A is decoded inside gemm_f8mx_kernel instead of by its pre-pass (0 = never).

@@ -376,6 +376,32 @@ def test_fp8_fake_quantize_extreme_ranges(scale):
         np.testing.assert_array_equal(y.cpu().numpy().view(np.uint32), yr.view(np.uint32))
 
 
+@pytest.mark.parametrize("M", [2, 3, 4, 5])
+@pytest.mark.parametrize("mxv", [6.0, 0.37, 448.0, 3e-3])
+def test_fp8_fake_quantize_ties_and_binade_edges(M, mxv):
+    """Exact ties (the midpoint between two grid values) and values next to them, in every binade of
+    the quantizer from below its smallest normal one up to maxval, zero and float subnormals, both
+    signs: the kernel's bit-level rounding (fq_apply) against the oracle's literal formula."""
+    E = 7 - M
+    bias = float(np.rint(2 ** E - np.log2(mxv) + np.log2(2 - 2.0 ** -M) - 1))
+    vals = [0.0, -0.0, 1e-45, -1e-45, 1e-40, 1.17549435e-38, mxv, -mxv, mxv * 1.5, np.nextafter(np.float32(mxv), 0)]
+    for ls in range(1, int(2 ** E + 2)):
+        q = 2.0 ** (max(ls, 1) - M - bias)
+        for m in range(2 ** M, 2 ** (M + 1), max(1, 2 ** M // 8)):
+            for tie in (m + 0.5, m + 1.5):
+                v = np.float32(tie * q)
+                vals += [v, np.nextafter(v, np.float32(np.inf)), np.nextafter(v, np.float32(0)), -v]
+        for m in range(0, 2 ** M):  # the fixed-quantum band below the smallest normal binade
+            v = np.float32((m + 0.5) * 2.0 ** (1 - M - bias))
+            vals += [v, -v, np.nextafter(v, np.float32(np.inf))]
+    x = np.array(vals, dtype=np.float32).reshape(1, -1)
+    mx = np.array([mxv], np.float32)
+    y, b = fa().fp8_fake_quantize(t(x), t(mx), 8, M, per_row=False)
+    yr, br = orc.fp8_fake_quant(x, mx, E, M, per_row=False)
+    np.testing.assert_array_equal(b.cpu().numpy().reshape(-1), br)
+    np.testing.assert_array_equal(y.cpu().numpy().view(np.uint32), yr.view(np.uint32))
+
+
 # ------------------------------------------------------------------------------ qamaa
 @pytest.mark.parametrize("case", META["g6"], ids=lambda c: c["key"])
 def test_qamaa_matmul(case):
