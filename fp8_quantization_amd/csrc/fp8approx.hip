@@ -1115,7 +1115,11 @@ static int run_dense(DenseArgs a, void *ws, size_t wsb, hipStream_t s) {
     const unsigned units = (unsigned)((a.mpad / DN_U) * (a.npad / DN_U));
     if (a.fmt == FP8A_DENSE_BF16) {  // (A straight from its fp32 source)
         dn_pack<true, 2><<<gb, 256, 0, s>>>(a);
-        if (a.conv) dn_gemm_bf16<true><<<tiles, 256, 0, s>>>(a);
+        static const bool no_pw1 = getenv("FP8A_NO_PW1") != nullptr;  // (A/B runs)
+        const bool pw1 = !no_pw1 && a.conv && a.kh == 1 && a.kw == 1 && a.sh == 1 && a.sw == 1 && a.ph == 0 && a.pw == 0 &&
+                         4 * a.C * a.H * a.W * (a.M / (a.Ho * a.Wo)) < (1ll << 31);  // (x through a 32-bit buffer)
+        if (pw1) dn_gemm_bf16<true, true><<<tiles, 256, 0, s>>>(a);
+        else if (a.conv) dn_gemm_bf16<true><<<tiles, 256, 0, s>>>(a);
         else dn_gemm_bf16<false><<<tiles, 256, 0, s>>>(a);
     } else if (a.fmt == FP8A_DENSE_E4M3) {
         dn_pack<false, 0><<<ga, 256, 0, s>>>(a);

@@ -55,15 +55,20 @@ __device__ __forceinline__ float fq_bias(float mx, int E, int M) {
 // floor(log2 |xc|) - M: q is xc rounded to M fraction bits (RNE), done on the float's bits (a carry
 // moves it to the next binade, as the rounding does).  Below it (or zero) the quantum is the fixed
 // 2^(1 - M - bias).  A non-finite or huge bias (degenerate maxval) takes the literal formula.
+// rint(xc / 2^k) 2^k without the IEEE division: the quotient is exact (a power-of-two scaling) and
+// is formed as xc 2^-k, in two exact steps when 2^-k itself overflows (k < -126: then |xc| <= maxval
+// is tiny and xc 2^64 cannot overflow); 2^k = 0 (k < -149) leaves the division's (x / 0) * 0 = NaN,
+// formed as (x inf) * 0.
+__device__ __forceinline__ float fq_step(float xc, int k) {
+    const float t = (k >= -126) ? xc * p2(-k) : (xc * 18446744073709551616.0f) * p2(-k - 64);
+    const float r = rintf(t) * p2(k);
+    return k < -149 ? rintf(xc * __builtin_huge_valf()) * p2(k) : r;  // (x / 0 = x inf: the same NaN)
+}
 __device__ __forceinline__ float fq_apply_lit(float xc, float bias, int M) {
     int e;
     frexpf(xc, &e);
     const float ls = (xc == 0.0f) ? 1.0f : fmaxf((float)(e - 1) + bias, 1.0f);
-    const int k = (int)(ls - (float)M - bias);
-    const float sc = p2(k);
-    // sc is a power of two: x / sc == x * 2^-k exactly (same exact quotient, one rounding) while
-    // 2^-k is finite -- a multiply instead of the IEEE division sequence
-    return (k >= -126) ? rintf(xc * p2(-k)) * sc : rintf(xc / sc) * sc;
+    return fq_step(xc, (int)(ls - (float)M - bias));
 }
 // The literal formula with the clamp: the form inside the GEMM kernels (loads, epilogues, word
 // emission), where fq_apply_fast's extra live constants cost a wave per SIMD
@@ -82,9 +87,7 @@ __device__ __forceinline__ float fq_apply_fast(float v, float mx, float bias, in
     // (a float subnormal at or above 2^(1 - bias), bias > 127: per-binade steps below the float's
     // normal range -- the literal formula)
     if (ax < 1.17549435e-38f && ax >= t1) return fq_apply_lit(xc, bias, M);
-    const int k = 1 - M - ib;
-    const float sc = p2(k);
-    const float lo = (k >= -126) ? rintf(xc * p2(-k)) * sc : rintf(xc / sc) * sc;
+    const float lo = fq_step(xc, 1 - M - ib);
     return ax >= t1 ? __uint_as_float(u) : lo;
 }
 

@@ -405,8 +405,14 @@ __device__ __forceinline__ bool dn_bf16_exact(uint32_t u) {
     return (u & 0xFFFFu) == 0u && e != 0x7F800000u && (e != 0u || (u & 0x7FFFFFFFu) == 0u);
 }
 
-template <bool CONV>
-__global__ __launch_bounds__(256, 2) void dn_gemm_bf16(const DenseArgs p) {
+// PW1: a 1 x 1, stride-1, unpadded convolution (every MobileNetV2 / ResNet pointwise layer): A (m, k)
+// = x[img][k][pixel], one pointer per row and a per-k stride of Ho Wo floats, no window arithmetic
+#ifndef FP8A_DN_BF16_WAVES
+#define FP8A_DN_BF16_WAVES 3  // min waves per SIMD of the conv forms (2: 168-194 VGPRs; 3: config 1 30.1k -> 34.5k
+                              // images/s; the matmul form stays at 2: it spills at 3)
+#endif
+template <bool CONV, bool PW1 = false>
+__global__ __launch_bounds__(256, CONV ? FP8A_DN_BF16_WAVES : 2) void dn_gemm_bf16(const DenseArgs p) {
     __shared__ __attribute__((aligned(16))) DnSmem16 sm;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wr = __builtin_amdgcn_readfirstlane(wv >> 1), wc = __builtin_amdgcn_readfirstlane(wv & 1);
@@ -429,9 +435,24 @@ __global__ __launch_bounds__(256, 2) void dn_gemm_bf16(const DenseArgs p) {
     const DnQv qv = dn_qv(p.fz);
     float ra[32];
     bool aok = true;
+    // (PW1: hi0 / wi0 are the pixel's own row / column.  x through a buffer resource of exactly its
+    // bytes (< 2^31, run_dense): rows past M read 0; the k offset is wave-uniform (ah = tid / 128),
+    // so each load is one VGPR offset (the pixel) + one SGPR offset (the channel plane))
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(p.x), (short)0, PW1 ? (int)(4 * p.C * p.H * p.W * (p.M / max(p.Ho * p.Wo, (int64_t)1))) : 0,
+        0x00020000);
+    const uint32_t voff = PW1 ? (uint32_t)(4 * (img * p.C * p.H * p.W + hi0 * p.W + wi0)) : 0u;
+    const uint32_t pstride4 = (uint32_t)(4 * p.H * p.W);
     auto load_a = [&](int64_t k0) {
         const int64_t kb = k0 + 32 * ah;
-        if (CONV) {
+        if (CONV && PW1) {
+            const uint32_t kbu = (uint32_t)__builtin_amdgcn_readfirstlane((int)kb);
+#pragma unroll
+            for (int e = 0; e < 32; ++e)
+                ra[e] = kbu + e < (uint32_t)p.K
+                            ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, (int)voff, (int)((kbu + e) * pstride4), 0))
+                            : 0.0f;
+        } else if (CONV) {
             int64_t c = kb / khw;
             int t = (int)(kb - c * khw), i = t / p.kw, j = t - i * p.kw;
 #pragma unroll
