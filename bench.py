@@ -426,6 +426,15 @@ def run(args, dev, rank=0, world=1):
         }
         if args.no_approx and cuda:
             gbs = op_bytes / (op_ms / 1e3) / 1e9 if op_ms > 0 else None
+            # the dense GEMM kernel alone (fp8a_kernel_time's dense slot: HIP events around each
+            # dn_gemm* launch; its MAC slot carries the launches' algorithmic bytes)
+            dk = ktime.get("dense", {})
+            dk_s = dk.get("ms", 0.0) / 1e3
+            dk_gbs = dk["macs"] / dk_s / 1e9 if dk_s > 0 else None
+            dpmc_name, dpmc = pmc_summary("dn_gemm_bf16", args.arch, args.expo_width, args.mant_width, args.batch,
+                                          strict=True)
+            dtraffic = dpmc.get("bytes_per_launch")
+            dhbm = dtraffic * dk["dispatches"] / dk_s / 1e9 if (dtraffic and dk_s > 0) else None
             res["roofline"] = {
                 "bound": "hbm",
                 "kernel": "dn_gemm_bf16 (csrc/gemm_dense.h: the exact product on the bf16 matrix core, "
@@ -435,8 +444,16 @@ def run(args, dev, rank=0, world=1):
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": gbs / HBM_PEAK_GBS if gbs else None,
-                "traffic": pmc_traffic("dn_gemm_bf16", args.arch, args.expo_width, args.mant_width, args.batch,
-                                       strict=True),
+                "traffic": dtraffic,
+                "kernel_achieved": dk_gbs,
+                "kernel_frac": dk_gbs / HBM_PEAK_GBS if dk_gbs else None,
+                "kernel_avg_ms": dk_s * 1e3 / dk["launches"] if dk.get("launches") else None,
+                "kernel_algorithmic_bytes_per_launch": dk["macs"] / dk["launches"] if dk.get("launches") else None,
+                "hbm_gbs": dhbm,
+                "hbm_frac": dhbm / HBM_PEAK_GBS if dhbm else None,
+                "valu_busy": dpmc.get("valu_busy"),
+                "wave_cycles": dpmc.get("wave_cycles"),
+                "pmc_summary": f"profiles/{dpmc_name}" if dpmc_name else None,
                 "algorithmic": f"fp32 operands read once + fp32 output written once: {op_bytes / launches:.4g} B per "
                                f"launch avg over {launches} launches, {avg_s * 1e3:.3f} ms avg launch (HIP events); "
                                f"{2.0 * op_macs / (op_ms / 1e3) / 1e12 if op_ms > 0 else 0:.1f} TFLOP/s of exact "

@@ -38,7 +38,7 @@ struct TbxArgs {
 
 __device__ __forceinline__ uint32_t tbx_word(float v, const FqIn &fq, float fmx, float fbias, uint32_t lowm,
                                              uint32_t mmask, int M, bool &bad) {
-    if (fq.mx) v = fq_apply_fast(v, fmx, fbias, fq.M, fq.S);
+    if (fq.mx) v = fq_apply(v, fmx, fbias, fq.M, fq.S);
     const uint32_t u = __float_as_uint(v), ua = u & 0x7FFFFFFFu;
     bad |= (ua != 0u) && ((ua & lowm) != 0u || ua < 0x20800000u || ua > 0x58800000u);
     return ua == 0u ? 0u : ((u & 0xFF800000u) | (((ua >> (23 - M)) & mmask) << 6));
@@ -318,7 +318,7 @@ __global__ __launch_bounds__(256) void v5dw_decode_a(const float *x, int64_t n, 
     const DFmt f = dfmt(E, M, fq.mx ? (int)fbias : *bA, false);
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         float v = x[i];
-        if (fq.mx) v = fq_apply_fast(v, fmx, fbias, fq.M, fq.S);
+        if (fq.mx) v = fq_apply(v, fmx, fbias, fq.M, fq.S);
         int e, m;
         exact_dec(v, f, true, e, m);
         out[i] = (v < 0.0f ? 0x80000000u : 0u) | ((uint32_t)(m * 8) << 16) | (uint32_t)(e * (1 << M) + m);

@@ -452,7 +452,7 @@ __global__ __launch_bounds__(256) void fp8_quantize_kernel(const float *x, int64
         const int64_t r = per_row ? idx / inner : 0;
         const float mx = maxval[r];
         const float bias = fq_bias(mx, E, M);
-        out[idx] = fq_apply_fast(x[idx], mx, bias, M, sign_bits);
+        out[idx] = fq_apply(x[idx], mx, bias, M, sign_bits);
         if ((idx % inner) == 0) {
             if (bias_out) bias_out[r] = bias;
             if (ibias_out) ibias_out[r] = (int32_t)bias;
@@ -1113,25 +1113,49 @@ static int run_dense(DenseArgs a, void *ws, size_t wsb, hipStream_t s) {
     const dim3 gb((unsigned)((a.npad + 255) / 256), (unsigned)(a.kpad / 32));
     const unsigned tiles = (unsigned)((a.mpad / DN_T) * (a.npad / DN_T));
     const unsigned units = (unsigned)((a.mpad / DN_U) * (a.npad / DN_U));
+    // (kernel timing: the GEMM launch alone, its algorithmic bytes -- fp32 A read once, fp32 C
+    // written once, the packed B image read once -- in the MAC slot)
+    KernelEv kev{};
+    auto kev_begin = [&]() {
+        if (!g_ktime) return;
+        kev.a = pool_event();
+        kev.b = pool_event();
+        kev.path = PATH_DENSE;
+        kev.dispatches = 1;
+        kev.macs = 4.0 * ((double)a.M * a.K + (double)a.M * a.N) +
+                   (a.fmt == FP8A_DENSE_BF16 ? 2.0 : 1.0) * (double)a.npad * a.kpad;
+        if (kev.a && kev.b) (void)hipEventRecord(kev.a, s);
+    };
+    auto kev_end = [&]() {
+        if (g_ktime && kev.a && kev.b) {
+            (void)hipEventRecord(kev.b, s);
+            g_kev.push_back(kev);
+        }
+    };
     if (a.fmt == FP8A_DENSE_BF16) {  // (A straight from its fp32 source)
         dn_pack<true, 2><<<gb, 256, 0, s>>>(a);
-        static const bool no_pw1 = getenv("FP8A_NO_PW1") != nullptr;  // (A/B runs)
-        const bool pw1 = !no_pw1 && a.conv && a.kh == 1 && a.kw == 1 && a.sh == 1 && a.sw == 1 && a.ph == 0 && a.pw == 0 &&
-                         4 * a.C * a.H * a.W * (a.M / (a.Ho * a.Wo)) < (1ll << 31);  // (x through a 32-bit buffer)
-        if (pw1) dn_gemm_bf16<true, true><<<tiles, 256, 0, s>>>(a);
+        kev_begin();
+        static const bool no_af = getenv("FP8A_NO_PW1") != nullptr;  // (A/B runs: the 64-bit indexing)
+        const bool x32 = !no_af && a.conv && 4 * a.C * a.H * a.W * (a.M / (a.Ho * a.Wo)) < (1ll << 31);
+        const bool pw1 = x32 && a.kh == 1 && a.kw == 1 && a.sh == 1 && a.sw == 1 && a.ph == 0 && a.pw == 0;
+        if (pw1) dn_gemm_bf16<true, 1><<<tiles, 256, 0, s>>>(a);
+        else if (x32) dn_gemm_bf16<true, 2><<<tiles, 256, 0, s>>>(a);
         else if (a.conv) dn_gemm_bf16<true><<<tiles, 256, 0, s>>>(a);
         else dn_gemm_bf16<false><<<tiles, 256, 0, s>>>(a);
     } else if (a.fmt == FP8A_DENSE_E4M3) {
         dn_pack<false, 0><<<ga, 256, 0, s>>>(a);
         dn_pack<true, 0><<<gb, 256, 0, s>>>(a);
+        kev_begin();
         if (a.conv) dn_gemm<0, true><<<tiles, 256, 0, s>>>(a);
         else dn_gemm<0, false><<<tiles, 256, 0, s>>>(a);
     } else {
         dn_pack<false, 1><<<ga, 256, 0, s>>>(a);
         dn_pack<true, 1><<<gb, 256, 0, s>>>(a);
+        kev_begin();
         if (a.conv) dn_gemm<1, true><<<tiles, 256, 0, s>>>(a);
         else dn_gemm<1, false><<<tiles, 256, 0, s>>>(a);
     }
+    kev_end();
     dn_fix<<<std::min(units, 2048u), 256, 0, s>>>(a);
     return hip_check("fp8a dense launch");
 }

@@ -51,10 +51,9 @@ __device__ __forceinline__ float fq_bias(float mx, int E, int M) {
 // quantize_to_fp8_ste_MM's forward (fp8_quantizer.py:97-173) on one value, bias = fq_bias(mx):
 //   xc = clamp(v), ls = max(floor(log2 |xc|) + bias, 1) (1 for xc = 0), k = ls - M - bias,
 //   q = rint(xc / 2^k) 2^k.
-// A normal-float xc at or above the quantizer's smallest normal binade 2^(1 - bias) has k =
-// floor(log2 |xc|) - M: q is xc rounded to M fraction bits (RNE), done on the float's bits (a carry
-// moves it to the next binade, as the rounding does).  Below it (or zero) the quantum is the fixed
-// 2^(1 - M - bias).  A non-finite or huge bias (degenerate maxval) takes the literal formula.
+// (Round 5 measured a bit-level form -- RNE on the float's bits at or above the smallest normal
+// binade -- against this one: 7 % slower on the fake-quant kernel, no faster in the depthwise
+// stages or the dense GEMM, so the literal form stays.)
 // rint(xc / 2^k) 2^k without the IEEE division: the quotient is exact (a power-of-two scaling) and
 // is formed as xc 2^-k, in two exact steps when 2^-k itself overflows (k < -126: then |xc| <= maxval
 // is tiny and xc 2^64 cannot overflow); 2^k = 0 (k < -149) leaves the division's (x / 0) * 0 = NaN,
@@ -70,25 +69,8 @@ __device__ __forceinline__ float fq_apply_lit(float xc, float bias, int M) {
     const float ls = (xc == 0.0f) ? 1.0f : fmaxf((float)(e - 1) + bias, 1.0f);
     return fq_step(xc, (int)(ls - (float)M - bias));
 }
-// The literal formula with the clamp: the form inside the GEMM kernels (loads, epilogues, word
-// emission), where fq_apply_fast's extra live constants cost a wave per SIMD
 __device__ __forceinline__ float fq_apply(float v, float mx, float bias, int M, int sign_bits) {
     return fq_apply_lit(fminf(fmaxf(v, sign_bits ? -mx : 0.0f), mx), bias, M);
-}
-// The same bits with fewer VALU operations: the streaming passes (the fake-quant kernel, operand
-// pre-decodes, depthwise window stages), which are VALU-bound
-__device__ __forceinline__ float fq_apply_fast(float v, float mx, float bias, int M, int sign_bits) {
-    const float xc = fminf(fmaxf(v, sign_bits ? -mx : 0.0f), mx);
-    if (!(fabsf(bias) < 1048576.0f)) return fq_apply_lit(xc, bias, M);
-    const int ib = (int)bias, sh = 23 - M;
-    uint32_t u = __float_as_uint(xc);
-    u = (u + ((1u << (sh - 1)) - 1u) + ((u >> sh) & 1u)) & ~((1u << sh) - 1u);
-    const float t1 = ldexpf(1.0f, 1 - ib), ax = fabsf(xc);
-    // (a float subnormal at or above 2^(1 - bias), bias > 127: per-binade steps below the float's
-    // normal range -- the literal formula)
-    if (ax < 1.17549435e-38f && ax >= t1) return fq_apply_lit(xc, bias, M);
-    const float lo = fq_step(xc, 1 - M - ib);
-    return ax >= t1 ? __uint_as_float(u) : lo;
 }
 
 // Word-image hand-off (round 4, fp8a_conv2d_chain): a convolution's store also writes the NEXT

@@ -77,25 +77,22 @@ __device__ __forceinline__ void dn_put_bias(const FqIn &q, const float *mx, floa
 // The fused quantizers' bias outputs (what each reference quantizer's forward leaves in custom_bias),
 // written by the first kernel of the layer: the per-tensor ones by channel 0's thread, a per-channel
 // weight quantizer's by each channel's
-__device__ __forceinline__ void dn_bias_out(const DnFuse &f, int64_t n) {
+__device__ __forceinline__ void dn_bias_out(const DnFuse &f, int64_t n, bool row = true) {
     if (n == 0) {
         if (f.qin.mx) dn_put_bias(f.qin, f.qin.mx, f.bo[0], f.ibo[0], 0);
         if (f.rq.mx) dn_put_bias(f.rq, f.rq.mx, f.bo[1], f.ibo[1], 0);
         if (f.oq.mx) dn_put_bias(f.oq, f.oq.mx, f.bo[2], f.ibo[2], 0);
     }
-    if (f.wq.mx && (f.wq_row || n == 0)) dn_put_bias(f.wq, f.wq.mx + (f.wq_row ? n : 0), f.bo[3], f.ibo[3], f.wq_row ? n : 0);
+    if (f.wq.mx && (f.wq_row ? row : n == 0))
+        dn_put_bias(f.wq, f.wq.mx + (f.wq_row ? n : 0), f.bo[3], f.ibo[3], f.wq_row ? n : 0);
 }
 // ... with no product to run (empty reduction or output): one thread per channel
 __global__ __launch_bounds__(256) void dn_bias_kernel(const DnFuse f, int64_t N) {
     const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (n < N || n == 0) dn_bias_out(f, n);
+    if (n < N || n == 0) dn_bias_out(f, n, n < N);  // (no channel rows when N = 0)
 }
 __device__ __forceinline__ float dn_in(const DnFuse &f, const DnQv &q, float v) {
     return f.qin.mx ? fq_apply(v, q.qmx, q.qb, f.qin.M, f.qin.S) : v;
-}
-// ... with fq_apply_fast (the depthwise window stages: VALU-bound)
-__device__ __forceinline__ float dn_in_fast(const DnFuse &f, const DnQv &q, float v) {
-    return f.qin.mx ? fq_apply_fast(v, q.qmx, q.qb, f.qin.M, f.qin.S) : v;
 }
 __device__ __forceinline__ float dn_out(const DnFuse &f, const DnQv &q, int64_t c, float v) {
     if (f.rq.mx) v = fq_apply(v, q.rmx, q.rb, f.rq.M, f.rq.S);
@@ -405,13 +402,15 @@ __device__ __forceinline__ bool dn_bf16_exact(uint32_t u) {
     return (u & 0xFFFFu) == 0u && e != 0x7F800000u && (e != 0u || (u & 0x7FFFFFFFu) == 0u);
 }
 
-// PW1: a 1 x 1, stride-1, unpadded convolution (every MobileNetV2 / ResNet pointwise layer): A (m, k)
-// = x[img][k][pixel], one pointer per row and a per-k stride of Ho Wo floats, no window arithmetic
+// AF (conv A addressing, x below 2^31 bytes, run_dense): 1 = a 1 x 1, stride-1, unpadded
+// convolution (every MobileNetV2 / ResNet pointwise layer): A (m, k) = x[img][k][pixel], one pixel
+// offset per row and a per-k channel-plane offset; 2 = any window: the (channel, ky, kx) of each k
+// wave-uniform (scalar), per element two adds and the bounds test in 32 bits; 0 = 64-bit indexing
 #ifndef FP8A_DN_BF16_WAVES
 #define FP8A_DN_BF16_WAVES 3  // min waves per SIMD of the conv forms (2: 168-194 VGPRs; 3: config 1 30.1k -> 34.5k
                               // images/s; the matmul form stays at 2: it spills at 3)
 #endif
-template <bool CONV, bool PW1 = false>
+template <bool CONV, int AF = 0>
 __global__ __launch_bounds__(256, CONV ? FP8A_DN_BF16_WAVES : 2) void dn_gemm_bf16(const DenseArgs p) {
     __shared__ __attribute__((aligned(16))) DnSmem16 sm;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -435,23 +434,41 @@ __global__ __launch_bounds__(256, CONV ? FP8A_DN_BF16_WAVES : 2) void dn_gemm_bf
     const DnQv qv = dn_qv(p.fz);
     float ra[32];
     bool aok = true;
-    // (PW1: hi0 / wi0 are the pixel's own row / column.  x through a buffer resource of exactly its
+    // (AF 1: hi0 / wi0 are the pixel's own row / column.  x through a buffer resource of exactly its
     // bytes (< 2^31, run_dense): rows past M read 0; the k offset is wave-uniform (ah = tid / 128),
-    // so each load is one VGPR offset (the pixel) + one SGPR offset (the channel plane))
+    // so each load is one VGPR offset (the pixel / image) + one SGPR offset (the channel plane))
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float *>(p.x), (short)0, PW1 ? (int)(4 * p.C * p.H * p.W * (p.M / max(p.Ho * p.Wo, (int64_t)1))) : 0,
+        const_cast<float *>(p.x), (short)0, AF ? (int)(4 * p.C * p.H * p.W * (p.M / max(p.Ho * p.Wo, (int64_t)1))) : 0,
         0x00020000);
-    const uint32_t voff = PW1 ? (uint32_t)(4 * (img * p.C * p.H * p.W + hi0 * p.W + wi0)) : 0u;
+    const uint32_t voff = AF == 1 ? (uint32_t)(4 * (img * p.C * p.H * p.W + hi0 * p.W + wi0))
+                                  : (uint32_t)(4 * img * p.C * p.H * p.W);
     const uint32_t pstride4 = (uint32_t)(4 * p.H * p.W);
+    const int hi0i = (int)hi0, wi0i = (int)wi0, iH = (int)p.H, iW = (int)p.W;
     auto load_a = [&](int64_t k0) {
         const int64_t kb = k0 + 32 * ah;
-        if (CONV && PW1) {
+        if (CONV && AF == 1) {
             const uint32_t kbu = (uint32_t)__builtin_amdgcn_readfirstlane((int)kb);
 #pragma unroll
             for (int e = 0; e < 32; ++e)
                 ra[e] = kbu + e < (uint32_t)p.K
                             ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, (int)voff, (int)((kbu + e) * pstride4), 0))
                             : 0.0f;
+        } else if (CONV && AF == 2) {
+            const int kbu = __builtin_amdgcn_readfirstlane((int)kb);
+            int c = kbu / khw;
+            int t = kbu - c * khw, i = t / p.kw, j = t - i * p.kw;
+#pragma unroll
+            for (int e = 0; e < 32; ++e) {
+                const int hi = hi0i + i * p.dh, wi = wi0i + j * p.dw;
+                const bool ok = arow && kbu + e < (int)p.K && (unsigned)hi < (unsigned)iH && (unsigned)wi < (unsigned)iW;
+                ra[e] = ok ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, (int)(voff + 4u * (uint32_t)(hi * iW + wi)),
+                                                                                  (int)((uint32_t)c * pstride4), 0))
+                           : 0.0f;
+                if (++j == p.kw) {
+                    j = 0;
+                    if (++i == p.kh) { i = 0; ++c; }
+                }
+            }
         } else if (CONV) {
             int64_t c = kb / khw;
             int t = (int)(kb - c * khw), i = t / p.kw, j = t - i * p.kw;
@@ -751,7 +768,7 @@ __global__ __launch_bounds__(256) void dn_dw3_kernel(const DwArgs p) {
     if (blockIdx.x == 0)
         for (int c = tid; c < p.C; c += 256) dn_bias_out(p.fz, c);
     dw_stage(p.x, P0, npl, p.H, p.W, hi0, DW_OX, p.RS, p.WS, p.inv_w, p.inv_hw, p.RB == p.Ho, dw_sm,
-             [&](float v) { return dn_in_fast(p.fz, qv, v); });
+             [&](float v) { return dn_in(p.fz, qv, v); });
     __syncthreads();
     for (int e = tid; e < npl * pout; e += 256) {
         const int pl = dw_div(e, pout, p.inv_pout), rem = e - pl * pout;
@@ -818,10 +835,10 @@ __global__ __launch_bounds__(256) void dn_dw3g_kernel(const DwArgs p) {
     if (p.fz.qin.mx) {
         for (int i = 4 * tid; i < 4 * nq; i += 1024) {
             float4 v = *reinterpret_cast<const float4 *>(img + i);
-            v.x = dn_in_fast(p.fz, qv, v.x);
-            v.y = dn_in_fast(p.fz, qv, v.y);
-            v.z = dn_in_fast(p.fz, qv, v.z);
-            v.w = dn_in_fast(p.fz, qv, v.w);
+            v.x = dn_in(p.fz, qv, v.x);
+            v.y = dn_in(p.fz, qv, v.y);
+            v.z = dn_in(p.fz, qv, v.z);
+            v.w = dn_in(p.fz, qv, v.w);
             *reinterpret_cast<float4 *>(img + i) = v;
         }
         __syncthreads();

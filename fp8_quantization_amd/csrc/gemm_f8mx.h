@@ -281,7 +281,7 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
     uint32_t sehi = 0;  // 255 - the smallest se of this thread's nonzero E5M2 words (xm_record_se)
     const DFmt fv5 = dfmt(p.E, p.Mw, bA, false);  // (wfmt 4: the v5 decode, clip_OF)
     auto word = [&](float v, bool &ok) {
-        if (p.fqin.mx) v = fq_apply_fast(v, fmx, fbias, p.fqin.M, p.fqin.S);
+        if (p.fqin.mx) v = fq_apply(v, fmx, fbias, p.fqin.M, p.fqin.S);
         if (p.wfmt == 4) return v5_word_a(v, fv5);
         if (p.wfmt == 2) return tt16_word_a(v, emnA, bA, ok, win);
         if (p.wfmt) return tt_word_a(v, p.Mw, emnA, ok);

@@ -80,7 +80,9 @@ int fp8a_path_stats(uint64_t *out, int reset);
  * (not its operand pre-passes, split-K reduction or gated exact kernel).  fp8a_kernel_time
  * synchronises on the recorded events and writes, per launch path in fp8a_path_stats order,
  * out[4 * path + 0..3] = (summed kernel milliseconds, launches, kernel dispatches, approx-MACs
- * M * N * K); reset != 0 forgets the recorded launches.  Host-side, single-threaded use.
+ * M * N * K -- for the dense path, whose exact-product GEMM launches (dn_gemm*) are recorded too:
+ * their algorithmic bytes, fp32 A read + fp32 C written + the packed B image read); reset != 0
+ * forgets the recorded launches.  Host-side, single-threaded use.
  */
 int fp8a_kernel_timing(int enable);
 int fp8a_kernel_time(double *out, int reset);

@@ -17,6 +17,8 @@ declare -A SPEC=(
   [c5_r50_e3m4]="gemm_tt16_kernel resnet50 3 4 512"
   [c5_r50_e2m5]="gemm_tt_kernel resnet50 2 5 512"
   [mbv2_e4m3]="gemm_f8mx_kernel mobilenet_v2 4 3 512"
+  [mbv2_e4m3_dw]="conv_tbs_kernel mobilenet_v2 4 3 512"
+  [c1_mbv2_noapprox_dw]="dn_dw3g_kernel mobilenet_v2 4 3 512 --no-approx"
 )
 TAGS="$*"; [ -n "$TAGS" ] || TAGS="c2_r18_e4m3"
 for t in $TAGS; do
