@@ -400,4 +400,129 @@ __global__ __launch_bounds__(256) void conv_v5dw_kernel(const uint32_t *aw, cons
     if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(gate, 1u);
 }
 
+// conv_v5dw_kernel's terms with both pre-passes fused in (option "v5ds", the default): the
+// workgroup's contiguous source range of x is copied raw into LDS by LDS-DMA (dn_dw3g_kernel's
+// staging, padding not stored), each value is turned in place into its v5 word (the input
+// quantizer first when fused -- v5dw_decode_a), the PB planes' 9 tap words are built from the
+// weights (v5dw_decode_b), then thread = 4 consecutive outputs of a row, the window's words read
+// once, the terms in (ky, kx) order from zero: the same bits as conv_v5dw_kernel without the word
+// image's write and read (8 B per input value) and two launches.  Depthwise 3 x 3, stride S both
+// ways, dilation 1.  The gate rule is conv_v5dw_kernel's (the result bias's range).
+template <int S>
+__global__ __launch_bounds__(256) void conv_v5ds_kernel(const float *x, const float *w, float *y, const DwArgs p,
+                                                        FqIn fq, float *fqb, int32_t *fqi, const int32_t *bA,
+                                                        const int32_t *bW, const int32_t *bR, TablePack tab,
+                                                        uint32_t flags, int E, uint32_t *gate, const float2 *ep,
+                                                        int ep_act, float ep_lo, float ep_hi) {
+    constexpr int M = 2, NC = 3 * S + 3;
+    extern __shared__ float dw_sm[];
+    const int tid = threadIdx.x, wv = tid >> 6;
+    const int band = (int)(blockIdx.x % (unsigned)p.nb);
+    const int64_t P0 = (int64_t)(blockIdx.x / (unsigned)p.nb) * p.PB;
+    const int npl = (int)min((int64_t)p.PB, p.planes - P0);
+    const int oh0 = band * p.RB, nrow = min(p.RB, p.Ho - oh0), hi0 = oh0 * S - p.ph;
+    const int hw = p.H * p.W;
+    const bool plane_mode = p.RB == p.Ho;
+    const int rlo = plane_mode ? 0 : max(hi0, 0), rhi = plane_mode ? p.H : min(hi0 + p.RS, p.H);
+    const int n = plane_mode ? npl * hw : (rhi - rlo) * p.W;
+    const int64_t g0 = P0 * hw + (int64_t)rlo * p.W, a0 = g0 & ~(int64_t)3;
+    const int lead = (int)(g0 - a0), nq = (lead + n + 3) >> 2;
+    float *img = dw_sm;
+    uint2 *sB = reinterpret_cast<uint2 *>(dw_sm + p.nimg);  // [PB][9] tap words
+    const float *src = x + a0;
+    for (int q0 = 0; q0 < nq; q0 += 256) {
+        const int q = q0 + tid;
+        if (q < nq) {
+            if (a0 + 4 * (int64_t)q + 4 <= p.nx) {
+                __builtin_amdgcn_global_load_lds(src + 4 * q, img + 4 * (q0 + 64 * wv), 16, 0, 0);
+            } else {
+                for (int e = 0; e < 4; ++e)
+                    if (a0 + 4 * (int64_t)q + e < p.nx) img[4 * q + e] = src[4 * q + e];
+            }
+        }
+    }
+    const float fmx = fq.mx ? *fq.mx : 0.0f, fbias = fq.mx ? fq_bias(fmx, fq.E, fq.M) : 0.0f;
+    if (fq.mx && blockIdx.x == 0 && tid == 0) {
+        *fqb = fbias;
+        *fqi = (int32_t)fbias;
+    }
+    const int a_b = fq.mx ? (int)fbias : *bA, r_b = *bR;
+    const int c0 = (int)(P0 % p.C);
+    for (int d = tid; d < npl * 9; d += 256) {  // v5dw_decode_b for the block's planes
+        const int pl = d / 9;
+        int c = c0 + pl;
+        c -= dw_div(c, p.C, p.inv_c) * p.C;
+        const int b_b = bW[c];
+        const float v = w[(int64_t)c * 9 + d - 9 * pl];
+        int e, m;
+        exact_dec(v, dfmt(E, M, b_b, false), true, e, m);
+        const int32_t cb = (e - (a_b + b_b - r_b)) * (1 << M) + m;
+        uint32_t row = 0;
+        for (int ma = 0; ma < 4; ++ma) row |= ((uint32_t)(uint8_t)tab.raw[(ma << M) | m]) << (8 * ma);
+        sB[d] = make_uint2(((uint32_t)cb << 1) | (v < 0.0f ? 1u : 0u), row);
+    }
+    __syncthreads();  // (waits for the LDS-DMA)
+    {  // in place: value -> (input quantizer) -> v5 word (v5dw_decode_a)
+        const DFmt f = dfmt(E, M, a_b, false);
+        uint32_t *iw = reinterpret_cast<uint32_t *>(img);
+        for (int i = tid; i < 4 * nq; i += 256) {
+            float v = img[i];
+            if (fq.mx) v = fq_apply(v, fmx, fbias, fq.M, fq.S);
+            int e, m;
+            exact_dec(v, f, true, e, m);
+            iw[i] = (v < 0.0f ? 0x80000000u : 0u) | ((uint32_t)(m * 8) << 16) | (uint32_t)(e * (1 << M) + m);
+        }
+    }
+    __syncthreads();
+    const uint32_t *iw = reinterpret_cast<const uint32_t *>(img);
+    const int32_t maxi = ((1 << E) << M) - 1;
+    const bool bad = !(r_b >= -90 && r_b <= 120);
+    const uint32_t lin0 = (uint32_t)(127 - r_b) << 23;
+    const float csub = __uint_as_float((uint32_t)(126 - r_b) << 23);  // 2^(1 - bR - M), M = 2
+    const int nqd = (p.Wo + 3) >> 2, pq = p.RB * nqd;
+    for (int e = tid; e < npl * pq; e += 256) {
+        const int pl = dw_div(e, pq, p.inv_pq), rem = e - pl * pq;
+        const int orow = dw_div(rem, nqd, p.inv_nqd), qd = rem - orow * nqd;
+        if (orow >= nrow) continue;
+        const int r0 = (oh0 + orow) * S - p.ph, cl = 4 * S * qd - p.pw;
+        const uint32_t *xs = iw + lead + pl * hw + (r0 - rlo) * p.W + cl;
+        const uint2 *wb = sB + pl * 9;
+        bool cok[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) cok[c] = (unsigned)(cl + c) < (unsigned)p.W;
+        float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+            const bool rok = (unsigned)(r0 + ky) < (unsigned)p.H;
+            uint32_t col[NC];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) col[c] = (rok && cok[c]) ? xs[ky * p.W + c] : 0u;
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+                const uint2 b = wb[3 * ky + kx];
+                const int32_t cb = (int32_t)b.x >> 1;
+                const uint32_t sb = b.x << 31;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t wa = col[j * S + kx];
+                    const int32_t tv = __builtin_amdgcn_sbfe((int32_t)b.y, (wa >> 16) & 31u, 8);  // T[m_a][m_b]
+                    int32_t r = (int32_t)(wa & 0xFFu) + cb + tv;
+                    r = v5_ofuf(r, maxi, M, flags);
+                    const float vn = __uint_as_float(((uint32_t)r << (23 - M)) + lin0);
+                    const float vs = (float)r * csub;
+                    const float v = ((uint32_t)r < (1u << M)) ? vs : vn;
+                    acc[j] += __uint_as_float(__float_as_uint(v) ^ ((wa & 0x80000000u) ^ sb));
+                }
+            }
+        }
+        int co = c0 + pl;
+        co -= dw_div(co, p.C, p.inv_c) * p.C;
+        float *yo = y + ((P0 + pl) * p.Ho + oh0 + orow) * p.Wo + 4 * qd;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (4 * qd + j < p.Wo) yo[j] = epi(ep, ep_act, ep_lo, ep_hi, co, acc[j]);
+    }
+    if (__syncthreads_or(bad ? 1 : 0) && tid == 0) atomicOr(gate, 1u);
+}
+
 }  // namespace fp8a

@@ -676,6 +676,9 @@ static int g_opt_tbs = getenv("FP8A_TBS") ? atoi(getenv("FP8A_TBS")) : 1;
 // default: config 1 26.1k -> 28.3k images/s), the register-staged dn_dw3_kernel (1) or the general
 // dn_group_conv (0); the same bits.  FP8A_DW3=<n> sets it at load.
 static int g_opt_dw3 = getenv("FP8A_DW3") ? atoi(getenv("FP8A_DW3")) : 2;
+// "v5ds": the v5 depthwise 3 x 3 on the staged conv_v5ds_kernel (1, default) or on the word
+// pre-passes + conv_v5dw_kernel (0); the same bits.  FP8A_V5DS=<n> sets it at load.
+static int g_opt_v5ds = getenv("FP8A_V5DS") ? atoi(getenv("FP8A_V5DS")) : 1;
 // "dw_target": outputs per workgroup the LDS-staged depthwise kernels aim at (plan_dw3 / plan_tbs;
 // halved until the window fits dw_lds).  FP8A_DW_TARGET=<n>.
 static int g_opt_dw_target = getenv("FP8A_DW_TARGET") ? atoi(getenv("FP8A_DW_TARGET")) : 4096;
@@ -1320,6 +1323,11 @@ int fp8a_set_option(const char *name, int value) {
         g_opt_dw_target = std::max(256, value);
         return old;
     }
+    if (strcmp(name, "v5ds") == 0) {
+        const int old = g_opt_v5ds;
+        g_opt_v5ds = value;
+        return old;
+    }
     if (strcmp(name, "dw3") == 0) {
         const int old = g_opt_dw3;
         g_opt_dw3 = value;
@@ -1746,7 +1754,32 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
                              sh == sw && (sw == 1 || sw == 2) && items < (1ll << 31) && Ho * Wo < (1ll << 31) &&
                              workspace != nullptr && workspace_bytes >= FLAG_BYTES + awb + (size_t)(Cout * kh * kw) * 8;
         uint32_t *gate = nullptr;
-        if (v5dw_ok) {
+        // the staged form (conv_v5ds_kernel: both pre-passes fused): depthwise 3 x 3, dilation 1
+        DwArgs d{};
+        size_t lds = 0;
+        const bool v5ds = v5dw_ok && g_opt_v5ds && kh == 3 && kw == 3 && dh == 1 && H < (1 << 20) && W < (1 << 20) &&
+                          Cout < (1 << 20) && H * W < (1ll << 22) && [&]() {
+                              d.planes = Bn * Cout; d.C = (int)Cout; d.H = (int)H; d.W = (int)W;
+                              d.Ho = (int)Ho; d.Wo = (int)Wo; d.ph = ph; d.pw = pw; d.nx = nx;
+                              if (!plan_dw3(d, sh, lds, true)) return false;
+                              lds = (size_t)d.nimg * 4 + (size_t)d.PB * 9 * 8;  // (tap words: 8 B)
+                              return lds <= 65536;
+                          }();
+        if (v5ds) {
+            gate = (uint32_t *)workspace;
+            if (hipMemsetAsync(gate, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a gate reset");
+            const unsigned g = (unsigned)(((d.planes + d.PB - 1) / d.PB) * d.nb);
+            if (sh == 1)
+                conv_v5ds_kernel<1><<<g, 256, lds, s>>>(x, w, y, d, fq, fqb, fqi, bA, bW, bR, tp, flags, E, gate, ep,
+                                                        act, act_lo, act_hi);
+            else
+                conv_v5ds_kernel<2><<<g, 256, lds, s>>>(x, w, y, d, fq, fqb, fqi, bA, bW, bR, tp, flags, E, gate, ep,
+                                                        act, act_lo, act_hi);
+            rc = hip_check("fp8a_conv2d (v5 depthwise, staged)");
+            if (rc) return rc;
+            if (fq.mx) bA = fqi;
+            ++g_paths[PATH_FAST];
+        } else if (v5dw_ok) {
             gate = (uint32_t *)workspace;
             uint32_t *aw = (uint32_t *)((char *)workspace + FLAG_BYTES);
             uint2 *bwd = (uint2 *)((char *)workspace + FLAG_BYTES + awb);

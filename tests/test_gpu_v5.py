@@ -155,6 +155,52 @@ def test_v5_depthwise_e5m2_word_form(stride, sw):
         assert same_bits(y[:, c].reshape(-1), seq).all(), f"channel {c}: not the literal k-order sum"
 
 
+V5DS_SHAPES = [  # (Bn, C, H, W, stride): MobileNetV2 geometries (whole planes and row bands), ragged ones
+    (2, 32, 112, 112, 1), (2, 96, 112, 112, 2), (2, 144, 56, 56, 2), (3, 192, 28, 28, 1), (4, 576, 14, 14, 2),
+    (5, 960, 7, 7, 1), (1, 3, 5, 9, 1), (2, 5, 13, 7, 2), (1, 4, 9, 300, 1), (1, 2, 1, 1, 1)]
+
+
+@pytest.mark.parametrize("shape", V5DS_SHAPES, ids=lambda c: "x".join(map(str, c)))
+@pytest.mark.parametrize("qin", [False, True])
+def test_v5_depthwise_staged_form_bit_identical(shape, qin):
+    """The staged v5 depthwise kernel (conv_v5ds_kernel, option "v5ds" = 1: LDS-DMA window, both word
+    pre-passes fused, 4 outputs per thread) against the pre-pass + conv_v5dw_kernel form (v5ds = 0):
+    the same bits, with and without the fused input quantizer and its bias."""
+    from fp8_quantization_amd import _lib
+    from fp8_quantization_amd.approx_ops import approx_conv2d
+    Bn, C, H, W, s = shape
+    rng = np.random.default_rng(Bn * C + H * W + s + int(qin))
+    x = np.ldexp(1.0 + rng.integers(0, 4, size=(Bn, C, H, W)) / 4.0, rng.integers(-14, 6, size=(Bn, C, H, W)))
+    x[rng.random(x.shape) < 0.3] = 0.0
+    x = (x * rng.choice([-1.0, 1.0], size=x.shape)).astype(np.float32)
+    if qin:
+        x = x * np.float32(1.37)  # off the grid: the fused quantizer rounds it
+    w = np.ldexp(1.0 + rng.integers(0, 4, size=(C, 1, 3, 3)) / 4.0, rng.integers(-12, 4, size=(C, 1, 3, 3)))
+    w = (w * rng.choice([-1.0, 1.0], size=w.shape)).astype(np.float32)
+    bW = t(rng.integers(14, 20, size=C).astype(np.int32), torch.int32)
+    bR = torch.tensor([12], dtype=torch.int32, device=DEV)
+    tab = torch.as_tensor(np.array([[0, -1, 2, 0], [1, 0, -2, 1], [0, 3, 0, -1], [-3, 1, 1, 0]], np.int32))
+    fl = orc.flags_v5(True, True, True)
+    kw = dict(flags=fl, stride=(s, s), padding=(1, 1), groups=C)
+    bA = None if qin else torch.tensor([16], dtype=torch.int32, device=DEV)
+    q = (torch.tensor([20.0], device=DEV), 8, 2, 1) if qin else None
+
+    def run():
+        r = approx_conv2d(t(x), t(w), 5, 2, bA, bW, bR, tab, qin=q, **kw)
+        return (r[0], r[1]) if qin else (r, None)
+
+    old = _lib.set_option("v5ds", 1)
+    try:
+        y1, b1 = run()
+        _lib.set_option("v5ds", 0)
+        y0, b0 = run()
+    finally:
+        _lib.set_option("v5ds", old)
+    assert torch.equal(y1.view(torch.int32), y0.view(torch.int32))
+    if qin:
+        assert torch.equal(b1, b0)
+
+
 def _e5m2_codes(bias):
     e = np.repeat(np.arange(32), 4)
     m = np.tile(np.arange(4), 32)
