@@ -990,11 +990,13 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
         return fail(FP8A_EINVAL, "internal: fused input quantization without the matrix-core path");
     if (mode == TM_F8 && a.Mw != 3 && !a.aw) mode = mode0;  // (gemm_fast_kernel's TM_F8 form is E4M3 only)
     ++g_paths[!a.aw ? PATH_FAST : a.wfmt == 0 ? PATH_F8MX : a.wfmt == 1 ? PATH_TT : a.wfmt == 4 ? PATH_V5MX : PATH_TT16];
-    // word-image emission (fp8a_conv2d_chain): every store form emits the next convolution's words
-    // except the v5 matrix-core kernel's (gemm_v5mx_kernel: store_tile<false>); its unsplit launch
-    // marks the image invalid instead (emit_prep_kernel set the header valid before this launch), so
-    // the consumer's gated pre-pass re-decodes its input from y
-    if (a.em.w != nullptr && a.aw && a.wfmt == 4 && a.splits == 1) {
+    // word-image emission (fp8a_conv2d_chain): the E4M3 / E5M2 matrix-core kernel and the VALU
+    // kernel emit the next convolution's words from their store; the tile-table and v5 matrix-core
+    // kernels do not (store_tile<false>: the emission code cost gemm_tt16_kernel 32 SGPR spills and a
+    // 38 % slower E3M4 layer set, round 4 -> 5), so their unsplit launch marks the image invalid
+    // instead (emit_prep_kernel set the header valid before this launch) and the consumer's gated
+    // pre-pass re-decodes its input from y
+    if (a.em.w != nullptr && a.aw && a.wfmt != 0 && a.splits == 1) {
         if (hipMemsetAsync(a.em.invalid, 1, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a word image header");
         a.em.w = nullptr;
     }

@@ -296,7 +296,7 @@ __global__ __launch_bounds__(NT * tt_rh<MW>()) void gemm_tt_kernel(const GemmArg
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int j = 0; j < TN; ++j) o[i][j] = ct[(ety * TM + i) * XM_CP + etx * TN + j];
-            store_tile(p, split, m0 + 64 * hs, n0, ety, etx, o);
+            store_tile<false>(p, split, m0 + 64 * hs, n0, ety, etx, o);
         }
     }
 }

@@ -260,7 +260,7 @@ __global__ __launch_bounds__(NT, 6) void gemm_tt16_kernel(const GemmArgs p) {
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j) acc[i][j] = ct[(ety * TM + i) * XM_CP + etx * TN + j];
-        store_tile(p, split, m0 + 64 * hs, n0, ety, etx, acc);
+        store_tile<false>(p, split, m0 + 64 * hs, n0, ety, etx, acc);
     }
 }
 #endif  // FP8A_OWN_TT
