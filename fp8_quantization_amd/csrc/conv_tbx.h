@@ -283,6 +283,111 @@ __global__ __launch_bounds__(256) void conv_tbs_kernel(const float *x, const flo
     if (__syncthreads_or(bad ? 1 : 0) && tid == 0) atomicOr(gate, 1u);
 }
 
+// conv_tbs_kernel with dn_dw3g_kernel's staging (option "tbs" = 2, the default): the source range
+// copied raw into LDS by LDS-DMA (padding not stored: a tap outside the plane reads the zero word),
+// each value turned into its table-form word in place (input quantizer, tbx_word and its window /
+// grid checks), then 4 outputs per thread as conv_tbs_kernel: the same terms in the same order,
+// the same bits, the same gate.
+template <int S, int M>
+__global__ __launch_bounds__(256) void conv_tbsg_kernel(const float *x, const float *w, float *y, const DwArgs p,
+                                                        FqIn fq, float *fq_bias_out, int32_t *fq_ibias_out,
+                                                        const int32_t *bA, const int32_t *bW, const int32_t *bR,
+                                                        TablePack tab, uint32_t *gate, const float2 *ep, int ep_act,
+                                                        float ep_lo, float ep_hi) {
+    constexpr int NC = 3 * S + 3;
+    constexpr uint32_t LOWM = (1u << (23 - M)) - 1u, MMASK = (1u << M) - 1u;
+    extern __shared__ float dw_sm[];
+    const int tid = threadIdx.x, wv = tid >> 6;
+    const int band = (int)(blockIdx.x % (unsigned)p.nb);
+    const int64_t P0 = (int64_t)(blockIdx.x / (unsigned)p.nb) * p.PB;
+    const int npl = (int)min((int64_t)p.PB, p.planes - P0);
+    const int oh0 = band * p.RB, nrow = min(p.RB, p.Ho - oh0), hi0 = oh0 * S - p.ph;
+    const int hw = p.H * p.W;
+    const bool plane_mode = p.RB == p.Ho;
+    const int rlo = plane_mode ? 0 : max(hi0, 0), rhi = plane_mode ? p.H : min(hi0 + p.RS, p.H);
+    const int n = plane_mode ? npl * hw : (rhi - rlo) * p.W;
+    const int64_t g0 = P0 * hw + (int64_t)rlo * p.W, a0 = g0 & ~(int64_t)3;
+    const int lead = (int)(g0 - a0), nq = (lead + n + 3) >> 2;
+    float *img = dw_sm;
+    float2 *sL = reinterpret_cast<float2 *>(dw_sm + p.nimg);  // the table (64 entries)
+    uint2 *sB = reinterpret_cast<uint2 *>(sL + 64);           // [PB][9] {c_b bits, m_b << 3}
+    const float *src = x + a0;
+    for (int q0 = 0; q0 < nq; q0 += 256) {
+        const int q = q0 + tid;
+        if (q < nq) {
+            if (a0 + 4 * (int64_t)q + 4 <= p.nx) {
+                __builtin_amdgcn_global_load_lds(src + 4 * q, img + 4 * (q0 + 64 * wv), 16, 0, 0);
+            } else {
+                for (int e = 0; e < 4; ++e)
+                    if (a0 + 4 * (int64_t)q + e < p.nx) img[4 * q + e] = src[4 * q + e];
+            }
+        }
+    }
+    const float fmx = fq.mx ? *fq.mx : 0.0f, fbias = fq.mx ? fq_bias(fmx, fq.E, fq.M) : 0.0f;
+    if (fq.mx && blockIdx.x == 0 && tid == 0) {
+        *fq_bias_out = fbias;
+        *fq_ibias_out = (int32_t)fbias;
+    }
+    const int a_b = fq.mx ? (int32_t)fbias : *bA, r_b = *bR;
+    bool bad = !(a_b >= 2 && a_b <= 120 && r_b >= 2 && r_b <= 120);
+    if (tid < 64) sL[tid] = tbx_lut_entry<M>(tid, tab, r_b);
+    const int c0 = (int)(P0 % p.C);
+    for (int d = tid; d < npl * 9; d += 256) {
+        const int pl = d / 9;
+        int c = c0 + pl;
+        c -= dw_div(c, p.C, p.inv_c) * p.C;
+        const int wb = bW[c];
+        bad |= !(wb >= 2 && wb <= 120);
+        const uint32_t bw = __float_as_uint(w[(int64_t)c * 9 + d - 9 * pl]), bwa = bw & 0x7FFFFFFFu;
+        bad |= (bwa != 0u) && ((bwa & LOWM) != 0u || bwa < 0x20800000u || bwa > 0x58800000u);
+        sB[d] = make_uint2(bw & 0xFF800000u, ((bwa >> (23 - M)) & MMASK) << 3);
+    }
+    __syncthreads();  // (waits for the LDS-DMA)
+    uint32_t *iw = reinterpret_cast<uint32_t *>(img);
+    {  // in place: value -> its word (the source range only: the lead / tail words are never read)
+        const int i0 = lead, i1 = lead + n;
+        for (int i = i0 + tid; i < i1; i += 256) iw[i] = tbx_word(img[i], fq, fmx, fbias, LOWM, MMASK, M, bad);
+    }
+    __syncthreads();
+    const uint32_t q0exp = (uint32_t)(127 - r_b) << 23;
+    const float twoq = __uint_as_float((uint32_t)(128 - r_b) << 23);
+    const char *lut = reinterpret_cast<const char *>(sL);
+    const int nqd = (p.Wo + 3) >> 2, pq = p.RB * nqd;
+    for (int e = tid; e < npl * pq; e += 256) {
+        const int pl = dw_div(e, pq, p.inv_pq), rem = e - pl * pq;
+        const int orow = dw_div(rem, nqd, p.inv_nqd), qd = rem - orow * nqd;
+        if (orow >= nrow) continue;
+        const int r0 = (oh0 + orow) * S - p.ph, cl = 4 * S * qd - p.pw;
+        const uint32_t *xs = iw + lead + pl * hw + (r0 - rlo) * p.W + cl;
+        const uint2 *wb = sB + pl * 9;
+        bool cok[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) cok[c] = (unsigned)(cl + c) < (unsigned)p.W;
+        float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+            const bool rok = (unsigned)(r0 + ky) < (unsigned)p.H;
+            uint32_t col[NC];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) col[c] = (rok && cok[c]) ? xs[ky * p.W + c] : 0u;
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+                const uint2 b = wb[3 * ky + kx];
+                const float cB = __uint_as_float(b.x);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[j] += tbx_term(col[j * S + kx], cB, b.y, lut, q0exp, twoq);
+            }
+        }
+        int co = c0 + pl;
+        co -= dw_div(co, p.C, p.inv_c) * p.C;
+        float *yo = y + ((P0 + pl) * p.Ho + oh0 + orow) * p.Wo + 4 * qd;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (4 * qd + j < p.Wo) yo[j] = epi(ep, ep_act, ep_lo, ep_hi, co, acc[j]);
+    }
+    if (__syncthreads_or(bad ? 1 : 0) && tid == 0) atomicOr(gate, 1u);
+}
+
 // (round 3's alternative depthwise forms conv_dwx_kernel -- band-staged in LDS -- and
 // conv_dwg_kernel -- an fp32 gather -- measured slower than conv_tbx_kernel and were
 // removed in round 4.)

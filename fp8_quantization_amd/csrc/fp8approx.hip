@@ -669,9 +669,11 @@ static hipEvent_t pool_event() {
 // "tbx_rw": output rows per thread of conv_tbx_kernel (1 or 2; 2 needs undilated rows).
 // FP8A_TBX_RW=<n> sets it at load.
 static int g_opt_tbx_rw = getenv("FP8A_TBX_RW") ? atoi(getenv("FP8A_TBX_RW")) : 2;
-// "tbs": the table-form depthwise 3x3 on the LDS-staged conv_tbs_kernel with the word pre-pass
-// fused (1, default) or on tbx_decode_a + conv_tbx_kernel (0; the same bits).  FP8A_TBS=<n>.
-static int g_opt_tbs = getenv("FP8A_TBS") ? atoi(getenv("FP8A_TBS")) : 1;
+// "tbs": the table-form depthwise 3x3 on the LDS-DMA-staged conv_tbsg_kernel (2, default:
+// MobileNetV2 E4M3 21.7k -> 22.8k, config 3 v9 19.6k -> 20.5k images/s), the register-staged
+// conv_tbs_kernel (1), both with the word pre-pass fused, or on tbx_decode_a + conv_tbx_kernel (0);
+// the same bits.  FP8A_TBS=<n>.
+static int g_opt_tbs = getenv("FP8A_TBS") ? atoi(getenv("FP8A_TBS")) : 2;
 // "dw3": the exact depthwise 3x3 on the LDS-DMA-staged, 4-outputs-per-thread dn_dw3g_kernel (2,
 // default: config 1 26.1k -> 28.3k images/s), the register-staged dn_dw3_kernel (1) or the general
 // dn_group_conv (0); the same bits.  FP8A_DW3=<n> sets it at load.
@@ -1659,7 +1661,27 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
             if (hipMemsetAsync(gate, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a gate reset");
             TbsArgs tb{};
             size_t tlds = 0;
-            if (g_opt_tbs && !use_img && cig == 1 && kh == 3 && dh == 1 && plan_tbs(tb, sw, Bn * Cout, Cout, H, W, Ho, Wo,
+            // tbs = 2 (default): the LDS-DMA-staged conv_tbsg_kernel
+            DwArgs dg{};
+            size_t glds = 0;
+            const bool tbsg = g_opt_tbs == 2 && !use_img && cig == 1 && kh == 3 && dh == 1 && H < (1 << 20) &&
+                              W < (1 << 20) && Cout < (1 << 20) && H * W < (1ll << 22) && [&]() {
+                                  dg.planes = Bn * Cout; dg.C = (int)Cout; dg.H = (int)H; dg.W = (int)W;
+                                  dg.Ho = (int)Ho; dg.Wo = (int)Wo; dg.ph = ph; dg.pw = pw; dg.nx = Bn * Cin * H * W;
+                                  if (!plan_dw3(dg, sw, glds, true)) return false;
+                                  glds = (size_t)dg.nimg * 4 + 64 * 8 + (size_t)dg.PB * 9 * 8;
+                                  return glds <= 65536;
+                              }();
+            if (tbsg) {
+                const unsigned gb = (unsigned)(((dg.planes + dg.PB - 1) / dg.PB) * dg.nb);
+#define FP8A_TBSG(S_, M_) conv_tbsg_kernel<S_, M_><<<gb, 256, glds, s>>>(x, w, y, dg, fq, fqb, fqi, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi)
+                if (Mw == 2) { if (sw == 1) FP8A_TBSG(1, 2); else FP8A_TBSG(2, 2); }
+                else { if (sw == 1) FP8A_TBSG(1, 3); else FP8A_TBSG(2, 3); }
+#undef FP8A_TBSG
+                if (fq.mx) bA = fqi;
+                rc = hip_check("fp8a_conv2d (tensor-bias groups, LDS-DMA staged table form)");
+                if (rc) return rc;
+            } else if (g_opt_tbs && !use_img && cig == 1 && kh == 3 && dh == 1 && plan_tbs(tb, sw, Bn * Cout, Cout, H, W, Ho, Wo,
                                                                                   ph, pw, tlds)) {
                 const unsigned gb = (unsigned)(((tb.planes + tb.PB - 1) / tb.PB) * tb.nb);
 #define FP8A_TBS(S_, M_) conv_tbs_kernel<S_, M_><<<gb, 256, tlds, s>>>(x, w, y, tb, fq, fqb, fqi, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi)

@@ -90,8 +90,8 @@ int fp8a_kernel_time(double *out, int reset);
 /*
  * Runtime options (A/B measurements, tests, diagnostics):
  * "tbx_rw" (default 2; FP8A_TBX_RW) -- output rows per thread of the table-form depthwise kernel;
- * "tbs" (default 1; FP8A_TBS) -- the LDS-staged table-form depthwise kernel (0: the word-image
- * gather); "dw3" (default 2; FP8A_DW3) -- the exact depthwise 3x3: 2 = window staged by LDS-DMA,
+ * "tbs" (default 2; FP8A_TBS) -- the table-form depthwise kernel: 2 = window staged by LDS-DMA,
+ * 1 = register-staged, both with the word pre-pass fused; 0 = the word-image gather (same bits); "dw3" (default 2; FP8A_DW3) -- the exact depthwise 3x3: 2 = window staged by LDS-DMA,
  * 4 outputs per thread; 1 = register-staged window; 0 = the general grouped kernel (same bits);
  * "dw_target" / "dw_lds" -- outputs / LDS bytes per workgroup of those staged kernels;
  * "v5ds" (default 1; FP8A_V5DS) -- the v5 (E5M2, adder wrap) depthwise 3x3 on the staged kernel

@@ -246,12 +246,15 @@ def test_two_row_and_staged_forms_bit_identical(fmt, cfg):
         y2, g2 = _dw_raw(x, w, bA, bW, bR, tab, FL, s, 1, fmt=fmt)
         _lib.set_option("tbs", 1)
         y3, g3 = _dw_raw(x, w, bA, bW, bR, tab, FL, s, 1, fmt=fmt)
+        _lib.set_option("tbs", 2)  # the LDS-DMA-staged conv_tbsg_kernel
+        y4, g4 = _dw_raw(x, w, bA, bW, bR, tab, FL, s, 1, fmt=fmt)
     finally:
         _lib.set_option("tbx_rw", old)
         _lib.set_option("tbs", old_tbs)
-    assert g1 == 0 and g2 == 0 and g3 == 0
+    assert g1 == 0 and g2 == 0 and g3 == 0 and g4 == 0
     assert np.array_equal(y1.view(np.uint32), y2.view(np.uint32))
     assert np.array_equal(y1.view(np.uint32), y3.view(np.uint32))
+    assert np.array_equal(y1.view(np.uint32), y4.view(np.uint32))
 
 
 @pytest.mark.parametrize("fmt", [(4, 3), (5, 2)], ids=["E4M3", "E5M2"])
@@ -277,7 +280,11 @@ def test_staged_form_full_model_bit_identical(fmt):
     try:
         with torch.no_grad():
             y0 = m(x).cpu().numpy()
+        _lib.set_option("tbs", 2 if old != 2 else 1)  # the other staged form
+        with torch.no_grad():
+            y2 = m(x).cpu().numpy()
     finally:
         _lib.set_option("tbs", old)
     assert np.isfinite(y1).all()
     assert np.array_equal(y0.view(np.uint32), y1.view(np.uint32))
+    assert np.array_equal(y0.view(np.uint32), y2.view(np.uint32))
