@@ -37,9 +37,12 @@ class WordChain:
         in_img = self.in_image if qin is not None else None
         out = None
         nxt = self.next_layer
-        # (only an ungrouped launch emits; single-output-channel-group layers only consume)
-        nq = nxt.chain_input_quantizer() if nxt is not None and layer.groups == 1 else None
+        # (an ungrouped launch emits the E4M3 / E5M2 and table forms; a v5 depthwise launch the v5 form
+        # (3): the staged kernel's store -- any other launch flags the image invalid)
+        nq = nxt.chain_input_quantizer() if nxt is not None else None
         form = nxt.chain_wants_image() if nq is not None else 0
+        if form and layer.groups != 1 and form != 3:
+            form = 0
         if form:
             Bn, _, H, W = x.shape
             kh, kw = layer.kernel_size
@@ -69,7 +72,8 @@ class ChainConsumerMixin:
 
     def chain_wants_image(self):
         """The input word image this layer's launch would read: 0 none, 1 the matrix-core form, 2 the
-        tensor-bias table form (single-output-channel groups; fp8a_conv2d_wants_image)."""
+        tensor-bias table form (single-output-channel groups), 3 the v5 matrix-core form
+        (fp8a_conv2d_wants_image)."""
         # keyed on the layer's approx parameters and the library's option generation (an option such
         # as af32_maxct changes the answer), so the table is not rebuilt and re-listed every forward
         from . import _lib
@@ -88,7 +92,7 @@ class ChainConsumerMixin:
     def chain_image(self, in_shape, device, form=1):
         """This layer's input word image buffer (allocated and initialised once per shape): with
         this layer's padding as border (form 1), or none (form 2, the table form's plain words)."""
-        pad = tuple(self.padding) if form == 1 else (0, 0)
+        pad = tuple(self.padding) if form != 2 else (0, 0)
         key = (tuple(in_shape), pad, str(device))
         cached = getattr(self, "_chain_img", None)
         if cached is None or cached[0] != key:

@@ -518,7 +518,7 @@ __global__ __launch_bounds__(256) void conv_v5ds_kernel(const float *x, const fl
                                                         FqIn fq, float *fqb, int32_t *fqi, const int32_t *bA,
                                                         const int32_t *bW, const int32_t *bR, TablePack tab,
                                                         uint32_t flags, int E, uint32_t *gate, const float2 *ep,
-                                                        int ep_act, float ep_lo, float ep_hi) {
+                                                        int ep_act, float ep_lo, float ep_hi, EmitW em) {
     constexpr int M = 2, NC = 3 * S + 3;
     extern __shared__ float dw_sm[];
     const int tid = threadIdx.x, wv = tid >> 6;
@@ -585,6 +585,14 @@ __global__ __launch_bounds__(256) void conv_v5ds_kernel(const float *x, const fl
     const uint32_t lin0 = (uint32_t)(127 - r_b) << 23;
     const float csub = __uint_as_float((uint32_t)(126 - r_b) << 23);  // 2^(1 - bR - M), M = 2
     const int nqd = (p.Wo + 3) >> 2, pq = p.RB * nqd;
+    // word-image emission for the next (v5 matrix-core, unpadded) convolution: v5_word_a of its input
+    // quantizer's fq(y) at its own bias (the image header, emit_prep_kernel) -- xm_decode_a's words
+    float emx = 0.0f, efb = 0.0f;
+    if (em.w) {
+        emx = __uint_as_float(__builtin_amdgcn_readfirstlane((int)em.invalid[1]));
+        efb = __uint_as_float(__builtin_amdgcn_readfirstlane((int)em.invalid[2]));
+    }
+    const DFmt efmt = dfmt(em.Mw == 2 ? 5 : 4, em.Mw, (int)efb, false);
     for (int e = tid; e < npl * pq; e += 256) {
         const int pl = dw_div(e, pq, p.inv_pq), rem = e - pl * pq;
         const int orow = dw_div(rem, nqd, p.inv_nqd), qd = rem - orow * nqd;
@@ -623,11 +631,21 @@ __global__ __launch_bounds__(256) void conv_v5ds_kernel(const float *x, const fl
         int co = c0 + pl;
         co -= dw_div(co, p.C, p.inv_c) * p.C;
         float *yo = y + ((P0 + pl) * p.Ho + oh0 + orow) * p.Wo + 4 * qd;
+        uint32_t *wo = em.w ? em.w + ((uint32_t)(P0 + pl) * (uint32_t)em.awH + (uint32_t)(oh0 + orow + em.awph)) *
+                                         (uint32_t)em.awW + (uint32_t)em.awpw + 4u * (uint32_t)qd
+                            : nullptr;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-            if (4 * qd + j < p.Wo) yo[j] = epi(ep, ep_act, ep_lo, ep_hi, co, acc[j]);
+            if (4 * qd + j < p.Wo) {
+                const float o = epi(ep, ep_act, ep_lo, ep_hi, co, acc[j]);
+                yo[j] = o;
+                if (wo) wo[j] = v5_word_a(fq_apply(o, emx, efb, em.fq.M, em.fq.S), efmt);
+            }
     }
-    if (__syncthreads_or(bad ? 1 : 0) && tid == 0) atomicOr(gate, 1u);
+    if (__syncthreads_or(bad ? 1 : 0) && tid == 0) {
+        atomicOr(gate, 1u);
+        if (em.w) atomicOr(em.invalid, 1u);  // (the literal kernel rewrites y: the words are stale)
+    }
 }
 
 }  // namespace fp8a

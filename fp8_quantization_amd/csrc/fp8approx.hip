@@ -962,7 +962,7 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
             // the input's word image from the previous launch (fp8a_conv2d_chain): its words replace
             // the A pre-pass, which then runs gated (only to write the fused quantizer's bias, or to
             // re-decode x if the image arrived invalid)
-            const bool use_img = a.in_img != nullptr && !tt && !v5mx && a.conv && a.fqin.mx != nullptr;
+            const bool use_img = a.in_img != nullptr && !tt && a.conv && a.fqin.mx != nullptr;
             if (use_img) a.aw = a.in_img + 64;
             a.af32 = !tt && !v5mx && !use_img && xm_af32(a) ? 1 : 0;
             const int64_t rows = a.conv ? a.M / (a.Ho * a.Wo) : a.M, cols = a_words / std::max<int64_t>(rows, 1);
@@ -998,7 +998,7 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     // 38 % slower E3M4 layer set, round 4 -> 5), so their unsplit launch marks the image invalid
     // instead (emit_prep_kernel set the header valid before this launch) and the consumer's gated
     // pre-pass re-decodes its input from y
-    if (a.em.w != nullptr && a.aw && a.wfmt != 0 && a.splits == 1) {
+    if (a.em.w != nullptr && (a.em.form == 2 || (a.aw && a.wfmt != 0 && a.splits == 1))) {
         if (hipMemsetAsync(a.em.invalid, 1, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a word image header");
         a.em.w = nullptr;
     }
@@ -1604,7 +1604,7 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
                        uint32_t flags, const float *bn, int act, float act_lo, float act_hi, void *workspace,
                        size_t workspace_bytes, hipStream_t s, FqIn fq, float *fqb, int32_t *fqi, float *xq,
                        const float *res = nullptr, int post_act = 0, float post_lo = 0.0f, float post_hi = 0.0f,
-                       FqIn post_fq = FqIn{}, const uint32_t *in_img = nullptr, const EmitW &em = EmitW{}) {
+                       FqIn post_fq = FqIn{}, const uint32_t *in_img = nullptr, const EmitW &em_in = EmitW{}) {
     const float2 *ep = reinterpret_cast<const float2 *>(bn);
     if (ep && (((uintptr_t)bn) & 7) != 0) return fail(FP8A_EINVAL, "bn parameters must be 8-byte aligned");
     int rc = check_format(E, Mw);
@@ -1627,6 +1627,12 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
         return hip_check("fp8a input fake-quant");
     };
     const bool post = res || post_act || post_fq.mx;
+    // v5 words (form 2) come from the staged v5 depthwise kernel only: any other launch flags them invalid
+    EmitW em = em_in;
+    if (em.w && (em.form == 2) != ((flags & F_V5) && cog == 1 && !post && groups > 1)) {
+        if (hipMemsetAsync(em.invalid, 1, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a word image header");
+        em = EmitW{};
+    }
     if (res && (res == y || (((uintptr_t)res) & 15) != 0))
         return fail(FP8A_EINVAL, "the residual must be a 16-byte aligned tensor other than the output");
     if (cog == 1 && !(flags & F_V5)) {  // v5 never had tensor-bias semantics: it takes the GEMM path
@@ -1793,17 +1799,21 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
             gate = (uint32_t *)workspace;
             if (hipMemsetAsync(gate, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a gate reset");
             const unsigned g = (unsigned)(((d.planes + d.PB - 1) / d.PB) * d.nb);
+            // (it emits the next convolution's v5 words when fp8a_conv2d_chain asked for them, em.form 2)
+            const EmitW emv = em.w && em.form == 2 ? em : EmitW{};
             if (sh == 1)
                 conv_v5ds_kernel<1><<<g, 256, lds, s>>>(x, w, y, d, fq, fqb, fqi, bA, bW, bR, tp, flags, E, gate, ep,
-                                                        act, act_lo, act_hi);
+                                                        act, act_lo, act_hi, emv);
             else
                 conv_v5ds_kernel<2><<<g, 256, lds, s>>>(x, w, y, d, fq, fqb, fqi, bA, bW, bR, tp, flags, E, gate, ep,
-                                                        act, act_lo, act_hi);
+                                                        act, act_lo, act_hi, emv);
             rc = hip_check("fp8a_conv2d (v5 depthwise, staged)");
             if (rc) return rc;
             if (fq.mx) bA = fqi;
             ++g_paths[PATH_FAST];
         } else if (v5dw_ok) {
+            if (em.w && hipMemsetAsync(em.invalid, 1, sizeof(uint32_t), s) != hipSuccess)  // (no emission here)
+                return hip_check("fp8a word image header");
             gate = (uint32_t *)workspace;
             uint32_t *aw = (uint32_t *)((char *)workspace + FLAG_BYTES);
             uint2 *bwd = (uint2 *)((char *)workspace + FLAG_BYTES + awb);
@@ -1830,6 +1840,8 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
             ++g_paths[PATH_FAST];
         } else {
             ++g_paths[PATH_EXACT];
+            if (em.w && hipMemsetAsync(em.invalid, 1, sizeof(uint32_t), s) != hipSuccess)  // (no emission here)
+                return hip_check("fp8a word image header");
             if (fq.mx) {
                 fq_bias_kernel<<<1, 1, 0, s>>>(fq, fqb, fqi);
                 bA = fqi;
@@ -2011,6 +2023,10 @@ int fp8a_conv2d_wants_image(int64_t Cout, int kh, int kw, int ph, int pw, int gr
         return tbx ? 2 : 0;
     }
     if (groups != 1 || no_mx()) return 0;
+    // the v5 matrix-core form (gemm_v5mx_kernel): its words (v5_word_a) when unpadded (an image's
+    // border holds the E4M3 / E5M2 form's zero word, fp8a_word_image_init); emitted by the staged
+    // v5 depthwise kernel only (conv_v5ds_kernel) -- every other producer flags the image invalid
+    if (flags & F_V5) return (v5mx_form(Mw, flags, TM_V5) && ph == 0 && pw == 0) ? 3 : 0;
     if (!f8_form(E, Mw, flags & ~F_TB, mode)) return 0;
     if (kh == 1 && kw == 1 && ph == 0 && pw == 0) {  // xm_af32: fp32 staging up to af32_maxct column tiles
         const int64_t bnt = 16 * xm_ncg(Cout), ct = (Cout + bnt - 1) / bnt;
@@ -2057,10 +2073,14 @@ int fp8a_conv2d_chain(const float *x, const float *w, float *y, int64_t Bn, int6
         if (!next_maxval || !next_bR || next_mbits < 1 || qE < 1 || !(next_Mw == 2 || next_Mw == 3) || next_ph < 0 ||
             next_pw < 0)
             return fail(FP8A_EINVAL, "bad next-convolution parameters for the word image");
-        if (next_form != 0 && next_form != 1) return fail(FP8A_EINVAL, "bad word image form");
+        if (next_form < 0 || next_form > 2) return fail(FP8A_EINVAL, "bad word image form");
         // (the table form's words: the consumer's plain [Bn][C][Ho][Wo] layout, no border)
-        const WordImage wi = next_form ? word_image(Ho, Wo, 0, 0) : word_image(Ho, Wo, next_ph, next_pw);
-        const bool can = groups == 1 && Cout > 1 && Ho > 0 && Wo > 0 && Bn * Cout * Ho * Wo < (1ll << 31) &&
+        const WordImage wi = next_form == 1 ? word_image(Ho, Wo, 0, 0) : word_image(Ho, Wo, next_ph, next_pw);
+        // (form 2, v5 words: the staged v5 depthwise producer -- conv2d_impl flags the image invalid
+        // where that kernel does not run; form 0 / 1: ungrouped producers)
+        const bool prod = next_form == 2 ? (flags & F_V5) && groups > 1 && Cin == groups && Cout == groups
+                                         : groups == 1;
+        const bool can = prod && Cout > 1 && Ho > 0 && Wo > 0 && Bn * Cout * Ho * Wo < (1ll << 31) &&
                          Bn * Cout * wi.H * wi.W < (1ll << 30);
         // the header: valid (0) with the next quantizer's constants before this launch emits,
         // invalid (nonzero) when it cannot emit

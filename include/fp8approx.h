@@ -328,16 +328,19 @@ int fp8a_word_image_init(void *image, int64_t Bn, int64_t C, int64_t H, int64_t 
  *             next_maxval (per tensor) / next_nbits / next_mbits / next_sign_bits, result bias
  *             next_bR and mantissa width next_Mw (3: E4M3, 2: E5M2); next_form = the next
  *             convolution's fp8a_conv2d_wants_image - 1 (0: matrix-core words in an image of
- *             next_ph / next_pw; 1: table-form words, image of ph = pw = 0).  y is written as well.
- *             Where this call cannot emit (groups > 1, Cout == 1, or the v5 matrix-core form, whose
-             store does not emit) the image is flagged invalid.
+ *             next_ph / next_pw; 1: table-form words, image of ph = pw = 0; 2: the v5 matrix-core
+ *             form's words, emitted by a v5 depthwise 3x3 producer on its staged kernel).  y is
+ *             written as well.  Where this call cannot emit (groups > 1 outside form 2, Cout == 1,
+ *             a tile-table or v5 matrix-core producer, whose store does not emit) the image is
+ *             flagged invalid.
  * Results are bit-identical to the unchained calls.  workspace: fp8a_conv2d_block_workspace_size().
  */
 /* The word image a convolution of this shape / format would read as in_image: 1 = the matrix-core
  * path's (ungrouped, Cout > 1, E4M3 / E5M2 with s2n + qbma and a {0,1} or zero table, not a 1x1
  * unpadded convolution staged from fp32; images of its padding), 2 = the tensor-bias table form's
  * (single-output-channel groups, 3-wide undilated rows, stride 1 / 2; images with ph = pw = 0),
- * 0 = none: emitting an image for it would be wasted. */
+ * 3 = the v5 matrix-core form's (unpadded convolutions), 0 = none: emitting an image for it would
+ * be wasted. */
 int fp8a_conv2d_wants_image(int64_t Cout, int kh, int kw, int ph, int pw, int groups, int E, int Mw,
                             const int32_t *table, uint32_t flags, int sh, int sw, int dh, int dw);
 int fp8a_conv2d_chain(const float *x, const float *w, float *y, int64_t Bn, int64_t Cin, int64_t H,

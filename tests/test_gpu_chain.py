@@ -234,3 +234,68 @@ def test_table_form_handoff_to_depthwise(E, M, stride):
     torch.cuda.synchronize()
     assert int(img[:4].view(torch.int32).item()) == 0, "the emitted image was flagged invalid"
     assert torch.equal(_bits(z), _bits(z2)) and torch.equal(ib, ib2)
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_v5_depthwise_handoff_to_v5_gemm(stride):
+    """A v5 depthwise layer (the staged conv_v5ds_kernel) emitting the v5 matrix-core words of the
+    next 1x1 convolution's input (fp8a_conv2d_chain next_form 2): the image stays valid, and the
+    consumer reading it gives the unchained result bit for bit, with the same input-quantizer bias."""
+    from fp8_quantization_amd.approx_ops import approx_conv2d, make_flags_v5, new_word_image
+    g = torch.Generator().manual_seed(7 + stride)
+    C, H = 24, 15
+    x = _grid(g, (2, C, H, H), 2).to(DEV)
+    wd = _grid(g, (C, 1, 3, 3), 2, -8, 0, 0.0).to(DEV)
+    wp = _grid(g, (40, C, 1, 1), 2, -8, 0, 0.0).to(DEV)
+    tab = torch.as_tensor(np.array([[0, -1, 2, 0], [1, 0, -2, 1], [0, 3, 0, -1], [-3, 1, 1, 0]], np.int32))
+    fl = make_flags_v5(True, True, True)
+    bWd = torch.full((C,), 18, dtype=torch.int32, device=DEV)
+    bWp = torch.full((40,), 20, dtype=torch.int32, device=DEV)
+    bR = torch.tensor([12], dtype=torch.int32, device=DEV)
+    qin1 = (torch.tensor([9.0], device=DEV), 8, 2, 1)
+    qin2 = (torch.tensor([3.5], device=DEV), 8, 2, 1)
+    Ho = (H + 2 - 3) // stride + 1
+    img = new_word_image(2, C, Ho, Ho, 0, 0, DEV)
+    args1 = dict(flags=fl, stride=(stride, stride), padding=(1, 1), groups=C)
+    y, _, _ = approx_conv2d(x, wd, 5, 2, None, bWd, bR, tab, qin=qin1, chain=(None, (img, (0, 0), qin2, bR, 2, 2)),
+                            **args1)
+    y0, _, _ = approx_conv2d(x, wd, 5, 2, None, bWd, bR, tab, qin=qin1, **args1)
+    torch.cuda.synchronize()
+    assert torch.equal(_bits(y), _bits(y0))
+    assert int(img[:4].view(torch.int32).item()) == 0, "the staged v5 depthwise producer did not emit"
+    z, ib, _ = approx_conv2d(y, wp, 5, 2, None, bWp, bR, tab, qin=qin2, flags=fl)
+    z2, ib2, _ = approx_conv2d(y, wp, 5, 2, None, bWp, bR, tab, qin=qin2, flags=fl, chain=(img, None))
+    assert torch.equal(_bits(z), _bits(z2)) and torch.equal(ib, ib2)
+
+
+def test_mobilenet_v5_logits_identical_with_chain(monkeypatch):
+    """BASELINE config 3's v5 mode (MobileNetV2 E5M2, approx_version 5 with the OF / UF switches):
+    logits with the depthwise -> projection hand-off on and off, to the bit."""
+    from fp8_quantization_amd import chain
+    from fp8_quantization_amd.mobilenet_workload import mobilenet_v2_approx
+    torch.manual_seed(3)
+    m = mobilenet_v2_approx(input_size=64, n_class=100, bn_stats_batches=1, device=DEV, expo_width=5, mant_width=2,
+                            dnsmp_factor=3, with_approx=True, with_s2nn2s_opt=True, quant_btw_mult_accu=True,
+                            approx_version=5, withComp=True, sim_hw_add_OFUF=True, with_OF_opt=True,
+                            with_UF_opt=True).to(DEV).eval()
+    g = torch.Generator().manual_seed(4)
+    m.quantized()
+    m.estimate_ranges()
+    with torch.no_grad():
+        m(torch.randn((2, 3, 64, 64), generator=g).to(DEV))
+    m.fix_ranges()
+    x = torch.randn((3, 3, 64, 64), generator=g).to(DEV)
+    emitted = []
+    orig_done = chain.WordChain.done
+
+    def done(self, ch):
+        orig_done(self, ch)
+        emitted.append(self.emitted is not None)
+    monkeypatch.setattr(chain.WordChain, "done", done)
+    with torch.no_grad():
+        on = m(x)
+    assert sum(emitted) >= 10, emitted  # the depthwise layers emitted
+    monkeypatch.setattr(chain, "CHAIN", False)
+    with torch.no_grad():
+        off = m(x)
+    assert torch.equal(_bits(on), _bits(off)), "logits differ with the v5 word-image hand-off"
