@@ -678,6 +678,9 @@ static int g_opt_tbs = getenv("FP8A_TBS") ? atoi(getenv("FP8A_TBS")) : 2;
 // default: config 1 26.1k -> 28.3k images/s), the register-staged dn_dw3_kernel (1) or the general
 // dn_group_conv (0); the same bits.  FP8A_DW3=<n> sets it at load.
 static int g_opt_dw3 = getenv("FP8A_DW3") ? atoi(getenv("FP8A_DW3")) : 2;
+// "dn_direct": exact convolutions with K <= 32 and N <= 64 on dn_direct_kernel (1, default) or on
+// the bf16 matrix-core GEMM (0).  FP8A_DN_DIRECT=<n> sets it at load.
+static int g_opt_dn_direct = getenv("FP8A_DN_DIRECT") ? atoi(getenv("FP8A_DN_DIRECT")) : 1;
 // "v5ds": the v5 depthwise 3 x 3 on the staged conv_v5ds_kernel (1, default) or on the word
 // pre-passes + conv_v5dw_kernel (0); the same bits.  FP8A_V5DS=<n> sets it at load.
 static int g_opt_v5ds = getenv("FP8A_V5DS") ? atoi(getenv("FP8A_V5DS")) : 1;
@@ -1098,6 +1101,26 @@ static int run_dense(DenseArgs a, void *ws, size_t wsb, hipStream_t s) {
                                                        (size_t)a.M, s);
         return e == hipSuccess ? FP8A_OK : hip_check("fp8a dense fill");
     }
+    // a small convolution (the stem: K = 27, N = 32) as direct fp32 FMAs (dn_direct_kernel; option
+    // "dn_direct", default 1): a 128 x 128 MFMA tile would carry 32 live columns and 27 of 64 k
+    if (g_opt_dn_direct && a.conv && a.K <= DD_K && a.N <= DD_N) {
+        KernelEv kev{};
+        if (g_ktime) {
+            kev.a = pool_event();
+            kev.b = pool_event();
+            kev.path = PATH_DENSE;
+            kev.dispatches = 1;
+            kev.macs = 4.0 * ((double)a.M * a.K + (double)a.M * a.N) + 4.0 * (double)a.N * a.K;
+            if (kev.a && kev.b) (void)hipEventRecord(kev.a, s);
+        }
+        const unsigned g = (unsigned)std::min<int64_t>((a.M + 255) / 256, 1 << 20);
+        dn_direct_kernel<<<g, 256, 0, s>>>(a);
+        if (g_ktime && kev.a && kev.b) {
+            (void)hipEventRecord(kev.b, s);
+            g_kev.push_back(kev);
+        }
+        return hip_check("fp8a dense direct launch");
+    }
     a.mpad = round_up(a.M, DN_T);
     a.npad = round_up(a.N, DN_T);
     a.kpad = round_up(a.K, 32);
@@ -1325,6 +1348,11 @@ int fp8a_set_option(const char *name, int value) {
     if (strcmp(name, "dw_target") == 0) {
         const int old = g_opt_dw_target;
         g_opt_dw_target = std::max(256, value);
+        return old;
+    }
+    if (strcmp(name, "dn_direct") == 0) {
+        const int old = g_opt_dn_direct;
+        g_opt_dn_direct = value;
         return old;
     }
     if (strcmp(name, "v5ds") == 0) {

@@ -652,6 +652,61 @@ __global__ __launch_bounds__(256) void dn_fix(const DenseArgs p) {
     }
 }
 
+// Small exact convolutions (K = Cin kh kw <= 32 and N = Cout <= 64: the stem conv of MobileNetV2 /
+// ResNet, a 128 x 128 MFMA tile with 32 live columns and a 64-deep stage for 27 k): thread = output
+// pixel, every channel, fp32 FMAs in k order from zero -- dn_fix's arithmetic, the fp32 contraction
+// of the original operands, so no fallback units.  The weights (through the fused weight quantizer)
+// sit in LDS as [N][32] rows read by 16-byte broadcasts, the pixel's K inputs (through the fused input
+// quantizer) in registers; per channel the stores are coalesced over pixels.
+constexpr int DD_K = 32, DD_N = 64;
+__global__ __launch_bounds__(256) void dn_direct_kernel(const DenseArgs p) {
+    __shared__ __attribute__((aligned(16))) float swt[DD_N * DD_K];
+    const int tid = threadIdx.x, K = (int)p.K, N = (int)p.N;
+    for (int d = tid; d < N * DD_K; d += 256) {
+        const int n = d / DD_K, k = d - n * DD_K;
+        swt[d] = k < K ? dn_w(p.fz, n, p.w[(int64_t)k * p.sbk + n * p.sbn]) : 0.0f;
+    }
+    if (blockIdx.x == 0)
+        for (int n = tid; n < N; n += 256) dn_bias_out(p.fz, n);
+    __syncthreads();
+    const DnQv qv = dn_qv(p.fz);
+    const int64_t hw = p.Ho * p.Wo;
+    const int khw = p.kh * p.kw;
+    for (int64_t m = (int64_t)blockIdx.x * 256 + tid; m < p.M; m += (int64_t)gridDim.x * 256) {
+        const int64_t img = m / hw, pix = m - img * hw, ho = pix / p.Wo, wo = pix - ho * p.Wo;
+        float a[DD_K];
+        int c = 0, i = 0, j = 0;
+#pragma unroll
+        for (int k = 0; k < DD_K; ++k) {
+            float v = 0.0f;
+            if (k < K) {
+                v = dn_in(p.fz, qv, dn_conv_elem(p, img, ho, wo, c, i, j));
+                if (++j == p.kw) {
+                    j = 0;
+                    if (++i == p.kh) { i = 0; ++c; }
+                }
+            }
+            a[k] = v;
+        }
+        (void)khw;
+        float *yo = p.y + img * N * hw + pix;
+        for (int n = 0; n < N; ++n) {
+            const float4 *wr = reinterpret_cast<const float4 *>(swt + n * DD_K);
+            float acc = 0.0f;
+#pragma unroll
+            for (int q = 0; q < DD_K / 4; ++q) {
+                if (4 * q >= K) break;
+                const float4 wv = wr[q];
+                if (4 * q + 0 < K) acc = __fmaf_rn(a[4 * q + 0], wv.x, acc);
+                if (4 * q + 1 < K) acc = __fmaf_rn(a[4 * q + 1], wv.y, acc);
+                if (4 * q + 2 < K) acc = __fmaf_rn(a[4 * q + 2], wv.z, acc);
+                if (4 * q + 3 < K) acc = __fmaf_rn(a[4 * q + 3], wv.w, acc);
+            }
+            yo[(int64_t)n * hw] = dn_out(p.fz, qv, n, acc);
+        }
+    }
+}
+
 // n / d for 0 <= n < 2^22 through the float reciprocal (inv = 1 / d rounded): the float quotient
 // is off by at most one, the remainder's sign and range fix it.
 __device__ __forceinline__ int dw_div(int n, int d, float inv) {

@@ -94,6 +94,8 @@ int fp8a_kernel_time(double *out, int reset);
  * 1 = register-staged, both with the word pre-pass fused; 0 = the word-image gather (same bits); "dw3" (default 2; FP8A_DW3) -- the exact depthwise 3x3: 2 = window staged by LDS-DMA,
  * 4 outputs per thread; 1 = register-staged window; 0 = the general grouped kernel (same bits);
  * "dw_target" / "dw_lds" -- outputs / LDS bytes per workgroup of those staged kernels;
+ * "dn_direct" (default 1; FP8A_DN_DIRECT) -- exact convolutions with Cin kh kw <= 32 and Cout <= 64
+ * (the stem) as direct fp32 FMAs instead of the bf16 matrix-core GEMM;
  * "v5ds" (default 1; FP8A_V5DS) -- the v5 (E5M2, adder wrap) depthwise 3x3 on the staged kernel
  * with both word pre-passes fused (0: the pre-passes + the word-form kernel; same bits);
  * "xm_ncg" (default 0 = by N; FP8A_XM_NCG) -- gemm_f8mx_kernel's tile width forced to 16 x 1 / 2

@@ -253,3 +253,46 @@ def test_depthwise_lds_form_matches_general_kernel(shape, fused, form):
     assert torch.equal(torch.isnan(y_new), torch.isnan(y_old))
     fin = ~torch.isnan(y_old)
     assert torch.equal(y_new[fin], y_old[fin])
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 33, 33, 32, 3, 2, 1), (1, 3, 20, 17, 16, 3, 1, 1), (2, 2, 9, 9, 64, 4, 2, 0),
+                                   (1, 32, 8, 8, 8, 1, 1, 0)], ids=lambda c: "x".join(map(str, c)))
+@pytest.mark.parametrize("fused", [False, True])
+def test_small_conv_direct_form(shape, fused):
+    """Small exact convolutions (K = Cin kh kw <= 32, Cout <= 64: the stem) on dn_direct_kernel (option
+    "dn_direct" = 1) against the bf16 matrix-core form (0) and the float64 product: fp32 FMAs in k
+    order, so within a few ulps of the matrix core's sum; with the config-1 tail (weight / input
+    quantizers, rq, BN, clamp) fused, the quantizers' biases identical."""
+    from fp8_quantization_amd import _lib
+    from fp8_quantization_amd.approx_ops import dense_conv2d, dense_conv2d_fused, dense_format
+    Bn, C, H, W, Co, k, s, p = shape
+    g = torch.Generator().manual_seed(Bn * C + H + Co + k)
+    x = (torch.randn(Bn, C, H, W, generator=g) * 2).to(DEV)
+    w = (torch.randn(Co, C, k, k, generator=g) * 0.3).to(DEV)
+
+    def run():
+        if not fused:
+            return dense_conv2d(x, w.bfloat16().float(), dense_format(3), (s, s), (p, p)), None
+        ep = torch.stack((torch.rand(Co, generator=g) + 0.5, torch.randn(Co, generator=g)), 1).to(DEV).contiguous()
+        return dense_conv2d_fused(x, w, 1, (s, s), (p, p), qin=(torch.tensor([6.0], device=DEV), 8, 3, 1),
+                                  rq=(torch.tensor([40.0], device=DEV), 8, 3, 1), bn=(ep, 1, 0.0, 6.0),
+                                  wq=(torch.rand(Co, generator=g).to(DEV) + 0.2, 8, 3, 1))
+
+    old = _lib.set_option("dn_direct", 1)
+    try:
+        g.manual_seed(3)
+        y1, b1 = run()
+        _lib.set_option("dn_direct", 0)
+        g.manual_seed(3)
+        y0, b0 = run()
+    finally:
+        _lib.set_option("dn_direct", old)
+    if fused:
+        assert all(torch.equal(b1[key], b0[key]) for key in b0)
+        d = (y1 - y0).abs()
+        # (the fused rq rounds to the FP8 grid: a last-bit sum difference can move a value one step)
+        assert (d == 0).float().mean() > 0.995
+    else:
+        ref = torch.nn.functional.conv2d(x.double(), w.bfloat16().double(), stride=s, padding=p)
+        assert torch.allclose(y1.double(), ref, rtol=1e-5, atol=1e-4)
+        assert torch.allclose(y1, y0, rtol=1e-5, atol=1e-5)
