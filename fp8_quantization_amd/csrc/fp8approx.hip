@@ -14,6 +14,8 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -175,6 +177,8 @@ __device__ __forceinline__ float load_A(const GemmArgs &p, int64_t m, int64_t k)
     return fq_apply(v, mx, fq_bias(mx, p.fqin.E, p.fqin.M), p.fqin.M, p.fqin.S);
 }
 
+__device__ __forceinline__ void gemm_exact_units(const GemmArgs &p, uint32_t f, const DFmt &fA, const DFmt &fR, bool tb);
+
 __global__ __launch_bounds__(256) void gemm_exact_kernel(const GemmArgs p) {
     const bool tb = p.flags & F_TB;
     const DFmt fA = dfmt(p.E, p.Mw, *p.bA, tb), fR = dfmt(p.E, p.Mw, *p.bR, tb);
@@ -205,9 +209,24 @@ __global__ __launch_bounds__(256) void gemm_exact_kernel(const GemmArgs p) {
     }
     // Gated after a fast launch: nothing to do unless it flagged (uniform per grid; the grid is
     // capped, so the no-op case costs one small launch); then only the marked 64 x 64 units
-    // (every unit with FB_ALL), one unit per block step: thread = (row, 16 columns).
+    // (every unit with FB_ALL), one unit per block step: thread = (row, 16 columns).  The kernel
+    // ends the launch: it reports the flag word to the caller (flag_out) and leaves the flag
+    // arena zero for the next launch on the stream (arena_release).
     const uint32_t f = __hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if ((f & FB_ANY) == 0u) return;
+    if (f == 0u) {  // no flag bit, so no unit mark either: only the pre-passes' extremes to clear
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            p.flag[1] = 0u;
+            p.flag[2] = 0u;
+            if (p.flag_out) *p.flag_out = 0u;
+        }
+        return;
+    }
+    if (f & FB_ANY) gemm_exact_units(p, f, fA, fR, tb);
+    arena_release(p.flag, f, p.flag_out, p.urow, p.urow ? (size_t)(p.nur + p.nuc + p.nur * p.nuc) : 0);
+}
+
+// The marked units of a flagged launch (gemm_exact_kernel); every thread returns here.
+__device__ __forceinline__ void gemm_exact_units(const GemmArgs &p, uint32_t f, const DFmt &fA, const DFmt &fR, bool tb) {
     const bool all = (f & FB_ALL) != 0u || p.urow == nullptr;
     const int64_t nur = (p.M + 63) >> 6, nuc = (p.N + 63) >> 6;
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_fallback[0], 1ull);
@@ -314,10 +333,16 @@ __global__ __launch_bounds__(256) void conv_tb_direct_kernel(const float *x, con
                                                              int dw, int groups, int64_t Ho, int64_t Wo, int E,
                                                              int Mw, const int32_t *bA, const int32_t *bW,
                                                              const int32_t *bR, TablePack tab, uint32_t flags,
-                                                             const uint32_t *gate, const float2 *ep, int ep_act,
-                                                             float ep_lo, float ep_hi, FqIn fq) {
-    // after conv_tb_fast_kernel: run only if it flagged inputs outside its exactness window
-    if (gate != nullptr && __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
+                                                             uint32_t *gate, uint32_t *gate_out, const float2 *ep,
+                                                             int ep_act, float ep_lo, float ep_hi, FqIn fq) {
+    // after conv_tb_fast_kernel: run only if it flagged inputs outside its exactness window.  The
+    // gate word is the stream's flag arena (flag_arena): this kernel reports it to the caller's
+    // workspace word (gate_out) and leaves it zero (arena_release)
+    const uint32_t gv = gate != nullptr ? __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 1u;
+    if (gv == 0u) {
+        if (gate_out != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *gate_out = 0u;
+        return;
+    }
     if (gate != nullptr && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_fallback[3], 1ull);
     const int64_t total = Bn * Cout * Ho * Wo;
     const int64_t cpg = Cin / groups;   // input channels per group
@@ -347,6 +372,7 @@ __global__ __launch_bounds__(256) void conv_tb_direct_kernel(const float *x, con
                 }
         y[idx] = epi(ep, ep_act, ep_lo, ep_hi, co, s + part);
     }
+    if (gate != nullptr) arena_release(gate, gv, gate_out, nullptr, 0);
 }
 
 // Single-output-channel groups (depthwise) with the tensor-bias semantics, fast form.
@@ -880,6 +906,41 @@ static bool xm_af32(const GemmArgs &a) {
     return a.A != nullptr && a.M * a.lda * 4 < (1ll << 32) && a.lda >= a.K;
 }
 
+// The fallback-flag arena of a (device, stream): the flag word, the pre-passes' extremes, the
+// gated kernel's block counter and the per-unit marks of the launches on that stream.  Zeroed once
+// when (re)allocated; every launch's last kernel leaves it zero (arena_release), so launches need
+// no fill.  A launch that stops early (a launch error) leaves marks behind: the next launch on the
+// stream then reruns marked units exactly -- the same bits, more time.  Grows by reallocation
+// (after the stream drains).
+struct FlagArena {
+    uint32_t *p = nullptr;
+    size_t bytes = 0;
+};
+static uint32_t *flag_arena(hipStream_t s, size_t need) {
+    static std::mutex mu;
+    static std::map<std::pair<int, uintptr_t>, FlagArena> arenas;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lock(mu);
+    FlagArena &ar = arenas[{dev, (uintptr_t)s}];
+    if (ar.bytes >= need) return ar.p;
+    const size_t nb = std::max(need, std::max(2 * ar.bytes, (size_t)65536));
+    if (ar.p) {
+        if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
+        (void)hipFree(ar.p);
+        ar = FlagArena{};
+    }
+    void *p = nullptr;
+    if (hipMalloc(&p, nb) != hipSuccess) return nullptr;
+    if (hipMemsetAsync(p, 0, nb, s) != hipSuccess) {
+        (void)hipFree(p);
+        return nullptr;
+    }
+    ar.p = (uint32_t *)p;
+    ar.bytes = nb;
+    return ar.p;
+}
+
 // Fast tiled kernel + gated exact kernel (int-bias path), or the exact kernel alone (tb path).
 static int run_qamaa(GemmArgs &a, hipStream_t s);
 
@@ -916,26 +977,25 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
         return hip_check("fp8a exact gemm launch");
     }
     if (ws == nullptr || ws_bytes < FLAG_BYTES) return fail(FP8A_EINVAL, "matmul workspace too small");
-    a.flag = (uint32_t *)ws;
-    // the per-unit fallback marks when the workspace holds them (else a fallback reruns the launch)
+    // the flag word and the per-unit fallback marks live in the library's flag arena (zero on
+    // entry, left zero by gemm_exact_kernel: no fill per launch); the workspace's first word
+    // receives the final flag word, and its head stays reserved (the layout of the size queries)
     static const bool no_units = getenv("FP8A_NO_UNITS") != nullptr;  // diagnostics: whole-launch fallbacks
-    const bool units = !no_units && ws_bytes >= head_bytes(a.M, a.N);
-    const size_t head = units ? head_bytes(a.M, a.N) : FLAG_BYTES;
+    const size_t head = ws_bytes >= head_bytes(a.M, a.N) ? head_bytes(a.M, a.N) : FLAG_BYTES;
+    a.flag = flag_arena(s, head_bytes(a.M, a.N));
+    if (a.flag == nullptr) return hip_check("fp8a flag arena");
+    a.flag_out = (uint32_t *)ws;
     a.nur = (a.M + 63) / 64;
     a.nuc = (a.N + 63) / 64;
-    a.urow = units ? (uint8_t *)ws + FLAG_BYTES : nullptr;
-    a.ucol = units ? a.urow + a.nur : nullptr;
-    a.utile = units ? a.ucol + a.nuc : nullptr;
+    a.urow = no_units ? nullptr : (uint8_t *)a.flag + FLAG_BYTES;
+    a.ucol = no_units ? nullptr : a.urow + a.nur;
+    a.utile = no_units ? nullptr : a.ucol + a.nuc;
     // split-K when the caller's workspace holds the partials (else one split)
     a.splits = choose_splits(a.M, a.N, a.K);
     if (a.splits > 1 && ws_bytes < head + splitk_bytes(a.M, a.N, a.K)) a.splits = 1;
     const int64_t kt = (a.K + BK - 1) / BK;
     a.kchunk = ((kt + a.splits - 1) / a.splits) * BK;
     a.part = a.splits > 1 ? (float *)((char *)ws + head) : nullptr;
-    // flag word + unit marks zeroed by one fill
-    if (hipMemsetAsync(ws, 0, units ? FLAG_BYTES + (size_t)(a.nur + a.nuc + a.nur * a.nuc) : sizeof(uint32_t), s) !=
-        hipSuccess)
-        return hip_check("fp8a flag reset");
     // the matrix-core E4M3 kernel and the tile-table kernel (E3M4 / E2M5) need their pre-decoded
     // operands in the workspace (else gemm_fast_kernel runs); FP8A_NO_MX=1 forces the latter
     a.aw = nullptr;
@@ -1035,7 +1095,7 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     static const bool dbg = getenv("FP8A_DEBUG_FLAGS") != nullptr;  // diagnostics: the flag word per launch
     if (!rc && dbg) {
         uint32_t f = 0;
-        if (hipStreamSynchronize(s) == hipSuccess && hipMemcpy(&f, a.flag, sizeof(f), hipMemcpyDeviceToHost) == hipSuccess)
+        if (hipStreamSynchronize(s) == hipSuccess && hipMemcpy(&f, a.flag_out, sizeof(f), hipMemcpyDeviceToHost) == hipSuccess)
             fprintf(stderr, "fp8a flag M=%lld N=%lld K=%lld E=%d M=%d wfmt=%d flag=%u\n", (long long)a.M, (long long)a.N,
                     (long long)a.K, a.E, a.Mw, a.aw ? a.wfmt : -1, f);
     }
@@ -1687,12 +1747,12 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
             if (rc) return rc;
         }
         if (tbx_ok) {
-            gate = (uint32_t *)workspace;
+            gate = flag_arena(s, FLAG_BYTES);
+            if (gate == nullptr) return hip_check("fp8a flag arena");
             // the input's table-form words from the producing launch (fp8a_conv2d_chain, next_form 1:
             // header + [Bn][Cin][H][W] words of fq_in(x)); the pre-pass then runs gated on its header
             const bool use_img = in_img != nullptr && fq.mx != nullptr;
             uint32_t *aw = use_img ? const_cast<uint32_t *>(in_img) + 64 : (uint32_t *)((char *)workspace + FLAG_BYTES);
-            if (hipMemsetAsync(gate, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a gate reset");
             TbsArgs tb{};
             size_t tlds = 0;
             // tbs = 2 (default): the LDS-DMA-staged conv_tbsg_kernel
@@ -1750,8 +1810,8 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
             if (rc) return rc;
             }
         } else if (fast_ok) {
-            gate = (uint32_t *)workspace;
-            if (hipMemsetAsync(gate, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a gate reset");
+            gate = flag_arena(s, FLAG_BYTES);
+            if (gate == nullptr) return hip_check("fp8a flag arena");
             dim3 grid((unsigned)((Ho * Wo + 255) / 256), (unsigned)Cout, (unsigned)Bn);
             conv_tb_fast_kernel<<<grid, 256, 0, s>>>(x, w, y, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups,
                                                      Ho, Wo, Mw, bA, bW, bR, tp, flags | F_TB, gate, ep, act, act_lo,
@@ -1762,12 +1822,12 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
         const unsigned eb = (unsigned)(fast_ok ? std::min<int64_t>((total + 255) / 256, 4096) : (total + 255) / 256);
         if (fast_ok) {  // gated, grid-capped: a no-op launch unless the fast kernel flagged
             conv_tb_direct_kernel<true><<<eb, 256, 0, s>>>(x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw,
-                                                    groups, Ho, Wo, E, Mw, bA, bW, bR, tp, flags | F_TB, gate, ep,
-                                                    act, act_lo, act_hi, fq);
+                                                    groups, Ho, Wo, E, Mw, bA, bW, bR, tp, flags | F_TB, gate,
+                                                    (uint32_t *)workspace, ep, act, act_lo, act_hi, fq);
         } else {
             conv_tb_direct_kernel<true><<<eb, 256, 0, s>>>(x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw,
-                                                     groups, Ho, Wo, E, Mw, bA, bW, bR, tp, flags | F_TB, nullptr, ep,
-                                                     act, act_lo, act_hi, FqIn{});
+                                                     groups, Ho, Wo, E, Mw, bA, bW, bR, tp, flags | F_TB, nullptr,
+                                                     nullptr, ep, act, act_lo, act_hi, FqIn{});
         }
         return hip_check("fp8a_conv2d (tensor-bias groups)");
     }
@@ -1824,8 +1884,8 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
                               return lds <= 65536;
                           }();
         if (v5ds) {
-            gate = (uint32_t *)workspace;
-            if (hipMemsetAsync(gate, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a gate reset");
+            gate = flag_arena(s, FLAG_BYTES);
+            if (gate == nullptr) return hip_check("fp8a flag arena");
             const unsigned g = (unsigned)(((d.planes + d.PB - 1) / d.PB) * d.nb);
             // (it emits the next convolution's v5 words when fp8a_conv2d_chain asked for them, em.form 2)
             const EmitW emv = em.w && em.form == 2 ? em : EmitW{};
@@ -1842,10 +1902,10 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
         } else if (v5dw_ok) {
             if (em.w && hipMemsetAsync(em.invalid, 1, sizeof(uint32_t), s) != hipSuccess)  // (no emission here)
                 return hip_check("fp8a word image header");
-            gate = (uint32_t *)workspace;
+            gate = flag_arena(s, FLAG_BYTES);
+            if (gate == nullptr) return hip_check("fp8a flag arena");
             uint32_t *aw = (uint32_t *)((char *)workspace + FLAG_BYTES);
             uint2 *bwd = (uint2 *)((char *)workspace + FLAG_BYTES + awb);
-            if (hipMemsetAsync(gate, 0, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a gate reset");
             // (the input quantizer applied here, its bias written for the kernels after: bA = fqi)
             v5dw_decode_a<<<(unsigned)std::min<int64_t>((nx + 255) / 256, 8192), 256, 0, s>>>(x, nx, aw, E, Mw, bA, fq,
                                                                                                fqb, fqi);
@@ -1878,7 +1938,7 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
         // (x unquantized when fq is set: the literal kernel applies fq to every loaded value)
         conv_tb_direct_kernel<false><<<(unsigned)std::min<int64_t>((total + 255) / 256, 16384), 256, 0, s>>>(
             x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups, Ho, Wo, E, Mw, bA, bW, bR, tp, flags,
-            gate, ep, act, act_lo, act_hi, fq);
+            gate, gate ? (uint32_t *)workspace : nullptr, ep, act, act_lo, act_hi, fq);
         return hip_check("fp8a_conv2d (v5 depthwise, direct)");
     }
     for (int g = 0; g < groups; ++g) {

@@ -350,33 +350,50 @@ __global__ __launch_bounds__(256) void xm_decode_a(const GemmArgs p) {
     const float *in0 = p.conv ? p.X + p.cbase * hw : p.A;
     const bool vec = (lim0 % 4 == 0) && (cols % 4 == 0) && (istride % 4 == 0) && (((uintptr_t)in0 & 15) == 0) &&
                      (((uintptr_t)out & 15) == 0);
-    for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) {
-        const float *in = p.conv ? p.X + (r * p.Cin + p.cbase) * hw : p.A + r * p.lda;
-        const int64_t lim = p.conv ? cols : p.K;
-        const int64_t o = r * cols;
-        bool badr = false;
-        if (vec) {
-            for (int64_t i = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x); i < cols;
-                 i += 4 * (int64_t)gridDim.x * blockDim.x) {
-                uint4 w = make_uint4(zw, zw, zw, zw);
-                if (i < lim) {
-                    const float4 v = *reinterpret_cast<const float4 *>(in + i);
-                    bool ok0 = true, ok1 = true, ok2 = true, ok3 = true;
-                    w = make_uint4(word(v.x, ok0), word(v.y, ok1), word(v.z, ok2), word(v.w, ok3));
-                    badr |= !(ok0 && ok1 && ok2 && ok3);
+    if (vec) {
+        // the (row, 4-column chunk) grid flattened over every thread of the launch (a row of a
+        // matrix A is often shorter than the block's 1024 columns: ViT's 768); (row, chunk)
+        // advanced by the thread count's quotient and remainder, so no division in the loop.
+        // (< 2^30 words: run_gemm's fits32)
+        const uint32_t c4n = (uint32_t)(cols / 4), lim4 = (uint32_t)(lim0 / 4), nq = (uint32_t)rows * c4n;
+        const uint32_t nthr = gridDim.x * gridDim.y * blockDim.x;
+        const uint32_t tid = (blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
+        const uint32_t dr = nthr / c4n, dc = nthr - dr * c4n;
+        uint32_t r = tid / c4n, c = tid - r * c4n;
+        for (uint32_t q = tid; q < nq; q += nthr) {
+            uint4 w = make_uint4(zw, zw, zw, zw);
+            if (c < lim4) {
+                const float4 v = *reinterpret_cast<const float4 *>(in0 + (int64_t)r * istride + 4 * c);
+                bool ok0 = true, ok1 = true, ok2 = true, ok3 = true;
+                w = make_uint4(word(v.x, ok0), word(v.y, ok1), word(v.z, ok2), word(v.w, ok3));
+                if (!(ok0 && ok1 && ok2 && ok3)) {
+                    fb_rows(p, (int64_t)r * orows, ((int64_t)r + 1) * orows);
+                    bad = true;
                 }
-                st4(o + i, w);
             }
-        } else {
+            st4((int64_t)r * cols + 4 * c, w);
+            c += dc;
+            r += dr;
+            if (c >= c4n) {
+                c -= c4n;
+                ++r;
+            }
+        }
+    } else {
+        for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) {
+            const float *in = p.conv ? p.X + (r * p.Cin + p.cbase) * hw : p.A + r * p.lda;
+            const int64_t lim = p.conv ? cols : p.K;
+            const int64_t o = r * cols;
+            bool badr = false;
             for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cols;
                  i += (int64_t)gridDim.x * blockDim.x) {
                 bool ok = true;
                 st1(o + i, (i < lim) ? word(in[i], ok) : zw);
                 badr |= !ok;
             }
+            if (badr) fb_rows(p, r * orows, (r + 1) * orows);
+            bad |= badr;
         }
-        if (badr) fb_rows(p, r * orows, (r + 1) * orows);
-        bad |= badr;
     }
     if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(p.flag, fb_bits(p, biasbad));
     if (__syncthreads_or(win ? 0 : 1) && threadIdx.x == 0) atomicOr(p.flag, 4u);  // gemm_tt16_kernel's window (A)

@@ -192,3 +192,56 @@ def test_flag_only_workspace_runs_valu_form():
     assert flag == 0
     ref, S = _conv_ref(x, w, bA, bW, bR, _tab(), FL, 1, 1, 1, 1)
     _close(_nhwc(y), ref, S)
+
+
+def test_flag_arena_is_clean_after_a_fallback():
+    """The flag word and the unit marks live in the library's per-stream flag arena, which the
+    gated exact kernel leaves zero (csrc/fp8approx.hip: flag_arena, arena_release): a flagged
+    launch, then clean launches of other shapes on the same stream report flag 0 and run no
+    exact unit, then a flagged launch again reports its flag -- each result against the oracle."""
+    from fp8_quantization_amd import _lib
+    rng = np.random.default_rng(21)
+    bA, bR = 10, 7
+    xb = _grid(rng, (2, 16, 9, 9), bA, zero_frac=0.3)
+    xb[1, 3, 4, 4] = 0.3  # off the grid: marks the second image's row units
+    wb = _grid(rng, (32, 16, 3, 3), 15)
+    bWb = np.full(32, 15, np.int32)
+    xg = _grid(rng, (3, 16, 13, 13), bA, zero_frac=0.45, lo_code=1)
+    bWg = rng.integers(14, 17, size=40).astype(np.int32)
+    wg = _grid(rng, (40, 16, 3, 3), bWg[:, None, None, None], lo_code=2)
+    for rep in range(2):
+        _lib.fallback_stats(reset=True)
+        y, flag = _conv_raw(xb, wb, bA, bWb, bR, _tab(), FL, 1, 1, 1, 1)
+        assert flag != 0 and _lib.fallback_stats()["exact_units"] > 0
+        ref, S = _conv_ref(xb, wb, bA, bWb, bR, _tab(), FL, 1, 1, 1, 1)
+        _close(_nhwc(y), ref, S, "flagged")
+        _lib.fallback_stats(reset=True)
+        for _ in range(2):
+            y, flag = _conv_raw(xg, wg, bA, bWg, bR, _tab(), FL, 1, 1, 1, 1)
+            assert flag == 0, f"stale flag after a fallback (repeat {rep})"
+            ref, S = _conv_ref(xg, wg, bA, bWg, bR, _tab(), FL, 1, 1, 1, 1)
+            _close(_nhwc(y), ref, S, "clean")
+        st = _lib.fallback_stats()
+        assert st["exact_launches"] == 0 and st["exact_units"] == 0, st
+
+
+@pytest.mark.parametrize("shape", [(300, 768, 272), (97, 100, 300), (1030, 64, 264), (3, 1024, 400)])
+def test_matmul_dense_rows_predecode(shape):
+    """A with lda = K % 4 == 0: the A pre-pass's 16-byte form, its (row, chunk) grid flattened over
+    the launch; K not a multiple of the 64-wide K-step leaves zero words at the row ends.  N > 192:
+    more than 3 column tiles, so the pre-pass runs (xm_af32)."""
+    Mr, K, N = shape
+    rng = np.random.default_rng(Mr * 7 + K)
+    bA, bR = 10, 7
+    A = _grid(rng, (Mr, K), bA, zero_frac=0.4)
+    bB = rng.integers(14, 17, size=N).astype(np.int32)
+    W = _grid(rng, (N, K), bB[:, None])
+    C, flag = _matmul_raw(A, K, W, 1, K, Mr, N, K, bA, bB, bR, _tab(), FL)
+    assert flag == 0
+    ref, S = orc.matmul(A, W.T, E, M, bA, bB, bR, _tab(), FL, with_abs=True)
+    _close(C, ref, S, str(shape))
+    A[Mr // 2, K - 1] = 0.3  # off the grid: only that row's unit falls back
+    C, flag = _matmul_raw(A, K, W, 1, K, Mr, N, K, bA, bB, bR, _tab(), FL)
+    assert flag != 0
+    ref, S = orc.matmul(A, W.T, E, M, bA, bB, bR, _tab(), FL, with_abs=True)
+    _close(C, ref, S, str(shape) + " flagged")

@@ -288,3 +288,30 @@ def test_staged_form_full_model_bit_identical(fmt):
     assert np.isfinite(y1).all()
     assert np.array_equal(y0.view(np.uint32), y1.view(np.uint32))
     assert np.array_equal(y0.view(np.uint32), y2.view(np.uint32))
+
+
+def test_gate_arena_is_clean_after_a_fallback():
+    """The depthwise gate word is the stream's flag arena (fp8approx.hip: flag_arena), left zero by
+    the gated direct kernel: a flagged launch, then a clean one reports gate 0 and runs no
+    fallback launch, then a flagged one again reports its gate."""
+    from fp8_quantization_amd import _lib
+    rng = np.random.default_rng(5)
+    bA, bR = 10, 9
+    tab = gio.load("g2_matmul.npz")["E4M3_table_nocomp"]
+    xb = _grid(rng, (2, 8, 9, 9), bA, zero_frac=0.3)
+    xb[1, 2, 4, 4] = 0.3
+    bW = np.full(8, 13, np.int32)
+    w = _grid(rng, (8, 1, 3, 3), 13)
+    xg = _grid(rng, (2, 8, 9, 9), bA, zero_frac=0.3)
+    cols = torch.nn.functional.unfold(torch.from_numpy(xg), (3, 3), padding=1).transpose(1, 2).reshape(-1, 72).numpy()
+    for _ in range(2):
+        _, gate = _dw_raw(xb, w, bA, bW, bR, tab, FL, 1, 1)
+        assert gate != 0
+        _lib.fallback_stats(reset=True)
+        y, gate = _dw_raw(xg, w, bA, bW, bR, tab, FL, 1, 1)
+        assert gate == 0 and _lib.fallback_stats()["tb_launches"] == 0
+        for c in range(8):
+            ref, S = orc.matmul(cols[:, c * 9:(c + 1) * 9], w[c].reshape(9, 1), E, M, bA, bW[c:c + 1], bR, tab,
+                                FL | orc.TB, with_abs=True)
+            got = y[:, c].reshape(-1, 1).astype(np.float64)
+            assert np.all(np.abs(got - ref) <= gio.sum_tolerance(S.astype(np.float64))), f"channel {c}"
