@@ -95,6 +95,9 @@ def parse(argv=None):
     ap.add_argument("--cal-batch", type=int, default=64)
     ap.add_argument("--with-comp", action="store_true", help="withComp=True (E4M3: all-zero error table)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="time eager forwards (default on a GPU: the forward captured once into a HIP graph, each "
+                         "timed step one replay of it -- every kernel still runs; the launch gaps go)")
     ap.add_argument("--cpu-columns", type=int, default=48, help="output columns per layer in the CPU sample")
     ap.add_argument("--arch", default="resnet18", choices=sorted(ARCH_NAMES),
                     help="resnet18 = the headline (BASELINE configs[1]); the others are BASELINE configs 3-5 "
@@ -254,6 +257,45 @@ def cpu_baseline(shapes, table, cols):
                                       ratio=full / (cache[(Mi, K)] * ncol)))
 
 
+def capture_forward(model, x, warm, sync):
+    """The forward captured into one HIP graph (torch.cuda.CUDAGraph over hipGraph) on a side
+    stream warmed by `warm` eager forwards first (the library's per-stream flag arena and torch's
+    allocator settle there); returns (info, replay) where replay() runs the captured forward and
+    all-gathers its logits.  The replayed logits must equal an eager forward's bit for bit, else
+    (or if capture fails) info["captured"] is False and the caller times eager forwards."""
+    from fp8_quantization_amd.distributed import gather_logits
+    info = {"captured": False}
+    try:
+        gs = torch.cuda.Stream()
+        gs.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(gs):
+            for _ in range(max(1, warm)):
+                model(x)
+        torch.cuda.current_stream().wait_stream(gs)
+        sync()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=gs):
+            out = model(x)
+        ref = model(x)
+        graph.replay()
+        sync()
+        same = bool(torch.equal(ref.view(torch.int32), out.view(torch.int32)))
+        info.update(captured=same, replay_matches_eager_bitwise=same)
+        if not same:
+            return info, None
+    except Exception as e:  # noqa: BLE001 -- report and time eager forwards instead
+        info["error"] = f"{type(e).__name__}: {e}"[:300]
+        sync()
+        return info, None
+
+    def replay():
+        graph.replay()
+        return gather_logits(out)
+    info["note"] = ("timed steps = replays of the captured forward (every kernel of the forward runs each step); "
+                    "roofline / fallback / path figures from the same number of eager steps after them")
+    return info, replay
+
+
 def run(args, dev, rank=0, world=1):
     """The benchmark on an initialised process group (world > 1) or alone; returns rank 0's
     JSON dict (None on the other ranks).  On a CPU device (the gloo rehearsal in
@@ -299,9 +341,10 @@ def run(args, dev, rank=0, world=1):
     def step():
         return gather_logits(model(x))  # one RCCL all-gather of logits per step (N > 1)
 
-    with torch.no_grad():
-        for _ in range(args.warmup):
-            step()
+    def instrumented(fn):
+        """K steps of fn with the per-op HIP events (approx_ops._PROFILE), the product kernels'
+        HIP events (fp8a_kernel_timing) and the fallback / path counters on; returns the wall
+        time between the two barrier + synchronize brackets and the op events."""
         sync()
         if world > 1:
             dist.barrier()
@@ -314,14 +357,40 @@ def run(args, dev, rank=0, world=1):
             fa._lib.kernel_timing(True)  # HIP events around each GEMM's product kernel (fp8a_kernel_timing)
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            step()
+            fn()
         sync()
         if world > 1:
             dist.barrier()
-        elapsed = time.perf_counter() - t0
-        prof, am._PROFILE = am._PROFILE or [], None
+        el = time.perf_counter() - t0
+        pr, am._PROFILE = am._PROFILE or [], None
         if cuda:
             fa._lib.kernel_timing(False)
+        return el, pr
+
+    graph_info = None
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        if cuda and not args.no_graph:
+            graph_info, replay = capture_forward(model, x, args.warmup, sync)
+        if graph_info and graph_info.get("captured"):
+            # the timed steps replay the captured forward; the per-kernel HIP events and counters come
+            # from the same number of eager steps right after (a replayed graph carries no host-side
+            # per-launch events)
+            sync()
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                replay()
+            sync()
+            if world > 1:
+                dist.barrier()
+            elapsed = time.perf_counter() - t0
+            eager_elapsed, prof = instrumented(step)
+            graph_info["eager_images_per_s"] = world * args.batch * args.steps / eager_elapsed
+        else:
+            elapsed, prof = instrumented(step)
     # how many launches / 64x64 output units of the timed steps left the fast path (a regression
     # there would otherwise be invisible in the line)
     fallback = fa._lib.fallback_stats() if cuda else None
@@ -462,6 +531,8 @@ def run(args, dev, rank=0, world=1):
             }
             res["dense_fp32_units"] = dict(dense_fb, note="timed steps only: dense launches with 64x64 units "
                                                           "recomputed in fp32 (blocks not exact in e4m3 / e5m2)")
+        if graph_info is not None:
+            res["hip_graph"] = graph_info
         if fallback is not None and not args.no_approx:
             res["fallback"] = dict(fallback, approx_launches=len(prof),
                                    note="timed steps only: exact_launches = launches whose gated exact kernel "

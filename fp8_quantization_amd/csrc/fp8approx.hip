@@ -210,19 +210,12 @@ __global__ __launch_bounds__(256) void gemm_exact_kernel(const GemmArgs p) {
     // Gated after a fast launch: nothing to do unless it flagged (uniform per grid; the grid is
     // capped, so the no-op case costs one small launch); then only the marked 64 x 64 units
     // (every unit with FB_ALL), one unit per block step: thread = (row, 16 columns).  The kernel
-    // ends the launch: it reports the flag word to the caller (flag_out) and leaves the flag
-    // arena zero for the next launch on the stream (arena_release).
+    // ends the launch: it reports the flag word to the caller (flag_out) and zeroes the flag
+    // arena's other slot (arena_clear: the previous launch's words)
+    arena_clear(p.arena_clr, p.arena_clr16);
     const uint32_t f = __hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (f == 0u) {  // no flag bit, so no unit mark either: only the pre-passes' extremes to clear
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
-            p.flag[1] = 0u;
-            p.flag[2] = 0u;
-            if (p.flag_out) *p.flag_out = 0u;
-        }
-        return;
-    }
+    if (p.flag_out && blockIdx.x == 0 && threadIdx.x == 0) *p.flag_out = f;
     if (f & FB_ANY) gemm_exact_units(p, f, fA, fR, tb);
-    arena_release(p.flag, f, p.flag_out, p.urow, p.urow ? (size_t)(p.nur + p.nuc + p.nur * p.nuc) : 0);
 }
 
 // The marked units of a flagged launch (gemm_exact_kernel); every thread returns here.
@@ -333,16 +326,16 @@ __global__ __launch_bounds__(256) void conv_tb_direct_kernel(const float *x, con
                                                              int dw, int groups, int64_t Ho, int64_t Wo, int E,
                                                              int Mw, const int32_t *bA, const int32_t *bW,
                                                              const int32_t *bR, TablePack tab, uint32_t flags,
-                                                             uint32_t *gate, uint32_t *gate_out, const float2 *ep,
-                                                             int ep_act, float ep_lo, float ep_hi, FqIn fq) {
+                                                             const uint32_t *gate, uint32_t *gate_out, uint4 *clr,
+                                                             uint32_t clr16, const float2 *ep, int ep_act,
+                                                             float ep_lo, float ep_hi, FqIn fq) {
     // after conv_tb_fast_kernel: run only if it flagged inputs outside its exactness window.  The
-    // gate word is the stream's flag arena (flag_arena): this kernel reports it to the caller's
-    // workspace word (gate_out) and leaves it zero (arena_release)
+    // gate word is a slot of the stream's flag arena (flag_arena): this kernel reports it to the
+    // caller's workspace word (gate_out) and zeroes the arena's other slot (arena_clear)
+    arena_clear(clr, clr16);
     const uint32_t gv = gate != nullptr ? __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 1u;
-    if (gv == 0u) {
-        if (gate_out != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *gate_out = 0u;
-        return;
-    }
+    if (gate_out != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *gate_out = gv;
+    if (gv == 0u) return;
     if (gate != nullptr && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_fallback[3], 1ull);
     const int64_t total = Bn * Cout * Ho * Wo;
     const int64_t cpg = Cin / groups;   // input channels per group
@@ -372,7 +365,6 @@ __global__ __launch_bounds__(256) void conv_tb_direct_kernel(const float *x, con
                 }
         y[idx] = epi(ep, ep_act, ep_lo, ep_hi, co, s + part);
     }
-    if (gate != nullptr) arena_release(gate, gv, gate_out, nullptr, 0);
 }
 
 // Single-output-channel groups (depthwise) with the tensor-bias semantics, fast form.
@@ -906,40 +898,59 @@ static bool xm_af32(const GemmArgs &a) {
     return a.A != nullptr && a.M * a.lda * 4 < (1ll << 32) && a.lda >= a.K;
 }
 
-// The fallback-flag arena of a (device, stream): the flag word, the pre-passes' extremes, the
-// gated kernel's block counter and the per-unit marks of the launches on that stream.  Zeroed once
-// when (re)allocated; every launch's last kernel leaves it zero (arena_release), so launches need
-// no fill.  A launch that stops early (a launch error) leaves marks behind: the next launch on the
-// stream then reruns marked units exactly -- the same bits, more time.  Grows by reallocation
-// (after the stream drains).
+// The fallback-flag arena of a (device, stream): two slots, used by the launches on the stream in
+// turn, each holding one launch's flag word, the pre-passes' extremes and its per-unit marks.  A
+// launch finds its slot zero; its last kernel (the gated exact / literal kernel) zeroes the other
+// slot's words, which the previous launch used (arena_clear) -- so launches need no fill, and the
+// clearing races nothing.  Zeroed once when (re)allocated; grows by reallocation after the stream
+// drains.  A launch that stops before its last kernel (a launch error) leaves its successor a slot
+// with stale words: that launch then reruns the marked units exactly -- the same bits, more time.
 struct FlagArena {
     uint32_t *p = nullptr;
-    size_t bytes = 0;
+    size_t slot = 0;       // bytes per slot
+    int cur = 0;           // the slot the next launch uses
+    size_t dirty[2] = {0, 0};
 };
-static uint32_t *flag_arena(hipStream_t s, size_t need) {
+struct ArenaLease {
+    uint32_t *mine = nullptr;  // this launch's slot (zero)
+    uint4 *clr = nullptr;      // the other slot, and its 16-byte words the last kernel zeroes
+    uint32_t clr16 = 0;
+};
+static bool flag_arena(hipStream_t s, size_t need, ArenaLease &l) {
     static std::mutex mu;
     static std::map<std::pair<int, uintptr_t>, FlagArena> arenas;
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    need = (need + 255) & ~(size_t)255;
     std::lock_guard<std::mutex> lock(mu);
     FlagArena &ar = arenas[{dev, (uintptr_t)s}];
-    if (ar.bytes >= need) return ar.p;
-    const size_t nb = std::max(need, std::max(2 * ar.bytes, (size_t)65536));
-    if (ar.p) {
-        if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
-        (void)hipFree(ar.p);
-        ar = FlagArena{};
+    if (ar.slot < need) {
+        const size_t slot = std::max(need, std::max(2 * ar.slot, (size_t)65536));
+        if (ar.p) {
+            if (hipStreamSynchronize(s) != hipSuccess) return false;
+            (void)hipFree(ar.p);
+            ar = FlagArena{};
+        }
+        void *p = nullptr;
+        if (hipMalloc(&p, 2 * slot) != hipSuccess) return false;
+        if (hipMemsetAsync(p, 0, 2 * slot, s) != hipSuccess) {
+            (void)hipFree(p);
+            return false;
+        }
+        ar.p = (uint32_t *)p;
+        ar.slot = slot;
     }
-    void *p = nullptr;
-    if (hipMalloc(&p, nb) != hipSuccess) return nullptr;
-    if (hipMemsetAsync(p, 0, nb, s) != hipSuccess) {
-        (void)hipFree(p);
-        return nullptr;
-    }
-    ar.p = (uint32_t *)p;
-    ar.bytes = nb;
-    return ar.p;
+    const int other = 1 - ar.cur;
+    l.mine = ar.p + (size_t)ar.cur * (ar.slot / 4);
+    l.clr = reinterpret_cast<uint4 *>(ar.p + (size_t)other * (ar.slot / 4));
+    l.clr16 = (uint32_t)(ar.dirty[other] / 16);
+    ar.dirty[other] = 0;
+    ar.dirty[ar.cur] = need;
+    ar.cur = other;
+    return true;
 }
+// grid blocks of 256 threads that clear a lease's other slot in about four 16-byte stores each
+static unsigned clear_blocks(const ArenaLease &l) { return (l.clr16 + 1023) / 1024; }
 
 // Fast tiled kernel + gated exact kernel (int-bias path), or the exact kernel alone (tb path).
 static int run_qamaa(GemmArgs &a, hipStream_t s);
@@ -982,9 +993,12 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     // receives the final flag word, and its head stays reserved (the layout of the size queries)
     static const bool no_units = getenv("FP8A_NO_UNITS") != nullptr;  // diagnostics: whole-launch fallbacks
     const size_t head = ws_bytes >= head_bytes(a.M, a.N) ? head_bytes(a.M, a.N) : FLAG_BYTES;
-    a.flag = flag_arena(s, head_bytes(a.M, a.N));
-    if (a.flag == nullptr) return hip_check("fp8a flag arena");
+    ArenaLease lease;
+    if (!flag_arena(s, head_bytes(a.M, a.N), lease)) return hip_check("fp8a flag arena");
+    a.flag = lease.mine;
     a.flag_out = (uint32_t *)ws;
+    a.arena_clr = lease.clr;
+    a.arena_clr16 = lease.clr16;
     a.nur = (a.M + 63) / 64;
     a.nuc = (a.N + 63) / 64;
     a.urow = no_units ? nullptr : (uint8_t *)a.flag + FLAG_BYTES;
@@ -1089,7 +1103,7 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
         rc = hip_check("fp8a split-K reduce launch");
         if (rc) return rc;
     }
-    const unsigned ublocks = (unsigned)std::min<int64_t>(a.nur * a.nuc, 4096);
+    const unsigned ublocks = std::max((unsigned)std::min<int64_t>(a.nur * a.nuc, 4096), clear_blocks(lease));
     gemm_exact_kernel<<<ublocks, 256, 0, s>>>(a);
     rc = hip_check("fp8a gated exact gemm launch");
     static const bool dbg = getenv("FP8A_DEBUG_FLAGS") != nullptr;  // diagnostics: the flag word per launch
@@ -1731,6 +1745,7 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
         if (rc) return rc;
         const int64_t total = Bn * Cout * Ho * Wo;
         uint32_t *gate = nullptr;
+        ArenaLease lease;  // (gate: a slot of the stream's flag arena, flag_arena)
         // fast form: needs s2n on and golden_clip_OF off (else every launch would fall back)
         const bool fast_ok = (flags & F_S2N) && !(flags & F_GCLIP) && workspace != nullptr &&
                              workspace_bytes >= FLAG_BYTES && Cout <= 65535 && Bn <= 65535;
@@ -1747,8 +1762,8 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
             if (rc) return rc;
         }
         if (tbx_ok) {
-            gate = flag_arena(s, FLAG_BYTES);
-            if (gate == nullptr) return hip_check("fp8a flag arena");
+            if (!flag_arena(s, FLAG_BYTES, lease)) return hip_check("fp8a flag arena");
+            gate = lease.mine;
             // the input's table-form words from the producing launch (fp8a_conv2d_chain, next_form 1:
             // header + [Bn][Cin][H][W] words of fq_in(x)); the pre-pass then runs gated on its header
             const bool use_img = in_img != nullptr && fq.mx != nullptr;
@@ -1810,8 +1825,8 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
             if (rc) return rc;
             }
         } else if (fast_ok) {
-            gate = flag_arena(s, FLAG_BYTES);
-            if (gate == nullptr) return hip_check("fp8a flag arena");
+            if (!flag_arena(s, FLAG_BYTES, lease)) return hip_check("fp8a flag arena");
+            gate = lease.mine;
             dim3 grid((unsigned)((Ho * Wo + 255) / 256), (unsigned)Cout, (unsigned)Bn);
             conv_tb_fast_kernel<<<grid, 256, 0, s>>>(x, w, y, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups,
                                                      Ho, Wo, Mw, bA, bW, bR, tp, flags | F_TB, gate, ep, act, act_lo,
@@ -1821,13 +1836,13 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
         }
         const unsigned eb = (unsigned)(fast_ok ? std::min<int64_t>((total + 255) / 256, 4096) : (total + 255) / 256);
         if (fast_ok) {  // gated, grid-capped: a no-op launch unless the fast kernel flagged
-            conv_tb_direct_kernel<true><<<eb, 256, 0, s>>>(x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw,
-                                                    groups, Ho, Wo, E, Mw, bA, bW, bR, tp, flags | F_TB, gate,
-                                                    (uint32_t *)workspace, ep, act, act_lo, act_hi, fq);
+            conv_tb_direct_kernel<true><<<std::max(eb, clear_blocks(lease)), 256, 0, s>>>(
+                x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups, Ho, Wo, E, Mw, bA, bW, bR, tp,
+                flags | F_TB, gate, (uint32_t *)workspace, lease.clr, lease.clr16, ep, act, act_lo, act_hi, fq);
         } else {
             conv_tb_direct_kernel<true><<<eb, 256, 0, s>>>(x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw,
                                                      groups, Ho, Wo, E, Mw, bA, bW, bR, tp, flags | F_TB, nullptr,
-                                                     nullptr, ep, act, act_lo, act_hi, FqIn{});
+                                                     nullptr, nullptr, 0u, ep, act, act_lo, act_hi, FqIn{});
         }
         return hip_check("fp8a_conv2d (tensor-bias groups)");
     }
@@ -1872,6 +1887,7 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
                              sh == sw && (sw == 1 || sw == 2) && items < (1ll << 31) && Ho * Wo < (1ll << 31) &&
                              workspace != nullptr && workspace_bytes >= FLAG_BYTES + awb + (size_t)(Cout * kh * kw) * 8;
         uint32_t *gate = nullptr;
+        ArenaLease lease;  // (gate: a slot of the stream's flag arena, flag_arena)
         // the staged form (conv_v5ds_kernel: both pre-passes fused): depthwise 3 x 3, dilation 1
         DwArgs d{};
         size_t lds = 0;
@@ -1884,8 +1900,8 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
                               return lds <= 65536;
                           }();
         if (v5ds) {
-            gate = flag_arena(s, FLAG_BYTES);
-            if (gate == nullptr) return hip_check("fp8a flag arena");
+            if (!flag_arena(s, FLAG_BYTES, lease)) return hip_check("fp8a flag arena");
+            gate = lease.mine;
             const unsigned g = (unsigned)(((d.planes + d.PB - 1) / d.PB) * d.nb);
             // (it emits the next convolution's v5 words when fp8a_conv2d_chain asked for them, em.form 2)
             const EmitW emv = em.w && em.form == 2 ? em : EmitW{};
@@ -1902,8 +1918,8 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
         } else if (v5dw_ok) {
             if (em.w && hipMemsetAsync(em.invalid, 1, sizeof(uint32_t), s) != hipSuccess)  // (no emission here)
                 return hip_check("fp8a word image header");
-            gate = flag_arena(s, FLAG_BYTES);
-            if (gate == nullptr) return hip_check("fp8a flag arena");
+            if (!flag_arena(s, FLAG_BYTES, lease)) return hip_check("fp8a flag arena");
+            gate = lease.mine;
             uint32_t *aw = (uint32_t *)((char *)workspace + FLAG_BYTES);
             uint2 *bwd = (uint2 *)((char *)workspace + FLAG_BYTES + awb);
             // (the input quantizer applied here, its bias written for the kernels after: bA = fqi)
@@ -1936,9 +1952,10 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
             }
         }
         // (x unquantized when fq is set: the literal kernel applies fq to every loaded value)
-        conv_tb_direct_kernel<false><<<(unsigned)std::min<int64_t>((total + 255) / 256, 16384), 256, 0, s>>>(
+        conv_tb_direct_kernel<false><<<std::max((unsigned)std::min<int64_t>((total + 255) / 256, 16384),
+                                                clear_blocks(lease)), 256, 0, s>>>(
             x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups, Ho, Wo, E, Mw, bA, bW, bR, tp, flags,
-            gate, gate ? (uint32_t *)workspace : nullptr, ep, act, act_lo, act_hi, fq);
+            gate, gate ? (uint32_t *)workspace : nullptr, lease.clr, lease.clr16, ep, act, act_lo, act_hi, fq);
         return hip_check("fp8a_conv2d (v5 depthwise, direct)");
     }
     for (int g = 0; g < groups; ++g) {

@@ -114,7 +114,7 @@ struct GemmArgs {
     int nchw;
     int64_t hw, ctot, coff;
     uint32_t *flag;  // device word: set by the fast kernel when the exact kernel must run (FB_* bits);
-                     // the library's flag arena (flag_arena, fp8approx.hip), zero between launches
+                     // a slot of the library's flag arena (flag_arena, fp8approx.hip), zero on entry
     // per-unit fallback marks (64 x 64 output units): urow[row unit] / ucol[column unit] for an
     // operand outside the fast path's window, utile[row unit * nuc + column unit] for a tile whose
     // terms left it; the gated exact kernel recomputes only the marked units.  nullptr (a
@@ -176,6 +176,8 @@ struct GemmArgs {
     const uint32_t *in_img; // the input's word image (header + words) a previous launch emitted, or nullptr
     TablePack tab;
     uint32_t *flag_out;  // the caller's workspace word that receives the launch's final flag word
+    uint4 *arena_clr;    // the flag arena's other slot, and its 16-byte words to zero (arena_clear)
+    uint32_t arena_clr16;
 };
 
 // Fallback flag word bits: FB_ANY = some output unit needs the exact kernel, FB_ALL = every
@@ -195,31 +197,13 @@ __device__ __forceinline__ uint32_t fb_bits(const GemmArgs &p, bool all = false)
     return (all || p.urow == nullptr) ? (FB_ANY | FB_ALL) : FB_ANY;
 }
 
-// The flag arena (fp8approx.hip: flag_arena) is zero between launches: the gated kernel that ends
-// a launch clears what the launch set.  A flagged launch is cleared by its LAST block to finish
-// (the arena's word 3 counts finished blocks; every block's reads of the flag word and the marks
-// happen before its increment): it reports the flag word to the caller (out), then zeroes the
-// `mark_bytes` of unit marks, the pre-passes' words 1-2, the counter and the flag word.  Every
-// thread of the block calls it.
-__device__ __forceinline__ void arena_release(uint32_t *arena, uint32_t f, uint32_t *out, uint8_t *marks,
-                                              size_t mark_bytes) {
-    bool last = false;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        last = atomicAdd(arena + 3, 1u) == gridDim.x - 1;
-    }
-    if (!__syncthreads_or(last ? 1 : 0)) return;
-    __threadfence();
-    uint32_t *mw = reinterpret_cast<uint32_t *>(marks);  // (the marks region is 256-byte aligned and sized)
-    for (size_t i = threadIdx.x; i < (mark_bytes + 3) / 4; i += blockDim.x) mw[i] = 0u;
-    if (threadIdx.x == 0) {
-        if (out) *out = f;
-        arena[1] = 0u;
-        arena[2] = 0u;
-        arena[3] = 0u;
-        arena[0] = 0u;
-    }
+// The flag arena (fp8approx.hip: flag_arena) has two slots per stream that launches use in turn:
+// a launch finds its slot zero, and its last (gated) kernel zeroes the OTHER slot -- the words the
+// previous launch left there, which nothing reads any more -- with every thread of its grid
+// (16-byte stores; no fill launch, no counter, no ordering against the launch's own reads).
+__device__ __forceinline__ void arena_clear(uint4 *clr, uint32_t n16) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += gridDim.x * blockDim.x)
+        clr[i] = make_uint4(0u, 0u, 0u, 0u);
 }
 
 // Mark the row units of output rows [m_lo, m_hi) / the column unit of column n / the units of

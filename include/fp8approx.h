@@ -229,7 +229,9 @@ int fp8a_terms(const float *A, int64_t lda, const float *B, int64_t sbk, int64_t
  * the reference does (approx_calculation.py:800-809), other groups the int-bias semantics.
  * workspace: device scratch of fp8a_conv2d_workspace_size() bytes (the off-grid flag word
  * and split-K partial sums; no im2col image: the GEMM gathers its operand rows from x).  A
- * smaller workspace that still holds the flag word runs without split-K.
+ * smaller workspace that still holds the flag word runs without split-K.  Its first word receives
+ * the launch's final flag word; the flags and unit marks themselves live in the library's
+ * per-stream flag arena (no fill per launch; the first call on a stream allocates it).
  */
 size_t fp8a_conv2d_workspace_size(int64_t Bn, int64_t Cin, int64_t H, int64_t W, int64_t Cout,
                                   int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw,
