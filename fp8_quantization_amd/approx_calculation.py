@@ -278,7 +278,8 @@ class ApproxLinearMixin(ApproxOpMixin):
             pq, pt = None, None
             if post is not None:
                 pq = post[4]
-                pt = (post[0].reshape(-1, weight.shape[0]),) + tuple(post[1:4]) + ((qt(pq) if pq is not None else None),)
+                res = post[0].reshape(-1, weight.shape[0]) if post[0] is not None else None
+                pt = (res,) + tuple(post[1:4]) + ((qt(pq) if pq is not None else None),)
             out, ib, ob = approx_matmul_block(
                 x.detach(), weight.detach().t(), E, M,
                 None if qin is not None else self._default_bias(self.get_acts_fp_bias(), E, x.device),

@@ -838,9 +838,13 @@ static bool tt_form(int Mw, uint32_t flags, const TablePack &tab) {
 // +23 % on the ResNet-18 layer set) and for K >= 256 (+2-9 %); on short K its per-tile prologue
 // (the frame shift's bias range, two barriers) outweighs the gain (MobileNetV2 E3M4 -3 %), and
 // gemm_tt_kernel<4, F7> runs.  FP8A_NO_TT16=1 keeps gemm_tt_kernel everywhere.
+// (option "tt16_mink": the smallest K of an unsigned-table launch on the f16 form; default 64 since
+// round 5: ResNet-50 E3M4 2,045 -> 2,082 images/s with its K = 64 / 128 / 147 launches on the f16
+// form, profiles/r05_tt16_mink/ -- round 3's tt16 lost 3 % there)
+static int g_opt_tt16_mink = getenv("FP8A_TT16_MINK") ? std::max(0, atoi(getenv("FP8A_TT16_MINK"))) : 64;
 static bool tt16_form(int Mw, bool f7, int64_t K) {
     static const bool no_tt16 = getenv("FP8A_NO_TT16") != nullptr;
-    return !no_tt16 && Mw == 4 && (f7 || K >= 256);
+    return !no_tt16 && Mw == 4 && (f7 || K >= g_opt_tt16_mink);
 }
 
 static bool no_mx() {
@@ -1074,8 +1078,9 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     // kernels do not (store_tile<false>: the emission code cost gemm_tt16_kernel 32 SGPR spills and a
     // 38 % slower E3M4 layer set, round 4 -> 5), so their unsplit launch marks the image invalid
     // instead (emit_prep_kernel set the header valid before this launch) and the consumer's gated
-    // pre-pass re-decodes its input from y
-    if (a.em.w != nullptr && (a.em.form == 2 || (a.aw && a.wfmt != 0 && a.splits == 1))) {
+    // pre-pass re-decodes its input from y (likewise under a GELU tail, which the emitting store
+    // compiles out)
+    if (a.em.w != nullptr && (a.em.form == 2 || (a.aw && a.wfmt != 0 && a.splits == 1) || a.post_act == 2)) {
         if (hipMemsetAsync(a.em.invalid, 1, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a word image header");
         a.em.w = nullptr;
     }
@@ -1402,6 +1407,11 @@ int fp8a_set_option(const char *name, int value) {
     if (strcmp(name, "af32_maxct") == 0) {
         const int old = g_opt_af32_maxct;
         g_opt_af32_maxct = std::max(0, value);
+        return old;
+    }
+    if (strcmp(name, "tt16_mink") == 0) {
+        const int old = g_opt_tt16_mink;
+        g_opt_tt16_mink = std::max(0, value);
         return old;
     }
     if (strcmp(name, "tbx_rw") == 0) {
@@ -2040,6 +2050,7 @@ int fp8a_conv2d_block(const float *x, const float *w, float *y, int64_t Bn, int6
                       int out_nbits, int out_mbits, int out_sign_bits, float *out_bias_out, int32_t *out_ibias_out,
                       void *workspace, size_t workspace_bytes, fp8a_stream_t stream) {
     hipStream_t s = (hipStream_t)stream;
+    if (post_act != 0 && post_act != 1) return fail(FP8A_EINVAL, "conv2d_block: post_act is 0 or 1");
     FqIn fin{}, fout{};
     if (in_maxval) {
         const int qE = in_nbits - in_sign_bits - in_mbits;
@@ -2150,6 +2161,7 @@ int fp8a_conv2d_chain(const float *x, const float *w, float *y, int64_t Bn, int6
                       void *in_image, void *out_image, int next_ph, int next_pw, const float *next_maxval,
                       int next_nbits, int next_mbits, int next_sign_bits, const int32_t *next_bR, int next_Mw,
                       int next_form, void *workspace, size_t workspace_bytes, fp8a_stream_t stream) {
+    if (post_act != 0 && post_act != 1) return fail(FP8A_EINVAL, "conv2d_chain: post_act is 0 or 1");
     hipStream_t s = (hipStream_t)stream;
     if ((in_image && ((uintptr_t)in_image & 255)) || (out_image && ((uintptr_t)out_image & 255)))
         return fail(FP8A_EINVAL, "word images must be 256-byte aligned");
@@ -2238,6 +2250,7 @@ int fp8a_matmul_block(const float *A, int64_t lda, const float *B, int64_t sbk, 
     hipStream_t s = (hipStream_t)stream;
     if (lda < K || ldc < N) return fail(FP8A_EINVAL, "leading dimension smaller than extent");
     if (flags & (F_TB | F_V5)) return fail(FP8A_EINVAL, "matmul_block: int-bias v9 path only");
+    if (post_act < 0 || post_act > 2) return fail(FP8A_EINVAL, "matmul_block: post_act is 0, 1 or 2");
     if (bn && (((uintptr_t)bn) & 7) != 0) return fail(FP8A_EINVAL, "bn parameters must be 8-byte aligned");
     if (res && (res == C || (((uintptr_t)res) & 15) != 0))
         return fail(FP8A_EINVAL, "the residual must be a 16-byte aligned tensor other than the output");

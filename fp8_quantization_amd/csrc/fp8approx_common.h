@@ -166,7 +166,7 @@ struct GemmArgs {
     float *fq_bias;
     int32_t *fq_ibias;
     // block-output epilogue (fp8a_conv2d_block): after BN / activation, y += res (same index as
-    // y), then the post clamp (post_act), then the block's output quantizer (post_fq)
+    // y), then the post clamp (post_act 1) or GELU (post_act 2), then the block's output quantizer (post_fq)
     const float *res;
     int post_act;
     float post_lo, post_hi;
@@ -229,23 +229,35 @@ __device__ __forceinline__ float post_bias(const GemmArgs &p) {
     return p.post_fq.mx ? fq_bias(*p.post_fq.mx, p.post_fq.E, p.post_fq.M) : 0.0f;
 }
 
+// nn.GELU() (approximate='none') in fp32 as ATen's GeluCUDAKernelImpl evaluates it:
+// x * 0.5 * (1 + erf(x * M_SQRT1_2)), left to right, the same device erff (ocml)
+__device__ __forceinline__ float gelu_erf(float x) {
+    return x * 0.5f * (1.0f + erff(x * (float)M_SQRT1_2));
+}
+
+// GELU = false compiles the GELU tail out (the word-emitting store of gemm_f8mx_kernel, whose
+// registers are at its occupancy budget; the host never pairs GELU with emission).
+template <bool GELU = true>
 __device__ __forceinline__ float post_tail(const GemmArgs &p, float v, float pb) {
-    if (p.post_act) v = fminf(fmaxf(v, p.post_lo), p.post_hi);
+    if (p.post_act == 1) v = fminf(fmaxf(v, p.post_lo), p.post_hi);
+    else if (GELU && p.post_act == 2) v = gelu_erf(v);
     if (p.post_fq.mx) v = fq_apply(v, *p.post_fq.mx, pb, p.post_fq.M, p.post_fq.S);
     return v;
 }
 
+template <bool GELU = true>
 __device__ __forceinline__ float post1(const GemmArgs &p, int64_t o, float v, float pb) {
     if (p.res) v += p.res[o];
-    return post_tail(p, v, pb);
+    return post_tail<GELU>(p, v, pb);
 }
 
+template <bool GELU = true>
 __device__ __forceinline__ float4 post4(const GemmArgs &p, int64_t o, float4 v, float pb) {
     if (p.res) {
         const float4 r = *reinterpret_cast<const float4 *>(p.res + o);
         v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
     }
-    return make_float4(post_tail(p, v.x, pb), post_tail(p, v.y, pb), post_tail(p, v.z, pb), post_tail(p, v.w, pb));
+    return make_float4(post_tail<GELU>(p, v.x, pb), post_tail<GELU>(p, v.y, pb), post_tail<GELU>(p, v.z, pb), post_tail<GELU>(p, v.w, pb));
 }
 
 // y = x * scale + shift with scale = gamma * invstd, shift = beta - mean * scale (ATen's eval
@@ -394,7 +406,8 @@ __device__ __forceinline__ bool stage_decode(float x, int M, uint32_t emn, bool 
 // epilogue when unsplit.
 // EMIT = false compiles the word-image emission out (gemm_f8mx_kernel's non-emitting instances:
 // the emission code alone pushed that kernel past its 80-VGPR budget).
-template <bool EMIT = true>
+// GELU = false: the GELU tail compiled out as well (gemm_f8mx_kernel's emitting instances).
+template <bool EMIT = true, bool GELU = true>
 __device__ __forceinline__ void store_tile(const GemmArgs &p, int64_t split, int64_t m0, int64_t n0, int ty, int tx,
                                            float (&acc)[TM][TN]) {
     const bool partial = p.splits > 1;
@@ -417,13 +430,13 @@ __device__ __forceinline__ void store_tile(const GemmArgs &p, int64_t split, int
     uint32_t sehi = 0;
     auto fin1 = [&](int64_t o, float v) {
         if (partial) return v;
-        v = post1(q, o, v, pb);
+        v = post1<GELU>(q, o, v, pb);
         if (emit) emit1(q, ec, o, v, sehi);
         return v;
     };
     auto fin4 = [&](int64_t o, float4 v) {
         if (partial) return v;
-        v = post4(q, o, v, pb);
+        v = post4<GELU>(q, o, v, pb);
         if (emit) emit4(q, ec, o, v, sehi);
         return v;
     };

@@ -857,7 +857,7 @@ __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j) acc[i][j] = ct[(64 * sub + ety * TM + i) * CP + cb * TN + j];
-        store_tile<EMIT>(p, split, m0 + SR * h + 64 * sub, n0, ety, cb, acc);
+        store_tile<EMIT, !EMIT>(p, split, m0 + SR * h + 64 * sub, n0, ety, cb, acc);  // (GELU tails: run_gemm never emits)
     }
     FP8A_CLK_END
 }

@@ -307,13 +307,14 @@ def fused_block_tail(block, features, x, residual_fn, clamp, in_image=None, next
     return (h, img) if with_image else h
 
 
-def fused_linear_tail(block, dense, x, residual, dropout=None):
+def fused_linear_tail(block, dense, x, residual, dropout=None, gelu=False):
     """block.quantize_activations(dropout(dense(x)) + residual) as one launch of dense's fused
     linear (fp8a_matmul_block), for the ViT blocks (vit_quantized_approx.py:137-156, 256-262):
     same conditions as fused_block_tail (per-tensor FPQuantizer in the fixed-range state, or
     activation quantization off) plus an inactive dropout.  Returns None when the tail must run
     unfused.  Same result bit for bit as the reference's order (product, + bias, + residual,
-    quantize)."""
+    quantize).  residual None with gelu: block.quantize_activations(gelu(dense(x))), the MLP's
+    first half (vit_quantized_approx.py:117-135; post_act 2 of fp8a_matmul_block)."""
     from .quantization.fp8_quantizer import FPQuantizer
     from .quantization.quantization_manager import Qstates
     if not FUSE_BLOCK or not hasattr(dense, "tail_ok") or not dense.tail_ok():
@@ -327,8 +328,9 @@ def fused_linear_tail(block, dense, x, residual, dropout=None):
         if getattr(mgr, "state", None) != Qstates.fix_ranges or not isinstance(q, FPQuantizer) \
                 or q.maxval.numel() != 1:
             return None
-    if residual.shape[:-1] != x.shape[:-1] or residual.shape[-1] != dense.out_features:
-        return None
-    if residual.dtype != torch.float32 or not residual.is_contiguous() or residual.data_ptr() % 16:
-        return None  # fp8a_matmul_block takes a dense, 16-byte aligned float32 residual
-    return dense(x, post=(residual, 0, 0.0, 0.0, q))
+    if residual is not None:
+        if residual.shape[:-1] != x.shape[:-1] or residual.shape[-1] != dense.out_features:
+            return None
+        if residual.dtype != torch.float32 or not residual.is_contiguous() or residual.data_ptr() % 16:
+            return None  # fp8a_matmul_block takes a dense, 16-byte aligned float32 residual
+    return dense(x, post=(residual, 2 if gelu else 0, 0.0, 0.0, q))

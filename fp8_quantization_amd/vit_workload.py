@@ -236,6 +236,11 @@ class QuantizedViTImmediate(QuantizedActivation):
         self.intermediate_act_fn = orig.intermediate_act_fn
 
     def forward(self, h):
+        act = self.intermediate_act_fn
+        if isinstance(act, nn.GELU) and act.approximate == "none":  # dense + GELU + quantize: one launch
+            fused = fused_linear_tail(self, self.dense, h, None, gelu=True)
+            if fused is not None:
+                return fused
         return self.quantize_activations(self.intermediate_act_fn(self.dense(h)))
 
 

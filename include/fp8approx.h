@@ -100,7 +100,9 @@ int fp8a_kernel_time(double *out, int reset);
  * with both word pre-passes fused (0: the pre-passes + the word-form kernel; same bits);
  * "xm_ncg" (default 0 = by N; FP8A_XM_NCG) -- gemm_f8mx_kernel's tile width forced to 16 x 1 / 2
  * / 4 columns; "af32_maxct" (default 3; FP8A_AF32_MAXCT) -- the most column tiles for which a 1x1
- * conv / matrix A is decoded inside gemm_f8mx_kernel instead of by its pre-pass (0 = never).
+ * conv / matrix A is decoded inside gemm_f8mx_kernel instead of by its pre-pass (0 = never);
+ * "tt16_mink" (default 64; FP8A_TT16_MINK) -- the smallest K of an E3M4 launch (unsigned error
+ * table) on the packed-f16 tile-table kernel (shorter K: the f32 form).
  * All of these change the schedule only: the outputs are bit-identical.  Returns the previous value, or FP8A_EINVAL
  * for an unknown name.  Not synchronised with launches in flight on other threads.
  */
@@ -286,7 +288,8 @@ int fp8a_conv2d_qin(const float *x, const float *w, float *y, int64_t Bn, int64_
  * block's activation quantizer; mobilenet_v2_quantized_approx.py:11-23: quantize(x + conv(x))):
  *   y = fq_out(clamp(bn_act(conv(fq_in(x))) + res, post_lo, post_hi))
  * in_maxval NULL: x is already quantized and bA is used (else as fp8a_conv2d_qin).  res: NULL or
- * a 16-byte aligned tensor of y's shape (not y itself).  post_act 0: no clamp.  out_maxval NULL:
+ * a 16-byte aligned tensor of y's shape (not y itself).  post_act 0: no clamp, 1: the clamp
+ * (anything else: FP8A_EINVAL).  out_maxval NULL:
  * no output quantizer; else its bias is written to out_bias_out / out_ibias_out.  Not for
  * single-output-channel groups (EINVAL).  workspace: fp8a_conv2d_block_workspace_size() bytes.
  */
@@ -371,7 +374,9 @@ int fp8a_conv2d_chain(const float *x, const float *w, float *y, int64_t Bn, int6
  * by that per-tensor FP8 quantizer inside the operand pre-decode where the E4M3 matrix-core
  * path runs (else by one pass into the workspace) and its bias is written to in_bias_out /
  * in_ibias_out.  res: NULL or a 16-byte aligned [M][ldc] tensor (not C).  post / out_* as
- * fp8a_conv2d_block.  int-bias v9 path only (no TB / V5 flags).
+ * fp8a_conv2d_block, plus post_act 2: GELU (nn.GELU(), erf form, as ATen evaluates it in fp32)
+ * in place of the clamp -- vit_quantized_approx.py:117-135's dense, GELU, quantize in one launch.
+ * int-bias v9 path only (no TB / V5 flags).
  * workspace: fp8a_matmul_block_workspace_size() bytes.
  */
 size_t fp8a_matmul_block_workspace_size(int64_t M, int64_t N, int64_t K);

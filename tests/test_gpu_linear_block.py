@@ -110,3 +110,54 @@ def test_linear_operator_fixed_range_forward(version):
         wq, b = m.get_params()
         ref = m.approx_multiply(xq, wq.t(), m.get_acts_fp_bias(), m.get_weights_fp_bias(), m.get_res_fp_bias()) + b
     assert np.array_equal(_bits(got), _bits(ref))
+
+
+GELU_CASES = [  # (M rows, K, N, E, M, with output quantizer)
+    (300, 192, 160, 4, 3, True),
+    (257, 768, 320, 4, 3, False),
+    (64, 4096, 128, 4, 3, True),     # split-K: the GELU tail in the reduction
+    (200, 256, 64, 3, 4, True),      # E3M4 tile-table kernel
+    (130, 96, 72, 2, 5, True),       # E2M5
+    (96, 160, 64, 4, 3, True, 1),    # bR = 1: the gated exact kernel's store
+]
+
+
+@pytest.mark.parametrize("case", GELU_CASES, ids=[f"{c[0]}x{c[1]}x{c[2]}-E{c[3]}M{c[4]}-q{int(c[5])}"
+                                                   + (f"-bR{c[6]}" if len(c) > 6 else "") for c in GELU_CASES])
+def test_matmul_block_gelu_tail_equals_torch_gelu(case):
+    """post_act 2: fq_out(gelu(fq_in(A) @ B + bias)) in one launch, bit-identical to the product,
+    then torch's nn.GELU() (the reference's intermediate_act_fn), then the output fake-quant --
+    vit_quantized_approx.py:117-135."""
+    Mr, K, N, E, M, with_q = case[:6]
+    x, wq, bw, bias, _ = _operands(Mr, K, N, E, M, seed=Mr * 3 + K + N)
+    table = get_error_table_NN(E, M, withComp=False, dnsmp_factor=3)
+    flags = ao.make_flags(with_approx=True, with_s2nn2s_opt=True, quant_btw_mult_accu=True)
+    in_mx = x.abs().amax().reshape(1)
+    xq, bx = ao.fp8_fake_quantize(x, in_mx, 8, M)
+    out_mx = torch.tensor([3.25], device=DEV)
+    bR = case[6] if len(case) > 6 else 2 ** (E - 1) + 3
+    ref = torch.nn.GELU()(ao.approx_matmul(xq, wq.t(), E, M, bx, bw, bR, table, flags=flags) + bias)
+    if with_q:
+        ref, bo = ao.fp8_fake_quantize(ref, out_mx, 8, M)
+    post = (None, 2, 0.0, 0.0, (out_mx, 8, M, 1) if with_q else None)
+    got, ib, ob = ao.approx_matmul_block(x, wq.t(), E, M, None, bw, bR, table, flags=flags, bias=bias,
+                                         qin=(in_mx, 8, M, 1), post=post)
+    assert np.array_equal(_bits(got), _bits(ref)), np.abs(got - ref).max().item()
+    if with_q:
+        assert ob.item() == bo.reshape(-1)[0].item()
+
+
+def test_conv_block_rejects_gelu_tail():
+    from fp8_quantization_amd import _lib
+    L = _lib.load()
+    x = torch.zeros((1, 4, 4, 4), device=DEV)
+    w = torch.zeros((4, 4, 1, 1), device=DEV)
+    y = torch.empty_like(x)
+    b = torch.zeros(4, dtype=torch.int32, device=DEV)
+    tab = torch.zeros((8, 8), dtype=torch.int32)
+    ws = torch.zeros(1 << 16, dtype=torch.uint8, device=DEV)
+    rc = L.fp8a_conv2d_block(_lib.dev_ptr(x), _lib.dev_ptr(w), _lib.dev_ptr(y), 1, 4, 4, 4, 4, 1, 1, 1, 1, 0, 0, 1, 1, 1,
+                             4, 3, _lib.dev_ptr(b), _lib.dev_ptr(b), _lib.dev_ptr(b), _lib.host_ptr(tab), 0, None, 0, 0.0,
+                             0.0, None, 0, 0, 0, None, None, None, 2, 0.0, 0.0, None, 0, 0, 0, None, None,
+                             _lib.dev_ptr(ws), ws.numel(), _lib.stream_ptr(DEV))
+    assert rc == -1

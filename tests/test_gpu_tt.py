@@ -146,7 +146,7 @@ def test_every_code_pair_bitexact(fmt, kind, shift):
     bA, bB = (1 << (E - 1)) + 2, (1 << (E - 1)) + 5
     bR = bA + bB - (1 << E) - shift
     # K = 256 with one nonzero K-step: each output is exactly one term, and K is long enough for
-    # E3M4's packed-f16 form (run_gemm picks it for K >= 256 or a signed table)
+    # E3M4's packed-f16 form (run_gemm picks it for K >= 64 -- option tt16_mink -- or a signed table)
     a = _all_codes(E, M, bA).reshape(-1, 1)
     b = _all_codes(E, M, bB).reshape(1, -1)
     K = 256
@@ -249,7 +249,7 @@ def test_e3m4_f16_window(case, kind):
     bA = 7
     bB = np.array([bA + o for o in boffs], np.int32)
     bR = int(bA + bB.min() + rdelta)
-    Mr, K, N = 96, 256, 64  # K >= 256: the packed-f16 form for both table kinds
+    Mr, K, N = 96, 256, 64  # K >= 64: the packed-f16 form for both table kinds
     A = _grid(rng, E, M, (Mr, K), bA, zero_frac=0.2, sub_frac=0.1)
     W = _grid(rng, E, M, (N, K), bB[:, None], zero_frac=0.1, sub_frac=0.1)
     tab, fl = _table(E, M, kind), _flags(kind)
