@@ -1047,10 +1047,19 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
             if (use_img) a.aw = a.in_img + 64;
             a.af32 = !tt && !v5mx && !use_img && xm_af32(a) ? 1 : 0;
             const int64_t rows = a.conv ? a.M / (a.Ho * a.Wo) : a.M, cols = a_words / std::max<int64_t>(rows, 1);
-            const dim3 ga((unsigned)std::min<int64_t>((cols + 255) / 256, 64), (unsigned)std::min<int64_t>(rows, 1024));
+            dim3 ga((unsigned)std::min<int64_t>((cols + 255) / 256, 64), (unsigned)std::min<int64_t>(rows, 1024));
+            {  // the pre-pass's flattened 16-byte form (xm_decode_a: unbordered, rows and columns in
+               // whole 16-byte chunks): a 1-D grid of about 4 chunks per thread
+                const int64_t hw = a.H * a.W, lim0 = a.conv ? cols : a.K, istride = a.conv ? a.Cin * hw : a.lda;
+                const float *in0 = a.conv ? a.X + a.cbase * hw : a.A;
+                const bool flat = !(a.conv && (a.awph | a.awpw)) && lim0 % 4 == 0 && cols % 4 == 0 && istride % 4 == 0 &&
+                                  ((uintptr_t)in0 & 15) == 0 && ((uintptr_t)a.aw & 15) == 0;
+                if (flat) ga = dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((a_words / 4 + 1023) / 1024, 8192)), 1);
+            }
             if (use_img) {
                 a.gate = a.in_img;
-                xm_decode_a<<<dim3(std::min(ga.x, 8u), std::min(ga.y, 64u)), 256, 0, s>>>(a);
+                xm_decode_a<<<ga.y == 1 ? dim3(std::min(ga.x, 512u)) : dim3(std::min(ga.x, 8u), std::min(ga.y, 64u)), 256, 0,
+                              s>>>(a);
                 a.gate = nullptr;
             } else if (!a.af32) {
                 xm_decode_a<<<ga, 256, 0, s>>>(a);

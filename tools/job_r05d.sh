@@ -1,15 +1,21 @@
 #!/bin/bash
-# Round 5, step d: the persistent depthwise kernels -- bit-identity tests, configs 1 / MobileNetV2
-# E4M3 / config 3 v9 bench lines; the E3M4 layer set (round-3 reference: 56.4 ms no-comp).
+# Round 5 (d2): the A pre-pass with 4 chunks in flight per thread and a 1-D grid: its tests, then
+# interleaved eager A/B lines against _ab/lib_before.so (same Python) on config 3 v5, MobileNetV2
+# E4M3 and ViT-B/16.
 set -o pipefail
-OUT=gpurun_out/${1:-r05d}; mkdir -p $OUT
-timeout -k 10 600 python -u -m pytest tests/test_gpu_grouped_conv.py tests/test_gpu_tbx.py tests/test_gpu_mbv2_layers.py -q -x \
-    --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1
-rc=$?; grep -E "^FAILED|^ERROR|passed|failed" $OUT/tests.log | tail -8; [ $rc -eq 0 ] || exit $rc
-for spec in "c1:--arch mobilenet_v2 --no-approx" "mb_e4m3:--arch mobilenet_v2" "c3_v9:--arch mobilenet_v2 --expo-width 5 --mant-width 2"; do
-  tag=${spec%%:*}; a=${spec#*:}
-  timeout -k 10 300 python bench.py $a --no-cpu-baseline --steps 10 > $OUT/bench_$tag.json 2> $OUT/bench_$tag.err || exit $?
-  echo "$tag $(python -c "import json; d=json.load(open('$OUT/bench_$tag.json')); print(round(d['value'],1))")"
+OUT=gpurun_out/r05d2; mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_f8mx.py tests/test_gpu_qin.py \
+    tests/test_gpu_chain.py tests/test_gpu_v5.py tests/test_gpu_linear_block.py > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
+tail -1 $OUT/tests.log
+for cfg in "v5 mobilenet_v2 5 2 512 --v5-ofuf" "e4m3 mobilenet_v2 4 3 512" "vit vit_b16 4 3 64"; do
+  set -- $cfg; T=$1; shift
+  for rep in 1 2; do
+    for v in before after; do
+      if [ $v = before ]; then export FP8A_LIB_PATH=$PWD/_ab/lib_before.so; else unset FP8A_LIB_PATH; fi
+      timeout -k 10 300 python bench.py --arch $1 --expo-width $2 --mant-width $3 --batch $4 $5 --no-cpu-baseline --no-graph \
+          > $OUT/${T}_${v}_$rep.json 2> $OUT/${T}_${v}_$rep.err || { tail -3 $OUT/${T}_${v}_$rep.err; exit 1; }
+      python -c "import json; d=json.load(open('$OUT/${T}_${v}_$rep.json')); print('$T $v $rep', round(d['value'],1), round(d['roofline']['op_avg_ms'],4))"
+    done
+  done
 done
-timeout -k 10 300 python tools/gemm_bench.py --mode w2u --reps 3 > $OUT/layers_e3m4.log 2>&1 || exit $?
-tail -1 $OUT/layers_e3m4.log
+unset FP8A_LIB_PATH
