@@ -885,11 +885,13 @@ static int64_t xm_a_words(const GemmArgs &a) {
 
 // gemm_f8mx_kernel reads A as fp32 and decodes it while staging (no xm_decode_a pass) for a 1x1
 // unpadded conv or a matrix A whose source lies within 32-bit byte offsets, when the launch has at
-// most FP8A_AF32_MAXCT column tiles (default 3; 0 = never): each column tile decodes its A
-// elements again (~25 VALU operations each), against the pre-pass's 8 B of HBM traffic per element
-// (MobileNetV2's projections: 2.9 ms of pre-pass per forward at batch 512).  Measured on ResNet-50
-// E4M3 (1x1 convs with 1 / 2 / 4 column tiles): at most 0 / 2 / 4 tiles 4610 / 4613 / 4543 images/s.
-static int g_opt_af32_maxct = getenv("FP8A_AF32_MAXCT") ? std::max(0, atoi(getenv("FP8A_AF32_MAXCT"))) : 3;
+// most FP8A_AF32_MAXCT column tiles (default 1; 0 = never): each column tile decodes its A
+// elements again (~25 VALU operations each), against the pre-pass's 8 B of HBM traffic per element.
+// Round 2 measured at most 0 / 2 / 4 tiles 4610 / 4613 / 4543 images/s on ResNet-50 E4M3 and chose
+// 3; with round 5's pre-pass (4 loads in flight per thread) at most 1 tile wins everywhere:
+// MobileNetV2 E4M3 23,877 -> 24,482, E5M2 v9 21,225 -> 21,561, ResNet-50 E4M3 4,790 -> 4,840
+// (profiles/r05_af32/).
+static int g_opt_af32_maxct = getenv("FP8A_AF32_MAXCT") ? std::max(0, atoi(getenv("FP8A_AF32_MAXCT"))) : 1;
 static bool xm_af32(const GemmArgs &a) {
     const int maxct = g_opt_af32_maxct;  // option "af32_maxct"
     const int64_t bnt = 16 * a.xncg, ct = (a.N + bnt - 1) / bnt;

@@ -41,7 +41,8 @@ def _with(opts, fn):
 
 
 WIDE = {"xm_ncg": 4, "af32_maxct": 0}               # the round-2 schedule
-VARIANTS = [{"xm_ncg": 0, "af32_maxct": 3},          # the default choice
+VARIANTS = [{"xm_ncg": 0, "af32_maxct": 1},          # the default choice
+            {"xm_ncg": 0, "af32_maxct": 3},
             {"xm_ncg": 1, "af32_maxct": 64}, {"xm_ncg": 2, "af32_maxct": 64}, {"xm_ncg": 4, "af32_maxct": 64},
             {"xm_ncg": 1, "af32_maxct": 0}, {"xm_ncg": 2, "af32_maxct": 0}]
 
@@ -136,7 +137,7 @@ def test_in_kernel_decode_falls_back():
     x[1, 5, 3, 7] = 0.3
     bW = np.full(24, 15, np.int32)
     w = _grid(rng, (24, 32, 1, 1), 15)
-    for v in ({"xm_ncg": 0, "af32_maxct": 3}, {"xm_ncg": 1, "af32_maxct": 64}):
+    for v in ({"xm_ncg": 0, "af32_maxct": 1}, {"xm_ncg": 1, "af32_maxct": 64}):
         y, flag = _with(v, lambda: _conv_raw(x, w, bA, bW, bR, _tab(), FL, 1, 0, 1, 1))
         assert flag != 0, f"{v}: the in-kernel decode did not flag the launch"
         ref, S = _conv_ref(x, w, bA, bW, bR, _tab(), FL, 1, 0, 1, 1)
