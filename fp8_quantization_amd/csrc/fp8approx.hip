@@ -892,10 +892,12 @@ static int64_t xm_a_words(const GemmArgs &a) {
 // MobileNetV2 E4M3 23,877 -> 24,482, E5M2 v9 21,225 -> 21,561, ResNet-50 E4M3 4,790 -> 4,840
 // (profiles/r05_af32/).
 static int g_opt_af32_maxct = getenv("FP8A_AF32_MAXCT") ? std::max(0, atoi(getenv("FP8A_AF32_MAXCT"))) : 1;
+// (a strided 1x1 conv's pre-pass decodes sh x sw input pixels per one the product reads, so the
+// fp32 staging is allowed up to sh x sw times as many column tiles: ResNet-18's downsampling convs)
+static int64_t af32_maxct(int sh, int sw) { return (int64_t)g_opt_af32_maxct * sh * sw; }
 static bool xm_af32(const GemmArgs &a) {
-    const int maxct = g_opt_af32_maxct;  // option "af32_maxct"
     const int64_t bnt = 16 * a.xncg, ct = (a.N + bnt - 1) / bnt;
-    if (ct > maxct) return false;
+    if (ct > (a.conv ? af32_maxct(a.sh, a.sw) : g_opt_af32_maxct)) return false;  // option "af32_maxct"
     if (a.conv) {
         if (a.kh != 1 || a.kw != 1 || a.ph != 0 || a.pw != 0) return false;
         const int64_t bn = a.M / (a.Ho * a.Wo);
@@ -2157,7 +2159,7 @@ int fp8a_conv2d_wants_image(int64_t Cout, int kh, int kw, int ph, int pw, int gr
     if (!f8_form(E, Mw, flags & ~F_TB, mode)) return 0;
     if (kh == 1 && kw == 1 && ph == 0 && pw == 0) {  // xm_af32: fp32 staging up to af32_maxct column tiles
         const int64_t bnt = 16 * xm_ncg(Cout), ct = (Cout + bnt - 1) / bnt;
-        if (ct <= g_opt_af32_maxct) return 0;
+        if (ct <= af32_maxct(sh, sw)) return 0;
     }
     return 1;
 }

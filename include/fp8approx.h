@@ -99,7 +99,7 @@ int fp8a_kernel_time(double *out, int reset);
  * "v5ds" (default 1; FP8A_V5DS) -- the v5 (E5M2, adder wrap) depthwise 3x3 on the staged kernel
  * with both word pre-passes fused (0: the pre-passes + the word-form kernel; same bits);
  * "xm_ncg" (default 0 = by N; FP8A_XM_NCG) -- gemm_f8mx_kernel's tile width forced to 16 x 1 / 2
- * / 4 columns; "af32_maxct" (default 1; FP8A_AF32_MAXCT) -- the most column tiles for which a 1x1
+ * / 4 columns; "af32_maxct" (default 1, times sh x sw for a strided conv; FP8A_AF32_MAXCT) -- the most column tiles for which a 1x1
  * conv / matrix A is decoded inside gemm_f8mx_kernel instead of by its pre-pass (0 = never);
  * "tt16_mink" (default 64; FP8A_TT16_MINK) -- the smallest K of an E3M4 launch (unsigned error
  * table) on the packed-f16 tile-table kernel (shorter K: the f32 form).
