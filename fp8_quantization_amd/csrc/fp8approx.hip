@@ -1121,7 +1121,10 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
         rc = hip_check("fp8a split-K reduce launch");
         if (rc) return rc;
     }
-    const unsigned ublocks = std::max((unsigned)std::min<int64_t>(a.nur * a.nuc, 4096), clear_blocks(lease));
+    // (at most 512 blocks: the kernel is a no-op but for the arena clearing unless the launch
+    // flagged, and its 268 VGPRs hold it at one wave per SIMD -- 4096 blocks cost ~7.5 us of wave
+    // launches per GEMM; a flagged launch loops its units over the blocks)
+    const unsigned ublocks = std::max((unsigned)std::min<int64_t>(a.nur * a.nuc, 512), clear_blocks(lease));
     gemm_exact_kernel<<<ublocks, 256, 0, s>>>(a);
     rc = hip_check("fp8a gated exact gemm launch");
     static const bool dbg = getenv("FP8A_DEBUG_FLAGS") != nullptr;  // diagnostics: the flag word per launch
