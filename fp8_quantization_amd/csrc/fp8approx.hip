@@ -29,6 +29,9 @@
 #include "gemm_dense.h"
 #include "conv_tbx.h"
 
+// (defined with C linkage below; run_gemm launches it too)
+extern "C" __global__ void fq_bias_kernel(fp8a::FqIn fq, float *bias_out, int32_t *ibias_out);
+
 namespace fp8a {
 
 // ------------------------------------------------------------------------- error handling
@@ -181,6 +184,11 @@ __device__ __forceinline__ void gemm_exact_units(const GemmArgs &p, uint32_t f, 
 
 __global__ __launch_bounds__(256) void gemm_exact_kernel(const GemmArgs p) {
     const bool tb = p.flags & F_TB;
+    if (p.post_bout != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {  // the output quantizer's bias
+        const float b = fq_bias(*p.post_fq.mx, p.post_fq.E, p.post_fq.M);
+        *p.post_bout = b;
+        *p.post_ibout = (int32_t)b;
+    }
     const DFmt fA = dfmt(p.E, p.Mw, *p.bA, tb), fR = dfmt(p.E, p.Mw, *p.bR, tb);
     if (p.flag == nullptr) {  // the tensor-bias path: the exact kernel is the product itself
         for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < p.M * p.N;
@@ -968,6 +976,11 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     int rc = check_format(a.E, a.Mw);
     if (rc) return rc;
     if (a.M < 0 || a.N < 0 || a.K < 0) return fail(FP8A_EINVAL, "negative extent");
+    if (a.post_bout && (a.M == 0 || a.N == 0 || a.K == 0)) {  // (no exact kernel below to write it)
+        fq_bias_kernel<<<1, 1, 0, s>>>(a.post_fq, a.post_bout, a.post_ibout);
+        const int rc0 = hip_check("fp8a output-quantizer bias");
+        if (rc0) return rc0;
+    }
     if (a.M == 0 || a.N == 0) return FP8A_OK;
     if (a.K == 0) {  // empty inner dimension: the reference's sum over an empty axis is 0
         if (a.nchw) return fail(FP8A_EINVAL, "empty convolution window");
@@ -1732,7 +1745,8 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
                        uint32_t flags, const float *bn, int act, float act_lo, float act_hi, void *workspace,
                        size_t workspace_bytes, hipStream_t s, FqIn fq, float *fqb, int32_t *fqi, float *xq,
                        const float *res = nullptr, int post_act = 0, float post_lo = 0.0f, float post_hi = 0.0f,
-                       FqIn post_fq = FqIn{}, const uint32_t *in_img = nullptr, const EmitW &em_in = EmitW{}) {
+                       FqIn post_fq = FqIn{}, const uint32_t *in_img = nullptr, const EmitW &em_in = EmitW{},
+                       float *post_bout = nullptr, int32_t *post_ibout = nullptr) {
     const float2 *ep = reinterpret_cast<const float2 *>(bn);
     if (ep && (((uintptr_t)bn) & 7) != 0) return fail(FP8A_EINVAL, "bn parameters must be 8-byte aligned");
     int rc = check_format(E, Mw);
@@ -1743,7 +1757,10 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
     if (Ho <= 0 || Wo <= 0) return fail(FP8A_EINVAL, "empty convolution output");
     const int64_t cog = Cout / groups, cig = Cin / groups;
     const int64_t Mrows = Bn * Ho * Wo, Ktot = Cin * kh * kw, Kg = cig * kh * kw;
-    if (Mrows == 0) return FP8A_OK;
+    if (Mrows == 0) {  // (the output quantizer's bias is still set, as its forward would)
+        if (post_bout) fq_bias_kernel<<<1, 1, 0, s>>>(post_fq, post_bout, post_ibout);
+        return post_bout ? hip_check("fp8a output-quantizer bias") : FP8A_OK;
+    }
     // non-fused input quantization: one fake-quant pass into xq, then the plain path on it
     auto materialize = [&]() -> int {
         const int64_t nx = Bn * Cin * H * W;
@@ -1860,7 +1877,8 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
             rc = hip_check("fp8a_conv2d (tensor-bias groups, fast)");
             if (rc) return rc;
         }
-        const unsigned eb = (unsigned)(fast_ok ? std::min<int64_t>((total + 255) / 256, 4096) : (total + 255) / 256);
+        // (gated: at most 1024 blocks -- a no-op launch unless the fast kernel flagged)
+        const unsigned eb = (unsigned)(fast_ok ? std::min<int64_t>((total + 255) / 256, 1024) : (total + 255) / 256);
         if (fast_ok) {  // gated, grid-capped: a no-op launch unless the fast kernel flagged
             conv_tb_direct_kernel<true><<<std::max(eb, clear_blocks(lease)), 256, 0, s>>>(
                 x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups, Ho, Wo, E, Mw, bA, bW, bR, tp,
@@ -2005,6 +2023,7 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
             a.bA = fqi;  // written by the A pre-decode before any kernel reads it
         }
         a.res = res; a.post_act = post_act; a.post_lo = post_lo; a.post_hi = post_hi; a.post_fq = post_fq;
+        a.post_bout = post_bout; a.post_ibout = post_ibout;
         if (groups == 1) {  // (fp8a_conv2d_chain only asks for these on ungrouped convolutions)
             a.in_img = in_img;
             a.em = em;
@@ -2080,10 +2099,7 @@ int fp8a_conv2d_block(const float *x, const float *w, float *y, int64_t Bn, int6
         const int qE = out_nbits - out_sign_bits - out_mbits;
         if (out_mbits < 1 || qE < 1) return fail(FP8A_EFORMAT, "bad FP8 quantizer format");
         if (!out_bias_out || !out_ibias_out) return fail(FP8A_EINVAL, "null pointer");
-        fout = FqIn{out_maxval, qE, out_mbits, out_sign_bits};
-        fq_bias_kernel<<<1, 1, 0, s>>>(fout, out_bias_out, out_ibias_out);
-        int rc = hip_check("fp8a output-quantizer bias");
-        if (rc) return rc;
+        fout = FqIn{out_maxval, qE, out_mbits, out_sign_bits};  // (its bias: written by the launch's gated exact kernel)
     }
     const size_t xq_bytes = fin.mx ? align256((size_t)(Bn * Cin * H * W) * sizeof(float)) : 0;
     if (workspace == nullptr || workspace_bytes < FLAG_BYTES + xq_bytes)
@@ -2092,7 +2108,8 @@ int fp8a_conv2d_block(const float *x, const float *w, float *y, int64_t Bn, int6
     float *xq = fin.mx ? (float *)((char *)workspace + rest) : nullptr;
     return conv2d_impl(x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups, E, Mw,
                        fin.mx ? nullptr : bA, bW, bR, table, flags, bn, act, act_lo, act_hi, workspace, rest, s, fin,
-                       in_bias_out, in_ibias_out, xq, res, post_act, post_lo, post_hi, fout);
+                       in_bias_out, in_ibias_out, xq, res, post_act, post_lo, post_hi, fout, nullptr, EmitW{},
+                       fout.mx ? out_bias_out : nullptr, fout.mx ? out_ibias_out : nullptr);
 }
 
 // ----------------------------------------------------------------------------- word-image chain
@@ -2194,10 +2211,7 @@ int fp8a_conv2d_chain(const float *x, const float *w, float *y, int64_t Bn, int6
         const int qE = out_nbits - out_sign_bits - out_mbits;
         if (out_mbits < 1 || qE < 1) return fail(FP8A_EFORMAT, "bad FP8 quantizer format");
         if (!out_bias_out || !out_ibias_out) return fail(FP8A_EINVAL, "null pointer");
-        fout = FqIn{out_maxval, qE, out_mbits, out_sign_bits};
-        fq_bias_kernel<<<1, 1, 0, s>>>(fout, out_bias_out, out_ibias_out);
-        int rc = hip_check("fp8a output-quantizer bias");
-        if (rc) return rc;
+        fout = FqIn{out_maxval, qE, out_mbits, out_sign_bits};  // (its bias: written by the launch's gated exact kernel)
     }
     EmitW em{};
     if (out_image) {
@@ -2243,7 +2257,7 @@ int fp8a_conv2d_chain(const float *x, const float *w, float *y, int64_t Bn, int6
     return conv2d_impl(x, w, y, Bn, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups, E, Mw,
                        fin.mx ? nullptr : bA, bW, bR, table, flags, bn, act, act_lo, act_hi, workspace, rest, s, fin,
                        in_bias_out, in_ibias_out, xq, res, post_act, post_lo, post_hi, fout,
-                       (const uint32_t *)in_image, em);
+                       (const uint32_t *)in_image, em, fout.mx ? out_bias_out : nullptr, fout.mx ? out_ibias_out : nullptr);
 }
 
 size_t fp8a_matmul_block_workspace_size(int64_t M, int64_t N, int64_t K) {
@@ -2284,10 +2298,7 @@ int fp8a_matmul_block(const float *A, int64_t lda, const float *B, int64_t sbk, 
         const int qE = out_nbits - out_sign_bits - out_mbits;
         if (out_mbits < 1 || qE < 1) return fail(FP8A_EFORMAT, "bad FP8 quantizer format");
         if (!out_bias_out || !out_ibias_out) return fail(FP8A_EINVAL, "null pointer");
-        fout = FqIn{out_maxval, qE, out_mbits, out_sign_bits};
-        fq_bias_kernel<<<1, 1, 0, s>>>(fout, out_bias_out, out_ibias_out);
-        int rc = hip_check("fp8a output-quantizer bias");
-        if (rc) return rc;
+        fout = FqIn{out_maxval, qE, out_mbits, out_sign_bits};  // (its bias: written by the launch's gated exact kernel)
     }
     const size_t xq_bytes = fin.mx ? align256((size_t)(M * K) * sizeof(float)) : 0;
     if (workspace == nullptr || workspace_bytes < FLAG_BYTES + xq_bytes)
@@ -2297,6 +2308,10 @@ int fp8a_matmul_block(const float *A, int64_t lda, const float *B, int64_t sbk, 
                            flags);
     a.ep = reinterpret_cast<const float2 *>(bn); a.ep_act = act; a.ep_lo = act_lo; a.ep_hi = act_hi;
     a.res = res; a.post_act = post_act; a.post_lo = post_lo; a.post_hi = post_hi; a.post_fq = fout;
+    if (fout.mx) {
+        a.post_bout = out_bias_out;
+        a.post_ibout = out_ibias_out;
+    }
     if (fin.mx && M > 0 && K > 0) {
         // fuse into the matrix-core pre-decode only where run_gemm will take that path (as conv2d_impl)
         TablePack tp;

@@ -178,6 +178,8 @@ struct GemmArgs {
     uint32_t *flag_out;  // the caller's workspace word that receives the launch's final flag word
     uint4 *arena_clr;    // the flag arena's other slot, and its 16-byte words to zero (arena_clear)
     uint32_t arena_clr16;
+    float *post_bout;    // post_fq's bias outputs (its custom_bias), written by gemm_exact_kernel, or nullptr
+    int32_t *post_ibout;
 };
 
 // Fallback flag word bits: FB_ANY = some output unit needs the exact kernel, FB_ALL = every
