@@ -274,7 +274,9 @@ def capture_forward(model, x, warm, sync):
         torch.cuda.current_stream().wait_stream(gs)
         sync()
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=gs):
+        # thread_local: other threads' HIP calls (the process group's watchdog on N > 1 ranks) stay
+        # legal while this thread captures
+        with torch.cuda.graph(graph, stream=gs, capture_error_mode="thread_local"):
             out = model(x)
         ref = model(x)
         graph.replay()
