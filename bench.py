@@ -375,6 +375,11 @@ def run(args, dev, rank=0, world=1):
             step()
         if cuda and not args.no_graph:
             graph_info, replay = capture_forward(model, x, args.warmup, sync)
+            if world > 1:  # every rank replays or none does: the timed loops must issue the same collectives
+                ok = torch.tensor([1 if graph_info.get("captured") else 0], dtype=torch.int32, device=dev)
+                dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+                if int(ok.item()) == 0 and graph_info.get("captured"):
+                    graph_info.update(captured=False, note="another rank's capture failed: eager forwards timed")
         if graph_info and graph_info.get("captured"):
             # the timed steps replay the captured forward; the per-kernel HIP events and counters come
             # from the same number of eager steps right after (a replayed graph carries no host-side
