@@ -89,6 +89,17 @@ def parse(argv=None):
                     help="ranks (one per GPU); without a launcher's WORLD_SIZE, N > 1 spawns the N ranks itself")
     ap.add_argument("--device", default="cuda", choices=("cuda", "cpu"),
                     help="cpu = the gloo rehearsal of the multi-rank flow (tests; approx ops need stand-ins)")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="N > 1 on GPUs: nccl (= RCCL over xGMI, the product) or gloo (host-staged collectives: "
+                         "the one-GPU rehearsal of the N-rank flow, with --share-device)")
+    ap.add_argument("--share-device", action="store_true",
+                    help="every rank on cuda:0 (rehearsal of N ranks on one leased GPU; needs --dist-backend gloo)")
+    ap.add_argument("--dump-logits", default=None,
+                    help="after the timed steps, one more (untimed) step; rank 0 saves its gathered logits "
+                         "there (.npy; tests)")
+    ap.add_argument("--shard-seed", type=int, default=None,
+                    help="seed offset of this process's input shard (default: its rank); lets a world-1 run "
+                         "reproduce rank r's shard")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=None, help="images per GPU per step (default 512; resnet18 1024, vit_b16 64, vit_fc 256)")
@@ -257,12 +268,18 @@ def cpu_baseline(shapes, table, cols):
                                       ratio=full / (cache[(Mi, K)] * ncol)))
 
 
-def capture_forward(model, x, warm, sync):
+CHECK_REPLAYS = 3  # replays compared bit for bit with the eager forward before timing
+
+
+def capture_forward(model, x, warm, sync, fallback_stats=None):
     """The forward captured into one HIP graph (torch.cuda.CUDAGraph over hipGraph) on a side
-    stream warmed by `warm` eager forwards first (the library's per-stream flag arena and torch's
-    allocator settle there); returns (info, replay) where replay() runs the captured forward and
-    all-gathers its logits.  The replayed logits must equal an eager forward's bit for bit, else
-    (or if capture fails) info["captured"] is False and the caller times eager forwards."""
+    stream warmed by `warm` eager forwards first (torch's allocator settles there; captured
+    launches keep their fallback flags in their own workspace, include/fp8approx.h, so the graph
+    never depends on the library's per-stream flag arena); returns (info, replay) where replay()
+    runs the captured forward and all-gathers its logits.  Each of CHECK_REPLAYS replays must
+    equal an eager forward bit for bit and leave the same fallback counters as that eager forward
+    (a replay that met stale flag words would recompute units it need not), else (or if capture
+    fails) info["captured"] is False and the caller times eager forwards."""
     from fp8_quantization_amd.distributed import gather_logits
     info = {"captured": False}
     try:
@@ -278,12 +295,20 @@ def capture_forward(model, x, warm, sync):
         # legal while this thread captures
         with torch.cuda.graph(graph, stream=gs, capture_error_mode="thread_local"):
             out = model(x)
+        fb = fallback_stats or (lambda reset=False: {})
+        fb(reset=True)
         ref = model(x)
-        graph.replay()
         sync()
-        same = bool(torch.equal(ref.view(torch.int32), out.view(torch.int32)))
-        info.update(captured=same, replay_matches_eager_bitwise=same)
-        if not same:
+        fb_eager = fb(reset=True)
+        same, fb_same = True, True
+        for _ in range(CHECK_REPLAYS):
+            graph.replay()
+            sync()
+            same &= bool(torch.equal(ref.view(torch.int32), out.view(torch.int32)))
+            fb_same &= fb(reset=True) == fb_eager
+        info.update(captured=same and fb_same, replay_matches_eager_bitwise=same, checked_replays=CHECK_REPLAYS,
+                    replay_fallback_matches_eager=fb_same, eager_fallback=fb_eager)
+        if not (same and fb_same):
             return info, None
     except Exception as e:  # noqa: BLE001 -- report and time eager forwards instead
         info["error"] = f"{type(e).__name__}: {e}"[:300]
@@ -304,6 +329,8 @@ def run(args, dev, rank=0, world=1):
     tests/test_distributed_cpu.py, approx ops replaced by stand-ins) the control flow is the same
     and the HIP-event roofline is omitted."""
     cuda = dev.type == "cuda"
+    from fp8_quantization_amd.distributed import comm_device
+    comm_dev = comm_device() if world > 1 else dev
 
     def sync():
         if cuda:
@@ -338,7 +365,8 @@ def run(args, dev, rank=0, world=1):
         h.remove()
     macs_img = approx_macs_per_image(shapes)  # (rank 0's calibration pass recorded the shapes)
 
-    x = synthetic_images(args.batch, 10 + rank, dev, in_shape)  # this rank's shard of the validation batch
+    shard = rank if args.shard_seed is None else args.shard_seed
+    x = synthetic_images(args.batch, 10 + shard, dev, in_shape)  # this rank's shard of the validation batch
 
     def step():
         return gather_logits(model(x))  # one RCCL all-gather of logits per step (N > 1)
@@ -374,16 +402,18 @@ def run(args, dev, rank=0, world=1):
         for _ in range(args.warmup):
             step()
         if cuda and not args.no_graph:
-            graph_info, replay = capture_forward(model, x, args.warmup, sync)
+            graph_info, replay = capture_forward(model, x, args.warmup, sync, fa._lib.fallback_stats)
             if world > 1:  # every rank replays or none does: the timed loops must issue the same collectives
-                ok = torch.tensor([1 if graph_info.get("captured") else 0], dtype=torch.int32, device=dev)
+                ok = torch.tensor([1 if graph_info.get("captured") else 0], dtype=torch.int32, device=comm_dev)
                 dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+                graph_info["all_ranks_captured"] = bool(int(ok.item()))
                 if int(ok.item()) == 0 and graph_info.get("captured"):
                     graph_info.update(captured=False, note="another rank's capture failed: eager forwards timed")
         if graph_info and graph_info.get("captured"):
             # the timed steps replay the captured forward; the per-kernel HIP events and counters come
             # from the same number of eager steps right after (a replayed graph carries no host-side
             # per-launch events)
+            fa._lib.fallback_stats(reset=True)  # (synchronises: outside the timed region)
             sync()
             if world > 1:
                 dist.barrier()
@@ -394,24 +424,34 @@ def run(args, dev, rank=0, world=1):
             if world > 1:
                 dist.barrier()
             elapsed = time.perf_counter() - t0
+            # the timed replays' own fallback counters (device-side: a replay counts them as an eager
+            # forward does)
+            graph_info["timed_replay_fallback"] = fa._lib.fallback_stats(reset=True)
             eager_elapsed, prof = instrumented(step)
             graph_info["eager_images_per_s"] = world * args.batch * args.steps / eager_elapsed
         else:
             elapsed, prof = instrumented(step)
+            eager_elapsed = elapsed
     # how many launches / 64x64 output units of the timed steps left the fast path (a regression
     # there would otherwise be invisible in the line)
     fallback = fa._lib.fallback_stats() if cuda else None
     paths = {k: v for k, v in fa._lib.path_stats().items() if v} if cuda else None
     dense_fb = fa._lib.dense_stats() if cuda else None
     ktime = fa._lib.kernel_time(reset=True) if cuda else {}
+    if args.dump_logits:  # one more step, after every counter was read (every rank: the gather is a collective)
+        with torch.no_grad():
+            final = step()
+        if rank == 0:
+            import numpy as np
+            np.save(args.dump_logits, final.float().cpu().numpy())
 
     op_ms = sum(s.elapsed_time(e) for (s, e, _, _) in prof)
     op_macs = sum(m for (_, _, m, _) in prof)
     op_bytes = sum(b for (_, _, _, b) in prof)
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, eager_elapsed], dtype=torch.float64, device=comm_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed, eager_elapsed = float(t[0].item()), float(t[1].item())
     images = world * args.batch * args.steps
 
     if rank == 0:
@@ -497,7 +537,8 @@ def run(args, dev, rank=0, world=1):
                             "resident waves, so it counts a wave's cycles inside a VALU instruction, not VALU pipe "
                             "occupancy; wave_cycles: SQ_WAIT_ANY / SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY shares",
                 "approx_macs_per_s": op_macs / (op_ms / 1e3) if op_ms > 0 else None,
-                "gemm_share_of_step": op_ms / 1e3 / elapsed,
+                # (op_ms comes from the eager instrumented steps: their share of those steps)
+                "gemm_share_of_step": op_ms / 1e3 / eager_elapsed,
             },
         }
         if args.no_approx and cuda:
@@ -534,7 +575,7 @@ def run(args, dev, rank=0, world=1):
                                f"launch avg over {launches} launches, {avg_s * 1e3:.3f} ms avg launch (HIP events); "
                                f"{2.0 * op_macs / (op_ms / 1e3) / 1e12 if op_ms > 0 else 0:.1f} TFLOP/s of exact "
                                f"products (fp8 MFMA dense peak {FP8_MFMA_PEAK_TFLOPS:.0f})",
-                "gemm_share_of_step": op_ms / 1e3 / elapsed,
+                "gemm_share_of_step": op_ms / 1e3 / eager_elapsed,
             }
             res["dense_fp32_units"] = dict(dense_fb, note="timed steps only: dense launches with 64x64 units "
                                                           "recomputed in fp32 (blocks not exact in e4m3 / e5m2)")
@@ -601,10 +642,15 @@ def main(argv=None, worker_init=None):
         if world > 1:
             dist.init_process_group("gloo", rank=rank, world_size=world)
     else:
-        dev = torch.device("cuda", local)
+        if args.share_device and args.dist_backend != "gloo":
+            raise SystemExit("bench.py: --share-device needs --dist-backend gloo (RCCL wants one GPU per rank)")
+        dev = torch.device("cuda", 0 if args.share_device else local)
         if world > 1:
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=dev)
+            torch.cuda.set_device(dev)
+            if args.dist_backend == "nccl":
+                dist.init_process_group("nccl", device_id=dev)
+            else:
+                dist.init_process_group("gloo", rank=rank, world_size=world)
     if world > 1:
         world = dist.get_world_size()
     res = run(args, dev, rank, world)

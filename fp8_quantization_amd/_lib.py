@@ -23,7 +23,8 @@ SYMBOLS = ("fp8a_version", "fp8a_last_error", "fp8a_fallback_stats", "fp8a_path_
            "fp8a_fp8_quantize", "fp8a_matmul_qamaa", "fp8a_conv2d_qamaa", "fp8a_matmul_block_workspace_size",
            "fp8a_matmul_block", "fp8a_dense_matmul_workspace_size", "fp8a_dense_matmul",
            "fp8a_dense_conv2d_workspace_size", "fp8a_dense_conv2d", "fp8a_grouped_conv2d", "fp8a_dense_conv2d_fused", "fp8a_dense_stats", "fp8a_clock_stats",
-           "fp8a_word_image_bytes", "fp8a_word_image_init", "fp8a_conv2d_chain", "fp8a_conv2d_wants_image")
+           "fp8a_word_image_bytes", "fp8a_word_image_init", "fp8a_conv2d_chain", "fp8a_conv2d_wants_image",
+           "fp8a_flag_arena_slot_bytes")
 
 _lib = None
 
@@ -94,6 +95,7 @@ def load():
                                      P, I, I, I, P, P, P, SZ, P], I),
         "fp8a_dense_stats": ([P, I], I),
         "fp8a_clock_stats": ([P, I], I),
+        "fp8a_flag_arena_slot_bytes": ([P], SZ),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -134,6 +136,11 @@ def dev_ptr(t):
 def host_ptr(t):
     assert t.device.type == "cpu" and t.is_contiguous()
     return ctypes.c_void_p(t.data_ptr())
+
+
+def flag_arena_slot_bytes(device=None):
+    """fp8a_flag_arena_slot_bytes of the current stream of `device` (0 before its first eager launch)."""
+    return int(load().fp8a_flag_arena_slot_bytes(stream_ptr(device)))
 
 
 def fallback_stats(reset=False):

@@ -470,7 +470,9 @@ def _conv2d_chain_op(x: torch.Tensor, w: torch.Tensor, bA: Optional[torch.Tensor
         raise AssertionError(f"approx_conv2d: epilogue parameters must be contiguous float32 [{Cout}, 2]")
     # (a single-output-channel-group consumer reads table-form words: an image without border)
     in_pad = (ph, pw) if groups == 1 else (0, 0)
-    out_pad = (next_ph, next_pw) if next_form == 0 else (0, 0)
+    # (form 1, the table form, has no border; forms 0 and 2 -- matrix-core and v5 words -- carry the
+    # consumer's padding, as fp8a_conv2d_chain sizes them)
+    out_pad = (0, 0) if next_form == 1 else (next_ph, next_pw)
     for img, shp in ((in_image, (Bn, Cin, H, W) + in_pad), (out_image, (Bn, Cout, Ho, Wo) + out_pad)):
         if img is not None and img.numel() < L.fp8a_word_image_bytes(*shp):
             raise AssertionError("approx_conv2d: word image smaller than fp8a_word_image_bytes")

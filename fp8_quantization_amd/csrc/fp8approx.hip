@@ -921,6 +921,17 @@ static bool xm_af32(const GemmArgs &a) {
 // clearing races nothing.  Zeroed once when (re)allocated; grows by reallocation after the stream
 // drains.  A launch that stops before its last kernel (a launch error) leaves its successor a slot
 // with stale words: that launch then reruns the marked units exactly -- the same bits, more time.
+//
+// Stream capture (a HIP graph being recorded on s): the arena's host-side rotation would be frozen
+// into the graph -- a forward with an odd number of launches would start every replay after the
+// first on a slot its own last launch left dirty, and the clear sizes would be those of capture
+// time.  So a captured launch never touches the arena: its words live in the head of the caller's
+// workspace (which the caller allocates per call; torch's allocator gives a graph its own pool),
+// zeroed by a fill kernel at the start of the launch (dev_fill: not a memset node), and it clears nothing.  Every replay then
+// starts from zero words whatever ran before it, eager launches keep their own rotation, and an
+// eager launch that grows the arena afterwards cannot touch memory a graph references.  Growth never
+// frees an arena (retired ones stay allocated: at most the size of the current one in total), so
+// it needs no stream synchronisation either.
 struct FlagArena {
     uint32_t *p = nullptr;
     size_t slot = 0;       // bytes per slot
@@ -932,27 +943,74 @@ struct ArenaLease {
     uint4 *clr = nullptr;      // the other slot, and its 16-byte words the last kernel zeroes
     uint32_t clr16 = 0;
 };
+// Is a graph being captured on s?  (-1: the query itself failed; the error is recorded)
+// In-stream fills as kernels of our own, not hipMemsetAsync / hipMemset2DAsync: under stream capture
+// a memset becomes a graph memset node, and on this ROCm such nodes did not refill their destination
+// on replays after the first (measured: tools/dbg_capture2.py, DESIGN.md §3r -- a captured launch's
+// flag words then held stale data).  A kernel node re-executes every replay like any other.
+__global__ __launch_bounds__(256) void fill_u8_kernel(uint8_t *p, size_t n, uint32_t v8) {
+    const uint32_t w = v8 * 0x01010101u;
+    const size_t lead = std::min(n, (size_t)((16 - ((uintptr_t)p & 15)) & 15)), n16 = (n - lead) / 16;
+    const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (size_t)gridDim.x * blockDim.x;
+    uint4 *q = reinterpret_cast<uint4 *>(p + lead);
+    for (size_t i = t0; i < n16; i += nt) q[i] = make_uint4(w, w, w, w);
+    for (size_t i = t0; i < lead; i += nt) p[i] = (uint8_t)v8;  // (bytes before the first 16-B boundary)
+    for (size_t i = lead + 16 * n16 + t0; i < n; i += nt) p[i] = (uint8_t)v8;  // (and after the last)
+}
+__global__ __launch_bounds__(256) void fill_rows_kernel(float *p, int64_t ld, int64_t w, int64_t h) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < w * h; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / w;
+        p[r * ld + (i - r * w)] = 0.0f;
+    }
+}
+static hipError_t dev_fill(void *p, int v, size_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    fill_u8_kernel<<<(unsigned)std::max<size_t>(1, std::min<size_t>((n / 16 + 255) / 256, 1024)), 256, 0, s>>>(
+        (uint8_t *)p, n, (uint32_t)(v & 0xFF));
+    return hipGetLastError();
+}
+static hipError_t dev_zero_rows(float *p, int64_t ld, int64_t w, int64_t h, hipStream_t s) {
+    if (w <= 0 || h <= 0) return hipSuccess;
+    fill_rows_kernel<<<(unsigned)std::min<int64_t>((w * h + 255) / 256, 8192), 256, 0, s>>>(p, ld, w, h);
+    return hipGetLastError();
+}
+static int stream_capturing(hipStream_t s) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) != hipSuccess) return -1;
+    static const bool dbg = getenv("FP8A_DEBUG_CAPTURE") != nullptr;  // diagnostics: the query per lease
+    if (dbg) fprintf(stderr, "fp8a lease stream=%p capturing=%d\n", (void *)s, (int)st);
+    return st == hipStreamCaptureStatusActive ? 1 : 0;
+}
+// The lease of a captured launch: `need` bytes at the head of its workspace, zeroed in-stream.
+static bool capture_lease(hipStream_t s, void *ws, size_t ws_bytes, size_t need, ArenaLease &l) {
+    if (ws == nullptr || ws_bytes < need) return false;
+    static const bool dbg = getenv("FP8A_DEBUG_CAPTURE") != nullptr;
+    if (dbg) fprintf(stderr, "fp8a capture lease ws=%p need=%zu ws_bytes=%zu\n", ws, need, ws_bytes);
+    if (dev_fill(ws, 0, need, s) != hipSuccess) return false;
+    l.mine = (uint32_t *)ws;
+    l.clr = nullptr;
+    l.clr16 = 0;
+    return true;
+}
+static std::mutex g_arena_mu;
+static std::map<std::pair<int, uintptr_t>, FlagArena> g_arenas;
 static bool flag_arena(hipStream_t s, size_t need, ArenaLease &l) {
-    static std::mutex mu;
-    static std::map<std::pair<int, uintptr_t>, FlagArena> arenas;
+    static std::vector<void *> retired;  // grown-out-of arenas: never freed (in-flight launches may use them)
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return false;
     need = (need + 255) & ~(size_t)255;
-    std::lock_guard<std::mutex> lock(mu);
-    FlagArena &ar = arenas[{dev, (uintptr_t)s}];
+    std::lock_guard<std::mutex> lock(g_arena_mu);
+    FlagArena &ar = g_arenas[{dev, (uintptr_t)s}];
     if (ar.slot < need) {
         const size_t slot = std::max(need, std::max(2 * ar.slot, (size_t)65536));
-        if (ar.p) {
-            if (hipStreamSynchronize(s) != hipSuccess) return false;
-            (void)hipFree(ar.p);
-            ar = FlagArena{};
-        }
         void *p = nullptr;
         if (hipMalloc(&p, 2 * slot) != hipSuccess) return false;
-        if (hipMemsetAsync(p, 0, 2 * slot, s) != hipSuccess) {
+        if (dev_fill(p, 0, 2 * slot, s) != hipSuccess) {
             (void)hipFree(p);
             return false;
         }
+        if (ar.p) retired.push_back(ar.p);
+        ar = FlagArena{};
         ar.p = (uint32_t *)p;
         ar.slot = slot;
     }
@@ -964,6 +1022,17 @@ static bool flag_arena(hipStream_t s, size_t need, ArenaLease &l) {
     ar.dirty[ar.cur] = need;
     ar.cur = other;
     return true;
+}
+// A depthwise launch's gate word: the workspace head under capture, else an arena slot.
+static bool dw_lease(hipStream_t s, void *ws, size_t ws_bytes, ArenaLease &l) {
+    const int cap = stream_capturing(s);
+    if (cap < 0) return false;
+    return cap ? capture_lease(s, ws, ws_bytes, FLAG_BYTES, l) : flag_arena(s, FLAG_BYTES, l);
+}
+static int lease_error() {
+    const int rc = hip_check("fp8a flag arena");
+    return rc ? rc : fail(FP8A_EHIP, "fp8a flag arena: no room for the flag words (under stream capture they need "
+                                     "the workspace head)");
 }
 // grid blocks of 256 threads that clear a lease's other slot in about four 16-byte stores each
 static unsigned clear_blocks(const ArenaLease &l) { return (l.clr16 + 1023) / 1024; }
@@ -984,7 +1053,7 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     if (a.M == 0 || a.N == 0) return FP8A_OK;
     if (a.K == 0) {  // empty inner dimension: the reference's sum over an empty axis is 0
         if (a.nchw) return fail(FP8A_EINVAL, "empty convolution window");
-        if (hipMemset2DAsync(a.C, a.ldc * sizeof(float), 0, a.N * sizeof(float), a.M, s) != hipSuccess)
+        if (dev_zero_rows(a.C, a.ldc, a.N, a.M, s) != hipSuccess)
             return hip_check("fp8a zero fill");
         return FP8A_OK;
     }
@@ -1015,14 +1084,17 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     static const bool no_units = getenv("FP8A_NO_UNITS") != nullptr;  // diagnostics: whole-launch fallbacks
     const size_t head = ws_bytes >= head_bytes(a.M, a.N) ? head_bytes(a.M, a.N) : FLAG_BYTES;
     ArenaLease lease;
-    if (!flag_arena(s, head_bytes(a.M, a.N), lease)) return hip_check("fp8a flag arena");
+    const int cap = stream_capturing(s);  // (captured: the words live in the workspace head, flag_arena)
+    if (cap < 0) return hip_check("fp8a stream capture query");
+    if (cap ? !capture_lease(s, ws, ws_bytes, head, lease) : !flag_arena(s, head_bytes(a.M, a.N), lease))
+        return lease_error();
     a.flag = lease.mine;
     a.flag_out = (uint32_t *)ws;
     a.arena_clr = lease.clr;
     a.arena_clr16 = lease.clr16;
     a.nur = (a.M + 63) / 64;
     a.nuc = (a.N + 63) / 64;
-    a.urow = no_units ? nullptr : (uint8_t *)a.flag + FLAG_BYTES;
+    a.urow = no_units || (cap && head < head_bytes(a.M, a.N)) ? nullptr : (uint8_t *)a.flag + FLAG_BYTES;
     a.ucol = no_units ? nullptr : a.urow + a.nur;
     a.utile = no_units ? nullptr : a.ucol + a.nuc;
     // split-K when the caller's workspace holds the partials (else one split)
@@ -1107,11 +1179,11 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
     // pre-pass re-decodes its input from y (likewise under a GELU tail, which the emitting store
     // compiles out)
     if (a.em.w != nullptr && (a.em.form == 2 || (a.aw && a.wfmt != 0 && a.splits == 1) || a.post_act == 2)) {
-        if (hipMemsetAsync(a.em.invalid, 1, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a word image header");
+        if (dev_fill(a.em.invalid, 1, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a word image header");
         a.em.w = nullptr;
     }
     KernelEv kev{};
-    if (g_ktime) {
+    if (g_ktime && !cap) {  // (no host-side events inside a captured graph)
         kev.a = pool_event();
         kev.b = pool_event();
         kev.path = !a.aw ? PATH_FAST : a.wfmt == 0 ? PATH_F8MX : a.wfmt == 1 ? PATH_TT : a.wfmt == 4 ? PATH_V5MX : PATH_TT16;
@@ -1121,7 +1193,7 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
         if (kev.a && kev.b) (void)hipEventRecord(kev.a, s);
     }
     launch_fast(mode, a, s);
-    if (g_ktime && kev.a && kev.b) {
+    if (g_ktime && !cap && kev.a && kev.b) {
         (void)hipEventRecord(kev.b, s);
         g_kev.push_back(kev);
     }
@@ -1157,7 +1229,7 @@ static int run_qamaa(GemmArgs &a, hipStream_t s) {
     if (a.qM < 1 || a.qE < 1) return fail(FP8A_EFORMAT, "bad qamaa quantizer format");
     if (!a.nchw && a.ldc != a.N) return fail(FP8A_EINVAL, "qamaa output must be dense");
     if (a.K == 0) {
-        if (hipMemsetAsync(a.C, 0, (size_t)a.M * a.N * sizeof(float), s) != hipSuccess) return hip_check("fill");
+        if (dev_fill(a.C, 0, (size_t)a.M * a.N * sizeof(float), s) != hipSuccess) return hip_check("fill");
     } else {
         a.splits = 1;
         a.kchunk = a.K;
@@ -1204,9 +1276,8 @@ static int run_dense(DenseArgs a, void *ws, size_t wsb, hipStream_t s) {
     if (a.M == 0 || a.N == 0) return FP8A_OK;
     ++g_paths[PATH_DENSE];
     if (a.K == 0) {
-        const hipError_t e = a.conv ? hipMemsetAsync(a.y, 0, (size_t)(a.M * a.N) * sizeof(float), s)
-                                    : hipMemset2DAsync(a.y, (size_t)a.ldc * sizeof(float), 0, (size_t)a.N * sizeof(float),
-                                                       (size_t)a.M, s);
+        const hipError_t e = a.conv ? dev_fill(a.y, 0, (size_t)(a.M * a.N) * sizeof(float), s)
+                                    : dev_zero_rows(a.y, a.ldc, a.N, a.M, s);
         return e == hipSuccess ? FP8A_OK : hip_check("fp8a dense fill");
     }
     // a small convolution (the stem: K = 27, N = 32) as direct fp32 FMAs (dn_direct_kernel; option
@@ -1396,6 +1467,14 @@ int fp8a_path_stats(uint64_t *out, int reset) {
     if (out == nullptr) return fail(FP8A_EINVAL, "null pointer");
     for (int i = 0; i < PATH_N; ++i) out[i] = reset ? g_paths[i].exchange(0) : g_paths[i].load();
     return FP8A_OK;
+}
+
+size_t fp8a_flag_arena_slot_bytes(fp8a_stream_t stream) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    std::lock_guard<std::mutex> lock(g_arena_mu);
+    const auto it = g_arenas.find({dev, (uintptr_t)stream});
+    return it == g_arenas.end() ? 0 : it->second.slot;
 }
 
 int fp8a_kernel_timing(int enable) {
@@ -1775,7 +1854,7 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
     // v5 words (form 2) come from the staged v5 depthwise kernel only: any other launch flags them invalid
     EmitW em = em_in;
     if (em.w && (em.form == 2) != ((flags & F_V5) && cog == 1 && !post && groups > 1)) {
-        if (hipMemsetAsync(em.invalid, 1, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a word image header");
+        if (dev_fill(em.invalid, 1, sizeof(uint32_t), s) != hipSuccess) return hip_check("fp8a word image header");
         em = EmitW{};
     }
     if (res && (res == y || (((uintptr_t)res) & 15) != 0))
@@ -1805,7 +1884,7 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
             if (rc) return rc;
         }
         if (tbx_ok) {
-            if (!flag_arena(s, FLAG_BYTES, lease)) return hip_check("fp8a flag arena");
+            if (!dw_lease(s, workspace, workspace_bytes, lease)) return lease_error();
             gate = lease.mine;
             // the input's table-form words from the producing launch (fp8a_conv2d_chain, next_form 1:
             // header + [Bn][Cin][H][W] words of fq_in(x)); the pre-pass then runs gated on its header
@@ -1868,7 +1947,7 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
             if (rc) return rc;
             }
         } else if (fast_ok) {
-            if (!flag_arena(s, FLAG_BYTES, lease)) return hip_check("fp8a flag arena");
+            if (!dw_lease(s, workspace, workspace_bytes, lease)) return lease_error();
             gate = lease.mine;
             dim3 grid((unsigned)((Ho * Wo + 255) / 256), (unsigned)Cout, (unsigned)Bn);
             conv_tb_fast_kernel<<<grid, 256, 0, s>>>(x, w, y, Cin, H, W, Cout, kh, kw, sh, sw, ph, pw, dh, dw, groups,
@@ -1944,7 +2023,7 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
                               return lds <= 65536;
                           }();
         if (v5ds) {
-            if (!flag_arena(s, FLAG_BYTES, lease)) return hip_check("fp8a flag arena");
+            if (!dw_lease(s, workspace, workspace_bytes, lease)) return lease_error();
             gate = lease.mine;
             const unsigned g = (unsigned)(((d.planes + d.PB - 1) / d.PB) * d.nb);
             // (it emits the next convolution's v5 words when fp8a_conv2d_chain asked for them, em.form 2)
@@ -1960,9 +2039,9 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
             if (fq.mx) bA = fqi;
             ++g_paths[PATH_FAST];
         } else if (v5dw_ok) {
-            if (em.w && hipMemsetAsync(em.invalid, 1, sizeof(uint32_t), s) != hipSuccess)  // (no emission here)
+            if (em.w && dev_fill(em.invalid, 1, sizeof(uint32_t), s) != hipSuccess)  // (no emission here)
                 return hip_check("fp8a word image header");
-            if (!flag_arena(s, FLAG_BYTES, lease)) return hip_check("fp8a flag arena");
+            if (!dw_lease(s, workspace, workspace_bytes, lease)) return lease_error();
             gate = lease.mine;
             uint32_t *aw = (uint32_t *)((char *)workspace + FLAG_BYTES);
             uint2 *bwd = (uint2 *)((char *)workspace + FLAG_BYTES + awb);
@@ -1988,7 +2067,7 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
             ++g_paths[PATH_FAST];
         } else {
             ++g_paths[PATH_EXACT];
-            if (em.w && hipMemsetAsync(em.invalid, 1, sizeof(uint32_t), s) != hipSuccess)  // (no emission here)
+            if (em.w && dev_fill(em.invalid, 1, sizeof(uint32_t), s) != hipSuccess)  // (no emission here)
                 return hip_check("fp8a word image header");
             if (fq.mx) {
                 fq_bias_kernel<<<1, 1, 0, s>>>(fq, fqb, fqi);
@@ -2231,7 +2310,7 @@ int fp8a_conv2d_chain(const float *x, const float *w, float *y, int64_t Bn, int6
                          Bn * Cout * wi.H * wi.W < (1ll << 30);
         // the header: valid (0) with the next quantizer's constants before this launch emits,
         // invalid (nonzero) when it cannot emit
-        if (!can && hipMemsetAsync(out_image, 1, sizeof(uint32_t), s) != hipSuccess)
+        if (!can && dev_fill(out_image, 1, sizeof(uint32_t), s) != hipSuccess)
             return hip_check("fp8a word image header");
         if (can) {
             emit_prep_kernel<<<1, 1, 0, s>>>((uint32_t *)out_image, FqIn{next_maxval, qE, next_mbits, next_sign_bits},

@@ -72,7 +72,8 @@ def broadcast_quant_state(model, src=0):
     buffer of every quantizer's maxval.  Ranks that never calibrated receive the calibrated
     (e.g. per-channel) shapes.  Both tensors are built on the collective's device (RCCL rejects
     host tensors; a quantizer that never ran a forward still holds its maxval on the host), and
-    each received maxval stays there -- the GPU the forward runs on under RCCL."""
+    each received maxval is moved to the model's device -- the GPU the forward runs on (the
+    collective's own device under RCCL; gloo on a GPU model stages through the host)."""
     ws, rank = world()
     if ws == 1:
         return
@@ -96,6 +97,9 @@ def broadcast_quant_state(model, src=0):
     else:
         flat = torch.empty(total, dtype=torch.float32, device=dev)
     dist.broadcast(flat, src)
+    # the ranges live where the model runs (gloo's host buffers are staging only)
+    p0 = next(iter(model.parameters()), None)
+    flat = flat.to(p0.device if p0 is not None else dev)
     off = 0
     for q, h in zip(qs, hdr.tolist()):
         n, sb, nd = h[0], h[1], h[2]
@@ -129,13 +133,17 @@ def calibrate_on_rank0(model, batches, src=0, quantized=False):
 
 
 def gather_logits(logits):
-    """All-gather equal-sized per-rank logits into [world * B, C] (rank order)."""
+    """All-gather equal-sized per-rank logits into [world * B, C] (rank order), returned on the
+    logits' device.  RCCL gathers in place on the GPU; gloo (the one-GPU rehearsal of N ranks,
+    bench.py --dist-backend gloo) stages GPU logits through the host."""
     ws, _ = world()
     if ws == 1:
         return logits
-    out = torch.empty((ws * logits.shape[0],) + tuple(logits.shape[1:]), dtype=logits.dtype, device=logits.device)
-    dist.all_gather_into_tensor(out, logits.contiguous())
-    return out
+    dev = comm_device()
+    src = logits.contiguous().to(dev)
+    out = torch.empty((ws * logits.shape[0],) + tuple(logits.shape[1:]), dtype=logits.dtype, device=dev)
+    dist.all_gather_into_tensor(out, src)
+    return out.to(logits.device)
 
 
 def gather_scored(logits, labels, batch):

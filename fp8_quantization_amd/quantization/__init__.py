@@ -8,7 +8,7 @@ hijacker forward ordering.  The FP8 quantizer arithmetic runs in libfp8approx.so
 from .fp8_quantizer import FPQuantizer, quantize_to_fp8_ste_MM  # noqa: F401
 from .range_estimators import (AllMinMaxEstimator, CurrentMinMaxEstimator, RangeEstimators,  # noqa: F401
                                RunningMinMaxEstimator)
-from .quantization_manager import QuantizationManager, Qstates  # noqa: F401
+from .quantization_manager import QuantizationManager, QuantizerNotInitializedError, Qstates  # noqa: F401
 from .base_quantized_classes import FP32Acts, QuantizedActivation, QuantizedModule  # noqa: F401
 from .hijacker import QuantizationHijacker, activations_set  # noqa: F401
 from .quantized_folded_bn import BNFusedHijacker  # noqa: F401

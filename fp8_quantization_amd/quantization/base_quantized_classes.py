@@ -13,7 +13,9 @@ from .range_estimators import CurrentMinMaxEstimator, RunningMinMaxEstimator
 
 
 def _set_layer_fix_ranges(layer):
-    if isinstance(layer, QuantizationManager):
+    # (base_quantized_classes.py:23-28: a model-wide fix skips managers whose quantizer is not
+    # initialized; QuantizationManager.fix_ranges on one raises QuantizerNotInitializedError)
+    if isinstance(layer, QuantizationManager) and layer.quantizer.is_initialized:
         layer.fix_ranges()
     if isinstance(layer, QuantizedModule):
         layer.fix_ranges_flag = True

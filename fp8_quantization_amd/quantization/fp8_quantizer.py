@@ -46,6 +46,8 @@ class FPQuantizer(nn.Module):
 
     @property
     def is_initialized(self):
+        # always True, as the reference's FPQuantizer (fp8_quantizer.py:252-254): it starts from a
+        # default maxval, so fix_ranges never raises for it (QuantizationManager.fix_ranges)
         return True
 
     def forward(self, x_float):

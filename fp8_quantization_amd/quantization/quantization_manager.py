@@ -2,13 +2,22 @@
 
 States: estimate_ranges (every call updates the range estimate, then quantizes),
 fix_ranges (quantize only).  get_fp_bias() exposes the quantizer's custom_bias, the bias the
-approx operators read (hijacker.py:130-137).
+approx operators read (hijacker.py:130-137).  fix_ranges raises QuantizerNotInitializedError
+for a quantizer that reports itself uninitialized (quantization_manager.py:93-98); the FP8
+quantizer always reports initialized, as the reference's does (fp8_quantizer.py:252-254).
 """
 import enum
 
 from torch import nn
 
 from .range_estimators import RangeEstimators
+
+
+class QuantizerNotInitializedError(Exception):
+    """quantization/quantizers/utils.py:6-12."""
+
+    def __init__(self):
+        super().__init__("Quantizer has  not been initialized yet")
 
 
 class Qstates(enum.Enum):
@@ -49,6 +58,8 @@ class QuantizationManager(nn.Module):
         self._set_state(Qstates.estimate_ranges)
 
     def fix_ranges(self):
+        if not self.quantizer.is_initialized:  # quantization_manager.py:93-98
+            raise QuantizerNotInitializedError()
         self._set_state(Qstates.fix_ranges)
 
     def estimate_ranges_train(self):

@@ -75,6 +75,13 @@ int fp8a_fallback_stats(uint64_t *out, int reset);
 int fp8a_path_stats(uint64_t *out, int reset);
 
 /*
+ * Diagnostics: the byte size of one slot of the flag arena of (current device, stream), 0 before
+ * the stream's first eager launch.  Slots only grow (a launch that needs more allocates a larger
+ * arena; the old one is retired, never freed, so launches still in flight keep valid memory).
+ */
+size_t fp8a_flag_arena_slot_bytes(fp8a_stream_t stream);
+
+/*
  * Kernel timing for benchmarks: while enabled (fp8a_kernel_timing(1); returns the previous
  * state), every GEMM records HIP events on its stream around its product kernel launch(es) only
  * (not its operand pre-passes, split-K reduction or gated exact kernel).  fp8a_kernel_time
@@ -233,7 +240,11 @@ int fp8a_terms(const float *A, int64_t lda, const float *B, int64_t sbk, int64_t
  * and split-K partial sums; no im2col image: the GEMM gathers its operand rows from x).  A
  * smaller workspace that still holds the flag word runs without split-K.  Its first word receives
  * the launch's final flag word; the flags and unit marks themselves live in the library's
- * per-stream flag arena (no fill per launch; the first call on a stream allocates it).
+ * per-stream flag arena (no fill per launch; the first call on a stream allocates it) -- except
+ * while a HIP graph is being captured on the stream: a captured launch keeps them in the head of
+ * its workspace (fp8a_*_workspace_size's layout reserves it), zeroed by a fill kernel at the start of
+ * the launch (no graph memset node: DESIGN.md §3r), so every replay
+ * starts from zero flags and graphs never reference the arena (capture-safe).
  */
 size_t fp8a_conv2d_workspace_size(int64_t Bn, int64_t Cin, int64_t H, int64_t W, int64_t Cout,
                                   int kh, int kw, int sh, int sw, int ph, int pw, int dh, int dw,

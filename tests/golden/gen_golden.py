@@ -26,7 +26,9 @@ Fixture groups:
   g8_mbv2.npz       model level: the reference's QuantizedMobileNetV2
                     (models/mobilenet_v2_quantized_approx.py) over its float MobileNetV2
                     (width 0.25, 32x32, 10 classes, random weights and BN statistics) through
-                    estimate -> fix -> approx: the initial state, every layer's biases, logits
+                    estimate -> fix -> approx: the initial state, every layer's biases, logits,
+                    and per approx layer of the fixed-range forward its run_forward operands /
+                    product and its own input / output (teacher-forced layer tests)
 
 Usage:  python tests/golden/gen_golden.py      (about a minute on 8 cores)
 """
@@ -429,8 +431,28 @@ def gen_g8():
         with torch.no_grad(), contextlib.redirect_stdout(io.StringIO()):
             model(x_cal)
         model.fix_ranges()
+        # per approx layer of the fixed-range forward: what run_forward received (the quantized
+        # input and weight, the layer's own bias) and returned -- the product the engine replaces --
+        # and the layer's own input / output (approx_calculation.py:822-917, 1007-1023;
+        # quantized_folded_bn.py:30-83): the engine is teacher-forced on these, layer by layer
+        rec, hooks = {}, []
+        for lname, mod in model.named_modules():
+            if isinstance(mod, (ac.QCustomBNConv2dTorch, ac.QCustomLinearTorch)):
+                def run_forward(x, weight, bias, offsets=None, _m=mod, _n=lname, _f=type(mod).run_forward):
+                    y = _f(_m, x, weight, bias, offsets)
+                    rec[_n + "__x"], rec[_n + "__w"], rec[_n + "__y"] = x.clone(), weight.clone(), y.clone()
+                    return y
+                mod.run_forward = run_forward
+
+                def io_hook(m, inp, outp, _n=lname):
+                    rec[_n + "__in"], rec[_n + "__out"] = inp[0].clone(), outp.clone()
+                hooks.append(mod.register_forward_hook(io_hook))
         with torch.no_grad(), contextlib.redirect_stdout(io.StringIO()):
             logits = model(x_ev)
+        for h in hooks:
+            h.remove()
+        for k, v in rec.items():
+            out[f"{name}__L__{k}"] = v.numpy()
         for k, v in state.items():
             out[f"{name}__state__{k}"] = v.numpy()
         biases = []

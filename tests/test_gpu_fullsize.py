@@ -89,3 +89,98 @@ def test_conv_full_size_sampled(cfg):
     yc = y.cpu().numpy()
     got = np.stack([yc[b, chans, ho, wo] for (b, ho, wo) in picks])
     assert np.all(np.abs(got.astype(np.float64) - Cref) <= gio.sum_tolerance(S)), cfg["name"]
+
+
+def test_bench_workload_batch1024_sampled_through_fused_chain():
+    """The headline's own launches: bench.py's ResNet-18 E4M3 workload (same construction,
+    calibration batch and seeds) at its timed batch of 1024 images of 224 x 224, run through the
+    fused / chained model path bench.py times (input quantizer inside the product, BN + ReLU in the
+    store, the word-image hand-off from layer1.0.conv1 into layer1.0.conv2, the block tail in
+    conv2's store).  The stem conv (M = 12.8 M rows, output 3.29 GB: the largest word image and
+    split-K layout of the forward), layer1.0.conv1 and layer1.0.conv2 are checked on 40 output
+    pixels x 16 channels against the oracle on the same operands: the epilogue is monotone, so the
+    kernel's output must lie between the epilogue applied to ref -/+ the sum bar
+    (|acc - ref| <= 1e-5 sum|v|), widened by a few fp32 roundings of the epilogue's own arithmetic."""
+    import bench
+    from fp8_quantization_amd import approx_calculation as ac
+    from fp8_quantization_amd.approx_ops import fp8_fake_quantize
+    from fp8_quantization_amd.distributed import calibrate_on_rank0
+
+    cfg = dict(expo_width=4, mant_width=3, dnsmp_factor=3, withComp=False, with_approx=True, with_s2nn2s_opt=True,
+               quant_btw_mult_accu=True)
+    torch.manual_seed(0)  # (bench.run's order: seed, build with 4 BN-statistics batches, calibrate on 64 images)
+    model, in_shape, _ = bench.build_workload("resnet18", cfg, 4, torch.device(DEV))
+    model = model.to(DEV).eval()
+    calibrate_on_rank0(model, [bench.synthetic_images(64, 1234, DEV, in_shape)], quantized=True)
+    x = bench.synthetic_images(1024, 10, DEV, in_shape)
+    rng = np.random.default_rng(1024)
+    conv0, calls = ac.approx_conv2d, []
+
+    def record(xin, w, E, M, bA, bW, bR, table=None, **kw):
+        out = conv0(xin, w, E, M, bA, bW, bR, table, **kw)
+        if len(calls) >= 3:
+            return out
+        y, ib = (out[0], out[1]) if isinstance(out, tuple) else (out, None)
+        if kw.get("qin") is not None:  # the fused input quantizer: x arrives unquantized
+            mx, nb, mb, sb = kw["qin"]
+            xq, qb = fp8_fake_quantize(xin, mx, nb, mb, sb)
+            assert torch.equal(qb.reshape(-1), ib.reshape(-1)), "input quantizer bias"
+            bA = ib
+        else:
+            xq = xin
+        k, s, p = w.shape[2], kw["stride"][0], kw["padding"][0]
+        Bn, Cout, Ho, Wo = y.shape
+        picks = [(int(rng.integers(Bn)), int(rng.integers(Ho)), int(rng.integers(Wo))) for _ in range(40)]
+        chans = np.sort(rng.choice(Cout, 16, replace=False))
+        rows = np.stack([torch.nn.functional.pad(xq[b], (p, p, p, p))[:, ho * s:ho * s + k, wo * s:wo * s + k]
+                         .reshape(-1).cpu().numpy() for (b, ho, wo) in picks])
+        ci = torch.from_numpy(chans).to(DEV)
+        got = np.stack([y[b, ci, ho, wo].cpu().numpy() for (b, ho, wo) in picks])
+        post = kw.get("post")
+        res = None
+        if post is not None and post[0] is not None:
+            res = np.stack([post[0][b, ci, ho, wo].cpu().numpy() for (b, ho, wo) in picks]).astype(np.float64)
+        calls.append(dict(rows=rows, w=w[ci].reshape(len(chans), -1).t().contiguous().cpu().numpy(),
+                          bA=int(bA.reshape(-1)[0].item()), bW=bW.reshape(-1)[ci].cpu().numpy().astype(np.int32),
+                          bR=int(bR.reshape(-1)[0].item()), table=np.ascontiguousarray(table.numpy(), np.int32),
+                          flags=int(kw["flags"]), ep=kw.get("epilogue"), post=post, res=res, got=got, chans=chans,
+                          chain=kw.get("chain") is not None, shape=tuple(y.shape)))
+        return out
+
+    ac.approx_conv2d = record
+    try:
+        with torch.no_grad():
+            model(x)
+    finally:
+        ac.approx_conv2d = conv0
+    assert len(calls) == 3 and calls[0]["shape"] == (1024, 64, 112, 112) and calls[2]["chain"]
+    for i, c in enumerate(calls):
+        ref, S = orc.matmul(c["rows"], c["w"], 4, 3, c["bA"], c["bW"], c["bR"], c["table"], c["flags"], with_abs=True)
+        tol = gio.sum_tolerance(S)
+        lo, hi = ref - tol, ref + tol
+        slop = np.zeros_like(ref)
+        if c["ep"] is not None:  # BN as one fma per channel, then the clamp activation
+            ss, act, alo, ahi = c["ep"]
+            ssn = ss.cpu().numpy().astype(np.float64)[c["chans"]]
+            sc, sh = ssn[:, 0], ssn[:, 1]
+            lo, hi = np.minimum(lo * sc, hi * sc) + sh, np.maximum(lo * sc, hi * sc) + sh
+            slop += 2.0 ** -23 * (np.abs(ref * sc) + np.abs(sh))
+            if act:
+                lo, hi = np.clip(lo, alo, ahi), np.clip(hi, alo, ahi)
+        post = c["post"]
+        if post is not None:  # the block tail: + residual, clamp, output quantizer (all monotone)
+            if c["res"] is not None:
+                lo, hi = lo + c["res"], hi + c["res"]
+                slop += 2.0 ** -23 * np.abs(c["res"])
+            lo, hi = lo - 2 * slop, hi + 2 * slop
+            slop = np.zeros_like(ref)
+            if post[1]:
+                lo, hi = np.clip(lo, post[2], post[3]), np.clip(hi, post[2], post[3])
+            if post[4] is not None:
+                mx, nb, mb, sb = post[4]
+                q = lambda v: fp8_fake_quantize(torch.from_numpy(v.astype(np.float32)).to(DEV), mx, nb, mb, sb)[0] \
+                    .cpu().numpy().astype(np.float64)  # noqa: E731
+                lo, hi = q(np.nextafter(lo.astype(np.float32), -np.inf)), q(np.nextafter(hi.astype(np.float32), np.inf))
+        got = c["got"].astype(np.float64)
+        bad = (got < lo - 2 * slop) | (got > hi + 2 * slop)
+        assert not bad.any(), f"layer {i} {c['shape']}: {np.count_nonzero(bad)} sampled outputs outside the bar"
