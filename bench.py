@@ -311,7 +311,9 @@ def capture_forward(model, x, warm, sync, fallback_stats=None):
         if not (same and fb_same):
             return info, None
     except Exception as e:  # noqa: BLE001 -- report and time eager forwards instead
+        import traceback
         info["error"] = f"{type(e).__name__}: {e}"[:300]
+        info["where"] = "".join(traceback.format_tb(e.__traceback__)[-4:])[-1500:]
         sync()
         return info, None
 
@@ -407,6 +409,8 @@ def run(args, dev, rank=0, world=1):
                 ok = torch.tensor([1 if graph_info.get("captured") else 0], dtype=torch.int32, device=comm_dev)
                 dist.all_reduce(ok, op=dist.ReduceOp.MIN)
                 graph_info["all_ranks_captured"] = bool(int(ok.item()))
+                if not graph_info.get("captured"):  # (rank 0 alone prints the line: say why here)
+                    print(f"bench.py rank {rank}: no graph timing: {json.dumps(graph_info)}", file=sys.stderr, flush=True)
                 if int(ok.item()) == 0 and graph_info.get("captured"):
                     graph_info.update(captured=False, note="another rank's capture failed: eager forwards timed")
         if graph_info and graph_info.get("captured"):
@@ -439,11 +443,20 @@ def run(args, dev, rank=0, world=1):
     dense_fb = fa._lib.dense_stats() if cuda else None
     ktime = fa._lib.kernel_time(reset=True) if cuda else {}
     if args.dump_logits:  # one more step, after every counter was read (every rank: the gather is a collective)
+        import numpy as np
+        from fp8_quantization_amd.distributed import quantizers
         with torch.no_grad():
-            final = step()
+            local = model(x)
+            final = gather_logits(local)
         if rank == 0:
-            import numpy as np
             np.save(args.dump_logits, final.float().cpu().numpy())
+        # (each rank: its own logits and FP8 state, for diagnosing a mismatch)
+        st = {"logits": local.float().cpu().numpy()}
+        for i, q in enumerate(quantizers(model)):
+            st[f"q{i}_maxval"] = q.maxval.float().cpu().numpy()
+            if isinstance(q.custom_bias, torch.Tensor):
+                st[f"q{i}_bias"] = q.custom_bias.float().cpu().numpy()
+        np.savez(f"{args.dump_logits}.rank{rank}.npz", **st)
 
     op_ms = sum(s.elapsed_time(e) for (s, e, _, _) in prof)
     op_macs = sum(m for (_, _, m, _) in prof)

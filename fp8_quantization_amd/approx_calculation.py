@@ -22,7 +22,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from . import _lib
-from .approx_ops import (_res_quant_params, approx_conv2d, approx_matmul, approx_matmul_block, bias_epilogue,
+from .approx_ops import (_bias_dev, _res_quant_params, approx_conv2d, approx_matmul, approx_matmul_block, bias_epilogue,
                          dense_conv2d, dense_format, dense_matmul, grouped_conv2d, make_flags, make_flags_v5, qamaa_conv2d,
                          qamaa_matmul)
 from .error_tables import get_comp_table_NN_v5, get_error_table_NN
@@ -70,7 +70,8 @@ class ApproxOpMixin:
     @staticmethod
     def _default_bias(b, E, device):
         # approx_calculation.py:766-767: a missing act/res bias falls back to 2^(E-1)
-        return b if b is not None else torch.tensor([2 ** (E - 1)], dtype=torch.int32, device=device)
+        # (a cached device tensor: no host-to-device copy per forward, which a captured graph forbids)
+        return b if b is not None else _bias_dev(2 ** (E - 1), device)
 
     def _qamaa_params(self):
         return _res_quant_params(self.res_quantizer)

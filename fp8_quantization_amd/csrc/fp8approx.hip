@@ -850,6 +850,8 @@ static bool tt_form(int Mw, uint32_t flags, const TablePack &tab) {
 // round 5: ResNet-50 E3M4 2,045 -> 2,082 images/s with its K = 64 / 128 / 147 launches on the f16
 // form, profiles/r05_tt16_mink/ -- round 3's tt16 lost 3 % there)
 static int g_opt_tt16_mink = getenv("FP8A_TT16_MINK") ? std::max(0, atoi(getenv("FP8A_TT16_MINK"))) : 64;
+// option "tt_band" (default 1; FP8A_TT_BAND): gemm_tt_kernel's band / zero wave-tile forms (gemm_tt.h)
+static int g_opt_tt_band = getenv("FP8A_TT_BAND") ? atoi(getenv("FP8A_TT_BAND")) : 1;
 static bool tt16_form(int Mw, bool f7, int64_t K) {
     static const bool no_tt16 = getenv("FP8A_NO_TT16") != nullptr;
     return !no_tt16 && Mw == 4 && (f7 || K >= g_opt_tt16_mink);
@@ -1128,6 +1130,7 @@ static int run_gemm(GemmArgs &a, const int32_t *table, void *ws, size_t ws_bytes
             a.ttf7 = 0;
             for (int i = 0; tt && i < (1 << (2 * a.Mw)); ++i) a.ttf7 |= a.tab.raw[i] < 0;
             a.wfmt = v5mx ? 4 : tt ? (tt16_form(a.Mw, a.ttf7, a.K) ? 2 : 1) : 0;
+            if (a.wfmt == 1 && !g_opt_tt_band) a.ebr = nullptr;  // (gemm_tt_kernel: no band test)
             a.xncg = tt ? 4 : xm_ncg(a.N);
             // the input's word image from the previous launch (fp8a_conv2d_chain): its words replace
             // the A pre-pass, which then runs gated (only to write the fused quantizer's bias, or to
@@ -1515,6 +1518,11 @@ int fp8a_set_option(const char *name, int value) {
     if (strcmp(name, "af32_maxct") == 0) {
         const int old = g_opt_af32_maxct;
         g_opt_af32_maxct = std::max(0, value);
+        return old;
+    }
+    if (strcmp(name, "tt_band") == 0) {
+        const int old = g_opt_tt_band;
+        g_opt_tt_band = value;
         return old;
     }
     if (strcmp(name, "tt16_mink") == 0) {

@@ -63,17 +63,24 @@ def broadcast_model_state(model, src=0):
                 off += n
 
 
-_HDR = 8  # per quantizer: numel, sign_bits, ndim, up to 5 dims
+_HDR = 16  # per quantizer: maxval numel, sign_bits, ndim, 5 dims; custom_bias numel (-1: None), ndim, 5 dims
 
 
 def broadcast_quant_state(model, src=0):
     """Make every rank's FP8 ranges identical to rank `src`'s with two broadcasts in all: one
-    int64 header [quantizers, 8] (maxval element count, sign_bits, maxval shape) and one float32
-    buffer of every quantizer's maxval.  Ranks that never calibrated receive the calibrated
-    (e.g. per-channel) shapes.  Both tensors are built on the collective's device (RCCL rejects
-    host tensors; a quantizer that never ran a forward still holds its maxval on the host), and
-    each received maxval is moved to the model's device -- the GPU the forward runs on (the
-    collective's own device under RCCL; gloo on a GPU model stages through the host)."""
+    int64 header [quantizers, 16] (maxval element count, sign_bits and shape; custom_bias element
+    count and shape) and one float32 buffer of every quantizer's maxval and custom_bias.  Ranks that
+    never calibrated receive the calibrated (e.g. per-channel) shapes.
+
+    custom_bias travels too: an activation / weight quantizer rewrites it on every forward, but the
+    res quantizer of a fixed-range approx layer runs only during calibration (hijacker.py:77-115),
+    so its custom_bias -- the layer's bR -- exists only where calibration ran; without it the other
+    ranks would fall back to 2^(E-1) (approx_calculation.py:766-767) and compute other products.
+
+    Both tensors are built on the collective's device (RCCL rejects host tensors; a quantizer that
+    never ran a forward still holds its maxval on the host), and each received tensor is moved to
+    the model's device -- the GPU the forward runs on (the collective's own device under RCCL; gloo
+    on a GPU model stages through the host)."""
     ws, rank = world()
     if ws == 1:
         return
@@ -85,15 +92,24 @@ def broadcast_quant_state(model, src=0):
     if rank == src:
         for i, q in enumerate(qs):
             shp = list(q.maxval.shape)
-            if len(shp) > _HDR - 3:
-                raise ValueError(f"maxval of rank {rank} has {len(shp)} dims; at most {_HDR - 3} are supported")
+            cb = q.custom_bias
+            cshp = list(cb.shape) if isinstance(cb, torch.Tensor) else []
+            if len(shp) > 5 or len(cshp) > 5:
+                raise ValueError(f"maxval / custom_bias of rank {rank} have more than 5 dims")
             hdr[i, :3 + len(shp)] = torch.tensor([q.maxval.numel(), int(q.sign_bits), len(shp)] + shp)
+            hdr[i, 8:10 + len(cshp)] = torch.tensor([cb.numel() if isinstance(cb, torch.Tensor) else -1, len(cshp)]
+                                                    + cshp)
     hdr = hdr.to(dev)
     dist.broadcast(hdr, src)
     hdr = hdr.cpu()
-    total = int(hdr[:, 0].sum())
+    total = int(hdr[:, 0].sum() + hdr[:, 8].clamp(min=0).sum())
     if rank == src:
-        flat = torch.cat([q.maxval.detach().reshape(-1).to(device=dev, dtype=torch.float32) for q in qs])
+        parts = []
+        for q in qs:
+            parts.append(q.maxval.detach().reshape(-1).to(device=dev, dtype=torch.float32))
+            if isinstance(q.custom_bias, torch.Tensor):
+                parts.append(q.custom_bias.detach().reshape(-1).to(device=dev, dtype=torch.float32))
+        flat = torch.cat(parts)
     else:
         flat = torch.empty(total, dtype=torch.float32, device=dev)
     dist.broadcast(flat, src)
@@ -106,6 +122,13 @@ def broadcast_quant_state(model, src=0):
         q.maxval = flat[off:off + n].clone().view(h[3:3 + nd])
         q.sign_bits = sb
         off += n
+        cn, cnd = h[8], h[9]
+        if cn >= 0:
+            cb = flat[off:off + cn].clone().view(h[10:10 + cnd])
+            if rank != src:
+                q.custom_bias = cb
+                cb._fp8a_i32 = cb.reshape(-1).to(torch.int32)  # (as fp8_fake_quantize leaves it)
+            off += cn
 
 
 def calibrate_on_rank0(model, batches, src=0, quantized=False):

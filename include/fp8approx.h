@@ -109,7 +109,8 @@ int fp8a_kernel_time(double *out, int reset);
  * / 4 columns; "af32_maxct" (default 1, times sh x sw for a strided conv; FP8A_AF32_MAXCT) -- the most column tiles for which a 1x1
  * conv / matrix A is decoded inside gemm_f8mx_kernel instead of by its pre-pass (0 = never);
  * "tt16_mink" (default 64; FP8A_TT16_MINK) -- the smallest K of an E3M4 launch (unsigned error
- * table) on the packed-f16 tile-table kernel (shorter K: the f32 form).
+ * table) on the packed-f16 tile-table kernel (shorter K: the f32 form); "tt_band" (default 1;
+ * FP8A_TT_BAND) -- gemm_tt_kernel's band / zero wave-tile forms (0 = the general form everywhere).
  * All of these change the schedule only: the outputs are bit-identical.  Returns the previous value, or FP8A_EINVAL
  * for an unknown name.  Not synchronised with launches in flight on other threads.
  */

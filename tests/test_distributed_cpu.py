@@ -42,6 +42,8 @@ def _worker(rank, ws, port, q):
         holder = torch.nn.Module()
         holder.q = FPQuantizer(n_bits=8, mantissa_bits=3, set_maxval=True)
         holder.q.maxval = torch.tensor([1.0 + rank])
+        # a res quantizer's custom_bias (bR) exists only where calibration ran: it must travel too
+        holder.q.custom_bias = torch.tensor([5.0]) if rank == 0 else None
         # a per-channel quantizer: rank 0 calibrated it ([3, 1] ranges, unsigned); the other rank
         # never ran a forward and holds its maxval on a device the collective cannot use (here
         # 'meta', on a GPU box the host while RCCL needs the GPU) -- it must not be touched
@@ -61,7 +63,9 @@ def _worker(rank, ws, port, q):
         m.register_buffer("mask", torch.tensor([rank == 0, rank == 1]))
         broadcast_model_state(m, src=0)
         state = dict(w=m.weight.tolist(), count=m.count.tolist(), mask=m.mask.tolist(), wdev=str(holder.w.maxval.device),
-                     wmax=holder.w.maxval.tolist(), wsign=holder.w.sign_bits)
+                     wmax=holder.w.maxval.tolist(), wsign=holder.w.sign_bits,
+                     qcb=holder.q.custom_bias.tolist(), qcb_i32=holder.q.custom_bias._fp8a_i32.tolist()
+                     if rank else [5], wcb=holder.w.custom_bias)
         # (tensors by value: a shared-memory handle can outlive this process and fail to open)
         q.put((rank, allg.numpy().copy(), topk_correct(allg, labels), float(holder.q.maxval[0]), (x @ w).numpy().copy(),
                state))
@@ -98,6 +102,7 @@ def test_gloo_world2_gather_and_broadcast():
         assert acc == res[0][2]
         assert st["wdev"] == "cpu" and st["wmax"] == [[0.5], [2.0], [8.0]] and st["wsign"] == 0
         assert st["w"] == [[0.0] * 3] * 2 and st["count"] == [7] and st["mask"] == [True, False]
+        assert st["qcb"] == [5.0] and st["qcb_i32"] == [5] and st["wcb"] is None
 
 
 # ---------------------------------------------------------------------------------------------

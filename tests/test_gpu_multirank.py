@@ -18,8 +18,11 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# (no BN-statistics estimation: it runs the float model on MIOpen, whose algorithm choice -- and so
+# the last bits of the statistics -- may differ between processes sharing the GPU; the state
+# broadcast makes the ranks agree, but a separate world-1 process would then calibrate another model)
 COMMON = ["--arch", "resnet18", "--batch", "4", "--steps", "2", "--warmup", "1", "--cal-batch", "4",
-          "--bn-stats-batches", "1", "--no-cpu-baseline"]
+          "--bn-stats-batches", "0", "--no-cpu-baseline"]
 
 
 def _bench(args, timeout=420):
@@ -38,7 +41,7 @@ def test_bench_two_ranks_on_one_gpu_match_world1_shards(tmp_path):
     line = _bench(["--gpus", "2", "--dist-backend", "gloo", "--share-device", "--dump-logits", two] + COMMON)
     assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 8 and line["config"]["parallelism"] == "dp2"
     hg = line["hip_graph"]
-    assert hg["captured"] and hg["all_ranks_captured"] and hg["replay_matches_eager_bitwise"], hg
+    assert hg["captured"] and hg["all_ranks_captured"] and hg["replay_matches_eager_bitwise"], json.dumps(hg)
     assert line["value"] > 0
     shards = []
     for r in (0, 1):

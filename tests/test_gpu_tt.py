@@ -279,3 +279,49 @@ def test_e3m4_above_top_binade_takes_f32_form(kind):
     assert flag == 4, f"flag {flag}"
     ref, S = orc.matmul(A, W.T, E, M, bA, bB, bR, tab, fl, with_abs=True)
     _close(C, ref, S, "above top binade")
+
+
+@pytest.mark.parametrize("regime", ["band", "zero", "mixed"])
+@pytest.mark.parametrize("fmt,kind", [((2, 5), "nocomp"), ((2, 5), "none"), ((3, 4), "nocomp")],
+                         ids=["E2M5", "E2M5-notable", "E3M4"])
+def test_band_and_zero_wave_tiles_bit_identical(fmt, kind, regime):
+    """gemm_tt_kernel's band / zero wave-tile forms (round 6, csrc/gemm_tt.h): a staged tile whose
+    products all lie below the result grid's smallest normal takes fma(t, c_a, cmin) - cmin per
+    term, one whose products all lie below half the subnormal quantum adds nothing.  Results are
+    bit-identical to the general form (option tt_band 0), within the sum bar of the oracle, and the
+    terms are bit-exact (a K-step-sparse layout makes every output one term).  E3M4 at K = 48 runs
+    gemm_tt_kernel<4> (the packed-f16 form starts at K = 64)."""
+    from fp8_quantization_amd import _lib
+    E, M = fmt
+    import zlib
+    rng = np.random.default_rng(zlib.crc32(f"{E}{kind}{regime}".encode()))
+    bA = (1 << (E - 1)) + 2
+    Mr, K, N = 300, 48 if E == 3 else 160, 80
+    A = _grid(rng, E, M, (Mr, K), bA, zero_frac=0.4)
+    bB = rng.integers((1 << (E - 1)) + 5, (1 << (E - 1)) + 8, size=N).astype(np.int32)
+    W = _grid(rng, E, M, (N, K), bB[:, None])
+    top = (1 << E) - bA + int((1 << E) - bB.min())  # >= the largest e_a + e_b + 2: |a b| < 2^top
+    # band: 2^top <= the grid's smallest normal 2^(1 - bR); zero: 2^top <= half its quantum 2^(-bR - M)
+    bR = {"band": 1 - top, "zero": -top - M, "mixed": bA + 2}[regime]
+    tab, fl = _table(E, M, kind), _flags(kind)
+    old = _lib.set_option("tt_band", 1)
+    try:
+        C1, f1 = _matmul_raw(A, K, W, 1, K, Mr, N, K, E, M, bA, bB, bR, tab, fl)
+        _lib.set_option("tt_band", 0)
+        C0, f0 = _matmul_raw(A, K, W, 1, K, Mr, N, K, E, M, bA, bB, bR, tab, fl)
+    finally:
+        _lib.set_option("tt_band", old)
+    assert f1 == 0 and f0 == 0
+    assert np.array_equal(C1.view(np.uint32), C0.view(np.uint32)), "band forms differ from the general form"
+    ref, S = orc.matmul(A, W.T, E, M, bA, bB, bR, tab, fl, with_abs=True)
+    _close(C1, ref, S, regime)
+    if regime == "zero":
+        assert not np.any(C1), "every product is below half the quantum: every term is 0"
+    # terms: one nonzero K-step per row (the others zero), so each output is a single term
+    As = np.zeros_like(A)
+    ks = rng.integers(0, K, size=Mr)
+    As[np.arange(Mr), ks] = A[np.arange(Mr), ks]
+    Ct, ft = _matmul_raw(As, K, W, 1, K, Mr, N, K, E, M, bA, bB, bR, tab, fl)
+    assert ft == 0
+    T = orc.terms(As, W.T, E, M, bA, bB, bR, tab, fl)  # [Mr, K, N]
+    _terms_equal(Ct, T[np.arange(Mr), ks, :])

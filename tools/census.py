@@ -132,6 +132,55 @@ def layer_census(xq, w, bR, M, table, groups, widths=(16, 64)):
                 zero_a_fraction=float(Z.sum() / (Z.sum() + H.sum())))
 
 
+def tile_census(xq, w, bR, groups, stride, padding, dilation, kblk, rowblk=64, colblk=16):
+    """Fraction of the tile-table kernels' wave-tiles (rowblk consecutive output rows x kblk
+    consecutive K-steps x colblk columns) whose products all lie below the result grid's smallest
+    normal 2^(1 - bR) -- where the Q_R rounding constant is the fixed cmin (a 4-op loop instead of
+    7, gemm_tt.h) -- and whose products all lie at or above it (6 ops, no max)."""
+    import torch.nn.functional as F
+    if w.dim() == 2:
+        A = xq.reshape(-1, xq.shape[-1])
+        Bs = [w.t()]
+        As = [A]
+    else:
+        cin_g, cout_g = xq.shape[1] // groups, w.shape[0] // groups
+        As, Bs = [], []
+        for g in range(groups):
+            cols = F.unfold(xq[:, g * cin_g:(g + 1) * cin_g], w.shape[2:], dilation=dilation, padding=padding,
+                            stride=stride)
+            As.append(cols.transpose(1, 2).reshape(-1, cols.shape[1]))
+            Bs.append(w[g * cout_g:(g + 1) * cout_g].reshape(cout_g, -1).t())
+    band = normal = total = 0.0
+    t = 1 - int(bR)
+    for A, B in zip(As, Bs):
+        ea = binades(A) - OFF
+        ea = torch.where(ea < -OFF, torch.full_like(ea, -10 ** 6), ea)  # zeros never raise the max
+        eb = binades(B) - OFF
+        eb = torch.where(eb < -OFF, torch.full_like(eb, -10 ** 6), eb)
+        M_, K_ = ea.shape
+        N_ = eb.shape[1]
+        pm, pk, pn = (-M_) % rowblk, (-K_) % kblk, (-N_) % colblk
+        big = 10 ** 6
+        ea_lo = torch.where(ea < -big // 2, torch.full_like(ea, big), ea)  # zeros never lower the min
+        eb_lo = torch.where(eb < -big // 2, torch.full_like(eb, big), eb)
+        ea = F.pad(ea, (0, pk, 0, pm), value=-big)
+        ea_lo = F.pad(ea_lo, (0, pk, 0, pm), value=big)
+        eb = F.pad(eb, (0, pn, 0, pk), value=-big)
+        eb_lo = F.pad(eb_lo, (0, pn, 0, pk), value=big)
+        Mb, Kb, Nb = ea.shape[0] // rowblk, ea.shape[1] // kblk, eb.shape[1] // colblk
+        amax = ea.reshape(Mb, rowblk, Kb, kblk).amax(dim=(1, 3))
+        amin = ea_lo.reshape(Mb, rowblk, Kb, kblk).amin(dim=(1, 3))
+        bmax = eb.reshape(Kb, kblk, Nb, colblk).amax(dim=(1, 3))
+        bmin = eb_lo.reshape(Kb, kblk, Nb, colblk).amin(dim=(1, 3))
+        for i0 in range(0, Mb, 4096):  # (chunks: [Mb, Kb, Nb] booleans)
+            hi = amax[i0:i0 + 4096, :, None] + bmax[None] + 2
+            lo = amin[i0:i0 + 4096, :, None] + bmin[None] - 1  # V >= 1/2 for the tables here (vmin >= -1)
+            band += float((hi <= t).sum())
+            normal += float((lo >= t).sum())
+            total += float(hi.numel())
+    return dict(band_only=band / max(total, 1), normal_only=normal / max(total, 1), wave_tiles=total)
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--arch", default="resnet50")
@@ -139,6 +188,8 @@ def main(argv=None):
     ap.add_argument("--mant-width", type=int, default=5)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--tiles", action="store_true", help="also the tile-table kernels' wave-tile census")
+    ap.add_argument("--tile-batch", type=int, default=8)
     args = ap.parse_args(argv)
     import bench
     from fp8_quantization_amd import approx_calculation as ac
@@ -163,6 +214,10 @@ def main(argv=None):
             mx, nb, mb, sb = kw["qin"]
             xq = fp8_fake_quantize(xin, mx, nb, mb, sb)[0]
         c = layer_census(xq, w, int(bR.reshape(-1)[0].item()), M_, table, kw.get("groups", 1))
+        if args.tiles:
+            xs = xq[:args.tile_batch]
+            c["tiles"] = tile_census(xs, w, int(bR.reshape(-1)[0].item()), kw.get("groups", 1), kw["stride"],
+                                     kw["padding"], kw["dilation"], 2 if M_ == 5 else 4)
         c.update(kind="conv", shape=list(w.shape), groups=kw.get("groups", 1),
                  macs=float(out[0].numel() if isinstance(out, tuple) else out.numel()) * w[0].numel())
         layers.append(c)
@@ -171,6 +226,8 @@ def main(argv=None):
     def mm(a, b, E_, M_, bA, bB, bR, table=None, **kw):
         out = mm0(a, b, E_, M_, bA, bB, bR, table, **kw)
         c = layer_census(a, b.t(), int(bR.reshape(-1)[0].item()), M_, table, 1)
+        if args.tiles:
+            c["tiles"] = tile_census(a, b.t(), int(bR.reshape(-1)[0].item()), 1, None, None, None, 2 if M_ == 5 else 4)
         c.update(kind="mm", shape=[b.shape[1], b.shape[0]], groups=1, macs=float(a.shape[0] * b.shape[0] * b.shape[1]))
         layers.append(c)
         return out
@@ -196,6 +253,10 @@ def main(argv=None):
                    segments={W: {k: v / s["nonzero_a_segments"] for k, v in s.items() if k != "nonzero_a_segments"}
                              for W, s in seg.items()},
                    zero_a_fraction=sum(c["zero_a_fraction"] for c in layers) / max(1, len(layers)))
+    if args.tiles:  # MAC-weighted over the layers
+        wsum = sum(c["macs"] for c in layers)
+        summary["wave_tiles"] = {k: sum(c["tiles"][k] * c["macs"] for c in layers) / wsum
+                                 for k in ("band_only", "normal_only")}
     print(json.dumps(summary))
     for i, c in enumerate(layers):
         p = c["products"]
@@ -203,7 +264,8 @@ def main(argv=None):
         print(f"{i:3d} {c['kind']} {c['shape']} g{c['groups']} bRnorm={c['t_norm']} vmin={c['vmin']} "
               f"prod safe {p['safe'] / max(p['nonzero'], 1):.3f} band {p['band'] / max(p['nonzero'], 1):.3f} "
               f"zero {p['zero'] / max(p['nonzero'], 1):.3f} | seg64 safe {s64['all_safe'] / max(s64['nonzero_a_segments'], 1):.3f} "
-              f"mixed {s64['mixed'] / max(s64['nonzero_a_segments'], 1):.3f}")
+              f"mixed {s64['mixed'] / max(s64['nonzero_a_segments'], 1):.3f}"
+              + (f" | tiles band {c['tiles']['band_only']:.3f} normal {c['tiles']['normal_only']:.3f}" if "tiles" in c else ""))
     if args.out:
         with open(args.out, "w") as f:
             json.dump(dict(summary=summary, layers=layers), f)
