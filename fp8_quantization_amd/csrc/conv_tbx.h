@@ -18,7 +18,7 @@
 //     carries that trigger value per (m_a, m_b) beside L.
 // Per term that is an LDS read, two multiplies and two compare-selects (~13 VALU ops against
 // ~30 for the general form).  A is pre-decoded once per launch into words (sign/exponent bits of
-// a | m_a << 6, so the table byte offset is one v_and_or with m_b << 3); each thread computes 4
+// a | m_a << 3, so the table byte offset is one v_and_or with m_b << 6); each thread computes 4
 // consecutive outputs of one row and gathers the input words they share once.  Off-grid inputs,
 // the exactness window and the bias window raise the gate word and conv_tb_direct_kernel
 // recomputes the launch exactly (as behind conv_tb_fast_kernel).
@@ -41,10 +41,10 @@ __device__ __forceinline__ uint32_t tbx_word(float v, const FqIn &fq, float fmx,
     if (fq.mx) v = fq_apply(v, fmx, fbias, fq.M, fq.S);
     const uint32_t u = __float_as_uint(v), ua = u & 0x7FFFFFFFu;
     bad |= (ua != 0u) && ((ua & lowm) != 0u || ua < 0x20800000u || ua > 0x58800000u);
-    return ua == 0u ? 0u : ((u & 0xFF800000u) | (((ua >> (23 - M)) & mmask) << 6));
+    return ua == 0u ? 0u : ((u & 0xFF800000u) | (((ua >> (23 - M)) & mmask) << 3));
 }
 
-// x (NCHW floats) -> words: (bits(x) & 0xFF800000) | (m << 6); 0 for zeros; gate on off-grid
+// x (NCHW floats) -> words: (bits(x) & 0xFF800000) | (m << 3); 0 for zeros; gate on off-grid
 // values / the exactness window (tensor-bias decode: every value at its own binade).
 // With fused input quantization (fq.mx set) the values are fq(x) and the quantizer's bias is
 // written to fq_bias / fq_ibias (the kernels' bA).
@@ -75,12 +75,15 @@ __global__ __launch_bounds__(256) void tbx_decode_a(const float *x, int64_t n, u
     if (__syncthreads_or(bad ? 1 : 0) && threadIdx.x == 0) atomicOr(gate, 1u);
 }
 
-// The table entry (L, F7 trigger) for (m_a, m_b) = (i >> 3, i & 7) at result bias r_b (the
-// derivation in the header; rows / columns past 2^M are unused).
+// The table entry (L, F7 trigger) for (m_b, m_a) = (i >> 3, i & 7) at result bias r_b (the
+// derivation in the header; rows / columns past 2^M are unused).  Layout [m_b][m_a] (round 6; was
+// [m_a][m_b]): a tap reads the 8 entries of its m_b, 8 B apart, so the lanes of a ds_read_b64
+// group hit distinct banks (the [m_a][m_b] layout put m_a and m_a + 4 on one bank: 56 % of the
+// kernel's LDS cycles were bank conflicts, profiles/r06_dw/).
 template <int M>
 __device__ __forceinline__ float2 tbx_lut_entry(int i, const TablePack &tab, int r_b) {
     constexpr float ULP = 1.0f / (1 << M);  // 2^-M
-    const int ma = i >> 3, mb = i & 7;
+    const int mb = i >> 3, ma = i & 7;
     const int tv = (ma < (1 << M) && mb < (1 << M)) ? tab.raw[(ma << M) | mb] : 0;
     const float u = (1.0f + ULP * ma) * (1.0f + ULP * mb);  // exact
     const float v = __fmaf_rn(1.0f + ULP * ma, 1.0f + ULP * mb, -ULP * (float)tv);
@@ -93,10 +96,11 @@ __device__ __forceinline__ float2 tbx_lut_entry(int i, const TablePack &tab, int
     return make_float2(L, __uint_as_float(f7));
 }
 
-// One term of the table form: input word wa, the tap's c_b and m_b << 3, the table in LDS.
-__device__ __forceinline__ float tbx_term(uint32_t wa, float cB, uint32_t mb8, const char *lut, uint32_t q0exp,
+// One term of the table form: input word wa (m_a << 3 in its bits 3-5), the tap's c_b and m_b << 6,
+// the table in LDS.
+__device__ __forceinline__ float tbx_term(uint32_t wa, float cB, uint32_t mb64, const char *lut, uint32_t q0exp,
                                           float twoq) {
-    const float2 e = *reinterpret_cast<const float2 *>(lut + ((wa & 0x1C0u) | mb8));
+    const float2 e = *reinterpret_cast<const float2 *>(lut + ((wa & 0x38u) | mb64));
     const float cab = __uint_as_float(wa & 0xFF800000u) * cB;  // exact
     float rv = e.x * cab;                                        // exact
     const float rs = __fmaf_rn(2.0f, rv, -copysignf(twoq, rv));  // expo field 0
@@ -165,7 +169,7 @@ __global__ __launch_bounds__(256) void conv_tbx_kernel(const uint32_t *aw, const
                         const uint32_t bw = __float_as_uint(wk[ky * KW + kx]), bwa = bw & 0x7FFFFFFFu;
                         bad |= (bwa != 0u) && ((bwa & LOWM) != 0u || bwa < 0x20800000u || bwa > 0x58800000u);
                         const float cB = __uint_as_float(bw & 0xFF800000u);
-                        const uint32_t mb8 = ((bwa >> (23 - M)) & MMASK) << 3;
+                        const uint32_t mb8 = ((bwa >> (23 - M)) & MMASK) << 6;  // (m_b << 6: the table row)
 #pragma unroll
                         for (int q = 0; q < TBX_TW; ++q)
                             acc[j][q] += tbx_term(col[q * SW + kx], cB, mb8, lut, q0exp, twoq);
@@ -235,7 +239,7 @@ __global__ __launch_bounds__(256) void conv_tbs_kernel(const float *x, const flo
         bad |= !(wb >= 2 && wb <= 120);
         const uint32_t bw = __float_as_uint(w[(int64_t)c * 9 + d - 9 * pl]), bwa = bw & 0x7FFFFFFFu;
         bad |= (bwa != 0u) && ((bwa & LOWM) != 0u || bwa < 0x20800000u || bwa > 0x58800000u);
-        sB[d] = make_uint2(bw & 0xFF800000u, ((bwa >> (23 - M)) & MMASK) << 3);
+        sB[d] = make_uint2(bw & 0xFF800000u, ((bwa >> (23 - M)) & MMASK) << 6);
     }
     dw_stage(x, P0, npl, t.H, t.W, hi0, t.pw, t.RS, t.WS, t.inv_w, t.inv_hw, t.RB == t.Ho, sw,
              [&](float v) { return tbx_word(v, fq, fmx, fbias, LOWM, MMASK, M, bad); });
@@ -288,8 +292,21 @@ __global__ __launch_bounds__(256) void conv_tbs_kernel(const float *x, const flo
 // each value turned into its table-form word in place (input quantizer, tbx_word and its window /
 // grid checks), then 4 outputs per thread as conv_tbs_kernel: the same terms in the same order,
 // the same bits, the same gate.
+// The staged depthwise kernels' tap rows (ky) run as a loop, not unrolled (round 6): unrolled, the
+// compiler hoisted every LDS read of the 36 terms and held the kernels at 116-126 VGPRs (4 waves /
+// SIMD, 42 % of the wave cycles waiting); rolled, 41-56 VGPRs: MobileNetV2 E4M3 +3 %, E5M2 v9 +3.3 %,
+// v5 +0.5 % (profiles/r06_dw/).  TBSG_WAVES: an occupancy floor for A/B builds (it spills).
+#ifndef TBSG_WAVES
+#define TBSG_WAVES 1
+#endif
+#ifndef TBSG_KYU
+#define TBSG_KYU 1
+#endif
+#ifndef V5DS_KYU
+#define V5DS_KYU 1
+#endif
 template <int S, int M>
-__global__ __launch_bounds__(256) void conv_tbsg_kernel(const float *x, const float *w, float *y, const DwArgs p,
+__global__ __launch_bounds__(256, TBSG_WAVES) void conv_tbsg_kernel(const float *x, const float *w, float *y, const DwArgs p,
                                                         FqIn fq, float *fq_bias_out, int32_t *fq_ibias_out,
                                                         const int32_t *bA, const int32_t *bW, const int32_t *bR,
                                                         TablePack tab, uint32_t *gate, const float2 *ep, int ep_act,
@@ -340,7 +357,7 @@ __global__ __launch_bounds__(256) void conv_tbsg_kernel(const float *x, const fl
         bad |= !(wb >= 2 && wb <= 120);
         const uint32_t bw = __float_as_uint(w[(int64_t)c * 9 + d - 9 * pl]), bwa = bw & 0x7FFFFFFFu;
         bad |= (bwa != 0u) && ((bwa & LOWM) != 0u || bwa < 0x20800000u || bwa > 0x58800000u);
-        sB[d] = make_uint2(bw & 0xFF800000u, ((bwa >> (23 - M)) & MMASK) << 3);
+        sB[d] = make_uint2(bw & 0xFF800000u, ((bwa >> (23 - M)) & MMASK) << 6);
     }
     __syncthreads();  // (waits for the LDS-DMA)
     uint32_t *iw = reinterpret_cast<uint32_t *>(img);
@@ -364,7 +381,7 @@ __global__ __launch_bounds__(256) void conv_tbsg_kernel(const float *x, const fl
 #pragma unroll
         for (int c = 0; c < NC; ++c) cok[c] = (unsigned)(cl + c) < (unsigned)p.W;
         float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
+#pragma unroll TBSG_KYU
         for (int ky = 0; ky < 3; ++ky) {
             const bool rok = (unsigned)(r0 + ky) < (unsigned)p.H;
             uint32_t col[NC];
@@ -604,7 +621,7 @@ __global__ __launch_bounds__(256) void conv_v5ds_kernel(const float *x, const fl
 #pragma unroll
         for (int c = 0; c < NC; ++c) cok[c] = (unsigned)(cl + c) < (unsigned)p.W;
         float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
+#pragma unroll V5DS_KYU
         for (int ky = 0; ky < 3; ++ky) {
             const bool rok = (unsigned)(r0 + ky) < (unsigned)p.H;
             uint32_t col[NC];

@@ -319,7 +319,7 @@ __device__ __forceinline__ uint32_t emit_word(const GemmArgs &p, const EmitCtx &
     if (p.em.form) {  // tbx_decode_a's word of q (a value off the grid / outside the window: invalid)
         const uint32_t u = __float_as_uint(q), ua = u & 0x7FFFFFFFu, M = (uint32_t)p.em.Mw;
         ok = ok && (ua == 0u || ((ua & ((1u << (23 - M)) - 1u)) == 0u && ua >= 0x20800000u && ua <= 0x58800000u));
-        return ua == 0u ? 0u : ((u & 0xFF800000u) | (((ua >> (23 - M)) & ((1u << M) - 1u)) << 6));
+        return ua == 0u ? 0u : ((u & 0xFF800000u) | (((ua >> (23 - M)) & ((1u << M) - 1u)) << 3));
     }
     return xm_word_a(q, p.em.Mw, xm_xbias(p.em.Mw), e.emn, e.bR, ok);
 }
