@@ -33,21 +33,32 @@
 
 namespace fp8a {
 
+// Sub-stages per staged tile: NS x TT16_XK K-steps share one barrier pair, one prefetch and one
+// table build phase (round 6: 2, was 1 -- the E2M5 tile-table kernel's lesson, §3r: the kernel's
+// per-tile overhead, not its math, was the larger share)
+#ifndef TT16_NSUB
+#define TT16_NSUB 2
+#endif
+#ifndef TT16_NSUB_F7
+#define TT16_NSUB_F7 TT16_NSUB  // (F7 doubles the LDS tables: 2 sub-stages = 40 KB, 4 blocks per CU)
+#endif
 template <bool F7> struct Tt16Cfg {
     static constexpr int RB = 8;             // 16-row blocks per wave
     static constexpr int BMR = 16 * RB;      // tile rows
     static constexpr int AWS = BMR + 16;     // A words per K-step in LDS (K-steps 16 banks apart)
-    static constexpr int APT = TT16_XK * BMR / NT;  // A words staged per thread
+    static constexpr int APT = TT16_XK * BMR / NT;  // A words staged per thread and sub-stage
+    static constexpr int NS = F7 ? TT16_NSUB_F7 : TT16_NSUB;
+    static constexpr int XKT = NS * TT16_XK;        // K-steps per staged tile
 };
 
 template <bool F7> struct Tt16Smem {
     using C = Tt16Cfg<F7>;
     union {
         struct {
-            uint32_t tt[TT16_XK * TT16_KS];                 // V c_b' pairs [kk][m_a][column pair]
-            uint32_t tg[F7 ? TT16_XK * TT16_KS : 1];        // sig_a sig_b c_b' pairs (F7)
+            uint32_t tt[C::XKT * TT16_KS];                  // V c_b' pairs [kk][m_a][column pair]
+            uint32_t tg[F7 ? C::XKT * TT16_KS : 1];         // sig_a sig_b c_b' pairs (F7)
             uint32_t img[F7 ? 256 : 128];                   // the static image, f16 [m_b][m_a]
-            uint32_t aw[TT16_XK * C::AWS];                  // A words [kk][row]
+            uint32_t aw[C::XKT * C::AWS];                   // A words [kk][row]
             int bmin, bmax;                                 // the tile's column biases
         } t;
         float ct[64 * XM_CP];  // epilogue transpose slice
@@ -58,7 +69,7 @@ template <bool F7> struct Tt16Smem {
 template <bool F7>
 __global__ __launch_bounds__(NT, 6) void gemm_tt16_kernel(const GemmArgs p) {
     using Cf = Tt16Cfg<F7>;
-    constexpr int RB = Cf::RB, BMR = Cf::BMR, AWS = Cf::AWS, APT = Cf::APT;
+    constexpr int RB = Cf::RB, BMR = Cf::BMR, AWS = Cf::AWS, APT = Cf::APT, NS = Cf::NS, XKT = Cf::XKT;
     __shared__ __attribute__((aligned(16))) Tt16Smem<F7> sm;
     auto &S = sm.u.t;
 
@@ -121,27 +132,31 @@ __global__ __launch_bounds__(NT, 6) void gemm_tt16_kernel(const GemmArgs p) {
     const __amdgpu_buffer_rsrc_t arsrc =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(p.aw), (short)0, -1, 0x00020000);
     const int khw = p.kh * p.kw;
-    uint32_t wa[APT];
-    uint2 wb;
+    uint32_t wa[NS][APT];
+    uint2 wb[NS];
     auto load_tile = [&](int k0) {
-        uint32_t ko;
-        if (p.conv) {
-            const int k = min(k0 + akk, K32 - 1);  // wave-uniform; clamped: the word image ends at channel K - 1
-            const uint32_t c = fastdiv((uint32_t)k, p.kk_mul, p.kk_shift);
-            const uint32_t t = (uint32_t)k - c * (uint32_t)khw;
-            const uint32_t ky = fastdiv(t, p.kw_mul, p.kw_shift);
-            const uint32_t kx = t - ky * (uint32_t)p.kw;
-            ko = 4u * (c * phw + ky * (uint32_t)p.dh * uW + kx * (uint32_t)p.dw);
-        } else {
-            ko = 4u * (uint32_t)k0;
-        }
-        ko = __builtin_amdgcn_readfirstlane(ko);
 #pragma unroll
-        for (int i = 0; i < APT; ++i) {
-            wa[i] = __builtin_amdgcn_raw_buffer_load_b32(arsrc, (int)aoff[i], (int)ko, 0);  // (past K: zeroed at staging)
+        for (int s = 0; s < NS; ++s) {
+            const int ks = k0 + TT16_XK * s;
+            uint32_t ko;
+            if (p.conv) {
+                const int k = min(ks + akk, K32 - 1);  // wave-uniform; clamped: the word image ends at channel K - 1
+                const uint32_t c = fastdiv((uint32_t)k, p.kk_mul, p.kk_shift);
+                const uint32_t t = (uint32_t)k - c * (uint32_t)khw;
+                const uint32_t ky = fastdiv(t, p.kw_mul, p.kw_shift);
+                const uint32_t kx = t - ky * (uint32_t)p.kw;
+                ko = 4u * (c * phw + ky * (uint32_t)p.dh * uW + kx * (uint32_t)p.dw);
+            } else {
+                ko = 4u * (uint32_t)ks;  // (the matrix words are zero-padded to Kpad)
+            }
+            ko = __builtin_amdgcn_readfirstlane(ko);
+#pragma unroll
+            for (int i = 0; i < APT; ++i) {
+                wa[s][i] = __builtin_amdgcn_raw_buffer_load_b32(arsrc, (int)aoff[i], (int)ko, 0);  // (past K: zeroed at staging)
+            }
+            const uint32_t kb = __builtin_amdgcn_readfirstlane((uint32_t)(ks - kbeg) * npad4);
+            wb[s] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(brsrc, (int)boff, (int)kb, 0));
         }
-        const uint32_t kb = __builtin_amdgcn_readfirstlane((uint32_t)(k0 - kbeg) * npad4);
-        wb = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(brsrc, (int)boff, (int)kb, 0));
     };
     load_tile(kbeg);
 
@@ -163,21 +178,26 @@ __global__ __launch_bounds__(NT, 6) void gemm_tt16_kernel(const GemmArgs p) {
     const char *tg0 = reinterpret_cast<const char *>(S.tg);
     __syncthreads();  // the static image is in LDS
 
-    for (int k0 = kbeg; k0 < kend; k0 += TT16_XK) {
+    for (int k0 = kbeg; k0 < kend; k0 += XKT) {
 #pragma unroll
-        for (int i = 0; i < APT; ++i)  // (K-steps past the group's last channel: zero words)
-            S.aw[akk * AWS + arow + 64 * i] = (p.conv && k0 + akk >= K32) ? 0u : wa[i];
-        {  // build: tt[bkk][m_a][cp] = (V(m_a, m_b1) c_b1' : V(m_a, m_b0) c_b0') for m_a = 8 rp .. 8 rp + 7
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int i = 0; i < APT; ++i)  // (K-steps past the group's last channel: zero words)
+                S.aw[(TT16_XK * s + akk) * AWS + arow + 64 * i] = (p.conv && k0 + TT16_XK * s + akk >= K32) ? 0u : wa[s][i];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {  // build: tt[kk][m_a][cp] = (V(m_a, m_b1) c_b1' : V(m_a, m_b0) c_b0') for m_a = 8 rp .. 8 rp + 7
+            const uint2 wbs = wb[s];
+            const int kkb = TT16_XK * s + bkk;
             auto cbf16 = [&](uint32_t w) -> uint32_t {  // f32 c_b bits -> f16 c_b' bits (0 for a zero B)
                 const int e = (int)((w >> 23) & 0xFFu) + sb16;  // f16 exponent field; <= 0: subnormal
                 const uint32_t mag = e >= 1 ? ((uint32_t)min(e, 30) << 10) : (e >= -9 ? (0x200u >> (-e)) : 0u);
                 return (w & 0x7F800000u) ? (((w >> 16) & 0x8000u) | mag) : 0u;
             };
-            const tt16_h2 cbh = __builtin_bit_cast(tt16_h2, cbf16(wb.x) | (cbf16(wb.y) << 16));  // (c_b1' : c_b0')
-            const uint4 v0 = *reinterpret_cast<const uint4 *>(&S.img[(wb.x & 15u) * 8 + 4 * rp]);
-            const uint4 v1 = *reinterpret_cast<const uint4 *>(&S.img[(wb.y & 15u) * 8 + 4 * rp]);
+            const tt16_h2 cbh = __builtin_bit_cast(tt16_h2, cbf16(wbs.x) | (cbf16(wbs.y) << 16));  // (c_b1' : c_b0')
+            const uint4 v0 = *reinterpret_cast<const uint4 *>(&S.img[(wbs.x & 15u) * 8 + 4 * rp]);
+            const uint4 v1 = *reinterpret_cast<const uint4 *>(&S.img[(wbs.y & 15u) * 8 + 4 * rp]);
             const uint32_t a0[4] = {v0.x, v0.y, v0.z, v0.w}, a1[4] = {v1.x, v1.y, v1.z, v1.w};
-            uint32_t *d = &S.tt[bkk * TT16_KS + 8 * rp * TT16_RS + cp];
+            uint32_t *d = &S.tt[kkb * TT16_KS + 8 * rp * TT16_RS + cp];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const tt16_h2 lo = __builtin_bit_cast(tt16_h2, __builtin_amdgcn_perm(a1[i], a0[i], 0x05040100u)) * cbh;
@@ -186,10 +206,10 @@ __global__ __launch_bounds__(NT, 6) void gemm_tt16_kernel(const GemmArgs p) {
                 d[(2 * i + 1) * TT16_RS] = __builtin_bit_cast(uint32_t, hi);
             }
             if (F7) {
-                const uint4 g0 = *reinterpret_cast<const uint4 *>(&S.img[128 + (wb.x & 15u) * 8 + 4 * rp]);
-                const uint4 g1 = *reinterpret_cast<const uint4 *>(&S.img[128 + (wb.y & 15u) * 8 + 4 * rp]);
+                const uint4 g0 = *reinterpret_cast<const uint4 *>(&S.img[128 + (wbs.x & 15u) * 8 + 4 * rp]);
+                const uint4 g1 = *reinterpret_cast<const uint4 *>(&S.img[128 + (wbs.y & 15u) * 8 + 4 * rp]);
                 const uint32_t b0[4] = {g0.x, g0.y, g0.z, g0.w}, b1[4] = {g1.x, g1.y, g1.z, g1.w};
-                uint32_t *e = &S.tg[bkk * TT16_KS + 8 * rp * TT16_RS + cp];
+                uint32_t *e = &S.tg[kkb * TT16_KS + 8 * rp * TT16_RS + cp];
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const tt16_h2 lo = __builtin_bit_cast(tt16_h2, __builtin_amdgcn_perm(b1[i], b0[i], 0x05040100u)) * cbh;
@@ -200,13 +220,15 @@ __global__ __launch_bounds__(NT, 6) void gemm_tt16_kernel(const GemmArgs p) {
             }
         }
         __syncthreads();
-        if (k0 + TT16_XK < kend) load_tile(k0 + TT16_XK);  // next tile's loads fly during this tile's math
+        if (k0 + XKT < kend) load_tile(k0 + XKT);  // next tile's loads fly during this tile's math
 
 #pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
         for (int b = 0; b < RB; ++b) {
-            const uint32_t w = S.aw[g * AWS + 16 * b + r16];
+            const uint32_t w = S.aw[(TT16_XK * s + g) * AWS + 16 * b + r16];
             const tt16_h2 c2 = __builtin_bit_cast(tt16_h2, w & TT16_EXP2);
-            const uint32_t a = ((w & 0x3FFu) << 1) + tbase;
+            const uint32_t a = ((w & 0x3FFu) << 1) + tbase + (uint32_t)(s * TT16_XK * TT16_KS * 4);
             uint32_t t[8], tg[F7 ? 8 : 1];
 #pragma unroll
             for (int c = 0; c < 4; ++c) {

@@ -10,6 +10,7 @@
 #   dwpmc       SQ / LDS counters of the staged depthwise kernels (tools/pmc_kernel.sh)
 #   dwab        staged depthwise A/B: lib/ab/libfp8approx_kyu1.so at several block plans
 #   v5ab        v5 / E5M2 v9 depthwise A/B: lib/ab/libfp8approx_v5k1.so
+#   tt16ab      E3M4 tile-table sub-stages per staged tile: default (2) vs lib/ab/ ns1 (1) and f7ns1 (F7 form: 1)
 #   multirank   two ranks on one GPU over gloo vs two world-1 runs (logits and FP8 state per rank)
 # A/B libraries: python -c "from fp8_quantization_amd import build_native as b; b.build(force=True,
 #   out='fp8_quantization_amd/lib/ab/<name>.so', extra=b.EXTRA + ['-D...'])"
@@ -86,6 +87,17 @@ v5ab() {
     L=""; [ $v = k1 ] && L=$K1
     bench_line $O v5_$v "$L" --arch mobilenet_v2 --batch 512 --expo-width 5 --mant-width 2 --v5-ofuf || return 1
     bench_line $O v9_$v "$L" --arch mobilenet_v2 --batch 512 --expo-width 5 --mant-width 2 || return 1
+  done
+}
+
+tt16ab() {
+  local O=gpurun_out/tt16ab; mkdir -p $O
+  timeout -k 10 900 python -u -m pytest tests/test_gpu_tt.py tests/test_gpu_model.py -q -x --timeout 300 -k "tt or E3M4 or e3m4" \
+    > $O/tests.log 2>&1 || { tail -5 $O/tests.log; return 1; }
+  tail -1 $O/tests.log
+  for v in ns2 ns1 f7ns1; do
+    L=""; [ $v != ns2 ] && L=$AB/libfp8approx_$v.so
+    bench_line $O r50_e3m4_$v "$L" --arch resnet50 --expo-width 3 --mant-width 4 --batch 512 || return 1
   done
 }
 
