@@ -118,6 +118,14 @@ __host__ __device__ constexpr int xm_xbias(int Mw) { return Mw == 2 ? 15 : 7; }
 // A words in LDS: [kk / 2][row][kk % 2] -- one ds_write_b64 stores (and one ds_read_b64 reads) a
 // row's words of a K-step pair; the pair arrays sit 32 banks apart, so the math loop's reads
 // (lane groups of K-step pairs g, g + 1) and the staging's stores are conflict-free.
+// B operand by LDS-DMA (option build, round 6; off): the staged tile's B pair words (XBK x TXN
+// 16-byte chunks, each read by the 4 build units of its column block) go global -> LDS by
+// global_load_lds_dwordx4 instead of through 8 prefetch VGPRs per thread.  The plain 128 x 64
+// instance then fits 6 waves / SIMD (76 VGPRs, no spill) -- and ran 4 % slower: ResNet-18 12,175
+// vs 12,673 images/s, ResNet-50 E4M3 4,671 vs 4,857 (profiles/r06_bdma/)
+#ifndef XM_BDMA
+#define XM_BDMA 0
+#endif
 template <int NCG, int RB>
 struct XmCfg {
     static constexpr int NT = 256;
@@ -138,6 +146,9 @@ struct XmCfg {
         uint32_t tt[XBK][TTK];  // c_b-applied pairs [kk][tx][row][j] (first: its byte offsets are the reads' immediates)
         uint32_t lut[XM_LUT_WORDS];
         uint32_t aw[XBK / 2][AWQ];  // A(m, k)'s word: cvt scale exponent << 23 | row << 3
+#if XM_BDMA
+        uint4 bw[XBK * TXN];        // the staged tile's B pair words [kk][column block], by LDS-DMA
+#endif
     };
     union Smem {
         Stage st;
@@ -522,6 +533,15 @@ __device__ unsigned long long g_clk[3];
 // 28.7 -> 25.5 ms, bench 11835 -> 12454 images/s at 5 waves (round 5)
 #define XM_WAVES 5
 #endif
+// the plain instance (staged words, no emission), with the B operand by LDS-DMA: 76 VGPRs, no spill
+// at 6 waves (the emitting / fp32-staging instances spill 7-28 there and stay at XM_WAVES).  (The
+// bound is a trait: a conditional expression in __launch_bounds__ works too, but the macro splits
+// on a template argument list's comma)
+#ifndef XM_WAVES_PLAIN
+#define XM_WAVES_PLAIN (XM_BDMA ? 6 : XM_WAVES)
+#endif
+template <bool AF32, bool EMIT> struct XmWaves { static constexpr int value = XM_WAVES; };
+template <> struct XmWaves<false, false> { static constexpr int value = XM_WAVES_PLAIN; };
 // The GEMM.  Tile BMT x BNT (XmCfg), 4 waves; wave wv = column group wc = wv % NCG (the 16
 // columns 16 wc .. 16 wc + 15, column blocks tx = 4 wc + c of the tile table) and row group
 // wr = wv / NCG (16 RB rows).  Math mapping: lane = (row r16 of each of the wave's RB 16-row
@@ -538,7 +558,7 @@ __device__ unsigned long long g_clk[3];
 // writes and re-reads 8 B per A element through HBM; staging-time decoding costs ~25 VALU
 // operations per element per column tile, the cheaper choice up to a few column tiles (run_gemm).
 template <int NCG, int RB, bool AF32, int XF, bool EMIT>
-__global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs p) {
+__global__ __launch_bounds__(256, (XmWaves<AF32, EMIT>::value)) void gemm_f8mx_kernel(const GemmArgs p) {
     using Cf = XmCfg<NCG, RB>;
     constexpr int XM = XmFmt<XF>::M, XB = XmFmt<XF>::XB;
     constexpr int NT = Cf::NT, BMT = Cf::BMT, BNT = Cf::BNT, TTK = Cf::TTK, APR = Cf::APR;
@@ -590,8 +610,15 @@ __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs
     const int bkk0 = 2 * (tid / (8 * TXN)) + ((tid >> 2) & 1);
     const uint32_t boff0 = (uint32_t)(kbeg + bkk0) * hq8 + (uint32_t)(n0 / 2 + 2 * btx) * 8u;  // pair 2 btx: 16-B aligned
     const bool build = NBU % NT == 0 || tid < NBU;  // (NCG = 1: half the threads build)
+#if XM_BDMA
+    // this thread's DMA chunk (tid < XBK TXN): K-step kbeg + tid / TXN, pairs n0 / 2 + 2 (tid % TXN) + {0, 1}
+    const float *bsrc = reinterpret_cast<const float *>(p.bqw) +
+                        ((size_t)(kbeg + tid / TXN) * (hq8 / 4) + (size_t)(n0 / 2 + 2 * (tid % TXN)) * 2);
+    (void)boff0;
+#else
     const __amdgpu_buffer_rsrc_t brsrc =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint2 *>(p.bqw), (short)0, -1, 0x00020000);
+#endif
 
     // A staging: thread = (rows arow + 64 i, K-step pair akp), K-steps 2 akp + r.  conv: lane =
     // row (consecutive pixels), akp = the wave (wave-uniform: the k -> (c, ky, kx) split and the
@@ -618,7 +645,9 @@ __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs
              : __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(p.aw), (short)0, -1, 0x00020000);
     const int khw = p.kh * p.kw;
     uint32_t wa[APR][2];
+#if !XM_BDMA
     uint4 wbq[BU];
+#endif
     auto load_tile = [&](int k0) {
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
@@ -654,6 +683,12 @@ __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs
                 wa[i][r] = __builtin_amdgcn_raw_buffer_load_b32(arsrc, (int)aoff[i], (int)ko, 0);
             }
         }
+#if XM_BDMA
+        // chunk tid = (K-step tid / TXN, column block tid % TXN) -> bw[tid]; a wave's 64 chunks land
+        // contiguously from its LDS base (the last, partial wave: lanes past the chunks stay off)
+        if (tid < XBK * TXN)
+            __builtin_amdgcn_global_load_lds(bsrc + (size_t)(k0 - kbeg) * (hq8 / 4), reinterpret_cast<float *>(&sm.bw[64 * wvu]), 16, 0, 0);  // (a uint4 * here: the host pass drops the kernel stubs)
+#else
         if (build) {
             const uint32_t kb = __builtin_amdgcn_readfirstlane((uint32_t)(k0 - kbeg) * hq8);
 #pragma unroll
@@ -661,6 +696,7 @@ __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs
                 wbq[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
                                                        brsrc, (int)boff0, (int)(kb + (uint32_t)(u * BKU) * hq8), 0));
         }
+#endif
     };
     load_tile(kbeg);
 
@@ -686,6 +722,9 @@ __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs
     const char *lut = reinterpret_cast<const char *>(sm.lut);
     const uint32_t wvo = (uint32_t)wc * 512u;  // the wave's first column block (4 wc) in a K-step of the table
     typedef const volatile __attribute__((address_space(3))) uint64_t xm_lds_u64;
+#if XM_BDMA
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's B chunks have landed (then the barrier: everyone's)
+#endif
     __syncthreads();  // the static table is in LDS before the first build reads it
 
     for (int k0 = kbeg; k0 < kend; k0 += XBK) {
@@ -723,7 +762,11 @@ __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs
         if (build) {
 #pragma unroll
             for (int u = 0; u < BU; ++u) {
+#if XM_BDMA
+                const uint4 b = sm.bw[(bkk0 + u * BKU) * TXN + btx];
+#else
                 const uint4 b = wbq[u];
+#endif
                 const uint2 s0 = *reinterpret_cast<const uint2 *>(lut + b.y + 8 * q4);
                 const uint2 s1 = *reinterpret_cast<const uint2 *>(lut + b.w + 8 * q4);
                 const xm_u2 a0 = __builtin_bit_cast(xm_u2, b.x), a1 = __builtin_bit_cast(xm_u2, b.z);
@@ -822,6 +865,9 @@ __global__ __launch_bounds__(256, XM_WAVES) void gemm_f8mx_kernel(const GemmArgs
                 dq[b] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, sel, dq[b], XF ? 1 : 0, 0, 0, sca, 0, 127);
             }
         }
+#if XM_BDMA
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the next tile's B chunks (read by the next build)
+#endif
         __syncthreads();
     }
 

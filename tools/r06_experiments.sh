@@ -11,6 +11,9 @@
 #   dwab        staged depthwise A/B: lib/ab/libfp8approx_kyu1.so at several block plans
 #   v5ab        v5 / E5M2 v9 depthwise A/B: lib/ab/libfp8approx_v5k1.so
 #   tt16ab      E3M4 tile-table sub-stages per staged tile: default (2) vs lib/ab/ ns1 (1) and f7ns1 (F7 form: 1)
+#   splitab     split-K choice: the default line and ResNet-50 E4M3 with FP8A_SPLITK unset / 1
+#   bdma        gemm_f8mx_kernel's B operand by LDS-DMA (plain instance at 6 waves): f8mx tests, then
+#               ResNet-18 / ResNet-50 E4M3 with the default, lib/ab/ w6all (every instance at 6) and nobdma
 #   multirank   two ranks on one GPU over gloo vs two world-1 runs (logits and FP8 state per rank)
 # A/B libraries: python -c "from fp8_quantization_amd import build_native as b; b.build(force=True,
 #   out='fp8_quantization_amd/lib/ab/<name>.so', extra=b.EXTRA + ['-D...'])"
@@ -98,6 +101,29 @@ tt16ab() {
   for v in ns2 ns1 f7ns1; do
     L=""; [ $v != ns2 ] && L=$AB/libfp8approx_$v.so
     bench_line $O r50_e3m4_$v "$L" --arch resnet50 --expo-width 3 --mant-width 4 --batch 512 || return 1
+  done
+}
+
+splitab() {
+  local O=gpurun_out/splitab; mkdir -p $O
+  bench_line $O r18_def "" || return 1
+  FP8A_SPLITK=1 bench_line $O r18_s1 "" || return 1
+  bench_line $O r50_def "" --arch resnet50 --batch 512 || return 1
+  FP8A_SPLITK=1 bench_line $O r50_s1 "" --arch resnet50 --batch 512 || return 1
+}
+
+bdma() {
+  local O=gpurun_out/bdma; mkdir -p $O
+  timeout -k 10 900 python -u -m pytest tests/test_gpu_f8mx.py tests/test_gpu_xm_shapes.py tests/test_gpu_f8_e5m2.py tests/test_gpu_chain.py \
+    -q -x --timeout 300 > $O/tests.log 2>&1 || { tail -5 $O/tests.log; return 1; }
+  tail -1 $O/tests.log
+  for v in def w6all nobdma; do
+    L=""; [ $v != def ] && L=$AB/libfp8approx_$v.so
+    bench_line $O r18_$v "$L" || return 1
+  done
+  for v in def nobdma; do
+    L=""; [ $v != def ] && L=$AB/libfp8approx_$v.so
+    bench_line $O r50_$v "$L" --arch resnet50 --batch 512 || return 1
   done
 }
 
