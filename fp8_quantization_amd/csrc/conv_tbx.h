@@ -100,10 +100,16 @@ __device__ __forceinline__ float2 tbx_lut_entry(int i, const TablePack &tab, int
 // the table in LDS.
 __device__ __forceinline__ float tbx_term(uint32_t wa, float cB, uint32_t mb64, const char *lut, uint32_t q0exp,
                                           float twoq) {
-    const float2 e = *reinterpret_cast<const float2 *>(lut + ((wa & 0x38u) | mb64));
+    // (mb64 masked: the offset is then provably small and the table's LDS base folds into the read's
+    // offset field; the mask is per tap, the terms share it)
+    const float2 e = *reinterpret_cast<const float2 *>(lut + ((wa & 0x38u) | (mb64 & 0x1C0u)));
     const float cab = __uint_as_float(wa & 0xFF800000u) * cB;  // exact
     float rv = e.x * cab;                                        // exact
-    const float rs = __fmaf_rn(2.0f, rv, -copysignf(twoq, rv));  // expo field 0
+    // expo field 0: 2 rv - sign 2^(1-bR), as sign x (2 |rv| - 2^(1-bR)) -- one fma with an abs
+    // modifier and a bfi, where the signed form cost a bfi, an xor and the fma (round 6).  The same
+    // value (RNE is odd-symmetric) but for |rv| = 2^-bR, rv < 0: -0 instead of +0, which no sum sees
+    // (the accumulators start at +0 and are never -0)
+    const float rs = copysignf(__fmaf_rn(2.0f, fabsf(rv), -twoq), rv);
     rv = ((__float_as_uint(rv) & 0x7F800000u) == q0exp) ? rs : rv;
     return (__float_as_uint(cab) == __float_as_uint(e.y)) ? fabsf(rv) : rv;  // F7
 }
@@ -305,6 +311,10 @@ __global__ __launch_bounds__(256) void conv_tbs_kernel(const float *x, const flo
 #ifndef V5DS_KYU
 #define V5DS_KYU 1
 #endif
+// conv_tbsg_kernel's dynamic LDS: table (512 B), taps (72 B per plane), the staged source from the
+// next 16-byte boundary (nimg floats) -- in floats, and the launch's byte count
+__host__ __device__ constexpr int tbsg_img_off(int PB) { return (128 + 18 * PB + 3) & ~3; }
+__host__ __device__ constexpr size_t tbsg_lds_bytes(int PB, int nimg) { return 4 * ((size_t)tbsg_img_off(PB) + nimg); }
 template <int S, int M>
 __global__ __launch_bounds__(256, TBSG_WAVES) void conv_tbsg_kernel(const float *x, const float *w, float *y, const DwArgs p,
                                                         FqIn fq, float *fq_bias_out, int32_t *fq_ibias_out,
@@ -325,9 +335,11 @@ __global__ __launch_bounds__(256, TBSG_WAVES) void conv_tbsg_kernel(const float 
     const int n = plane_mode ? npl * hw : (rhi - rlo) * p.W;
     const int64_t g0 = P0 * hw + (int64_t)rlo * p.W, a0 = g0 & ~(int64_t)3;
     const int lead = (int)(g0 - a0), nq = (lead + n + 3) >> 2;
-    float *img = dw_sm;
-    float2 *sL = reinterpret_cast<float2 *>(dw_sm + p.nimg);  // the table (64 entries)
-    uint2 *sB = reinterpret_cast<uint2 *>(sL + 64);           // [PB][9] {c_b bits, m_b << 3}
+    // the table first (round 6): its LDS address is then a link-time constant, which the reads'
+    // offset field carries (a per-term address add less); then the taps, then the staged source
+    float2 *sL = reinterpret_cast<float2 *>(dw_sm);            // the table (64 entries)
+    uint2 *sB = reinterpret_cast<uint2 *>(sL + 64);            // [PB][9] {c_b bits, m_b << 6}
+    float *img = dw_sm + tbsg_img_off(p.PB);
     const float *src = x + a0;
     for (int q0 = 0; q0 < nq; q0 += 256) {
         const int q = q0 + tid;

@@ -1908,7 +1908,7 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
                                   dg.planes = Bn * Cout; dg.C = (int)Cout; dg.H = (int)H; dg.W = (int)W;
                                   dg.Ho = (int)Ho; dg.Wo = (int)Wo; dg.ph = ph; dg.pw = pw; dg.nx = Bn * Cin * H * W;
                                   if (!plan_dw3(dg, sw, glds, true)) return false;
-                                  glds = (size_t)dg.nimg * 4 + 64 * 8 + (size_t)dg.PB * 9 * 8;
+                                  glds = tbsg_lds_bytes(dg.PB, dg.nimg);
                                   return glds <= 65536;
                               }();
             if (tbsg) {
