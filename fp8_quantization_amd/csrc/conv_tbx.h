@@ -311,10 +311,30 @@ __global__ __launch_bounds__(256) void conv_tbs_kernel(const float *x, const flo
 #ifndef V5DS_KYU
 #define V5DS_KYU 1
 #endif
-// conv_tbsg_kernel's dynamic LDS: table (512 B), taps (72 B per plane), the staged source from the
-// next 16-byte boundary (nimg floats) -- in floats, and the launch's byte count
-__host__ __device__ constexpr int tbsg_img_off(int PB) { return (128 + 18 * PB + 3) & ~3; }
+// Per-tap tables (round 6, option build TBSG_TAPT, off): each tap's 8 entries (m_a) with its c_b
+// applied, L(m_a, m_b) c_b, and its F7 trigger divided by c_b -- a term is then one multiply by c_a
+// (exact either way) and the trigger test is on c_a: the ky loop 160 -> 137 VALU instructions per 12
+// terms, 576 B of LDS per plane more -- and MobileNetV2 1.1-1.4 % slower (the per-block table build
+// and the smaller block plans it forces; profiles/r06_tapt/).  Bit-identical either way.
+#ifndef TBSG_TAPT
+#define TBSG_TAPT 0
+#endif
+// conv_tbsg_kernel's dynamic LDS: table (512 B), taps (72 B per plane), the per-tap tables (576 B
+// per plane), the staged source from the next 16-byte boundary (nimg floats) -- in floats, and the
+// launch's byte count; tbsg_tap_bytes: the per-plane bytes per tap for the block plan
+__host__ __device__ constexpr int tbsg_img_off(int PB) { return (128 + 18 * PB + (TBSG_TAPT ? 144 * PB : 0) + 3) & ~3; }
 __host__ __device__ constexpr size_t tbsg_lds_bytes(int PB, int nimg) { return 4 * ((size_t)tbsg_img_off(PB) + nimg); }
+__host__ __device__ constexpr int tbsg_tap_bytes() { return TBSG_TAPT ? 72 : 8; }
+
+// One term from a per-tap table (TBSG_TAPT): tap = the tap's 8 entries {L c_b, trigger / c_b}
+__device__ __forceinline__ float tbx_term_t(uint32_t wa, const char *tap, uint32_t q0exp, float twoq) {
+    const float2 e = *reinterpret_cast<const float2 *>(tap + (wa & 0x38u));
+    const uint32_t cab = wa & 0xFF800000u;                 // c_a (0 for a zero word)
+    float rv = e.x * __uint_as_float(cab);                  // exact: the same value as L (c_a c_b)
+    const float rs = copysignf(__fmaf_rn(2.0f, fabsf(rv), -twoq), rv);  // expo field 0 (tbx_term)
+    rv = ((__float_as_uint(rv) & 0x7F800000u) == q0exp) ? rs : rv;
+    return (cab == __float_as_uint(e.y)) ? fabsf(rv) : rv;  // F7: c_a c_b == trigger <=> c_a == trigger / c_b
+}
 template <int S, int M>
 __global__ __launch_bounds__(256, TBSG_WAVES) void conv_tbsg_kernel(const float *x, const float *w, float *y, const DwArgs p,
                                                         FqIn fq, float *fq_bias_out, int32_t *fq_ibias_out,
@@ -339,6 +359,7 @@ __global__ __launch_bounds__(256, TBSG_WAVES) void conv_tbsg_kernel(const float 
     // offset field carries (a per-term address add less); then the taps, then the staged source
     float2 *sL = reinterpret_cast<float2 *>(dw_sm);            // the table (64 entries)
     uint2 *sB = reinterpret_cast<uint2 *>(sL + 64);            // [PB][9] {c_b bits, m_b << 6}
+    float2 *sT = reinterpret_cast<float2 *>(sB + 9 * p.PB);    // (TBSG_TAPT) [PB][9][8] per-tap tables
     float *img = dw_sm + tbsg_img_off(p.PB);
     const float *src = x + a0;
     for (int q0 = 0; q0 < nq; q0 += 256) {
@@ -377,6 +398,18 @@ __global__ __launch_bounds__(256, TBSG_WAVES) void conv_tbsg_kernel(const float 
         const int i0 = lead, i1 = lead + n;
         for (int i = i0 + tid; i < i1; i += 256) iw[i] = tbx_word(img[i], fq, fmx, fbias, LOWM, MMASK, M, bad);
     }
+    if (TBSG_TAPT) {  // entry (tap d, m_a): {L(m_a, m_b) c_b, trigger / c_b} (never-matching for c_b = 0 or out of range)
+        for (int e = tid; e < npl * 72; e += 256) {
+            const uint2 b = sB[e >> 3];
+            const float2 l = sL[(b.y >> 3) + (e & 7)];
+            const uint32_t t = __float_as_uint(l.y), cb = b.x;
+            // trigger -2^(Et - 127) / (+-2^(Eb - 127)) = -+2^(Et - Eb): exponent field Et - Eb + 127
+            const int ef = (int)((t >> 23) & 0xFFu) - (int)((cb >> 23) & 0xFFu) + 127;
+            const bool ok = t != 0xFFFFFFFFu && (cb & 0x7F800000u) != 0u && ef >= 1 && ef <= 254;
+            const uint32_t tq = ok ? (((t ^ cb) & 0x80000000u) | ((uint32_t)ef << 23)) : 0xFFFFFFFFu;
+            sT[e] = make_float2(l.x * __uint_as_float(cb), __uint_as_float(tq));
+        }
+    }
     __syncthreads();
     const uint32_t q0exp = (uint32_t)(127 - r_b) << 23;
     const float twoq = __uint_as_float((uint32_t)(128 - r_b) << 23);
@@ -401,10 +434,16 @@ __global__ __launch_bounds__(256, TBSG_WAVES) void conv_tbsg_kernel(const float 
             for (int c = 0; c < NC; ++c) col[c] = (rok && cok[c]) ? xs[ky * p.W + c] : 0u;
 #pragma unroll
             for (int kx = 0; kx < 3; ++kx) {
-                const uint2 b = wb[3 * ky + kx];
-                const float cB = __uint_as_float(b.x);
+                if (TBSG_TAPT) {
+                    const char *tap = reinterpret_cast<const char *>(sT + 8 * (9 * pl + 3 * ky + kx));
 #pragma unroll
-                for (int j = 0; j < 4; ++j) acc[j] += tbx_term(col[j * S + kx], cB, b.y, lut, q0exp, twoq);
+                    for (int j = 0; j < 4; ++j) acc[j] += tbx_term_t(col[j * S + kx], tap, q0exp, twoq);
+                } else {
+                    const uint2 b = wb[3 * ky + kx];
+                    const float cB = __uint_as_float(b.x);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[j] += tbx_term(col[j * S + kx], cB, b.y, lut, q0exp, twoq);
+                }
             }
         }
         int co = c0 + pl;

@@ -1398,7 +1398,7 @@ static void launch_group_conv(const GcArgs &a, hipStream_t s) {
 // dn_dw3_kernel's block shape: about `target` outputs per workgroup (whole planes when a plane has
 // fewer, else bands of rows of one plane), the staged window within dw_lds bytes of LDS (default
 // 40 KB, four workgroups per CU: measured against 2 / 8 / 16 KB-windowed plans, §3l); false when even 256 outputs' window does not fit (very wide rows).
-static bool plan_dw3(DwArgs &a, int S, size_t &lds, bool raw = false) {
+static bool plan_dw3(DwArgs &a, int S, size_t &lds, bool raw = false, int tap_bytes = 4) {
     const int64_t op = (int64_t)a.Ho * a.Wo;
     for (int target = std::max(256, g_opt_dw_target); target >= 256; target /= 2) {
         int PB, RB;
@@ -1415,7 +1415,7 @@ static bool plan_dw3(DwArgs &a, int S, size_t &lds, bool raw = false) {
         // raw (dn_dw3g_kernel): the unpadded source range from its 16-byte-aligned start
         const int64_t nsrc = RB == a.Ho ? (int64_t)PB * a.H * a.W : (int64_t)std::min(RS, a.H) * a.W;
         a.nimg = (int)(4 * ((nsrc + 6) / 4));
-        const int64_t bytes = ((raw ? (int64_t)a.nimg : (int64_t)PB * RS * WS) + (int64_t)PB * 9) * 4;
+        const int64_t bytes = (raw ? (int64_t)a.nimg : (int64_t)PB * RS * WS) * 4 + (int64_t)PB * 9 * tap_bytes;
         if (bytes > std::min(65536, std::max(4096, g_opt_dw_lds))) continue;
         a.PB = PB; a.RB = RB; a.nb = (a.Ho + RB - 1) / RB; a.RS = RS; a.WS = WS;
         a.inv_c = 1.0f / a.C; a.inv_ws = 1.0f / WS; a.inv_pst = 1.0f / (RS * WS);
@@ -1907,7 +1907,7 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
                               W < (1 << 20) && Cout < (1 << 20) && H * W < (1ll << 22) && [&]() {
                                   dg.planes = Bn * Cout; dg.C = (int)Cout; dg.H = (int)H; dg.W = (int)W;
                                   dg.Ho = (int)Ho; dg.Wo = (int)Wo; dg.ph = ph; dg.pw = pw; dg.nx = Bn * Cin * H * W;
-                                  if (!plan_dw3(dg, sw, glds, true)) return false;
+                                  if (!plan_dw3(dg, sw, glds, true, tbsg_tap_bytes())) return false;
                                   glds = tbsg_lds_bytes(dg.PB, dg.nimg);
                                   return glds <= 65536;
                               }();

@@ -16,6 +16,8 @@
 #               ResNet-18 / ResNet-50 E4M3 with the default, lib/ab/ w6all (every instance at 6) and nobdma
 #   dwops       table-form depthwise with fewer VALU ops per term: tbx / chain tests, then MobileNetV2
 #               E4M3 and E5M2 v9 with the default vs lib/ab/libfp8approx_r6base.so (the previous commit)
+#   tapt        staged table-form depthwise with per-tap tables (TBSG_TAPT): depthwise / chain / model
+#               tests, then MobileNetV2 E4M3 and E5M2 v9 with the default vs lib/ab/libfp8approx_tapt0.so
 #   multirank   two ranks on one GPU over gloo vs two world-1 runs (logits and FP8 state per rank)
 # A/B libraries: python -c "from fp8_quantization_amd import build_native as b; b.build(force=True,
 #   out='fp8_quantization_amd/lib/ab/<name>.so', extra=b.EXTRA + ['-D...'])"
@@ -135,6 +137,18 @@ dwops() {
     -q -x --timeout 300 > $O/tests.log 2>&1 || { tail -5 $O/tests.log; return 1; }
   tail -1 $O/tests.log
   for v in def r6base; do
+    L=""; [ $v != def ] && L=$AB/libfp8approx_$v.so
+    bench_line $O mbv2_e4m3_$v "$L" --arch mobilenet_v2 --batch 512 || return 1
+    bench_line $O mbv2_e5m2_$v "$L" --arch mobilenet_v2 --batch 512 --expo-width 5 --mant-width 2 || return 1
+  done
+}
+
+tapt() {
+  local O=gpurun_out/tapt; mkdir -p $O
+  timeout -k 10 900 python -u -m pytest tests/test_gpu_tbx.py tests/test_gpu_chain.py tests/test_gpu_mbv2_layers.py \
+    tests/test_gpu_model.py -q -x --timeout 300 > $O/tests.log 2>&1 || { tail -5 $O/tests.log; return 1; }
+  tail -1 $O/tests.log
+  for v in def tapt0; do
     L=""; [ $v != def ] && L=$AB/libfp8approx_$v.so
     bench_line $O mbv2_e4m3_$v "$L" --arch mobilenet_v2 --batch 512 || return 1
     bench_line $O mbv2_e5m2_$v "$L" --arch mobilenet_v2 --batch 512 --expo-width 5 --mant-width 2 || return 1
