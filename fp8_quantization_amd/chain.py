@@ -37,11 +37,12 @@ class WordChain:
         in_img = self.in_image if qin is not None else None
         out = None
         nxt = self.next_layer
-        # (an ungrouped launch emits the E4M3 / E5M2 and table forms; a v5 depthwise launch the v5 form
-        # (3): the staged kernel's store -- any other launch flags the image invalid)
+        # (an ungrouped launch emits the E4M3 / E5M2 and table forms; a depthwise launch the matrix-core
+        # form (1: the staged table-form kernel, round 6) or the v5 form (3: the staged v5 kernel) --
+        # any other launch flags the image invalid)
         nq = nxt.chain_input_quantizer() if nxt is not None else None
         form = nxt.chain_wants_image() if nq is not None else 0
-        if form and layer.groups != 1 and form != 3:
+        if form and layer.groups != 1 and form not in (1, 3):
             form = 0
         if form:
             Bn, _, H, W = x.shape

@@ -340,7 +340,7 @@ __global__ __launch_bounds__(256, TBSG_WAVES) void conv_tbsg_kernel(const float 
                                                         FqIn fq, float *fq_bias_out, int32_t *fq_ibias_out,
                                                         const int32_t *bA, const int32_t *bW, const int32_t *bR,
                                                         TablePack tab, uint32_t *gate, const float2 *ep, int ep_act,
-                                                        float ep_lo, float ep_hi) {
+                                                        float ep_lo, float ep_hi, EmitW em) {
     constexpr int NC = 3 * S + 3;
     constexpr uint32_t LOWM = (1u << (23 - M)) - 1u, MMASK = (1u << M) - 1u;
     extern __shared__ float dw_sm[];
@@ -415,6 +415,20 @@ __global__ __launch_bounds__(256, TBSG_WAVES) void conv_tbsg_kernel(const float 
     const float twoq = __uint_as_float((uint32_t)(128 - r_b) << 23);
     const char *lut = reinterpret_cast<const char *>(sL);
     const int nqd = (p.Wo + 3) >> 2, pq = p.RB * nqd;
+    // word-image emission for the next (matrix-core) convolution, em.form 0 (round 6): the words
+    // xm_decode_a would write from this launch's y -- fq_next(y) -> xm_word_a, the same floats, bit
+    // for bit (emit_word) -- so the pointwise convolution after a depthwise one skips its pre-pass.
+    // The next quantizer's constants from the image header (emit_prep_kernel), wave-uniform.
+    float emx = 0.0f, efb = 0.0f;
+    uint32_t eemn = 0u, sehi = 0u;
+    int ebR = 0;
+    bool eok = true;
+    if (em.w) {
+        emx = __uint_as_float(__builtin_amdgcn_readfirstlane((int)em.invalid[1]));
+        efb = __uint_as_float(__builtin_amdgcn_readfirstlane((int)em.invalid[2]));
+        eemn = __builtin_amdgcn_readfirstlane(em.invalid[3]);
+        ebR = __builtin_amdgcn_readfirstlane((int)em.invalid[4]);
+    }
     for (int e = tid; e < npl * pq; e += 256) {
         const int pl = dw_div(e, pq, p.inv_pq), rem = e - pl * pq;
         const int orow = dw_div(rem, nqd, p.inv_nqd), qd = rem - orow * nqd;
@@ -449,11 +463,29 @@ __global__ __launch_bounds__(256, TBSG_WAVES) void conv_tbsg_kernel(const float 
         int co = c0 + pl;
         co -= dw_div(co, p.C, p.inv_c) * p.C;
         float *yo = y + ((P0 + pl) * p.Ho + oh0 + orow) * p.Wo + 4 * qd;
+        uint32_t *wo = em.w ? em.w + ((uint32_t)(P0 + pl) * (uint32_t)em.awH + (uint32_t)(oh0 + orow + em.awph)) *
+                                         (uint32_t)em.awW + (uint32_t)em.awpw + 4u * (uint32_t)qd
+                            : nullptr;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-            if (4 * qd + j < p.Wo) yo[j] = epi(ep, ep_act, ep_lo, ep_hi, co, acc[j]);
+            if (4 * qd + j < p.Wo) {
+                const float o = epi(ep, ep_act, ep_lo, ep_hi, co, acc[j]);
+                yo[j] = o;
+                if (wo) {
+                    const uint32_t wd = xm_word_a(fq_apply(o, emx, efb, em.fq.M, em.fq.S), em.Mw, xm_xbias(em.Mw), eemn,
+                                                  ebR, eok);
+                    wo[j] = wd;
+                    sehi = max(sehi, word_sehi(wd));
+                }
+            }
     }
-    if (__syncthreads_or(bad ? 1 : 0) && tid == 0) atomicOr(gate, 1u);
+    if (em.w) wave_max_atomic(em.invalid + 5, sehi);  // (every lane: the loop above has ended for all)
+    const bool ebad = em.w && !eok;
+    if (__syncthreads_or(bad ? 1 : 0) && tid == 0) {
+        atomicOr(gate, 1u);
+        if (em.w) atomicOr(em.invalid, 1u);  // (the exact kernel rewrites y: the words are stale)
+    }
+    if (__syncthreads_or(ebad ? 1 : 0) && tid == 0) atomicOr(em.invalid, 1u);  // (a word off the window)
 }
 
 // (round 3's alternative depthwise forms conv_dwx_kernel -- band-staged in LDS -- and

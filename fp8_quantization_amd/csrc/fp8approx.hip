@@ -1876,6 +1876,7 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
         const int64_t total = Bn * Cout * Ho * Wo;
         uint32_t *gate = nullptr;
         ArenaLease lease;  // (gate: a slot of the stream's flag arena, flag_arena)
+        bool emitted = false;  // (a requested word image: only the staged table-form kernel writes it)
         // fast form: needs s2n on and golden_clip_OF off (else every launch would fall back)
         const bool fast_ok = (flags & F_S2N) && !(flags & F_GCLIP) && workspace != nullptr &&
                              workspace_bytes >= FLAG_BYTES && Cout <= 65535 && Bn <= 65535;
@@ -1913,7 +1914,10 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
                               }();
             if (tbsg) {
                 const unsigned gb = (unsigned)(((dg.planes + dg.PB - 1) / dg.PB) * dg.nb);
-#define FP8A_TBSG(S_, M_) conv_tbsg_kernel<S_, M_><<<gb, 256, glds, s>>>(x, w, y, dg, fq, fqb, fqi, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi)
+                // (it emits the next matrix-core convolution's words when fp8a_conv2d_chain asked, em.form 0)
+                const EmitW emt = em.w && em.form == 0 ? em : EmitW{};
+                emitted = emt.w != nullptr;
+#define FP8A_TBSG(S_, M_) conv_tbsg_kernel<S_, M_><<<gb, 256, glds, s>>>(x, w, y, dg, fq, fqb, fqi, bA, bW, bR, tp, gate, ep, act, act_lo, act_hi, emt)
                 if (Mw == 2) { if (sw == 1) FP8A_TBSG(1, 2); else FP8A_TBSG(2, 2); }
                 else { if (sw == 1) FP8A_TBSG(1, 3); else FP8A_TBSG(2, 3); }
 #undef FP8A_TBSG
@@ -1975,6 +1979,8 @@ static int conv2d_impl(const float *x, const float *w, float *y, int64_t Bn, int
                                                      groups, Ho, Wo, E, Mw, bA, bW, bR, tp, flags | F_TB, nullptr,
                                                      nullptr, nullptr, 0u, ep, act, act_lo, act_hi, FqIn{});
         }
+        if (em.w && !emitted && dev_fill(em.invalid, 1, sizeof(uint32_t), s) != hipSuccess)  // (no emission here)
+            return hip_check("fp8a word image header");
         return hip_check("fp8a_conv2d (tensor-bias groups)");
     }
     // (a workspace below fp8a_conv2d_workspace_size but holding the flag word runs unsplit)
@@ -2312,8 +2318,10 @@ int fp8a_conv2d_chain(const float *x, const float *w, float *y, int64_t Bn, int6
         const WordImage wi = next_form == 1 ? word_image(Ho, Wo, 0, 0) : word_image(Ho, Wo, next_ph, next_pw);
         // (form 2, v5 words: the staged v5 depthwise producer -- conv2d_impl flags the image invalid
         // where that kernel does not run; form 0 / 1: ungrouped producers)
-        const bool prod = next_form == 2 ? (flags & F_V5) && groups > 1 && Cin == groups && Cout == groups
-                                         : groups == 1;
+        // (form 0 from a depthwise producer: the staged table-form kernel, round 6)
+        const bool dwp = groups > 1 && Cin == groups && Cout == groups;
+        const bool prod = next_form == 2 ? (flags & F_V5) && dwp
+                                         : groups == 1 || (next_form == 0 && dwp && !(flags & F_V5));
         const bool can = prod && Cout > 1 && Ho > 0 && Wo > 0 && Bn * Cout * Ho * Wo < (1ll << 31) &&
                          Bn * Cout * wi.H * wi.W < (1ll << 30);
         // the header: valid (0) with the next quantizer's constants before this launch emits,

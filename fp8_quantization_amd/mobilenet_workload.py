@@ -10,6 +10,7 @@ tensor-bias semantics.  Pretrained weights need the network, so weig
 random unless a state dict is loaded.
 """
 import math
+import os
 
 from torch import nn
 
@@ -81,6 +82,10 @@ class MobileNetV2(nn.Module):
         return self.classifier(x)
 
 
+# FP8A_MBV2_XCHAIN=0: the hand-off only inside the residual blocks (the round-5 wiring)
+XCHAIN = os.environ.get("FP8A_MBV2_XCHAIN", "1") != "0"
+
+
 class QuantizedInvertedResidual(QuantizedActivation):
     """mobilenet_v2_quantized_approx.py:11-23: the residual sum is re-quantized."""
 
@@ -90,12 +95,32 @@ class QuantizedInvertedResidual(QuantizedActivation):
         self.conv = quantize_sequential(inv_res_orig.conv, **quant_params)
 
     def forward(self, x):
+        return self.forward_chain(x)[0]
+
+    def forward_chain(self, x, in_image=None, next_layer=None):
+        """forward, with the word-image hand-off (chain.WordChain) between the block's convolutions
+        and to next_layer (the first convolution of the next block; round 6: also for the blocks
+        without a residual, and across blocks): in_image is x's word image.  Returns (output, the
+        image emitted for next_layer or None).  The same bits as forward without the hand-off."""
+        from . import chain
+        from .quantization.quantized_folded_bn import BNFusedHijacker
+        if not XCHAIN:
+            in_image = next_layer = None
         if self.use_res_connect:
-            fused = fused_block_tail(self, self.conv, x, lambda t: t, None)
+            fused = fused_block_tail(self, self.conv, x, lambda t: t, None, in_image=in_image, next_layer=next_layer,
+                                     with_image=True)
             if fused is not None:
                 return fused
-            return self.quantize_activations(x + self.conv(x))
-        return self.conv(x)
+            return self.quantize_activations(x + self.conv(x)), None
+        layers = list(self.conv)
+        if not XCHAIN or not chain.CHAIN or not all(isinstance(m, BNFusedHijacker) for m in layers):
+            return self.conv(x), None
+        h, img = x, in_image
+        for i, m in enumerate(layers):  # (the chain acts only in each layer's fused store)
+            ch = chain.WordChain(img, layers[i + 1] if i + 1 < len(layers) else next_layer)
+            h = m(h, chain=ch)
+            img = ch.emitted
+        return h, img
 
 
 class QuantizedMobileNetV2(QuantizedModel):
@@ -114,7 +139,16 @@ class QuantizedMobileNetV2(QuantizedModel):
             raise ValueError("Quantization setup '{}' not supported for MobilenetV2".format(quant_setup))
 
     def forward(self, x):
-        return self.classifier(self.flattener(self.features(x)))
+        # the features in order, the inverted-residual blocks handing word images to each other
+        mods = list(self.features)
+        img = None
+        for i, m in enumerate(mods):
+            if isinstance(m, QuantizedInvertedResidual):
+                nxt = mods[i + 1] if i + 1 < len(mods) else None
+                x, img = m.forward_chain(x, img, nxt.conv[0] if isinstance(nxt, QuantizedInvertedResidual) else None)
+            else:
+                x, img = m(x), None
+        return self.classifier(self.flattener(x))
 
 
 def mobilenet_v2_approx(input_size=224, width_mult=1.0, n_class=1000, bn_stats_batches=0, device=None, **cfg):

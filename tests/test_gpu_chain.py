@@ -7,7 +7,8 @@ A producer convolution writes, next to its fp32 output y, the consumer's A opera
     a split-K producer (the reduction emits), a producer whose gated exact kernel recomputes
     units (the exact kernel emits), E4M3 and E5M2;
   * an image flagged invalid is re-decoded from y (same result);
-  * a producer that cannot emit (grouped) flags the image invalid;
+  * a producer that cannot emit (grouped) flags the image invalid; a tensor-bias depthwise producer
+    (the staged table-form kernel) emits the next 1x1 convolution's matrix-core words (round 6);
   * model level: ResNet-18 / ResNet-50 logits bit-identical with the hand-off on and off, and the
     hand-off really ran (fewer full pre-passes: counted through the launch trace of a profiler-free
     counter, the consumer launches that read an image).
@@ -299,3 +300,75 @@ def test_mobilenet_v5_logits_identical_with_chain(monkeypatch):
     with torch.no_grad():
         off = m(x)
     assert torch.equal(_bits(on), _bits(off)), "logits differ with the v5 word-image hand-off"
+
+
+@pytest.mark.parametrize("E,M", [(4, 3), (5, 2)])
+@pytest.mark.parametrize("stride", [1, 2])
+def test_depthwise_handoff_to_matrix_core(E, M, stride):
+    """A tensor-bias depthwise layer (the staged table-form conv_tbsg_kernel) emitting the matrix-core
+    words of the next 1x1 convolution's input (fp8a_conv2d_chain next_form 0, round 6): its own output
+    unchanged, the image valid, and the consumer reading it gives the unchained result bit for bit,
+    with the same input-quantizer bias."""
+    from fp8_quantization_amd import _lib
+    from fp8_quantization_amd.approx_ops import approx_conv2d, make_flags, new_word_image
+    from fp8_quantization_amd.error_tables import get_error_table_NN
+    g = torch.Generator().manual_seed(17 + stride + M)
+    C, H = 24, 15
+    b = 2 ** (E - 1)
+    x = _grid(g, (2, C, H, H), M).to(DEV)
+    wd = _grid(g, (C, 1, 3, 3), M, -8, 0, 0.0).to(DEV)
+    wp = _grid(g, (40, C, 1, 1), M, -8, 0, 0.0).to(DEV)
+    tab = get_error_table_NN(E, M, False, 3, zero_table_ext=(E, M) == (5, 2))
+    fl = make_flags(True, True, True)
+    bWd = torch.full((C,), b + 6, dtype=torch.int32, device=DEV)
+    bWp = torch.full((40,), b + 6, dtype=torch.int32, device=DEV)
+    bR = torch.tensor([b], dtype=torch.int32, device=DEV)
+    qin1 = (torch.tensor([9.0], device=DEV), 8, M, 1)
+    qin2 = (torch.tensor([3.5], device=DEV), 8, M, 1)
+    Ho = (H + 2 - 3) // stride + 1
+    img = new_word_image(2, C, Ho, Ho, 0, 0, DEV)
+    args1 = dict(flags=fl, stride=(stride, stride), padding=(1, 1), groups=C)
+    y, _, _ = approx_conv2d(x, wd, E, M, None, bWd, bR, tab, qin=qin1, chain=(None, (img, (0, 0), qin2, bR, M)),
+                            **args1)
+    y0, _, _ = approx_conv2d(x, wd, E, M, None, bWd, bR, tab, qin=qin1, **args1)
+    torch.cuda.synchronize()
+    assert torch.equal(_bits(y), _bits(y0))
+    assert int(img[:4].view(torch.int32).item()) == 0, "the staged depthwise producer did not emit"
+    _lib.path_stats(reset=True)
+    z, ib, _ = approx_conv2d(y, wp, E, M, None, bWp, bR, tab, qin=qin2, flags=fl)
+    z2, ib2, _ = approx_conv2d(y, wp, E, M, None, bWp, bR, tab, qin=qin2, flags=fl, chain=(img, None))
+    assert _lib.path_stats(reset=True)["f8mx"] >= 2
+    assert torch.equal(_bits(z), _bits(z2)) and torch.equal(ib, ib2)
+
+
+@pytest.mark.parametrize("fmt", [(4, 3), (5, 2)])
+def test_mobilenet_v9_logits_identical_with_chain(fmt, monkeypatch):
+    """MobileNetV2 approx_v9 (E4M3, and config 3's E5M2): logits with every hand-off -- now also
+    depthwise -> projection on the matrix-core words -- on and off, to the bit."""
+    from fp8_quantization_amd import chain
+    from fp8_quantization_amd.mobilenet_workload import mobilenet_v2_approx
+    E, M = fmt
+    torch.manual_seed(5)
+    m = mobilenet_v2_approx(input_size=64, n_class=100, bn_stats_batches=1, device=DEV, expo_width=E,
+                            mant_width=M).to(DEV).eval()
+    g = torch.Generator().manual_seed(6)
+    m.quantized()
+    m.estimate_ranges()
+    with torch.no_grad():
+        m(torch.randn((2, 3, 64, 64), generator=g).to(DEV))
+    m.fix_ranges()
+    x = torch.randn((3, 3, 64, 64), generator=g).to(DEV)
+    emitted = []
+    orig_done = chain.WordChain.done
+
+    def done(self, ch):
+        orig_done(self, ch)
+        emitted.append(self.emitted is not None)
+    monkeypatch.setattr(chain.WordChain, "done", done)
+    with torch.no_grad():
+        on = m(x)
+    assert sum(emitted) >= 15, emitted  # within and across the blocks, depthwise producers included
+    monkeypatch.setattr(chain, "CHAIN", False)
+    with torch.no_grad():
+        off = m(x)
+    assert torch.equal(_bits(on), _bits(off)), "logits differ with the word-image hand-off"

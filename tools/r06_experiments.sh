@@ -18,6 +18,9 @@
 #               E4M3 and E5M2 v9 with the default vs lib/ab/libfp8approx_r6base.so (the previous commit)
 #   tapt        staged table-form depthwise with per-tap tables (TBSG_TAPT): depthwise / chain / model
 #               tests, then MobileNetV2 E4M3 and E5M2 v9 with the default vs lib/ab/libfp8approx_tapt0.so
+#   dwemit      depthwise -> 1x1 word-image hand-off (form 0 from conv_tbsg_kernel): chain / depthwise /
+#               model tests, then MobileNetV2 E4M3 and E5M2 v9 with the hand-off across blocks
+#               (FP8A_MBV2_XCHAIN) on and off
 #   multirank   two ranks on one GPU over gloo vs two world-1 runs (logits and FP8 state per rank)
 # A/B libraries: python -c "from fp8_quantization_amd import build_native as b; b.build(force=True,
 #   out='fp8_quantization_amd/lib/ab/<name>.so', extra=b.EXTRA + ['-D...'])"
@@ -152,6 +155,19 @@ tapt() {
     L=""; [ $v != def ] && L=$AB/libfp8approx_$v.so
     bench_line $O mbv2_e4m3_$v "$L" --arch mobilenet_v2 --batch 512 || return 1
     bench_line $O mbv2_e5m2_$v "$L" --arch mobilenet_v2 --batch 512 --expo-width 5 --mant-width 2 || return 1
+  done
+}
+
+dwemit() {
+  local O=gpurun_out/dwemit; mkdir -p $O
+  timeout -k 10 900 python -u -m pytest tests/test_gpu_chain.py tests/test_gpu_tbx.py tests/test_gpu_mbv2_layers.py \
+    tests/test_gpu_model.py tests/test_gpu_graph.py -q -x --timeout 300 > $O/tests.log 2>&1 || { tail -5 $O/tests.log; return 1; }
+  tail -1 $O/tests.log
+  bench_line $O mbv2_e4m3 "" --arch mobilenet_v2 --batch 512 || return 1
+  bench_line $O mbv2_e5m2 "" --arch mobilenet_v2 --batch 512 --expo-width 5 --mant-width 2 || return 1
+  for v in 0 1; do
+    FP8A_MBV2_XCHAIN=$v bench_line $O mbv2_e4m3_x$v "" --arch mobilenet_v2 --batch 512 || return 1
+    FP8A_MBV2_XCHAIN=$v bench_line $O mbv2_e5m2_x$v "" --arch mobilenet_v2 --batch 512 --expo-width 5 --mant-width 2 || return 1
   done
 }
 
