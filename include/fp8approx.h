@@ -349,9 +349,10 @@ int fp8a_word_image_init(void *image, int64_t Bn, int64_t C, int64_t H, int64_t 
  *             convolution's fp8a_conv2d_wants_image - 1 (0: matrix-core words in an image of
  *             next_ph / next_pw; 1: table-form words, image of ph = pw = 0; 2: the v5 matrix-core
  *             form's words, emitted by a v5 depthwise 3x3 producer on its staged kernel).  y is
- *             written as well.  Where this call cannot emit (groups > 1 outside form 2, Cout == 1,
- *             a tile-table or v5 matrix-core producer, whose store does not emit) the image is
- *             flagged invalid.
+ *             written as well; form 0 is also emitted by a tensor-bias depthwise 3x3 producer on
+ *             its staged table-form kernel (round 6).  Where this call cannot emit (other grouped
+ *             producers, Cout == 1, a tile-table or v5 matrix-core producer, whose store does not
+ *             emit, a depthwise launch on another kernel) the image is flagged invalid.
  * Results are bit-identical to the unchained calls.  workspace: fp8a_conv2d_block_workspace_size().
  */
 /* The word image a convolution of this shape / format would read as in_image: 1 = the matrix-core
